@@ -1,0 +1,236 @@
+// pybind11 module `docker_dist_nn_amd._native`: the host entry points of the gfx950 kernels and
+// the native runtime pieces (schedule generator/simulator, neuron-JSON weight IO, HIP graph
+// executor). Device pointers and HIP streams cross the boundary as integers
+// (torch.Tensor.data_ptr(), torch.cuda.Stream.cuda_stream); shapes are validated on the host
+// before any launch and a failed check raises instead of launching.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "kernels/elementwise.hpp"
+#include "kernels/gemm.hpp"
+#include "runtime/graph.hpp"
+#include "runtime/json_weights.hpp"
+#include "runtime/schedule.hpp"
+
+namespace py = pybind11;
+using dnn::GemmParams;
+
+static hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+template <class T>
+static T* P(uintptr_t p) {
+  return reinterpret_cast<T*>(p);
+}
+
+static void check(int rc, const char* what) {
+  if (rc != 0) {
+    std::string msg = std::string(what) + " failed: ";
+    if (std::string(what) == "gemm_bf16") msg += dnn::gemm_error_string(rc);
+    else msg += "precondition/launch error code " + std::to_string(rc);
+    if (rc == -9) msg += std::string(" (") + hipGetErrorString(hipGetLastError()) + ")";
+    throw std::invalid_argument(msg);
+  }
+}
+
+PYBIND11_MODULE(_native, m) {
+  m.doc() = "docker_dist_nn_amd native runtime + gfx950 HIP kernels";
+
+  m.def(
+      "gemm_bf16",
+      [](uintptr_t a, long lda, uintptr_t b, long ldb, uintptr_t c, long ldc, long c_split_stride,
+         uintptr_t bias, uintptr_t aux, long ld_aux, int M, int N, int K, int act, int accumulate,
+         int layout_a, int layout_b, int out_f32, int bm, int bn, int splits, uintptr_t stream) {
+        GemmParams p{};
+        p.A = P<const uint16_t>(a);
+        p.lda = lda;
+        p.B = P<const uint16_t>(b);
+        p.ldb = ldb;
+        p.C = P<void>(c);
+        p.ldc = ldc;
+        p.c_split_stride = c_split_stride;
+        p.bias = P<const float>(bias);
+        p.aux = P<const uint16_t>(aux);
+        p.ld_aux = ld_aux;
+        p.M = M;
+        p.N = N;
+        p.K = K;
+        p.act = act;
+        p.accumulate = accumulate;
+        check(dnn::gemm_bf16(p, layout_a, layout_b, out_f32, bm, bn, splits, S(stream)),
+              "gemm_bf16");
+      },
+      py::arg("a"), py::arg("lda"), py::arg("b"), py::arg("ldb"), py::arg("c"), py::arg("ldc"),
+      py::arg("c_split_stride"), py::arg("bias"), py::arg("aux"), py::arg("ld_aux"), py::arg("M"),
+      py::arg("N"), py::arg("K"), py::arg("act"), py::arg("accumulate"), py::arg("layout_a"),
+      py::arg("layout_b"), py::arg("out_f32"), py::arg("bm"), py::arg("bn"), py::arg("splits"),
+      py::arg("stream"));
+
+  m.def("softmax_xent",
+        [](uintptr_t logits, long ld_logits, uintptr_t labels, uintptr_t dz, long ld_dz, int rows,
+           int n_cls, int width, float scale, uintptr_t loss_sum, uintptr_t correct,
+           uintptr_t stream) {
+          check(dnn::softmax_xent(P<const float>(logits), ld_logits, P<const int>(labels),
+                                  P<uint16_t>(dz), ld_dz, rows, n_cls, width, scale,
+                                  P<float>(loss_sum), P<int>(correct), S(stream)),
+                "softmax_xent");
+        });
+  m.def("softmax_rows", [](uintptr_t logits, long ld_in, uintptr_t out, long ld_out, int rows,
+                           int n_cls, uintptr_t labels, uintptr_t pred, uintptr_t correct,
+                           uintptr_t stream) {
+    check(dnn::softmax_rows(P<const float>(logits), ld_in, P<float>(out), ld_out, rows, n_cls,
+                            P<const int>(labels), P<int>(pred), P<int>(correct), S(stream)),
+          "softmax_rows");
+  });
+  m.def("colsum_partial", [](uintptr_t x, long ld, int rows, int cols, int n_part, uintptr_t part,
+                             uintptr_t stream) {
+    check(dnn::colsum_partial(P<const uint16_t>(x), ld, rows, cols, n_part, P<float>(part),
+                              S(stream)),
+          "colsum_partial");
+  });
+  m.def("reduce_slabs", [](uintptr_t src, long stride, int n_src, long n, float scale,
+                           uintptr_t out, int accumulate, uintptr_t stream) {
+    check(dnn::reduce_slabs(P<const float>(src), stride, n_src, n, scale, P<float>(out),
+                            accumulate, S(stream)),
+          "reduce_slabs");
+  });
+  m.def("sgd_update", [](uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t shadow, long n,
+                         float lr, float mu, float wd, uintptr_t stream) {
+    check(dnn::sgd_update(P<float>(p), P<const float>(g), P<float>(mom), P<uint16_t>(shadow), n,
+                          lr, mu, wd, S(stream)),
+          "sgd_update");
+  });
+  m.def("adam_update",
+        [](uintptr_t p, uintptr_t g, uintptr_t mm, uintptr_t vv, uintptr_t shadow, long n,
+           float lr, float b1, float b2, float eps, float wd, int decoupled, float bc1, float bc2,
+           uintptr_t stream) {
+          check(dnn::adam_update(P<float>(p), P<const float>(g), P<float>(mm), P<float>(vv),
+                                 P<uint16_t>(shadow), n, lr, b1, b2, eps, wd, decoupled, bc1, bc2,
+                                 S(stream)),
+                "adam_update");
+        });
+  m.def("pack_bf16", [](uintptr_t in, long ld_in, int rows, int cols, uintptr_t out, long ld_out,
+                        int rows_p, int cols_p, uintptr_t stream) {
+    check(dnn::pack_bf16(P<const float>(in), ld_in, rows, cols, P<uint16_t>(out), ld_out, rows_p,
+                         cols_p, S(stream)),
+          "pack_bf16");
+  });
+  m.def("unpack_bf16", [](uintptr_t in, long ld_in, int rows, int cols, uintptr_t out,
+                          long ld_out, uintptr_t stream) {
+    check(dnn::unpack_bf16(P<const uint16_t>(in), ld_in, rows, cols, P<float>(out), ld_out,
+                           S(stream)),
+          "unpack_bf16");
+  });
+
+  // ---- runtime: pipeline schedules -------------------------------------------------------
+  py::enum_<dnn::OpKind>(m, "OpKind")
+      .value("FWD", dnn::OpKind::FWD)
+      .value("BWD", dnn::OpKind::BWD)
+      .value("WGRAD", dnn::OpKind::WGRAD)
+      .value("OPT", dnn::OpKind::OPT);
+  py::class_<dnn::SchedOp>(m, "SchedOp")
+      .def_readonly("kind", &dnn::SchedOp::kind)
+      .def_readonly("micro", &dnn::SchedOp::micro)
+      .def("__repr__", [](const dnn::SchedOp& o) {
+        static const char* n[] = {"F", "B", "W", "O"};
+        return std::string(n[(int)o.kind]) + std::to_string(o.micro);
+      });
+  m.def("make_schedule", &dnn::make_schedule, py::arg("kind"), py::arg("num_stages"),
+        py::arg("num_micro"), py::arg("stage"),
+        "Ordered compute ops of one pipeline stage for one training step.");
+  m.def("simulate_schedule", &dnn::simulate_schedule, py::arg("kind"), py::arg("num_stages"),
+        py::arg("num_micro"), py::arg("t_fwd"), py::arg("t_bwd"), py::arg("t_wgrad"),
+        py::arg("t_comm"),
+        "Event simulation of a step; returns (makespan, per-stage busy time, bubble fraction).");
+
+  // ---- runtime: neuron-JSON weight IO -----------------------------------------------------
+  m.def(
+      "parse_neuron_json",
+      [](const std::string& path) {
+        dnn::ParsedModel pm = dnn::parse_neuron_json_file(path);
+        py::list layers;
+        for (auto& L : pm.layers) {
+          py::dict d;
+          d["key"] = L.key;
+          d["type"] = L.type;
+          d["nodes"] = L.nodes;
+          d["activation"] = L.activation;
+          d["mixed_activation"] = L.mixed_activation;
+          d["in_dim"] = L.in_dim;
+          const py::ssize_t n_out = (py::ssize_t)L.bias.size();  // neurons actually present
+          py::array_t<float> w({n_out, (py::ssize_t)L.in_dim});
+          if (!L.weights.empty())
+            std::memcpy(w.mutable_data(), L.weights.data(), L.weights.size() * sizeof(float));
+          py::array_t<float> b(n_out);
+          if (n_out) std::memcpy(b.mutable_data(), L.bias.data(), L.bias.size() * sizeof(float));
+          d["weights"] = w;
+          d["bias"] = b;
+          layers.append(d);
+        }
+        py::dict out;
+        out["layers"] = layers;
+        out["layer_distribution"] = pm.layer_distribution;
+        out["has_distribution"] = pm.has_distribution;
+        out["wrapped"] = pm.wrapped;
+        out["stage_file"] = pm.stage_file;
+        return out;
+      },
+      py::arg("path"),
+      "Parse a reference model config / stage file into float32 weight matrices.");
+  m.def(
+      "write_neuron_json",
+      [](const std::string& path, const std::vector<py::array_t<float, py::array::c_style>>& ws,
+         const std::vector<py::array_t<float, py::array::c_style>>& bs,
+         const std::vector<std::string>& acts, const std::vector<std::string>& types,
+         const std::vector<int>& distribution, bool stage_file) {
+        std::vector<dnn::LayerOut> L(ws.size());
+        for (size_t i = 0; i < ws.size(); ++i) {
+          if (ws[i].ndim() != 2 || bs[i].ndim() != 1 || bs[i].shape(0) != ws[i].shape(0))
+            throw std::invalid_argument("weights must be [out,in] and bias [out]");
+          L[i].out = (int)ws[i].shape(0);
+          L[i].in = (int)ws[i].shape(1);
+          L[i].w = ws[i].data();
+          L[i].b = bs[i].data();
+          L[i].activation = acts.at(i);
+          L[i].type = types.at(i);
+        }
+        dnn::write_neuron_json_file(path, L, distribution, stage_file);
+      },
+      py::arg("path"), py::arg("weights"), py::arg("biases"), py::arg("activations"),
+      py::arg("types"), py::arg("layer_distribution"), py::arg("stage_file"));
+
+  m.def(
+      "parse_examples_json",
+      [](const std::string& path) {
+        dnn::ParsedExamples E = dnn::parse_examples_json_file(path);
+        py::array_t<float> x({(py::ssize_t)E.n, (py::ssize_t)E.dim});
+        if (!E.x.empty()) std::memcpy(x.mutable_data(), E.x.data(), E.x.size() * sizeof(float));
+        py::array_t<int> y((py::ssize_t)E.n);
+        if (!E.labels.empty())
+          std::memcpy(y.mutable_data(), E.labels.data(), E.labels.size() * sizeof(int));
+        py::dict out;
+        out["x"] = x;
+        out["labels"] = y;
+        out["outer_len"] = E.outer_len;
+        out["raw_list"] = E.raw_list;
+        return out;
+      },
+      py::arg("path"), "Parse an inputs JSON ({\"examples\": [...]}) into float32 + int32 arrays.");
+
+  // ---- runtime: HIP graph executor ------------------------------------------------------
+  py::class_<dnn::GraphExec>(m, "GraphExec")
+      .def(py::init<>())
+      .def("begin_capture", [](dnn::GraphExec& g, uintptr_t s) { g.begin_capture(S(s)); })
+      .def("end_capture", &dnn::GraphExec::end_capture)
+      .def("replay", [](dnn::GraphExec& g, uintptr_t s) { g.replay(S(s)); })
+      .def_property_readonly("captured", &dnn::GraphExec::captured)
+      .def_property_readonly("num_nodes", &dnn::GraphExec::num_nodes)
+      .def("reset", &dnn::GraphExec::reset);
+  m.def("device_sync", []() {
+    hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) throw std::runtime_error(hipGetErrorString(e));
+  });
+}

@@ -1,0 +1,364 @@
+// Memory-bound kernels of the training/inference step (gfx950). All vectorised to 16-byte
+// accesses (guide Guideline 13); each one replaces a piece of reference behaviour:
+//   softmax_xent   : fused softmax + cross-entropy forward/backward + argmax accuracy
+//                    (training replacement of the row softmax in
+//                    /root/reference/src/grpc_node.py:68-71 and the CE loss of
+//                    /root/reference/scripts/generate_mnist_pytorch.py:37,48)
+//   softmax_rows   : inference softmax (grpc_node.py:68-71) + argmax/label compare
+//                    (/root/reference/src/run_grpc_inference.py:192-193, 208-209)
+//   colsum_partial : bias gradient partial column sums of dZ
+//   reduce_slabs   : split-K slab / partial reduction into the flat gradient buffer
+//   sgd / adam     : fused multi-tensor optimizer over the flat fp32 master buffer, refreshing
+//                    the bf16 shadow weights in the same pass
+//   pack_bf16      : fp32 host data -> padded bf16 device layout (and back)
+#include "common.hpp"
+#include "elementwise.hpp"
+
+namespace dnn {
+
+// ------------------------------------------------------------------------------------------
+// softmax + cross-entropy, one wave per row (padded width <= 64*NCH columns).
+// dz = (softmax(logits) - onehot(label)) * scale in the first n_cls columns, 0 elsewhere.
+// Rows whose label is < 0 are padding: dz = 0 and no loss. loss_sum / correct are reduced per
+// block and added with one atomic each.
+// ------------------------------------------------------------------------------------------
+template <int NCH>
+__global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restrict__ logits,
+                                                           long ld_logits,
+                                                           const int* __restrict__ labels,
+                                                           u16* __restrict__ dz, long ld_dz,
+                                                           int rows, int n_cls, int width,
+                                                           float scale, float* loss_sum,
+                                                           int* correct) {
+  __shared__ float s_loss[4];
+  __shared__ int s_corr[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int row = blockIdx.x * 4 + wave;
+  float loss = 0.f;
+  int corr = 0;
+  if (row < rows) {
+    const float* lr = logits + (long)row * ld_logits;
+    const int label = labels[row];
+    float x[NCH];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 64 + lane;
+      x[c] = col < n_cls ? lr[col] : -INFINITY;
+      mx = fmaxf(mx, x[c]);
+    }
+    mx = wave_max(mx);
+    // argmax: lowest column index holding the max (np.argmax tie rule)
+    int amax = 1 << 30;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 64 + lane;
+      if (col < n_cls && x[c] == mx) amax = min(amax, col);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) amax = min(amax, __shfl_xor(amax, o, 64));
+    float se = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      x[c] = __expf(x[c] - mx);  // exp(-inf) = 0 for padding
+      se += x[c];
+    }
+    se = wave_sum(se);
+    const float inv = 1.f / se;
+    u16* dr = dz + (long)row * ld_dz;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 64 + lane;
+      if (col < width) {
+        float g = 0.f;
+        if (label >= 0 && col < n_cls) g = (x[c] * inv - (col == label ? 1.f : 0.f)) * scale;
+        dr[col] = f2bf(g);
+      }
+    }
+    if (label >= 0 && lane == 0) {
+      const float xl = lr[label];
+      loss = -(xl - mx - __logf(se));
+      corr = amax == label;
+    }
+  }
+  if (lane == 0) {
+    s_loss[wave] = loss;
+    s_corr[wave] = corr;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float l = s_loss[0] + s_loss[1] + s_loss[2] + s_loss[3];
+    const int cc = s_corr[0] + s_corr[1] + s_corr[2] + s_corr[3];
+    if (loss_sum && l != 0.f) atomicAdd(loss_sum, l);
+    if (correct && cc) atomicAdd(correct, cc);
+  }
+}
+
+int softmax_xent(const float* logits, long ld_logits, const int* labels, uint16_t* dz, long ld_dz,
+                 int rows, int n_cls, int width, float scale, float* loss_sum, int* correct,
+                 hipStream_t stream) {
+  if (rows <= 0 || n_cls <= 0 || n_cls > width || width > 256 || ld_logits < n_cls ||
+      ld_dz < width)
+    return -1;
+  const dim3 grid((rows + 3) / 4), block(256);
+  if (width <= 64)
+    hipLaunchKernelGGL(softmax_xent_kernel<1>, grid, block, 0, stream, logits, ld_logits, labels,
+                       dz, ld_dz, rows, n_cls, width, scale, loss_sum, correct);
+  else
+    hipLaunchKernelGGL(softmax_xent_kernel<4>, grid, block, 0, stream, logits, ld_logits, labels,
+                       dz, ld_dz, rows, n_cls, width, scale, loss_sum, correct);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
+// ------------------------------------------------------------------------------------------
+// Inference softmax over the first n_cls columns (rest zero) + optional argmax correctness.
+// ------------------------------------------------------------------------------------------
+template <int NCH>
+__global__ __launch_bounds__(256) void softmax_rows_kernel(const float* __restrict__ logits,
+                                                           long ld_in, float* __restrict__ out,
+                                                           long ld_out, int rows, int n_cls,
+                                                           const int* __restrict__ labels,
+                                                           int* __restrict__ pred, int* correct) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int row = blockIdx.x * 4 + wave;
+  if (row >= rows) return;
+  const float* lr = logits + (long)row * ld_in;
+  float x[NCH];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 64 + lane;
+    x[c] = col < n_cls ? lr[col] : -INFINITY;
+    mx = fmaxf(mx, x[c]);
+  }
+  mx = wave_max(mx);
+  int amax = 1 << 30;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 64 + lane;
+    if (col < n_cls && x[c] == mx) amax = min(amax, col);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) amax = min(amax, __shfl_xor(amax, o, 64));
+  float se = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    x[c] = __expf(x[c] - mx);
+    se += x[c];
+  }
+  se = wave_sum(se);
+  const float inv = 1.f / se;
+  if (out) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 64 + lane;
+      if (col < n_cls) out[(long)row * ld_out + col] = x[c] * inv;
+    }
+  }
+  if (lane == 0) {
+    if (pred) pred[row] = amax;
+    if (correct && labels && labels[row] == amax) atomicAdd(correct, 1);
+  }
+}
+
+int softmax_rows(const float* logits, long ld_in, float* out, long ld_out, int rows, int n_cls,
+                 const int* labels, int* pred, int* correct, hipStream_t stream) {
+  if (rows <= 0 || n_cls <= 0 || n_cls > 256 || ld_in < n_cls || (out && ld_out < n_cls))
+    return -1;
+  const dim3 grid((rows + 3) / 4), block(256);
+  if (n_cls <= 64)
+    hipLaunchKernelGGL(softmax_rows_kernel<1>, grid, block, 0, stream, logits, ld_in, out, ld_out,
+                       rows, n_cls, labels, pred, correct);
+  else
+    hipLaunchKernelGGL(softmax_rows_kernel<4>, grid, block, 0, stream, logits, ld_in, out, ld_out,
+                       rows, n_cls, labels, pred, correct);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
+// ------------------------------------------------------------------------------------------
+// Column partial sums of a bf16 [rows][ld] matrix (first `cols` columns, cols % 64 == 0).
+// Block = 64 columns x (32 row lanes); grid.y = number of partial row blocks. Writes
+// part[blockIdx.y][cols]; the optimizer-side reduce_slabs finishes the sum deterministically.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const u16* __restrict__ x, long ld,
+                                                             int rows, int cols, int rows_per,
+                                                             float* __restrict__ part) {
+  __shared__ float red[32][65];
+  const int cc = threadIdx.x & 7;   // 8-column chunk within the 64-column strip
+  const int rl = threadIdx.x >> 3;  // row lane 0..31
+  const int col0 = blockIdx.x * 64 + cc * 8;
+  const int r_begin = blockIdx.y * rows_per;
+  const int r_end = min(rows, r_begin + rows_per);
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int r = r_begin + rl; r < r_end; r += 32) {
+    const bf16x8_t v = *(const bf16x8_t*)(x + (long)r * ld + col0);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s[e] += bf2f((u16)v[e]);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[rl][cc * 8 + e] = s[e];
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float t = 0.f;
+#pragma unroll 8
+    for (int i = 0; i < 32; ++i) t += red[i][threadIdx.x];
+    part[(long)blockIdx.y * cols + blockIdx.x * 64 + threadIdx.x] = t;
+  }
+}
+
+int colsum_partial(const uint16_t* x, long ld, int rows, int cols, int n_part, float* part,
+                   hipStream_t stream) {
+  if (rows <= 0 || cols <= 0 || cols % 64 || ld % 8 || ld < cols || n_part <= 0) return -1;
+  if (((uintptr_t)x) & 15) return -5;
+  const int rows_per = (rows + n_part - 1) / n_part;
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3(cols / 64, n_part), dim3(256), 0, stream, x, ld,
+                     rows, cols, rows_per, part);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
+// ------------------------------------------------------------------------------------------
+// out[i] (+)= scale * sum_{s < n_src} src[s * stride + i], i < n  (n % 4 == 0)
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void reduce_slabs_kernel(const float* __restrict__ src,
+                                                           long stride, int n_src, long n4,
+                                                           float scale, float* __restrict__ out,
+                                                           int accumulate) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    f32x4_t a = *(const f32x4_t*)(src + i * 4);
+    for (int s = 1; s < n_src; ++s) a += *(const f32x4_t*)(src + s * stride + i * 4);
+    a *= scale;
+    if (accumulate) a += *(const f32x4_t*)(out + i * 4);
+    *(f32x4_t*)(out + i * 4) = a;
+  }
+}
+
+static int grid_for(long n4) {
+  long g = (n4 + 255) / 256;
+  return (int)(g < 2048 ? (g > 0 ? g : 1) : 2048);
+}
+
+int reduce_slabs(const float* src, long stride, int n_src, long n, float scale, float* out,
+                 int accumulate, hipStream_t stream) {
+  if (n <= 0 || n % 4 || n_src <= 0 || (n_src > 1 && stride % 4)) return -1;
+  if ((((uintptr_t)src) | ((uintptr_t)out)) & 15) return -5;
+  hipLaunchKernelGGL(reduce_slabs_kernel, dim3(grid_for(n / 4)), dim3(256), 0, stream, src, stride,
+                     n_src, n / 4, scale, out, accumulate);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
+// ------------------------------------------------------------------------------------------
+// Fused SGD (+momentum, +decoupled-from-nothing L2 weight decay like torch.optim.SGD):
+//   g' = g + wd * p ; v = mu * v + g' (if mu != 0) ; p -= lr * (v or g') ; shadow = bf16(p)
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                  float* __restrict__ mom, u16* __restrict__ shadow,
+                                                  long n4, float lr, float mu, float wd) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    f32x4_t pv = *(const f32x4_t*)(p + i * 4);
+    f32x4_t gv = *(const f32x4_t*)(g + i * 4);
+    gv += wd * pv;
+    if (mom) {
+      f32x4_t m = *(const f32x4_t*)(mom + i * 4);
+      m = mu * m + gv;
+      *(f32x4_t*)(mom + i * 4) = m;
+      gv = m;
+    }
+    pv -= lr * gv;
+    *(f32x4_t*)(p + i * 4) = pv;
+    if (shadow) {
+      bf16x4_t o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (short)f2bf(pv[e]);
+      *(bf16x4_t*)(shadow + i * 4) = o;
+    }
+  }
+}
+
+int sgd_update(float* p, const float* g, float* mom, uint16_t* shadow, long n, float lr, float mu,
+               float wd, hipStream_t stream) {
+  if (n <= 0 || n % 4) return -1;
+  hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n / 4)), dim3(256), 0, stream, p, g, mom, shadow,
+                     n / 4, lr, mu, wd);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
+// Adam / AdamW (torch.optim semantics; bc1 = 1/(1-b1^t), bc2 = 1/(1-b2^t) computed on the host).
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v,
+                                                   u16* __restrict__ shadow, long n4, float lr,
+                                                   float b1, float b2, float eps, float wd,
+                                                   int decoupled, float bc1, float bc2) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    f32x4_t pv = *(const f32x4_t*)(p + i * 4);
+    f32x4_t gv = *(const f32x4_t*)(g + i * 4);
+    if (decoupled) pv *= (1.f - lr * wd);
+    else gv += wd * pv;
+    f32x4_t mv = *(const f32x4_t*)(m + i * 4);
+    f32x4_t vv = *(const f32x4_t*)(v + i * 4);
+    mv = b1 * mv + (1.f - b1) * gv;
+    vv = b2 * vv + (1.f - b2) * gv * gv;
+    *(f32x4_t*)(m + i * 4) = mv;
+    *(f32x4_t*)(v + i * 4) = vv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) pv[e] -= lr * (mv[e] * bc1) / (sqrtf(vv[e] * bc2) + eps);
+    *(f32x4_t*)(p + i * 4) = pv;
+    if (shadow) {
+      bf16x4_t o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (short)f2bf(pv[e]);
+      *(bf16x4_t*)(shadow + i * 4) = o;
+    }
+  }
+}
+
+int adam_update(float* p, const float* g, float* m, float* v, uint16_t* shadow, long n, float lr,
+                float b1, float b2, float eps, float wd, int decoupled, float bc1, float bc2,
+                hipStream_t stream) {
+  if (n <= 0 || n % 4) return -1;
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4)), dim3(256), 0, stream, p, g, m, v, shadow,
+                     n / 4, lr, b1, b2, eps, wd, decoupled, bc1, bc2);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
+// ------------------------------------------------------------------------------------------
+// fp32 [rows][cols] (ld_in) -> bf16 [rows_p][cols_p] (ld_out) with zero padding, and back.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void pack_bf16_kernel(const float* __restrict__ in, long ld_in,
+                                                        int rows, int cols, u16* __restrict__ out,
+                                                        long ld_out, int rows_p, int cols_p) {
+  const long total = (long)rows_p * cols_p;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int r = (int)(i / cols_p), c = (int)(i % cols_p);
+    const float v = (r < rows && c < cols) ? in[(long)r * ld_in + c] : 0.f;
+    out[(long)r * ld_out + c] = f2bf(v);
+  }
+}
+
+int pack_bf16(const float* in, long ld_in, int rows, int cols, uint16_t* out, long ld_out,
+              int rows_p, int cols_p, hipStream_t stream) {
+  if (rows_p < rows || cols_p < cols || ld_out < cols_p || ld_in < cols) return -1;
+  const long total = (long)rows_p * cols_p;
+  hipLaunchKernelGGL(pack_bf16_kernel, dim3(grid_for((total + 3) / 4)), dim3(256), 0, stream, in,
+                     ld_in, rows, cols, out, ld_out, rows_p, cols_p);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
+__global__ __launch_bounds__(256) void unpack_bf16_kernel(const u16* __restrict__ in, long ld_in,
+                                                          int rows, int cols,
+                                                          float* __restrict__ out, long ld_out) {
+  const long total = (long)rows * cols;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int r = (int)(i / cols), c = (int)(i % cols);
+    out[(long)r * ld_out + c] = bf2f(in[(long)r * ld_in + c]);
+  }
+}
+
+int unpack_bf16(const uint16_t* in, long ld_in, int rows, int cols, float* out, long ld_out,
+                hipStream_t stream) {
+  if (rows <= 0 || cols <= 0 || ld_in < cols || ld_out < cols) return -1;
+  hipLaunchKernelGGL(unpack_bf16_kernel, dim3(grid_for(((long)rows * cols + 3) / 4)), dim3(256), 0,
+                     stream, in, ld_in, rows, cols, out, ld_out);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
+}  // namespace dnn

@@ -1,0 +1,28 @@
+// Host-visible launchers of csrc/kernels/elementwise.hip. All return 0 on success and a
+// negative code (nothing launched) when a host-side precondition fails.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dnn {
+
+int softmax_xent(const float* logits, long ld_logits, const int* labels, uint16_t* dz, long ld_dz,
+                 int rows, int n_cls, int width, float scale, float* loss_sum, int* correct,
+                 hipStream_t stream);
+int softmax_rows(const float* logits, long ld_in, float* out, long ld_out, int rows, int n_cls,
+                 const int* labels, int* pred, int* correct, hipStream_t stream);
+int colsum_partial(const uint16_t* x, long ld, int rows, int cols, int n_part, float* part,
+                   hipStream_t stream);
+int reduce_slabs(const float* src, long stride, int n_src, long n, float scale, float* out,
+                 int accumulate, hipStream_t stream);
+int sgd_update(float* p, const float* g, float* mom, uint16_t* shadow, long n, float lr, float mu,
+               float wd, hipStream_t stream);
+int adam_update(float* p, const float* g, float* m, float* v, uint16_t* shadow, long n, float lr,
+                float b1, float b2, float eps, float wd, int decoupled, float bc1, float bc2,
+                hipStream_t stream);
+int pack_bf16(const float* in, long ld_in, int rows, int cols, uint16_t* out, long ld_out,
+              int rows_p, int cols_p, hipStream_t stream);
+int unpack_bf16(const uint16_t* in, long ld_in, int rows, int cols, float* out, long ld_out,
+                hipStream_t stream);
+
+}  // namespace dnn

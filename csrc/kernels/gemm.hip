@@ -1,0 +1,281 @@
+// bf16 MFMA GEMM for gfx950 (MI355X) with fused training epilogues.
+//
+// Structure (cdna_hip_programming.md §5 "standard MFMA GEMM main loop"):
+//   * 256 threads = 4 waves in a 2x2 grid, each wave owns a (BM/2)x(BN/2) output sub-tile built
+//     from v_mfma_f32_16x16x32_bf16 fragments;
+//   * BK = 64; A and B tiles are staged global->LDS by LDS-DMA (global_load_lds_dwordx4, 1 KiB
+//     per wave-instruction) into two LDS buffers so the load of tile k+1 overlaps compute of k;
+//   * LDS images are XOR-swizzled so fragment reads are bank-conflict free; because the LDS-DMA
+//     destination is lane-linear, the swizzle is applied to the per-lane GLOBAL source address
+//     and the same involution is applied on the read (guide §5.4 rule 21);
+//   * contraction-contiguous tiles are read with ds_read_b128, output-dim-contiguous tiles with
+//     the transposing ds_read_b64_tr_b16 (guide §5.5 T10) -- this is what lets dgrad and wgrad
+//     consume W, dZ and X in their natural row-major layouts;
+//   * the epilogue stages the fp32 accumulators through LDS and stores whole 16-byte row chunks,
+//     fusing bias + activation (forward), activation-derivative masking from the stored
+//     activation output (dgrad), or fp32 split-K slab accumulation (wgrad);
+//   * workgroup ids are remapped so consecutive output tiles (sharing an A panel) land on the
+//     same XCD / L2 (guide §5.5 T1, bijective form).
+//
+// Reference parity: replaces the per-stage NumPy `np.dot(x, W) + b` + activation of
+// /root/reference/src/grpc_node.py:75-97 (forward) and adds the backward the reference only had
+// centrally (/root/reference/scripts/generate_mnist_pytorch.py:41-52).
+#include "common.hpp"
+#include "gemm.hpp"
+
+namespace dnn {
+
+// ---- LDS image swizzles -------------------------------------------------------------------
+// KMAJ image: [rows = BM or BN][64 k] bf16, 128-B rows of 8 16-B chunks; chunk' = c ^ ((r>>1)&7).
+// The 16 rows a ds_read_b128 lane group touches then cover all 16 slots of the 256-B bank row.
+__device__ __forceinline__ int k_swz(int r) { return (r >> 1) & 7; }
+
+// MNMAJ image: [64 k-rows][T cols] bf16 (T*2-byte rows). A transposed read by one 32-lane half
+// touches 8 k-rows x 32 B; the XOR (always even, so 32-B column pairs stay together) spreads the
+// 8 rows over distinct 32-B bank positions.
+template <int T>
+__device__ __forceinline__ int mn_swz(int r);
+template <>
+__device__ __forceinline__ int mn_swz<128>(int r) {
+  return ((r & 3) | (((r >> 3) & 1) << 2)) << 1;
+}
+template <>
+__device__ __forceinline__ int mn_swz<64>(int r) {
+  return (((r >> 1) & 1) | (((r >> 3) & 1) << 1)) << 1;
+}
+
+// Stage one operand tile (T entries of the M/N dim x 64 of K) into LDS with LDS-DMA.
+// Tile bytes = T*128 = T/8 KiB pieces; each of the 4 waves issues T/32 of them.
+template <int L, int T>
+__device__ __forceinline__ void stage_tile(const u16* __restrict__ g, long ld, int mn0, int k0,
+                                           char LDS_AS* dst, int wave, int lane) {
+  constexpr int NI = T / 32;
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int piece = i * 4 + wave;
+    const int chunk = piece * 64 + lane;
+    const u16* src;
+    if constexpr (L == KMAJ) {
+      const int r = chunk >> 3, ph = chunk & 7;
+      const int c = ph ^ k_swz(r);
+      src = g + (long)(mn0 + r) * ld + k0 + c * 8;
+    } else {
+      constexpr int CPR = T / 8;
+      const int r = chunk / CPR, ph = chunk % CPR;
+      const int c = ph ^ mn_swz<T>(r);
+      src = g + (long)(k0 + r) * ld + mn0 + c * 8;
+    }
+    __builtin_amdgcn_global_load_lds((const void*)src, (void LDS_AS*)(dst + piece * 1024), 16, 0, 0);
+  }
+}
+
+// Fragment of v_mfma_f32_16x16x32_bf16 for 16-wide block `blk` of the tile and k-step s (32 k):
+// lane l holds X[idx = l&15][k = 8*(l>>4) + j], j = 0..7 (guide §3 operand maps). The same form
+// serves A (idx = row m) and B (idx = column n).
+template <int L, int T>
+__device__ __forceinline__ bf16x8_t load_frag(const char LDS_AS* tile, int blk, int s, int lane) {
+  if constexpr (L == KMAJ) {
+    const int r = blk * 16 + (lane & 15);
+    const int c = 4 * s + (lane >> 4);
+    return *(const bf16x8_t LDS_AS*)(tile + r * 128 + ((c ^ k_swz(r)) << 4));
+  } else {
+    constexpr int RB = T * 2;
+    const int i = lane & 15, g = lane >> 4, q = i >> 2, p = i & 3;
+    const int ch = 2 * blk + (p >> 1);
+    const int r0 = 32 * s + 8 * g + q;
+    const int r1 = r0 + 4;
+    bf16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (bf16x4_t LDS_AS*)(tile + r0 * RB + ((ch ^ mn_swz<T>(r0)) << 4) + 8 * (p & 1)));
+    bf16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (bf16x4_t LDS_AS*)(tile + r1 * RB + ((ch ^ mn_swz<T>(r1)) << 4) + 8 * (p & 1)));
+    bf16x8_t f;
+    f.lo = lo;
+    f.hi = hi;
+    return f;
+  }
+}
+
+template <int A, int B>
+struct cmax {
+  static constexpr int v = A > B ? A : B;
+};
+
+template <int BM, int BN, int LA, int LB, bool OUT_F32>
+__global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmParams p, int tiles_n, int tiles_m,
+                                                        int nwg) {
+  constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
+  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
+  constexpr int CS_LD = BN + 4;  // fp32 epilogue staging row stride (floats)
+  constexpr int SMEM = cmax<2 * STAGE, BM * CS_LD * 4>::v;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  char LDS_AS* lds = (char LDS_AS*)smem;
+
+  // XCD-aware bijective remap: hardware deals block b to XCD group b%8; give each group a
+  // contiguous run of logical tiles (tile_n fastest -> neighbours share the A panel in L2).
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tn = wgid % tiles_n;
+  const int tm = (wgid / tiles_n) % tiles_m;
+  const int split = wgid / (tiles_n * tiles_m);
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kbase = split * p.K;
+  const int nk = p.K >> 6;
+
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  stage_tile<LA, BM>(p.A, p.lda, m0, kbase, lds, wave, lane);
+  stage_tile<LB, BN>(p.B, p.ldb, n0, kbase, lds + A_BYTES, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) {
+      char LDS_AS* nxt = lds + (buf ^ 1) * STAGE;
+      const int k0 = kbase + (kt + 1) * 64;
+      stage_tile<LA, BM>(p.A, p.lda, m0, k0, nxt, wave, lane);
+      stage_tile<LB, BN>(p.B, p.ldb, n0, k0, nxt + A_BYTES, wave, lane);
+    }
+    const char LDS_AS* sa = lds + buf * STAGE;
+    const char LDS_AS* sb = sa + A_BYTES;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8_t a[FM], b[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) a[i] = load_frag<LA, BM>(sa, wm * FM + i, s, lane);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) b[j] = load_frag<LB, BN>(sb, wn * FN + j, s, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- epilogue: accumulators -> LDS (fp32) -> 16-B row chunks to global --------------------
+  float LDS_AS* cs = (float LDS_AS*)lds;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * WM + i * 16 + (lane >> 4) * 4 + r;
+        const int col = wn * WN + j * 16 + (lane & 15);
+        cs[row * CS_LD + col] = acc[i][j][r];
+      }
+  __syncthreads();
+
+  constexpr int CPR = BN / 8;
+  constexpr int ITER = BM * CPR / 256;
+#pragma unroll 2
+  for (int it = 0; it < ITER; ++it) {
+    const int idx = threadIdx.x + it * 256;
+    const int row = idx / CPR, col = (idx % CPR) * 8;
+    const f32x4_t v0 = *(const f32x4_t LDS_AS*)(cs + row * CS_LD + col);
+    const f32x4_t v1 = *(const f32x4_t LDS_AS*)(cs + row * CS_LD + col + 4);
+    float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    const long gm = m0 + row, gn = n0 + col;
+    if (p.bias) {
+      const f32x4_t b0 = *(const f32x4_t*)(p.bias + gn);
+      const f32x4_t b1 = *(const f32x4_t*)(p.bias + gn + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] += b0[e];
+        v[e + 4] += b1[e];
+      }
+    }
+    if constexpr (OUT_F32) {
+      float* c = (float*)p.C + (long)split * p.c_split_stride + gm * p.ldc + gn;
+      f32x4_t o0 = {v[0], v[1], v[2], v[3]}, o1 = {v[4], v[5], v[6], v[7]};
+      if (p.accumulate) {
+        o0 += *(const f32x4_t*)c;
+        o1 += *(const f32x4_t*)(c + 4);
+      }
+      *(f32x4_t*)c = o0;
+      *(f32x4_t*)(c + 4) = o1;
+    } else {
+      if (p.aux) {
+        const bf16x8_t y = *(const bf16x8_t*)(p.aux + gm * p.ld_aux + gn);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = act_bwd(v[e], bf2f((u16)y[e]), p.act);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = act_fwd(v[e], p.act);
+      }
+      bf16x8_t o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (short)f2bf(v[e]);
+      *(bf16x8_t*)((u16*)p.C + gm * p.ldc + gn) = o;
+    }
+  }
+}
+
+typedef void (*gemm_fn)(GemmParams, int, int, int);
+
+template <int BM, int BN>
+static gemm_fn pick_layout(int la, int lb, int f32) {
+#define DNN_G(LA, LB, F) gemm_bf16_kernel<BM, BN, LA, LB, F>
+  if (la == KMAJ && lb == KMAJ) return f32 ? DNN_G(KMAJ, KMAJ, true) : DNN_G(KMAJ, KMAJ, false);
+  if (la == KMAJ && lb == MNMAJ) return f32 ? DNN_G(KMAJ, MNMAJ, true) : DNN_G(KMAJ, MNMAJ, false);
+  if (la == MNMAJ && lb == KMAJ) return f32 ? DNN_G(MNMAJ, KMAJ, true) : DNN_G(MNMAJ, KMAJ, false);
+  return f32 ? DNN_G(MNMAJ, MNMAJ, true) : DNN_G(MNMAJ, MNMAJ, false);
+#undef DNN_G
+}
+
+const char* gemm_error_string(int code) {
+  switch (code) {
+    case 0: return "ok";
+    case -1: return "unsupported tile size (bm, bn must be 64 or 128)";
+    case -2: return "M must be a multiple of bm and N a multiple of bn";
+    case -3: return "per-split K must be a positive multiple of 64";
+    case -4: return "leading dimensions must be multiples of 8 elements (16-byte rows)";
+    case -5: return "pointers must be 16-byte aligned";
+    case -6: return "bad layout code";
+    case -7: return "split-K > 1 requires fp32 output";
+    case -8: return "leading dimension smaller than the row it stores";
+    case -9: return "hip launch failed";
+    default: return "unknown gemm error";
+  }
+}
+
+int gemm_bf16(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, int splits,
+              hipStream_t stream) {
+  if (!((bm == 64 || bm == 128) && (bn == 64 || bn == 128))) return -1;
+  if (p.M <= 0 || p.N <= 0 || p.M % bm || p.N % bn) return -2;
+  if (p.K <= 0 || p.K % 64 || splits < 1) return -3;
+  if ((p.lda | p.ldb | p.ldc) % 8 || (p.aux && p.ld_aux % 8)) return -4;
+  auto mis = [](const void* q) { return ((uintptr_t)q) & 15; };
+  if (mis(p.A) || mis(p.B) || mis(p.C) || (p.aux && mis(p.aux)) || (p.bias && mis(p.bias)))
+    return -5;
+  if ((la != KMAJ && la != MNMAJ) || (lb != KMAJ && lb != MNMAJ)) return -6;
+  if (splits > 1 && !out_f32) return -7;
+  const long a_row = la == KMAJ ? (long)p.K * splits : p.M;
+  const long b_row = lb == KMAJ ? (long)p.K * splits : p.N;
+  if (p.lda < a_row || p.ldb < b_row || p.ldc < p.N || (p.aux && p.ld_aux < p.N)) return -8;
+
+  gemm_fn fn;
+  if (bm == 128 && bn == 128) fn = pick_layout<128, 128>(la, lb, out_f32);
+  else if (bm == 128) fn = pick_layout<128, 64>(la, lb, out_f32);
+  else if (bn == 128) fn = pick_layout<64, 128>(la, lb, out_f32);
+  else fn = pick_layout<64, 64>(la, lb, out_f32);
+
+  const int tiles_n = p.N / bn, tiles_m = p.M / bm;
+  const int nwg = tiles_n * tiles_m * splits;
+  hipLaunchKernelGGL(fn, dim3(nwg), dim3(256), 0, stream, p, tiles_n, tiles_m, nwg);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
+}  // namespace dnn

@@ -1,0 +1,42 @@
+// Host-visible interface of the bf16 MFMA GEMM family (csrc/kernels/gemm.hip).
+//
+// C[M,N] (+)= epilogue( sum_k A[m,k] * B[k,n] ), bf16 inputs, fp32 accumulation.
+// Each operand is stored either contraction-contiguous (KMAJ: [MN][K]) or
+// output-dim-contiguous (MNMAJ: [K][MN]); the three training GEMMs of a Linear layer are
+//   forward  Y  = X  . W^T : A = X  KMAJ , B = W  KMAJ   (W stored nn.Linear-style [out][in])
+//   dgrad    dX = dZ . W   : A = dZ KMAJ , B = W  MNMAJ
+//   wgrad    dW = dZ^T . X : A = dZ MNMAJ, B = X  MNMAJ  (contraction over the batch)
+// so no transposed copy of any tensor is ever materialised: MNMAJ tiles are read with the
+// gfx950 transposing LDS read (ds_read_b64_tr_b16).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dnn {
+
+enum Layout : int { KMAJ = 0, MNMAJ = 1 };
+
+struct GemmParams {
+  const uint16_t* A;  // bf16
+  long lda;           // elements between consecutive storage rows of A
+  const uint16_t* B;  // bf16
+  long ldb;
+  void* C;              // bf16 or f32
+  long ldc;
+  long c_split_stride;  // elements between split-K output slabs (f32 output only)
+  const float* bias;    // optional, [N] fp32, added in the epilogue
+  const uint16_t* aux;  // optional, bf16 activation output used for the backward mask
+  long ld_aux;
+  int M, N, K;     // K = contraction length handled by ONE split
+  int act;         // Act code: forward activation, or (with aux) the activation to differentiate
+  int accumulate;  // f32 output: C += result (split slab accumulation across micro-batches)
+};
+
+// Returns 0 on success, a negative code when a shape/alignment precondition fails
+// (nothing is launched then).
+int gemm_bf16(const GemmParams& p, int layout_a, int layout_b, int out_f32, int bm, int bn,
+              int splits, hipStream_t stream);
+
+const char* gemm_error_string(int code);
+
+}  // namespace dnn

@@ -1,0 +1,133 @@
+"""In-tree build of the native extension ``docker_dist_nn_amd._native`` for gfx950.
+
+Device code (``csrc/kernels/*.hip``) is compiled by ``hipcc --offload-arch=gfx950``; host-only
+runtime code (``csrc/runtime/*.cpp``, ``csrc/bindings.cpp``) by the host compiler against the HIP
+headers, which is what allows host-side sanitizer builds (``sanitize=True``: ASan/UBSan on the
+host objects only, GPU code untouched -- GPU ASan / xnack+ is not available on the pool).
+The result is one shared object placed next to this file, so it travels with the repository
+snapshot to the GPU box and is what the driver sees loaded.
+
+Usage: ``python -m docker_dist_nn_amd._build [--force] [--jobs N] [--sanitize]``.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import hashlib
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent
+ROOT = PKG_DIR.parent
+CSRC = ROOT / "csrc"
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
+ARCH = "gfx950"
+EXT_NAME = "_native" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so")
+
+
+def _hipcc() -> str:
+    p = ROCM / "bin" / "hipcc"
+    return str(p) if p.exists() else "hipcc"
+
+
+def _host_cxx() -> str:
+    for c in (os.environ.get("CXX"), "g++", "clang++"):
+        if c and shutil.which(c):
+            return c
+    return _hipcc()
+
+
+def _pybind_includes() -> list[str]:
+    import pybind11
+
+    inc = [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}"]
+    return inc
+
+
+def _sources() -> tuple[list[Path], list[Path]]:
+    dev = sorted((CSRC / "kernels").glob("*.hip"))
+    host = sorted((CSRC / "runtime").glob("*.cpp")) + [CSRC / "bindings.cpp"]
+    return dev, host
+
+
+def _header_digest() -> str:
+    h = hashlib.sha1()
+    for p in sorted(CSRC.rglob("*.hpp")) + sorted(CSRC.rglob("*.h")):
+        h.update(p.read_bytes())
+    return h.hexdigest()[:12]
+
+
+def _flags(sanitize: bool) -> tuple[list[str], list[str]]:
+    common = ["-O3", "-std=c++17", "-fPIC", f"-I{CSRC}", "-Wall", "-Wno-unused-function"]
+    dev = [_hipcc(), f"--offload-arch={ARCH}", *common, "-Wno-unused-result"]
+    host = [_host_cxx(), *common, f"-I{ROCM / 'include'}", "-D__HIP_PLATFORM_AMD__",
+            *_pybind_includes(), "-fvisibility=hidden"]
+    if sanitize:
+        host += ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-O1", "-g"]
+    return dev, host
+
+
+def _compile(cmd: list[str]) -> tuple[list[str], int, str]:
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    return cmd, r.returncode, r.stdout + r.stderr
+
+
+def build(force: bool = False, jobs: int | None = None, sanitize: bool = False,
+          verbose: bool = False) -> Path:
+    """Compile (incrementally) and link the extension; returns the path of the .so."""
+    dev_src, host_src = _sources()
+    tag = "asan" if sanitize else "rel"
+    obj_dir = ROOT / "build" / f"native-{tag}-{_header_digest()}"
+    obj_dir.mkdir(parents=True, exist_ok=True)
+    dev_cmd, host_cmd = _flags(sanitize)
+    out = PKG_DIR / (EXT_NAME if not sanitize else "_native_asan.so")
+
+    jobs_to_run, objs = [], []
+    for src in dev_src + host_src:
+        obj = obj_dir / (src.relative_to(CSRC).as_posix().replace("/", "__") + ".o")
+        objs.append(obj)
+        if force or not obj.exists() or obj.stat().st_mtime < src.stat().st_mtime:
+            base = dev_cmd if src.suffix == ".hip" else host_cmd
+            jobs_to_run.append([*base, "-c", str(src), "-o", str(obj)])
+
+    if jobs_to_run:
+        n = jobs or min(8, os.cpu_count() or 4)
+        with cf.ThreadPoolExecutor(max_workers=n) as ex:
+            for cmd, rc, log in ex.map(_compile, jobs_to_run):
+                if verbose or rc:
+                    sys.stderr.write(" ".join(cmd) + "\n" + log)
+                if rc:
+                    raise RuntimeError(f"native build failed compiling {cmd[-3]}")
+
+    newest = max(o.stat().st_mtime for o in objs)
+    if force or jobs_to_run or not out.exists() or out.stat().st_mtime < newest:
+        link = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(out),
+                *map(str, objs), f"-L{ROCM / 'lib'}", "-lamdhip64"]
+        if sanitize:
+            link += ["-fsanitize=address,undefined"]
+        cmd, rc, log = _compile(link)
+        if verbose or rc:
+            sys.stderr.write(" ".join(cmd) + "\n" + log)
+        if rc:
+            raise RuntimeError("native link failed")
+    return out
+
+
+def main(argv: list[str] | None = None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--jobs", type=int, default=None)
+    ap.add_argument("--sanitize", action="store_true")
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args(argv)
+    p = build(force=a.force, jobs=a.jobs, sanitize=a.sanitize, verbose=a.verbose)
+    print(p)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -1,0 +1,7 @@
+from .kernels import (KMAJ, MNMAJ, adam_update, colsum_partial, gemm, linear_dgrad, linear_fwd,
+                      linear_wgrad, pack_bf16, pick_splits, pick_tiles, reduce_slabs, sgd_update,
+                      softmax_rows, softmax_xent, unpack_bf16)
+
+__all__ = ["KMAJ", "MNMAJ", "adam_update", "colsum_partial", "gemm", "linear_dgrad",
+           "linear_fwd", "linear_wgrad", "pack_bf16", "pick_splits", "pick_tiles",
+           "reduce_slabs", "sgd_update", "softmax_rows", "softmax_xent", "unpack_bf16"]

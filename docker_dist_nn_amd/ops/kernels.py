@@ -1,0 +1,249 @@
+"""Tensor-level entry points of the compute kernels.
+
+Every op takes pre-allocated output tensors (the engine owns all step buffers, so a captured HIP
+graph replays with fixed pointers) and dispatches on the device of its inputs:
+
+* CUDA/HIP tensors -> the hand-written gfx950 kernels of ``csrc/kernels`` through the native
+  extension. There is deliberately NO PyTorch fallback on the GPU: if the extension is missing,
+  :func:`docker_dist_nn_amd.utils.native.native` raises.
+* CPU tensors -> :mod:`.reference`, a torch implementation with the same numerics contract
+  (bf16 operands, fp32 accumulation, bf16/fp32 outputs). It exists so the engine/pipeline/DP
+  logic is testable on CPU with the gloo backend, and it is the oracle of the GPU kernel tests.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ..models.mlp import ACT_CODE
+from ..utils.native import native
+from . import reference as ref
+
+KMAJ, MNMAJ = 0, 1
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _p(t: torch.Tensor | None) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def _rows(t: torch.Tensor, name: str, dtype: torch.dtype) -> None:
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError(f"{name}: expected a row-major 2-D tensor, got shape {tuple(t.shape)} "
+                         f"strides {t.stride()}")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+
+
+def _act(act) -> int:
+    return ACT_CODE[act] if isinstance(act, str) else int(act)
+
+
+# Residency model for tile choice: LDS/regs admit 2 (128x128), 3 (128x64 / 64x128) or
+# 4 (64x64) workgroups per CU; relative per-CU throughput of the tile shapes.
+_TILE_OCC = {(128, 128): 2, (128, 64): 3, (64, 128): 3, (64, 64): 4}
+_TILE_EFF = {(128, 128): 1.0, (128, 64): 0.82, (64, 128): 0.82, (64, 64): 0.62}
+NUM_CU = 256
+
+
+def pick_tiles(M: int, N: int, splits: int = 1) -> tuple[int, int]:
+    """Tile shape minimising modelled time = rounds of resident tiles x per-tile cost."""
+    best, best_t = None, math.inf
+    for (bm, bn) in _TILE_OCC:
+        if M % bm or N % bn:
+            continue
+        tiles = (M // bm) * (N // bn) * splits
+        # tiles resident on one CU share its matrix pipe: time ~ tiles per CU x tile cost
+        t = math.ceil(tiles / NUM_CU) * bm * bn / _TILE_EFF[(bm, bn)]
+        if t < best_t - 1e-9:
+            best, best_t = (bm, bn), t
+    if best is None:
+        raise ValueError(f"no tile divides M={M}, N={N} (pad to multiples of 64)")
+    return best
+
+
+def pick_splits(M: int, N: int, K_total: int, target_wg: int = 2 * NUM_CU) -> int:
+    """Split-K factor for the batch-contraction (wgrad) GEMM: enough workgroups, chunks >= 256."""
+    bm, bn = pick_tiles(M, N, 1)
+    tiles = (M // bm) * (N // bn)
+    s = 1
+    while (tiles * s < target_wg and K_total % (2 * s * 64) == 0 and K_total // (2 * s) >= 256):
+        s *= 2
+    return s
+
+
+def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=None, aux=None,
+         act=0, accumulate: bool = False, splits: int = 1, tiles: tuple[int, int] | None = None):
+    """C (+)= epilogue(A.B). See csrc/kernels/gemm.hpp for the layout/epilogue contract."""
+    act = _act(act)
+    out_f32 = c.dtype == torch.float32
+    if not a.is_cuda:
+        return ref.gemm(a, b, c, layout_a=layout_a, layout_b=layout_b, M=M, N=N, K=K, bias=bias,
+                        aux=aux, act=act, accumulate=accumulate, splits=splits)
+    _rows(a, "A", torch.bfloat16)
+    _rows(b, "B", torch.bfloat16)
+    if splits > 1:
+        if c.dim() != 3 or c.shape[0] < splits:
+            raise ValueError("split-K output must be [splits][M][N] fp32")
+        c_rows, split_stride = c[0], c.stride(0)
+    else:
+        c_rows, split_stride = (c if c.dim() == 2 else c[0]), 0
+    _rows(c_rows, "C", torch.float32 if out_f32 else torch.bfloat16)
+    if bias is not None and (bias.dtype != torch.float32 or bias.numel() < N):
+        raise ValueError("bias must be fp32 with >= N entries")
+    if aux is not None:
+        _rows(aux, "aux", torch.bfloat16)
+    # shape checks against the storage the kernel will touch
+    ka = K * splits
+    need_a = (M, ka) if layout_a == KMAJ else (ka, M)
+    need_b = (N, ka) if layout_b == KMAJ else (ka, N)
+    if a.shape[0] < need_a[0] or a.shape[1] < need_a[1]:
+        raise ValueError(f"A storage {tuple(a.shape)} too small for {need_a}")
+    if b.shape[0] < need_b[0] or b.shape[1] < need_b[1]:
+        raise ValueError(f"B storage {tuple(b.shape)} too small for {need_b}")
+    if c_rows.shape[0] < M or c_rows.shape[1] < N:
+        raise ValueError(f"C storage {tuple(c_rows.shape)} too small for {(M, N)}")
+    if aux is not None and (aux.shape[0] < M or aux.shape[1] < N):
+        raise ValueError("aux storage too small")
+    bm, bn = tiles or pick_tiles(M, N, splits)
+    native().gemm_bf16(_p(a), a.stride(0), _p(b), b.stride(0), _p(c_rows), c_rows.stride(0),
+                       split_stride, _p(bias), _p(aux), aux.stride(0) if aux is not None else 0,
+                       M, N, K, act, int(accumulate), layout_a, layout_b, int(out_f32), bm, bn,
+                       splits, _stream(a))
+    return c
+
+
+# ---- the three GEMMs of a Linear layer -----------------------------------------------------
+
+def linear_fwd(x, w, bias, y, act="relu"):
+    """y[M][Np] = act(x[M][Kp] . w[Np][Kp]^T + bias). y bf16 (activation) or fp32 (logits)."""
+    M, K = x.shape
+    N = w.shape[0]
+    return gemm(x, w, y, layout_a=KMAJ, layout_b=KMAJ, M=M, N=N, K=K, bias=bias, act=act)
+
+
+def linear_dgrad(dz, w, dx, y_prev=None, act_prev="linear"):
+    """dx[M][Kp] = (dz[M][Np] . w[Np][Kp]) * act_prev'(y_prev) (mask fused in the epilogue)."""
+    M, N = dz.shape
+    K = w.shape[1]
+    if y_prev is None:
+        act_prev = "linear"
+    return gemm(dz, w, dx, layout_a=KMAJ, layout_b=MNMAJ, M=M, N=K, K=N, aux=y_prev,
+                act=act_prev)
+
+
+def linear_wgrad(dz, x, slabs, splits=1, accumulate=False):
+    """slabs[s][Np][Kp] (+)= dz[rows_s]^T . x[rows_s] over the batch rows of split s (fp32)."""
+    R, N = dz.shape
+    K = x.shape[1]
+    if R % splits:
+        raise ValueError("rows must divide evenly into splits")
+    return gemm(dz, x, slabs, layout_a=MNMAJ, layout_b=MNMAJ, M=N, N=K, K=R // splits,
+                accumulate=accumulate, splits=splits)
+
+
+# ---- loss / reductions / optimizers ----------------------------------------------------------
+
+def softmax_xent(logits, labels, dz, n_cls, scale, loss_sum=None, correct=None):
+    rows, width = dz.shape
+    if not logits.is_cuda:
+        return ref.softmax_xent(logits, labels, dz, n_cls, scale, loss_sum, correct)
+    _rows(logits, "logits", torch.float32)
+    _rows(dz, "dz", torch.bfloat16)
+    if labels.dtype != torch.int32 or labels.numel() < rows or logits.shape[0] < rows:
+        raise ValueError("labels must be int32 with one entry per row")
+    native().softmax_xent(_p(logits), logits.stride(0), _p(labels), _p(dz), dz.stride(0), rows,
+                          n_cls, width, float(scale), _p(loss_sum), _p(correct),
+                          _stream(logits))
+
+
+def softmax_rows(logits, out, n_cls, labels=None, pred=None, correct=None):
+    rows = logits.shape[0]
+    if not logits.is_cuda:
+        return ref.softmax_rows(logits, out, n_cls, labels, pred, correct)
+    _rows(logits, "logits", torch.float32)
+    if out is not None:
+        _rows(out, "out", torch.float32)
+    native().softmax_rows(_p(logits), logits.stride(0), _p(out),
+                          out.stride(0) if out is not None else 0, rows, n_cls, _p(labels),
+                          _p(pred), _p(correct), _stream(logits))
+
+
+def colsum_partial(x, part, n_part=None):
+    """part[n_part][cols] = partial column sums of x (row blocks)."""
+    rows, cols = x.shape
+    n_part = n_part or part.shape[0]
+    if not x.is_cuda:
+        return ref.colsum_partial(x, part, n_part)
+    _rows(x, "x", torch.bfloat16)
+    if part.dtype != torch.float32 or not part.is_contiguous() or part.numel() < n_part * cols:
+        raise ValueError("part must be contiguous fp32 [n_part][cols]")
+    native().colsum_partial(_p(x), x.stride(0), rows, cols, n_part, _p(part), _stream(x))
+
+
+def reduce_slabs(src, n_src, stride, n, out, scale=1.0, accumulate=False):
+    """out[:n] (+)= scale * sum_s src_flat[s*stride : s*stride+n]."""
+    if not src.is_cuda:
+        return ref.reduce_slabs(src, n_src, stride, n, out, scale, accumulate)
+    if src.dtype != torch.float32 or out.dtype != torch.float32:
+        raise TypeError("reduce_slabs works on fp32")
+    if not (src.is_contiguous() and out.is_contiguous()):
+        raise ValueError("reduce_slabs needs contiguous buffers")
+    if (n_src - 1) * stride + n > src.numel() or out.numel() < n:
+        raise ValueError("reduce_slabs range out of bounds")
+    native().reduce_slabs(_p(src), stride, n_src, n, float(scale), _p(out), int(accumulate),
+                          _stream(src))
+
+
+def sgd_update(p, g, mom=None, shadow=None, lr=0.01, momentum=0.0, weight_decay=0.0):
+    if not p.is_cuda:
+        return ref.sgd_update(p, g, mom, shadow, lr, momentum, weight_decay)
+    n = p.numel()
+    if g.numel() != n or (mom is not None and mom.numel() != n) or (
+            shadow is not None and shadow.numel() != n):
+        raise ValueError("sgd buffers must have equal sizes")
+    native().sgd_update(_p(p), _p(g), _p(mom if momentum else None), _p(shadow), n, float(lr),
+                        float(momentum), float(weight_decay), _stream(p))
+
+
+def adam_update(p, g, m, v, shadow=None, lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
+                weight_decay=0.0, decoupled=False, step=1):
+    b1, b2 = betas
+    bc1 = 1.0 / (1.0 - b1 ** step)
+    bc2 = 1.0 / (1.0 - b2 ** step)
+    if not p.is_cuda:
+        return ref.adam_update(p, g, m, v, shadow, lr, b1, b2, eps, weight_decay, decoupled, bc1,
+                               bc2)
+    n = p.numel()
+    if any(t.numel() != n for t in (g, m, v)):
+        raise ValueError("adam buffers must have equal sizes")
+    native().adam_update(_p(p), _p(g), _p(m), _p(v), _p(shadow), n, float(lr), float(b1),
+                         float(b2), float(eps), float(weight_decay), int(decoupled), float(bc1),
+                         float(bc2), _stream(p))
+
+
+def pack_bf16(src, out):
+    """fp32 [rows][cols] -> padded bf16 out [rows_p][cols_p] (zero padding)."""
+    rows, cols = src.shape
+    rows_p, cols_p = out.shape
+    if not out.is_cuda:
+        return ref.pack_bf16(src, out)
+    if src.dtype != torch.float32 or out.dtype != torch.bfloat16:
+        raise TypeError("pack_bf16: fp32 -> bf16")
+    if src.stride(1) != 1 or out.stride(1) != 1:
+        raise ValueError("pack_bf16 needs row-major tensors")
+    native().pack_bf16(_p(src), src.stride(0), rows, cols, _p(out), out.stride(0), rows_p, cols_p,
+                       _stream(out))
+
+
+def unpack_bf16(src, out):
+    rows, cols = out.shape
+    if not src.is_cuda:
+        out.copy_(src[:rows, :cols].float())
+        return
+    native().unpack_bf16(_p(src), src.stride(0), rows, cols, _p(out), out.stride(0),
+                         _stream(src))

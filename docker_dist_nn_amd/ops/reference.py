@@ -1,0 +1,140 @@
+"""PyTorch reference implementations with the kernels' numerics contract.
+
+bf16 operands, fp32 accumulation, outputs rounded once to bf16 (or kept fp32). Used (a) as the
+CPU execution path so the engine, pipeline schedules and DP logic run in CPU tests with gloo,
+and (b) as the fp32 oracle for the GPU kernel tests.
+"""
+from __future__ import annotations
+
+import torch
+
+KMAJ, MNMAJ = 0, 1
+_LINEAR, _RELU, _SIGMOID = 0, 1, 2
+
+
+def act_fwd(v: torch.Tensor, act: int) -> torch.Tensor:
+    if act == _RELU:
+        return torch.clamp_min(v, 0.0)
+    if act == _SIGMOID:
+        return torch.sigmoid(v)
+    return v
+
+
+def act_bwd(g: torch.Tensor, y: torch.Tensor, act: int) -> torch.Tensor:
+    if act == _RELU:
+        return torch.where(y > 0, g, torch.zeros_like(g))
+    if act == _SIGMOID:
+        return g * y * (1.0 - y)
+    return g
+
+
+def _logical(a, b, layout_a, layout_b, M, N, Ktot):
+    A = a[:M, :Ktot] if layout_a == KMAJ else a[:Ktot, :M].t()
+    B = b[:N, :Ktot].t() if layout_b == KMAJ else b[:Ktot, :N]
+    return A.float(), B.float()
+
+
+def gemm(a, b, c, *, layout_a, layout_b, M, N, K, bias=None, aux=None, act=0, accumulate=False,
+         splits=1):
+    A, B = _logical(a, b, layout_a, layout_b, M, N, K * splits)
+    out_f32 = c.dtype == torch.float32
+    for s in range(splits):
+        acc = A[:, s * K:(s + 1) * K] @ B[s * K:(s + 1) * K, :]
+        if bias is not None:
+            acc = acc + bias[:N].float()
+        if out_f32:
+            dst = c[s] if c.dim() == 3 else c
+            if accumulate:
+                acc = acc + dst[:M, :N]
+            dst[:M, :N] = acc
+        else:
+            if aux is not None:
+                acc = act_bwd(acc, aux[:M, :N].float(), act)
+            else:
+                acc = act_fwd(acc, act)
+            c[:M, :N] = acc.to(c.dtype)
+    return c
+
+
+def softmax_xent(logits, labels, dz, n_cls, scale, loss_sum=None, correct=None):
+    rows, width = dz.shape
+    lg = logits[:rows, :n_cls].float()
+    lab = labels[:rows].long()
+    valid = lab >= 0
+    p = torch.softmax(lg, dim=1)
+    g = p.clone()
+    safe = lab.clamp_min(0)
+    g[torch.arange(rows), safe] -= 1.0
+    g = g * float(scale)
+    g[~valid] = 0.0
+    dz.zero_()
+    dz[:, :n_cls] = g.to(dz.dtype)
+    if loss_sum is not None:
+        logp = torch.log_softmax(lg, dim=1)
+        nll = -logp[torch.arange(rows), safe]
+        loss_sum += nll[valid].sum().to(loss_sum.dtype)
+    if correct is not None:
+        pred = torch.argmax(lg, dim=1)
+        correct += ((pred == lab) & valid).sum().to(correct.dtype)
+
+
+def softmax_rows(logits, out, n_cls, labels=None, pred=None, correct=None):
+    rows = logits.shape[0]
+    lg = logits[:rows, :n_cls].float()
+    if out is not None:
+        out[:rows, :n_cls] = torch.softmax(lg, dim=1)
+    am = torch.argmax(lg, dim=1)
+    if pred is not None:
+        pred[:rows] = am.to(pred.dtype)
+    if correct is not None and labels is not None:
+        correct += (am == labels[:rows].long()).sum().to(correct.dtype)
+
+
+def colsum_partial(x, part, n_part):
+    rows, cols = x.shape
+    per = (rows + n_part - 1) // n_part
+    xf = x.float()
+    for i in range(n_part):
+        part[i, :cols] = xf[i * per:min(rows, (i + 1) * per)].sum(0)
+
+
+def reduce_slabs(src, n_src, stride, n, out, scale=1.0, accumulate=False):
+    flat = src.reshape(-1)
+    acc = flat[:n].clone()
+    for s in range(1, n_src):
+        acc += flat[s * stride:s * stride + n]
+    acc *= scale
+    o = out.reshape(-1)
+    if accumulate:
+        o[:n] += acc
+    else:
+        o[:n] = acc
+
+
+def sgd_update(p, g, mom, shadow, lr, momentum, weight_decay):
+    gv = g + weight_decay * p if weight_decay else g.clone()
+    if momentum and mom is not None:
+        mom.mul_(momentum).add_(gv)
+        gv = mom
+    p.sub_(lr * gv)
+    if shadow is not None:
+        shadow.copy_(p.to(shadow.dtype))
+
+
+def adam_update(p, g, m, v, shadow, lr, b1, b2, eps, weight_decay, decoupled, bc1, bc2):
+    gv = g.clone()
+    if decoupled:
+        p.mul_(1.0 - lr * weight_decay)
+    elif weight_decay:
+        gv += weight_decay * p
+    m.mul_(b1).add_((1.0 - b1) * gv)
+    v.mul_(b2).add_((1.0 - b2) * gv * gv)
+    p.sub_(lr * (m * bc1) / (torch.sqrt(v * bc2) + eps))
+    if shadow is not None:
+        shadow.copy_(p.to(shadow.dtype))
+
+
+def pack_bf16(src, out):
+    rows, cols = src.shape
+    out.zero_()
+    out[:rows, :cols] = src.to(out.dtype)

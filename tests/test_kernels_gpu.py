@@ -1,0 +1,222 @@
+"""Numerics of the gfx950 HIP kernels against plain PyTorch fp32 references of the same op.
+
+GEMM checks use (1) small-integer operands, for which every product and partial sum is exact
+in fp32, so the kernel must match bit-for-bit -- this is what catches a transposed fragment map
+or a wrong LDS swizzle (guide §3: "always A=I-check with ASYMMETRIC B"); and (2) random data
+with bf16-level tolerances.
+"""
+import pytest
+import torch
+
+from docker_dist_nn_amd import ops
+from docker_dist_nn_amd.ops import KMAJ, MNMAJ
+from docker_dist_nn_amd.utils import native
+
+pytestmark = pytest.mark.gpu
+
+LAYOUTS = [(KMAJ, KMAJ), (KMAJ, MNMAJ), (MNMAJ, MNMAJ), (MNMAJ, KMAJ)]
+TILES = [(128, 128), (128, 64), (64, 128), (64, 64)]
+
+
+def _storage(layout, mn, k, gen, dev, integer):
+    shape = (mn, k) if layout == KMAJ else (k, mn)
+    if integer:
+        t = torch.randint(-3, 4, shape, generator=gen, dtype=torch.int32).float()
+    else:
+        t = torch.randn(shape, generator=gen)
+    return t.to(torch.bfloat16).to(dev)
+
+
+def _logical(t, layout, mn, k):
+    return t.float()[:mn, :k] if layout == KMAJ else t.float()[:k, :mn].t()
+
+
+def test_native_extension_is_loaded():
+    mod = native()
+    assert mod.__file__.endswith(".so")
+
+
+@pytest.mark.parametrize("la,lb", LAYOUTS)
+@pytest.mark.parametrize("bm,bn", TILES)
+def test_gemm_exact_integer(dev, la, lb, bm, bn):
+    gen = torch.Generator().manual_seed(1234 + 10 * la + lb + bm + 3 * bn)
+    M, N, K = 256, 192 if bn == 64 else 256, 320
+    a = _storage(la, M, K, gen, dev, True)
+    b = _storage(lb, N, K, gen, dev, True)
+    c = torch.empty(M, N, device=dev, dtype=torch.float32)
+    ops.gemm(a, b, c, layout_a=la, layout_b=lb, M=M, N=N, K=K, tiles=(bm, bn))
+    ref = _logical(a, la, M, K) @ _logical(b, lb, N, K).t()
+    torch.cuda.synchronize()
+    assert torch.equal(c, ref), (c - ref).abs().max()
+
+
+def test_gemm_identity_asymmetric(dev):
+    M = N = K = 128
+    eye = torch.eye(M, dtype=torch.bfloat16, device=dev)
+    b = (torch.arange(N * K, dtype=torch.float32).reshape(N, K) % 97).to(torch.bfloat16).to(dev)
+    c = torch.empty(M, N, device=dev)
+    ops.gemm(eye, b, c, layout_a=KMAJ, layout_b=KMAJ, M=M, N=N, K=K)
+    assert torch.equal(c, b.float().t())
+
+
+@pytest.mark.parametrize("la,lb", LAYOUTS)
+def test_gemm_random_bf16_out(dev, la, lb):
+    gen = torch.Generator().manual_seed(7)
+    M, N, K = 512, 384, 832
+    a = _storage(la, M, K, gen, dev, False)
+    b = _storage(lb, N, K, gen, dev, False)
+    bias = torch.randn(N, generator=gen).to(dev)
+    for act in ("linear", "relu", "sigmoid"):
+        c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        ops.gemm(a, b, c, layout_a=la, layout_b=lb, M=M, N=N, K=K, bias=bias, act=act)
+        ref = _logical(a, la, M, K) @ _logical(b, lb, N, K).t() + bias
+        ref = {"linear": ref, "relu": ref.clamp_min(0), "sigmoid": torch.sigmoid(ref)}[act]
+        torch.testing.assert_close(c.float(), ref, rtol=1.6e-2, atol=2e-2)
+
+
+def test_gemm_split_k_accumulate(dev):
+    gen = torch.Generator().manual_seed(3)
+    R, N, K, S = 1024, 128, 256, 4
+    dz = torch.randn(R, N, generator=gen).to(torch.bfloat16).to(dev)
+    x = torch.randn(R, K, generator=gen).to(torch.bfloat16).to(dev)
+    slabs = torch.empty(S, N, K, device=dev)
+    ops.linear_wgrad(dz, x, slabs, splits=S)
+    ops.linear_wgrad(dz, x, slabs, splits=S, accumulate=True)
+    full = 2 * dz.float().t() @ x.float()
+    torch.testing.assert_close(slabs.sum(0), full, rtol=1e-4, atol=1e-3)
+    part = dz.float()[: R // S].t() @ x.float()[: R // S]
+    torch.testing.assert_close(slabs[0], 2 * part, rtol=1e-4, atol=1e-3)
+
+
+def test_linear_triplet_matches_autograd(dev):
+    """fwd/dgrad(+relu mask)/wgrad of one hidden layer vs torch autograd in fp32."""
+    gen = torch.Generator().manual_seed(11)
+    M, K, N = 256, 832, 512
+    x = torch.rand(M, K, generator=gen).to(torch.bfloat16)
+    w = (torch.randn(N, K, generator=gen) * 0.05).to(torch.bfloat16)
+    b = torch.randn(N, generator=gen) * 0.1
+    g_out = torch.randn(M, N, generator=gen).to(torch.bfloat16)
+    xd, wd, bd, gd = x.to(dev), w.to(dev), b.to(dev), g_out.to(dev)
+    y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    ops.linear_fwd(xd, wd, bd, y, act="relu")
+    xr = x.float().requires_grad_()
+    wr = w.float().requires_grad_()
+    yr = torch.relu(xr @ wr.t() + b)
+    torch.testing.assert_close(y.float().cpu(), yr.detach(), rtol=1.6e-2, atol=1e-2)
+    # dz of this layer given upstream grad: dz = g * relu'(y)
+    dz = torch.where(y > 0, gd, torch.zeros_like(gd))
+    dx = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
+    ops.linear_dgrad(dz, wd, dx)
+    slabs = torch.empty(2, N, K, device=dev)
+    ops.linear_wgrad(dz, xd, slabs, splits=2)
+    yr.backward(g_out.float())
+    torch.testing.assert_close(dx.float().cpu(), xr.grad, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(slabs.sum(0).cpu(), wr.grad, rtol=2e-2, atol=5e-2)
+
+
+def test_dgrad_fused_mask(dev):
+    gen = torch.Generator().manual_seed(5)
+    M, N, K = 128, 128, 256
+    dz = torch.randn(M, N, generator=gen).to(torch.bfloat16).to(dev)
+    w = torch.randn(N, K, generator=gen).to(torch.bfloat16).to(dev)
+    y_prev = torch.randn(M, K, generator=gen).clamp_min(0).to(torch.bfloat16).to(dev)
+    dx = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
+    ops.linear_dgrad(dz, w, dx, y_prev=y_prev, act_prev="relu")
+    ref = (dz.float() @ w.float()) * (y_prev.float() > 0)
+    torch.testing.assert_close(dx.float(), ref, rtol=1.6e-2, atol=2e-2)
+
+
+def test_gemm_rejects_bad_shapes(dev):
+    a = torch.zeros(100, 64, device=dev, dtype=torch.bfloat16)
+    w = torch.zeros(64, 64, device=dev, dtype=torch.bfloat16)
+    y = torch.zeros(100, 64, device=dev, dtype=torch.bfloat16)
+    with pytest.raises(ValueError):
+        ops.linear_fwd(a, w, None, y)
+
+
+def test_softmax_xent(dev):
+    gen = torch.Generator().manual_seed(9)
+    rows, ncls, width = 300, 10, 64
+    logits = torch.randn(rows, width, generator=gen) * 3
+    labels = torch.randint(0, ncls, (rows,), generator=gen, dtype=torch.int32)
+    labels[::7] = -1  # padding rows
+    dz = torch.empty(rows, width, dtype=torch.bfloat16, device=dev)
+    loss = torch.zeros(1, device=dev)
+    corr = torch.zeros(1, dtype=torch.int32, device=dev)
+    ops.softmax_xent(logits.to(dev), labels.to(dev), dz, ncls, 1.0 / rows, loss, corr)
+    dz_r = torch.empty(rows, width, dtype=torch.bfloat16)
+    loss_r = torch.zeros(1)
+    corr_r = torch.zeros(1, dtype=torch.int32)
+    from docker_dist_nn_amd.ops import reference as ref
+    ref.softmax_xent(logits, labels, dz_r, ncls, 1.0 / rows, loss_r, corr_r)
+    torch.testing.assert_close(dz.float().cpu(), dz_r.float(), rtol=1e-2, atol=1e-4)
+    torch.testing.assert_close(loss.cpu(), loss_r, rtol=1e-5, atol=1e-3)
+    assert int(corr.item()) == int(corr_r.item())
+
+
+def test_softmax_rows_and_argmax(dev):
+    gen = torch.Generator().manual_seed(10)
+    rows, ncls = 257, 10
+    logits = torch.randn(rows, 64, generator=gen).to(dev)
+    out = torch.zeros(rows, 64, device=dev)
+    labels = torch.randint(0, ncls, (rows,), generator=gen, dtype=torch.int32).to(dev)
+    pred = torch.empty(rows, dtype=torch.int32, device=dev)
+    corr = torch.zeros(1, dtype=torch.int32, device=dev)
+    ops.softmax_rows(logits, out, ncls, labels, pred, corr)
+    p = torch.softmax(logits[:, :ncls], 1)
+    torch.testing.assert_close(out[:, :ncls], p, rtol=1e-5, atol=1e-6)
+    am = torch.argmax(logits[:, :ncls], 1)
+    assert torch.equal(pred.long(), am)
+    assert int(corr.item()) == int((am == labels.long()).sum())
+
+
+def test_colsum_and_reduce(dev):
+    gen = torch.Generator().manual_seed(4)
+    rows, cols, P = 1000, 192, 7
+    x = torch.randn(rows, cols, generator=gen).to(torch.bfloat16).to(dev)
+    part = torch.empty(P, cols, device=dev)
+    ops.colsum_partial(x, part)
+    out = torch.empty(cols, device=dev)
+    ops.reduce_slabs(part, P, cols, cols, out, scale=0.5)
+    torch.testing.assert_close(out, 0.5 * x.float().sum(0), rtol=1e-4, atol=1e-3)
+
+
+def test_sgd_and_adam_match_torch(dev):
+    gen = torch.Generator().manual_seed(2)
+    n = 4096
+    p0 = torch.randn(n, generator=gen)
+    g = torch.randn(n, generator=gen)
+    # SGD with momentum + weight decay vs torch.optim.SGD
+    p = p0.clone().to(dev)
+    mom = torch.zeros(n, device=dev)
+    sh = torch.empty(n, device=dev, dtype=torch.bfloat16)
+    tp = torch.nn.Parameter(p0.clone())
+    opt = torch.optim.SGD([tp], lr=0.1, momentum=0.9, weight_decay=0.01)
+    for _ in range(3):
+        ops.sgd_update(p, g.to(dev), mom, sh, lr=0.1, momentum=0.9, weight_decay=0.01)
+        tp.grad = g.clone()
+        opt.step()
+    torch.testing.assert_close(p.cpu(), tp.detach(), rtol=1e-5, atol=1e-6)
+    assert torch.equal(sh, p.to(torch.bfloat16))
+    # Adam vs torch.optim.Adam
+    p = p0.clone().to(dev)
+    m = torch.zeros(n, device=dev)
+    v = torch.zeros(n, device=dev)
+    tp = torch.nn.Parameter(p0.clone())
+    opt = torch.optim.Adam([tp], lr=1e-3)
+    for step in range(1, 4):
+        ops.adam_update(p, g.to(dev), m, v, None, lr=1e-3, step=step)
+        tp.grad = g.clone()
+        opt.step()
+    torch.testing.assert_close(p.cpu(), tp.detach(), rtol=1e-5, atol=1e-6)
+
+
+def test_pack_unpack(dev):
+    x = torch.rand(100, 784, device=dev)
+    out = torch.full((128, 832), 7.0, device=dev, dtype=torch.bfloat16)
+    ops.pack_bf16(x, out)
+    assert torch.equal(out[:100, :784], x.to(torch.bfloat16))
+    assert out[100:].abs().sum() == 0 and out[:, 784:].abs().sum() == 0
+    back = torch.empty(100, 784, device=dev)
+    ops.unpack_bf16(out, back)
+    assert torch.equal(back, x.to(torch.bfloat16).float())
