@@ -1,0 +1,171 @@
+"""Headline benchmark: samples/sec (whole node) of MNIST-FCNN training on N MI355X GPUs.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 it is launched
+by ``torch.distributed.run`` with one rank per GPU (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* in the
+env, RCCL over xGMI). W untimed warm-up steps, then EXACTLY K timed steps bracketed by a barrier
++ device synchronize on both sides; the max elapsed time over ranks is used; rank 0 prints one
+JSON line.
+
+Model: BASELINE.json config "784-512-256-128-10 MNIST FCNN bf16" (random init, synthetic
+MNIST-shaped data resident in HBM). One step = forward + backward + SGD update of the global
+batch (bf16 operands, fp32 accumulation/master weights), on our own gfx950 kernels.
+Parallel layout: ``--parallelism auto`` lets the planner pick pp x dp for N GPUs (see
+docker_dist_nn_amd/parallel/planner.py); ``ppS`` forces an S-stage pipeline, ``dpN`` pure data
+parallelism, ``ppSdpD`` both.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from docker_dist_nn_amd import NAMED_MODELS, MLPSpec  # noqa: E402
+from docker_dist_nn_amd.data import DeviceDataset, synthetic_mnist  # noqa: E402
+from docker_dist_nn_amd.engine import OptimConfig, Trainer  # noqa: E402
+from docker_dist_nn_amd.parallel.planner import Planner, parse_parallelism  # noqa: E402
+
+METRIC = "samples/sec (whole node) MNIST FCNN training at 1/2/4/8-stage pipeline"
+# Only published training throughput of the reference: centralized Keras 784-32-16-10,
+# batch 32, 54,000 samples in ~5 s/epoch (notebook …ipynb:302-361).
+BASELINE_SAMPLES_PER_S = 10_800.0
+MODEL_LABEL = {"mnist-fcnn": "784-512-256-128-10 MNIST FCNN",
+               "mlp8": "784-1024x7-10 MLP (8 Linear)", "mlp7": "784-1024x6-10 MLP",
+               "wide": "784-8192-8192-10 MLP"}
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--model", default="mnist-fcnn")
+    ap.add_argument("--batch", type=int, default=65536,
+                    help="rows per GPU per step (global batch = batch x N)")
+    ap.add_argument("--parallelism", default="auto")
+    ap.add_argument("--schedule", default="1f1b")
+    ap.add_argument("--micro", type=int, default=0, help="micro-batch rows (0 = planner)")
+    ap.add_argument("--lr", type=float, default=0.05)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--seed", type=int, default=0)
+    return ap.parse_args(argv)
+
+
+def main(argv=None):
+    a = parse_args(argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.gpus != world and world > 1:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    n = max(a.gpus, world)
+    spec = NAMED_MODELS.get(a.model) or MLPSpec.parse(a.model)
+
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    mesh = None
+    if world > 1:
+        from docker_dist_nn_amd.parallel.groups import build_mesh, init_distributed
+
+        init_distributed("nccl")
+    pp, dp = parse_parallelism(a.parallelism, n)
+    planner = Planner()
+    if pp is None:
+        plan = planner.best(spec, n, a.batch)
+    else:
+        plan = planner.evaluate(spec, pp, dp, a.batch * pp)
+    mb = a.micro or plan.micro_batch
+    rows = a.batch * plan.pp  # rows per replica per step (weak scaling: batch rows per GPU)
+    nm = max(1, rows // mb)
+    if mb * nm != rows or mb % 64:
+        raise SystemExit(f"batch {rows} must split into micro-batches of a multiple of 64")
+    if world > 1:
+        mesh = build_mesh(plan.pp, plan.dp)
+
+    tr = Trainer(spec, micro_batch=mb, num_micro=nm, distribution=plan.distribution,
+                 pp=plan.pp, dp=plan.dp, schedule=a.schedule, optim=OptimConfig(lr=a.lr),
+                 device=dev, seed=a.seed, mesh=mesh)
+    replica = mesh.replica if mesh else 0
+    x, y = synthetic_mnist(max(60000, 2 * rows), seed=a.seed + 1000 * replica)
+    data = DeviceDataset(x, y, rows, dev, kp=tr.stages[0].x_in.shape[1] if tr.first else None)
+
+    use_graph = world == 1 and not a.no_graph
+    step_i = 0
+
+    def one_step():
+        nonlocal step_i
+        xb, yb = data.batch(step_i)
+        tr.set_batch(xb if tr.first else None, yb if tr.last else None)
+        tr.step()
+        step_i += 1
+
+    if use_graph:
+        tr.set_batch(*data.batch(0))
+        tr.capture()
+    for _ in range(a.warmup):
+        one_step()
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize(dev)
+
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        one_step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    loss = tr.loss()
+    global_batch = rows * plan.dp
+    samples = global_batch * a.steps
+    value = samples / elapsed
+    out = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "samples/s",
+        "n_gpus": n,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(value / BASELINE_SAMPLES_PER_S, 1),
+        "dtype": "bf16",
+        "data": "synthetic (MNIST-shaped 784-feature inputs, teacher labels; random-init weights)",
+        "config": {
+            "model": MODEL_LABEL.get(a.model, spec.describe()),
+            "global_batch": global_batch,
+            "seq_len": None,
+            "parallelism": plan.parallelism,
+            "layer_distribution": plan.distribution,
+            "micro_batch": mb,
+            "num_micro": nm,
+            "schedule": a.schedule if plan.pp > 1 else "none",
+            "optimizer": "sgd",
+            "hip_graph": use_graph,
+        },
+        "model_tflops": round(spec.flops_per_sample_train() * value / 1e12, 1),
+        "last_loss": None if loss is None else round(loss, 5),
+    }
+    rank = int(os.environ.get("RANK", "0"))
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -15,6 +15,7 @@
 #include "kernels/gemm.hpp"
 #include "runtime/graph.hpp"
 #include "runtime/json_weights.hpp"
+#include "runtime/matrix_codec.hpp"
 #include "runtime/schedule.hpp"
 
 namespace py = pybind11;
@@ -43,8 +44,11 @@ PYBIND11_MODULE(_native, m) {
       "gemm_bf16",
       [](uintptr_t a, long lda, uintptr_t b, long ldb, uintptr_t c, long ldc, long c_split_stride,
          uintptr_t bias, uintptr_t aux, long ld_aux, int M, int N, int K, int act, int accumulate,
-         int layout_a, int layout_b, int out_f32, int bm, int bn, int splits, uintptr_t stream) {
+         int layout_a, int layout_b, int out_f32, int bm, int bn, int splits, uintptr_t stream,
+         uintptr_t colsum, long ld_colsum) {
         GemmParams p{};
+        p.colsum = P<float>(colsum);
+        p.ld_colsum = ld_colsum;
         p.A = P<const uint16_t>(a);
         p.lda = lda;
         p.B = P<const uint16_t>(b);
@@ -67,17 +71,23 @@ PYBIND11_MODULE(_native, m) {
       py::arg("c_split_stride"), py::arg("bias"), py::arg("aux"), py::arg("ld_aux"), py::arg("M"),
       py::arg("N"), py::arg("K"), py::arg("act"), py::arg("accumulate"), py::arg("layout_a"),
       py::arg("layout_b"), py::arg("out_f32"), py::arg("bm"), py::arg("bn"), py::arg("splits"),
-      py::arg("stream"));
+      py::arg("stream"), py::arg("colsum") = 0, py::arg("ld_colsum") = 0);
 
   m.def("softmax_xent",
         [](uintptr_t logits, long ld_logits, uintptr_t labels, uintptr_t dz, long ld_dz, int rows,
-           int n_cls, int width, float scale, uintptr_t loss_sum, uintptr_t correct,
-           uintptr_t stream) {
+           int n_cls, int width, float scale, uintptr_t loss_part, uintptr_t correct,
+           uintptr_t stream, uintptr_t colsum, long ld_colsum) {
           check(dnn::softmax_xent(P<const float>(logits), ld_logits, P<const int>(labels),
                                   P<uint16_t>(dz), ld_dz, rows, n_cls, width, scale,
-                                  P<float>(loss_sum), P<int>(correct), S(stream)),
+                                  P<float>(loss_part), P<int>(correct), P<float>(colsum),
+                                  ld_colsum, S(stream)),
                 "softmax_xent");
-        });
+        },
+        py::arg("logits"), py::arg("ld_logits"), py::arg("labels"), py::arg("dz"),
+        py::arg("ld_dz"), py::arg("rows"), py::arg("n_cls"), py::arg("width"), py::arg("scale"),
+        py::arg("loss_part"), py::arg("correct"), py::arg("stream"), py::arg("colsum") = 0,
+        py::arg("ld_colsum") = 0);
+  m.def("softmax_xent_blocks", &dnn::softmax_xent_blocks);
   m.def("softmax_rows", [](uintptr_t logits, long ld_in, uintptr_t out, long ld_out, int rows,
                            int n_cls, uintptr_t labels, uintptr_t pred, uintptr_t correct,
                            uintptr_t stream) {
@@ -219,6 +229,36 @@ PYBIND11_MODULE(_native, m) {
         return out;
       },
       py::arg("path"), "Parse an inputs JSON ({\"examples\": [...]}) into float32 + int32 arrays.");
+
+  // ---- runtime: protobuf Matrix codec (gRPC compat ingress) -----------------------------
+  m.def(
+      "decode_matrix",
+      [](py::bytes b) {
+        char* buf;
+        py::ssize_t n;
+        PYBIND11_BYTES_AS_STRING_AND_SIZE(b.ptr(), &buf, &n);
+        dnn::DecodedMatrix M;
+        {
+          py::gil_scoped_release nogil;
+          M = dnn::decode_matrix(reinterpret_cast<const uint8_t*>(buf), (size_t)n);
+        }
+        py::array_t<double> a({(py::ssize_t)M.rows, (py::ssize_t)M.cols});
+        if (!M.data.empty()) std::memcpy(a.mutable_data(), M.data.data(), M.data.size() * 8);
+        return a;
+      },
+      py::arg("data"), "Matrix wire bytes -> float64 [rows][cols]");
+  m.def(
+      "encode_matrix",
+      [](py::array_t<double, py::array::c_style | py::array::forcecast> a) {
+        if (a.ndim() != 2) throw std::invalid_argument("encode_matrix needs a 2-D array");
+        std::string s;
+        {
+          py::gil_scoped_release nogil;
+          s = dnn::encode_matrix(a.data(), (long)a.shape(0), (long)a.shape(1));
+        }
+        return py::bytes(s);
+      },
+      py::arg("array"), "float64 [rows][cols] -> Matrix wire bytes");
 
   // ---- runtime: HIP graph executor ------------------------------------------------------
   py::class_<dnn::GraphExec>(m, "GraphExec")

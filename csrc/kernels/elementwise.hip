@@ -17,53 +17,77 @@
 namespace dnn {
 
 // ------------------------------------------------------------------------------------------
-// softmax + cross-entropy, one wave per row (padded width <= 64*NCH columns).
+// softmax + cross-entropy. One wave per row, each wave walks XENT_ROWS_PER_WAVE rows, so a
+// block covers 4 * XENT_ROWS_PER_WAVE rows (padded width <= 64*NCH columns).
 // dz = (softmax(logits) - onehot(label)) * scale in the first n_cls columns, 0 elsewhere.
-// Rows whose label is < 0 are padding: dz = 0 and no loss. loss_sum / correct are reduced per
-// block and added with one atomic each.
+// Rows whose label is < 0 are padding: dz = 0 and no loss. The block's loss sum goes to
+// loss_part[blockIdx.x] (summed later in a fixed order: bitwise reproducible, no float
+// atomics); the correct-prediction count uses one integer atomic per block (exact).
 // ------------------------------------------------------------------------------------------
+constexpr int XENT_ROWS_PER_WAVE = 16;
+constexpr int XENT_ROWS_PER_BLOCK = 4 * XENT_ROWS_PER_WAVE;
+
 template <int NCH>
 __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restrict__ logits,
                                                            long ld_logits,
                                                            const int* __restrict__ labels,
                                                            u16* __restrict__ dz, long ld_dz,
                                                            int rows, int n_cls, int width,
-                                                           float scale, float* loss_sum,
-                                                           int* correct) {
+                                                           float scale, float* loss_part,
+                                                           int* correct, float* colsum,
+                                                           long ld_colsum) {
   __shared__ float s_loss[4];
   __shared__ int s_corr[4];
+  __shared__ float s_col[4][64 * NCH];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int row = blockIdx.x * 4 + wave;
-  float loss = 0.f;
-  int corr = 0;
-  if (row < rows) {
-    const float* lr = logits + (long)row * ld_logits;
-    const int label = labels[row];
-    float x[NCH];
-    float mx = -INFINITY;
+  const int row0 = blockIdx.x * XENT_ROWS_PER_BLOCK + wave * XENT_ROWS_PER_WAVE;
+  // prefetch every row of this wave first: 16 independent loads in flight instead of 16
+  // dependent round trips
+  float xs[XENT_ROWS_PER_WAVE][NCH];
+  int labs[XENT_ROWS_PER_WAVE];
+#pragma unroll
+  for (int k = 0; k < XENT_ROWS_PER_WAVE; ++k) {
+    const int row = row0 + k;
+    const bool ok = row < rows;
+    labs[k] = ok ? labels[row] : -1;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int col = c * 64 + lane;
-      x[c] = col < n_cls ? lr[col] : -INFINITY;
-      mx = fmaxf(mx, x[c]);
+      xs[k][c] = (ok && col < n_cls) ? logits[(long)row * ld_logits + col] : -INFINITY;
     }
+  }
+  float loss = 0.f;
+  int corr = 0;
+  float cs[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) cs[c] = 0.f;
+#pragma unroll
+  for (int k = 0; k < XENT_ROWS_PER_WAVE; ++k) {
+    const int row = row0 + k;
+    if (row >= rows) break;
+    const int label = labs[k];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) mx = fmaxf(mx, xs[k][c]);
     mx = wave_max(mx);
     // argmax: lowest column index holding the max (np.argmax tie rule)
     int amax = 1 << 30;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int col = c * 64 + lane;
-      if (col < n_cls && x[c] == mx) amax = min(amax, col);
+      if (col < n_cls && xs[k][c] == mx) amax = min(amax, col);
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) amax = min(amax, __shfl_xor(amax, o, 64));
-    float se = 0.f;
+    float e[NCH], se = 0.f, xl = -INFINITY;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
-      x[c] = __expf(x[c] - mx);  // exp(-inf) = 0 for padding
-      se += x[c];
+      e[c] = __expf(xs[k][c] - mx);  // exp(-inf) = 0 for padding
+      se += e[c];
+      if (c * 64 + lane == label) xl = xs[k][c];
     }
     se = wave_sum(se);
+    xl = wave_max(xl);
     const float inv = 1.f / se;
     u16* dr = dz + (long)row * ld_dz;
 #pragma unroll
@@ -71,42 +95,56 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
       const int col = c * 64 + lane;
       if (col < width) {
         float g = 0.f;
-        if (label >= 0 && col < n_cls) g = (x[c] * inv - (col == label ? 1.f : 0.f)) * scale;
-        dr[col] = f2bf(g);
+        if (label >= 0 && col < n_cls) g = (e[c] * inv - (col == label ? 1.f : 0.f)) * scale;
+        const u16 h = f2bf(g);
+        dr[col] = h;
+        cs[c] += bf2f(h);
       }
     }
     if (label >= 0 && lane == 0) {
-      const float xl = lr[label];
-      loss = -(xl - mx - __logf(se));
-      corr = amax == label;
+      loss += -(xl - mx - __logf(se));
+      corr += amax == label;
     }
   }
   if (lane == 0) {
     s_loss[wave] = loss;
     s_corr[wave] = corr;
   }
+  if (colsum) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) s_col[wave][c * 64 + lane] = cs[c];
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
-    const float l = s_loss[0] + s_loss[1] + s_loss[2] + s_loss[3];
+    const float l = (s_loss[0] + s_loss[1]) + (s_loss[2] + s_loss[3]);
     const int cc = s_corr[0] + s_corr[1] + s_corr[2] + s_corr[3];
-    if (loss_sum && l != 0.f) atomicAdd(loss_sum, l);
+    if (loss_part) loss_part[blockIdx.x] = l;
     if (correct && cc) atomicAdd(correct, cc);
+  }
+  if (colsum) {
+    for (int col = threadIdx.x; col < width; col += 256)
+      colsum[(long)blockIdx.x * ld_colsum + col] =
+          (s_col[0][col] + s_col[1][col]) + (s_col[2][col] + s_col[3][col]);
   }
 }
 
+int softmax_xent_blocks(int rows) { return (rows + XENT_ROWS_PER_BLOCK - 1) / XENT_ROWS_PER_BLOCK; }
+
 int softmax_xent(const float* logits, long ld_logits, const int* labels, uint16_t* dz, long ld_dz,
-                 int rows, int n_cls, int width, float scale, float* loss_sum, int* correct,
-                 hipStream_t stream) {
+                 int rows, int n_cls, int width, float scale, float* loss_part, int* correct,
+                 float* colsum, long ld_colsum, hipStream_t stream) {
   if (rows <= 0 || n_cls <= 0 || n_cls > width || width > 256 || ld_logits < n_cls ||
-      ld_dz < width)
+      ld_dz < width || (colsum && ld_colsum < width))
     return -1;
-  const dim3 grid((rows + 3) / 4), block(256);
+  const dim3 grid(softmax_xent_blocks(rows)), block(256);
   if (width <= 64)
     hipLaunchKernelGGL(softmax_xent_kernel<1>, grid, block, 0, stream, logits, ld_logits, labels,
-                       dz, ld_dz, rows, n_cls, width, scale, loss_sum, correct);
+                       dz, ld_dz, rows, n_cls, width, scale, loss_part, correct, colsum,
+                       ld_colsum);
   else
     hipLaunchKernelGGL(softmax_xent_kernel<4>, grid, block, 0, stream, logits, ld_logits, labels,
-                       dz, ld_dz, rows, n_cls, width, scale, loss_sum, correct);
+                       dz, ld_dz, rows, n_cls, width, scale, loss_part, correct, colsum,
+                       ld_colsum);
   return hipGetLastError() == hipSuccess ? 0 : -9;
 }
 
@@ -218,17 +256,44 @@ int colsum_partial(const uint16_t* x, long ld, int rows, int cols, int n_part, f
 
 // ------------------------------------------------------------------------------------------
 // out[i] (+)= scale * sum_{s < n_src} src[s * stride + i], i < n  (n % 4 == 0)
+// Split-K wgrad reductions have few outputs and many sources (up to 128 slabs), so a block is
+// TX float4-columns x TY source groups: each thread sums every TY-th slab with 4 independent
+// loads in flight, then the TY partials are combined through LDS in a fixed order
+// (bitwise reproducible).
 // ------------------------------------------------------------------------------------------
+template <int TY>
 __global__ __launch_bounds__(256) void reduce_slabs_kernel(const float* __restrict__ src,
                                                            long stride, int n_src, long n4,
                                                            float scale, float* __restrict__ out,
                                                            int accumulate) {
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
-    f32x4_t a = *(const f32x4_t*)(src + i * 4);
-    for (int s = 1; s < n_src; ++s) a += *(const f32x4_t*)(src + s * stride + i * 4);
-    a *= scale;
-    if (accumulate) a += *(const f32x4_t*)(out + i * 4);
-    *(f32x4_t*)(out + i * 4) = a;
+  constexpr int TX = 256 / TY;
+  __shared__ f32x4_t red[TY][TX];
+  const int tx = threadIdx.x % TX, ty = threadIdx.x / TX;
+  for (long base = (long)blockIdx.x * TX; base < n4; base += (long)gridDim.x * TX) {
+    const long i = base + tx;
+    f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
+    if (i < n4) {
+      const float* p = src + i * 4;
+      int s = ty;
+      for (; s + 3 * TY < n_src; s += 4 * TY) {
+        a0 += *(const f32x4_t*)(p + (long)s * stride);
+        a1 += *(const f32x4_t*)(p + (long)(s + TY) * stride);
+        a2 += *(const f32x4_t*)(p + (long)(s + 2 * TY) * stride);
+        a3 += *(const f32x4_t*)(p + (long)(s + 3 * TY) * stride);
+      }
+      for (; s < n_src; s += TY) a0 += *(const f32x4_t*)(p + (long)s * stride);
+    }
+    red[ty][tx] = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    if (ty == 0 && i < n4) {
+      f32x4_t t = red[0][tx];
+#pragma unroll
+      for (int k = 1; k < TY; ++k) t += red[k][tx];
+      t *= scale;
+      if (accumulate) t += *(const f32x4_t*)(out + i * 4);
+      *(f32x4_t*)(out + i * 4) = t;
+    }
+    __syncthreads();
   }
 }
 
@@ -241,8 +306,20 @@ int reduce_slabs(const float* src, long stride, int n_src, long n, float scale, 
                  int accumulate, hipStream_t stream) {
   if (n <= 0 || n % 4 || n_src <= 0 || (n_src > 1 && stride % 4)) return -1;
   if ((((uintptr_t)src) | ((uintptr_t)out)) & 15) return -5;
-  hipLaunchKernelGGL(reduce_slabs_kernel, dim3(grid_for(n / 4)), dim3(256), 0, stream, src, stride,
-                     n_src, n / 4, scale, out, accumulate);
+  const long n4 = n / 4;
+  auto grid = [&](int tx) {
+    long g = (n4 + tx - 1) / tx;
+    return dim3((unsigned)(g < 8192 ? g : 8192));
+  };
+  if (n_src >= 16)
+    hipLaunchKernelGGL(reduce_slabs_kernel<16>, grid(16), dim3(256), 0, stream, src, stride, n_src,
+                       n4, scale, out, accumulate);
+  else if (n_src >= 4)
+    hipLaunchKernelGGL(reduce_slabs_kernel<4>, grid(64), dim3(256), 0, stream, src, stride, n_src,
+                       n4, scale, out, accumulate);
+  else
+    hipLaunchKernelGGL(reduce_slabs_kernel<1>, grid(256), dim3(256), 0, stream, src, stride, n_src,
+                       n4, scale, out, accumulate);
   return hipGetLastError() == hipSuccess ? 0 : -9;
 }
 

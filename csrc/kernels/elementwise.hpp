@@ -6,9 +6,12 @@
 
 namespace dnn {
 
+// loss_part: one fp32 partial per block (softmax_xent_blocks(rows) entries); colsum (optional):
+// per-block column sums of dz ([blocks][ld_colsum]) = bias-gradient partials of the last layer
 int softmax_xent(const float* logits, long ld_logits, const int* labels, uint16_t* dz, long ld_dz,
-                 int rows, int n_cls, int width, float scale, float* loss_sum, int* correct,
-                 hipStream_t stream);
+                 int rows, int n_cls, int width, float scale, float* loss_part, int* correct,
+                 float* colsum, long ld_colsum, hipStream_t stream);
+int softmax_xent_blocks(int rows);
 int softmax_rows(const float* logits, long ld_in, float* out, long ld_out, int rows, int n_cls,
                  const int* labels, int* pred, int* correct, hipStream_t stream);
 int colsum_partial(const uint16_t* x, long ld, int rows, int cols, int n_part, float* part,

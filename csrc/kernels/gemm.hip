@@ -180,6 +180,8 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmParams p, int tiles_
 
   constexpr int CPR = BN / 8;
   constexpr int ITER = BM * CPR / 256;
+  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // this thread's column chunk is
+                                                            // fixed: 256 % CPR == 0
 #pragma unroll 2
   for (int it = 0; it < ITER; ++it) {
     const int idx = threadIdx.x + it * 256;
@@ -199,6 +201,10 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmParams p, int tiles_
     }
     if constexpr (OUT_F32) {
       float* c = (float*)p.C + (long)split * p.c_split_stride + gm * p.ldc + gn;
+      if (!p.accumulate && p.act != ACT_LINEAR) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = act_fwd(v[e], p.act);
+      }
       f32x4_t o0 = {v[0], v[1], v[2], v[3]}, o1 = {v[4], v[5], v[6], v[7]};
       if (p.accumulate) {
         o0 += *(const f32x4_t*)c;
@@ -217,8 +223,29 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmParams p, int tiles_
       }
       bf16x8_t o;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = (short)f2bf(v[e]);
+      for (int e = 0; e < 8; ++e) {
+        const u16 h = f2bf(v[e]);
+        o[e] = (short)h;
+        csum[e] += bf2f(h);
+      }
       *(bf16x8_t*)((u16*)p.C + gm * p.ldc + gn) = o;
+    }
+  }
+  if constexpr (!OUT_F32) {
+    if (p.colsum) {  // uniform across the block
+      __syncthreads();  // all reads of the staging tile are done
+      f32x4_t LDS_AS* red = (f32x4_t LDS_AS*)lds;
+      red[2 * threadIdx.x] = f32x4_t{csum[0], csum[1], csum[2], csum[3]};
+      red[2 * threadIdx.x + 1] = f32x4_t{csum[4], csum[5], csum[6], csum[7]};
+      __syncthreads();
+      if ((int)threadIdx.x < BN) {
+        const int col = threadIdx.x, cc = col >> 3, e = col & 7;
+        const float LDS_AS* rf = (const float LDS_AS*)lds;
+        float t = 0.f;
+#pragma unroll 4
+        for (int r = 0; r < 256 / CPR; ++r) t += rf[(r * CPR + cc) * 8 + e];
+        p.colsum[(long)tm * p.ld_colsum + n0 + col] = t;
+      }
     }
   }
 }
@@ -247,6 +274,7 @@ const char* gemm_error_string(int code) {
     case -7: return "split-K > 1 requires fp32 output";
     case -8: return "leading dimension smaller than the row it stores";
     case -9: return "hip launch failed";
+    case -10: return "colsum needs bf16 output and ld_colsum >= N";
     default: return "unknown gemm error";
   }
 }
@@ -262,6 +290,7 @@ int gemm_bf16(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, 
     return -5;
   if ((la != KMAJ && la != MNMAJ) || (lb != KMAJ && lb != MNMAJ)) return -6;
   if (splits > 1 && !out_f32) return -7;
+  if (p.colsum && (out_f32 || p.ld_colsum < p.N)) return -10;
   const long a_row = la == KMAJ ? (long)p.K * splits : p.M;
   const long b_row = lb == KMAJ ? (long)p.K * splits : p.N;
   if (p.lda < a_row || p.ldb < b_row || p.ldc < p.N || (p.aux && p.ld_aux < p.N)) return -8;

@@ -30,6 +30,8 @@ struct GemmParams {
   int M, N, K;     // K = contraction length handled by ONE split
   int act;         // Act code: forward activation, or (with aux) the activation to differentiate
   int accumulate;  // f32 output: C += result (split slab accumulation across micro-batches)
+  float* colsum;   // optional (bf16 output only): colsum[tile_m][n] = sum over the tile's rows
+  long ld_colsum;  //   of the stored (bf16-rounded) output -> bias-gradient partials of dgrad
 };
 
 // Returns 0 on success, a negative code when a shape/alignment precondition fails

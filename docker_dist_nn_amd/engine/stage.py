@@ -1,0 +1,323 @@
+"""One pipeline stage: a contiguous slice of Linear layers resident on one device.
+
+This is the MI355X replacement of the reference's stage worker
+(/root/reference/src/grpc_node.py:16-97), which held its layers' fp64 weights and ran
+``np.dot(x, W) + b`` + activation per request. A Stage instead owns, for one training step of
+``num_micro`` micro-batches of ``micro_batch`` rows:
+
+* parameters in ONE flat fp32 master buffer (padded [Np][Kp] weight + [Np] bias per layer),
+  a bf16 shadow of it that the GEMMs read, one flat fp32 gradient buffer (the unit of the DP
+  all-reduce) and flat optimizer state -- so the optimizer is a single fused kernel;
+* step buffers for every micro-batch (activations, dZ, logits, labels) laid out as
+  [num_micro * micro_batch] rows, so micro-batch j is a row slice and the deferred weight
+  gradient can run as ONE batch-contraction GEMM over all rows (or per micro-batch);
+* split-K wgrad slabs and bias-gradient partials, reduced deterministically (no atomics).
+
+Per layer the compute is three fused gfx950 kernels: forward GEMM with bias+activation
+epilogue, dgrad GEMM whose epilogue applies the previous layer's activation derivative (read
+from the stored activation -- no mask tensor), and the wgrad GEMM. The last layer of the last
+stage writes fp32 logits and runs the fused softmax-cross-entropy kernel.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..models.mlp import LayerGeom, MLPSpec, round_up
+
+_ALIGN = 64  # elements; keeps every layer's region 256-B aligned
+
+
+@dataclass
+class OptimConfig:
+    name: str = "sgd"
+    lr: float = 0.05
+    momentum: float = 0.0
+    weight_decay: float = 0.0
+    betas: tuple[float, float] = (0.9, 0.999)
+    eps: float = 1e-8
+    decoupled: bool = False
+
+
+class StageParams:
+    """Flat parameter / gradient / optimizer buffers of a stage's layers."""
+
+    def __init__(self, geoms: Sequence[LayerGeom], device: torch.device,
+                 optim: Optional[OptimConfig] = None):
+        self.geoms = list(geoms)
+        self.device = device
+        self.optim = optim or OptimConfig()
+        off = 0
+        self.w_off, self.b_off = [], []
+        for g in self.geoms:
+            self.w_off.append(off)
+            off = round_up(off + g.np_ * g.kp, _ALIGN)
+            self.b_off.append(off)
+            off = round_up(off + g.np_, _ALIGN)
+        self.numel = off
+        self.master = torch.zeros(off, dtype=torch.float32, device=device)
+        self.shadow = torch.zeros(off, dtype=torch.bfloat16, device=device)
+        self.grad = torch.zeros(off, dtype=torch.float32, device=device)
+        self.state: list[torch.Tensor] = []
+        self.step_count = 0
+        self._init_state()
+
+    def _init_state(self):
+        o = self.optim
+        if o.name == "sgd":
+            self.state = [torch.zeros_like(self.master)] if o.momentum else []
+        elif o.name in ("adam", "adamw"):
+            self.state = [torch.zeros_like(self.master), torch.zeros_like(self.master)]
+        else:
+            raise ValueError(f"unknown optimizer {o.name!r} (sgd | adam | adamw)")
+
+    # views ------------------------------------------------------------------------------
+    def w32(self, i):
+        g = self.geoms[i]
+        return self.master[self.w_off[i]:self.w_off[i] + g.np_ * g.kp].view(g.np_, g.kp)
+
+    def b32(self, i):
+        return self.master[self.b_off[i]:self.b_off[i] + self.geoms[i].np_]
+
+    def wbf(self, i):
+        g = self.geoms[i]
+        return self.shadow[self.w_off[i]:self.w_off[i] + g.np_ * g.kp].view(g.np_, g.kp)
+
+    def gw(self, i):
+        g = self.geoms[i]
+        return self.grad[self.w_off[i]:self.w_off[i] + g.np_ * g.kp]
+
+    def gb(self, i):
+        return self.grad[self.b_off[i]:self.b_off[i] + self.geoms[i].np_]
+
+    def layer_grad_range(self, i) -> tuple[int, int]:
+        """Flat [start, end) of layer i's W and b gradients (a DP all-reduce bucket)."""
+        end = self.b_off[i + 1] if i + 1 < len(self.geoms) else self.numel
+        return self.w_off[i], end
+
+    # weights in/out -----------------------------------------------------------------------
+    def load(self, weights: Sequence[np.ndarray], biases: Sequence[np.ndarray]) -> None:
+        """Set from unpadded [out][in] weights / [out] biases (any float dtype)."""
+        self.master.zero_()
+        for i, g in enumerate(self.geoms):
+            w = torch.as_tensor(np.asarray(weights[i], dtype=np.float32))
+            b = torch.as_tensor(np.asarray(biases[i], dtype=np.float32))
+            if tuple(w.shape) != (g.spec.out_dim, g.spec.in_dim):
+                raise ValueError(f"layer {g.index}: weight shape {tuple(w.shape)} != "
+                                 f"{(g.spec.out_dim, g.spec.in_dim)}")
+            self.w32(i)[:g.spec.out_dim, :g.spec.in_dim] = w.to(self.device)
+            self.b32(i)[:g.spec.out_dim] = b.to(self.device)
+        self.refresh_shadow()
+
+    def init_default(self, seed: int) -> None:
+        """nn.Linear default init, U(-1/sqrt(in), 1/sqrt(in)); seeded by GLOBAL layer index so
+        any stage split of the same model starts from identical weights."""
+        ws, bs = [], []
+        for g in self.geoms:
+            gen = torch.Generator().manual_seed(seed * 7919 + g.index)
+            bound = 1.0 / math.sqrt(g.spec.in_dim)
+            ws.append((torch.rand(g.spec.out_dim, g.spec.in_dim, generator=gen) * 2 - 1) * bound)
+            bs.append((torch.rand(g.spec.out_dim, generator=gen) * 2 - 1) * bound)
+        self.load([w.numpy() for w in ws], [b.numpy() for b in bs])
+
+    def refresh_shadow(self) -> None:
+        self.shadow.copy_(self.master.to(torch.bfloat16))
+
+    def export(self) -> tuple[list[np.ndarray], list[np.ndarray]]:
+        ws, bs = [], []
+        for i, g in enumerate(self.geoms):
+            ws.append(self.w32(i)[:g.spec.out_dim, :g.spec.in_dim].detach().cpu().numpy().copy())
+            bs.append(self.b32(i)[:g.spec.out_dim].detach().cpu().numpy().copy())
+        return ws, bs
+
+    # optimizer ----------------------------------------------------------------------------
+    def optimizer_step(self, lr: Optional[float] = None) -> None:
+        o = self.optim
+        lr = o.lr if lr is None else lr
+        self.step_count += 1
+        if o.name == "sgd":
+            ops.sgd_update(self.master, self.grad, self.state[0] if self.state else None,
+                           self.shadow, lr=lr, momentum=o.momentum, weight_decay=o.weight_decay)
+        else:
+            ops.adam_update(self.master, self.grad, self.state[0], self.state[1], self.shadow,
+                            lr=lr, betas=o.betas, eps=o.eps, weight_decay=o.weight_decay,
+                            decoupled=o.decoupled or o.name == "adamw", step=self.step_count)
+
+
+class Stage:
+    """Compute of one pipeline stage for one step (see module doc)."""
+
+    def __init__(self, spec: MLPSpec, layer_start: int, layer_end: int, *, micro_batch: int,
+                 num_micro: int, device: torch.device, global_batch: Optional[int] = None,
+                 optim: Optional[OptimConfig] = None, wgrad: str = "batched",
+                 stage_index: int = 0, num_stages: int = 1):
+        if not 0 <= layer_start < layer_end <= len(spec.layers):
+            raise ValueError("bad layer range")
+        if micro_batch <= 0 or micro_batch % 64:
+            raise ValueError("micro_batch must be a positive multiple of 64 (MFMA row tiles); "
+                             "pad the batch with label -1 rows")
+        self.spec = spec
+        self.l0, self.l1 = layer_start, layer_end
+        self.first = layer_start == 0
+        self.last = layer_end == len(spec.layers)
+        self.stage_index, self.num_stages = stage_index, num_stages
+        self.mb, self.nm = micro_batch, num_micro
+        self.rows = micro_batch * num_micro
+        self.device = device
+        self.global_batch = global_batch or self.rows
+        self.wgrad_mode = wgrad
+        self.geoms = [LayerGeom(i, spec.layers[i]) for i in range(layer_start, layer_end)]
+        self.params = StageParams(self.geoms, device, optim)
+        self.prev_act = spec.layers[layer_start - 1].activation if not self.first else "linear"
+        self.n_cls = spec.out_dim
+        self._alloc()
+
+    # -------------------------------------------------------------------------------------
+    def _alloc(self):
+        R, dev = self.rows, self.device
+        bf, f32 = torch.bfloat16, torch.float32
+        g0 = self.geoms[0]
+        self.x_in = torch.zeros(R, g0.kp, dtype=bf, device=dev)
+        self.acts: list[torch.Tensor] = []  # output of local layer i
+        for i, g in enumerate(self.geoms):
+            is_logits = self.last and i == len(self.geoms) - 1
+            self.acts.append(torch.zeros(R, g.np_, dtype=f32 if is_logits else bf, device=dev))
+        self.dz = [torch.zeros(R, g.np_, dtype=bf, device=dev) for g in self.geoms]
+        self.dx_send = None if self.first else torch.zeros(R, g0.kp, dtype=bf, device=dev)
+        self.labels = torch.full((R,), -1, dtype=torch.int32, device=dev) if self.last else None
+        self.xent_per_micro = ops.xent_blocks(self.mb)
+        self.loss_part = torch.zeros(self.xent_per_micro * self.nm, dtype=f32, device=dev)
+        self.correct = torch.zeros(1, dtype=torch.int32, device=dev)
+        # wgrad geometry: batched = one GEMM over all rows; per_micro = one per micro-batch
+        wrows = R if self.wgrad_mode == "batched" else self.mb
+        self.w_splits = [ops.pick_splits(g.np_, g.kp, wrows) for g in self.geoms]
+        self.slabs = [torch.zeros(s, g.np_, g.kp, dtype=f32, device=dev)
+                      for s, g in zip(self.w_splits, self.geoms)]
+        # Bias-gradient partials (column sums of dZ) come fused from whichever kernel produces
+        # dZ: the dgrad epilogue of the next local layer (one partial per output row tile), the
+        # softmax-CE kernel (one per 64-row block), or -- for a gradient received from the next
+        # stage -- a colsum kernel. self.bp[i] = partials per micro-batch.
+        self.bp = []
+        L = len(self.geoms)
+        for i in range(L):
+            if i < L - 1:
+                self.bp.append(self.mb // ops.dgrad_tiles(self.mb, self.geoms[i + 1].kp)[0])
+            elif self.last:
+                self.bp.append(ops.xent_blocks(self.mb))
+            else:
+                self.bp.append(max(1, self.mb // 1024))
+        self.bpart = [torch.zeros(self.bp[i] * self.nm, g.np_, dtype=f32, device=dev)
+                      for i, g in enumerate(self.geoms)]
+        self._w_done = 0
+
+    def rows_of(self, j: int) -> slice:
+        if not 0 <= j < self.nm:
+            raise IndexError(f"micro-batch {j} out of range [0, {self.nm})")
+        return slice(j * self.mb, (j + 1) * self.mb)
+
+    def input_of(self, i: int) -> torch.Tensor:
+        return self.x_in if i == 0 else self.acts[i - 1]
+
+    @property
+    def output(self) -> torch.Tensor:
+        """Activation sent to the next stage (bf16 [rows][Np])."""
+        return self.acts[-1]
+
+    @property
+    def grad_out(self) -> torch.Tensor:
+        """dZ of this stage's last layer, written by the next stage (received gradient)."""
+        return self.dz[-1]
+
+    # -------------------------------------------------------------------------------------
+    def begin_step(self) -> None:
+        self.correct.zero_()
+        self._w_done = 0
+
+    def forward(self, j: int) -> None:
+        r = self.rows_of(j)
+        p = self.params
+        for i, g in enumerate(self.geoms):
+            x = self.input_of(i)[r]
+            y = self.acts[i][r]
+            if self.last and i == len(self.geoms) - 1:
+                ops.linear_fwd(x, p.wbf(i), p.b32(i), y, act="linear")  # fp32 logits
+                k = j * self.xent_per_micro
+                ops.softmax_xent(y, self.labels[r], self.dz[i][r], self.n_cls,
+                                 1.0 / self.global_batch,
+                                 self.loss_part[k:k + self.xent_per_micro], self.correct,
+                                 colsum=self._bpart(i, j))
+            else:
+                ops.linear_fwd(x, p.wbf(i), p.b32(i), y, act=g.spec.activation)
+
+    def backward(self, j: int) -> None:
+        """dgrad chain of micro-batch j; dZ of the last local layer must already be present."""
+        r = self.rows_of(j)
+        p = self.params
+        if not self.last:  # dZ of our last layer arrived from the next stage
+            L = len(self.geoms) - 1
+            ops.colsum_partial(self.dz[L][r], self._bpart(L, j), self.bp[L])
+        for i in range(len(self.geoms) - 1, -1, -1):
+            if i > 0:
+                prev = self.geoms[i - 1].spec.activation
+                ops.linear_dgrad(self.dz[i][r], p.wbf(i), self.dz[i - 1][r],
+                                 y_prev=self.acts[i - 1][r], act_prev=prev,
+                                 colsum=self._bpart(i - 1, j))
+            elif not self.first:
+                # gradient for the previous stage, already multiplied by the derivative of its
+                # last layer's activation (its output is our input x_in)
+                ops.linear_dgrad(self.dz[0][r], p.wbf(0), self.dx_send[r], y_prev=self.x_in[r],
+                                 act_prev=self.prev_act)
+
+    def wgrad(self, j: int = -1) -> None:
+        """Weight/bias gradients for micro-batch j (slab-accumulated) or all rows (j = -1)."""
+        for i in range(len(self.geoms)):
+            self.wgrad_layer(i, j)
+        self._w_done += 1
+
+    def _bpart(self, i: int, j: int) -> torch.Tensor:
+        return self.bpart[i][j * self.bp[i]:(j + 1) * self.bp[i]]
+
+    def wgrad_layer(self, i: int, j: int = -1) -> None:
+        """Weight gradient GEMM of local layer i (bias partials were produced with dZ)."""
+        if j < 0:
+            r, accumulate = slice(0, self.rows), False
+        else:
+            if self.wgrad_mode == "batched":
+                raise RuntimeError("per-micro wgrad on a stage built with wgrad='batched'")
+            r, accumulate = self.rows_of(j), self._w_done > 0
+        ops.linear_wgrad(self.dz[i][r], self.input_of(i)[r], self.slabs[i],
+                         splits=self.w_splits[i], accumulate=accumulate)
+
+    def finalize_grads(self, layers: Optional[Sequence[int]] = None) -> None:
+        """Reduce split-K slabs / bias partials into the flat gradient buffer."""
+        p = self.params
+        for i in (range(len(self.geoms)) if layers is None else layers):
+            g = self.geoms[i]
+            n = g.np_ * g.kp
+            ops.reduce_slabs(self.slabs[i], self.w_splits[i], n, n, p.gw(i))
+            ops.reduce_slabs(self.bpart[i], self.bpart[i].shape[0], g.np_, g.np_, p.gb(i))
+
+    def optimizer_step(self, lr: Optional[float] = None) -> None:
+        self.params.optimizer_step(lr)
+
+    # convenience: a whole step when this stage holds the entire model ----------------------
+    def set_batch(self, x: torch.Tensor, labels: torch.Tensor) -> None:
+        self.x_in.copy_(x)
+        if self.labels is not None:
+            self.labels.copy_(labels)
+
+    def loss_sum(self) -> float:
+        """Sum of per-row CE losses of the last step (fixed-order fp64 host sum)."""
+        return float(self.loss_part.detach().cpu().double().sum())
+
+    def flops_per_step(self) -> float:
+        f = 0.0
+        for i, g in enumerate(self.geoms):
+            mult = 3 if (i > 0 or not self.first) else 2
+            f += 2.0 * mult * self.rows * g.np_ * g.kp
+        return f

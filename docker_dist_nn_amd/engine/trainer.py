@@ -1,0 +1,173 @@
+"""Training front-end: builds stages for a PP x DP layout and runs steps.
+
+Two modes:
+
+* local (``mesh=None``): every pipeline stage lives in this process on one device, joined by
+  zero-copy loopback hops. ``pp=1`` is the single-GPU path; its whole step -- all GEMMs, the
+  fused loss, wgrad reductions and the optimizer, ~20 kernels -- can be captured once into a
+  HIP graph (:meth:`capture`) and replayed with a single launch per step.
+* distributed (``mesh`` given): this rank owns stage ``mesh.stage`` of replica
+  ``mesh.replica``; hops are RCCL send/recv and gradients are all-reduced over the stage's DP
+  group, bucketed per layer and overlapped with the remaining weight-gradient GEMMs.
+
+The micro-batching / schedule replaces the reference's one-request-at-a-time synchronous chain
+(/root/reference/src/grpc_node.py:120-135); training itself is the reference's centralized
+recipe (/root/reference/scripts/generate_mnist_pytorch.py:35-52: logits -> softmax CE ->
+backward -> optimizer step) distributed over the stages.
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from ..models.mlp import MLPSpec
+from ..parallel.comm import DistPipe, LoopbackPipe
+from ..parallel.groups import Mesh
+from ..parallel.pipeline import GradSync, PipelineExecutor
+from ..partition import balanced_distribution, plan_stages
+from ..utils.native import native
+from .stage import OptimConfig, Stage
+
+
+def default_distribution(spec: MLPSpec, pp: int) -> list[int]:
+    """Balanced contiguous split by per-layer training FLOPs."""
+    return balanced_distribution([l.flops_per_sample_train for l in spec.layers], pp)
+
+
+class Trainer:
+    def __init__(self, spec: MLPSpec, *, micro_batch: int, num_micro: int = 1, pp: int = 1,
+                 dp: int = 1, distribution: Optional[Sequence[int]] = None,
+                 schedule: str = "1f1b", optim: Optional[OptimConfig] = None,
+                 device: Optional[torch.device] = None, seed: int = 0,
+                 mesh: Optional[Mesh] = None, wgrad: Optional[str] = None):
+        self.spec = spec
+        self.mesh = mesh
+        self.device = device or (torch.device("cuda", torch.cuda.current_device())
+                                 if torch.cuda.is_available() else torch.device("cpu"))
+        if mesh is not None:
+            pp, dp = mesh.pp, mesh.dp
+        self.pp, self.dp = pp, dp
+        dist_ = list(distribution) if distribution is not None else default_distribution(spec, pp)
+        self.plans = plan_stages(len(spec.layers), dist_)
+        if len(self.plans) != pp:
+            raise ValueError(f"layer_distribution {dist_} has {len(self.plans)} non-empty "
+                             f"stages but pp={pp}")
+        self.distribution = dist_
+        self.schedule = schedule
+        self.micro_batch, self.num_micro = micro_batch, num_micro
+        self.global_batch = micro_batch * num_micro * dp
+        self.optim = optim or OptimConfig()
+        wmode = wgrad or ("per_micro" if schedule in ("1f1b_w", "zb") else "batched")
+        mk = lambda p: Stage(spec, p.layer_start, p.layer_end, micro_batch=micro_batch,
+                             num_micro=num_micro, device=self.device,
+                             global_batch=self.global_batch, optim=self.optim, wgrad=wmode,
+                             stage_index=p.stage, num_stages=pp)
+        if mesh is None:
+            if dp != 1:
+                raise ValueError("data parallelism needs a distributed mesh (one rank per GPU)")
+            self.stages = [mk(p) for p in self.plans]
+            for st in self.stages:
+                st.params.init_default(seed)
+            self.pipe = LoopbackPipe(self.stages)
+            ids = [p.stage for p in self.plans]
+            sync = None
+        else:
+            st = mk(self.plans[mesh.stage])
+            st.params.init_default(seed)
+            self.stages = [st]
+            self.pipe = DistPipe(mesh, st)
+            ids = [mesh.stage]
+            sync = GradSync(mesh.dp_group, mesh.dp) if mesh.dp > 1 else None
+        self.executor = PipelineExecutor(self.stages, self.pipe, schedule, pp, ids, sync)
+        self._graph = None
+        self._stream = None
+        self.graph_nodes = 0
+        self.steps_done = 0
+
+    # -------------------------------------------------------------------------------------
+    @property
+    def first(self) -> Optional[Stage]:
+        return self.stages[0] if self.stages[0].first else None
+
+    @property
+    def last(self) -> Optional[Stage]:
+        return self.stages[-1] if self.stages[-1].last else None
+
+    def set_batch(self, x: Optional[torch.Tensor], labels: Optional[torch.Tensor]) -> None:
+        """x: this replica's [rows][Kp] bf16 inputs; labels: [rows] int32 (-1 = padding)."""
+        if self.first is not None:
+            if x is None:
+                raise ValueError("first stage needs inputs")
+            self.first.x_in.copy_(x)
+        if self.last is not None:
+            if labels is None:
+                raise ValueError("last stage needs labels")
+            self.last.labels.copy_(labels)
+
+    def step(self) -> None:
+        if self._graph is not None:
+            cur = torch.cuda.current_stream(self.device)
+            self._stream.wait_stream(cur)  # inputs written on the caller's stream
+            self._graph.replay(self._stream.cuda_stream)
+            cur.wait_stream(self._stream)
+        else:
+            self.executor.run_step()
+        self.steps_done += 1
+
+    def capture(self, warmup: int = 1) -> None:
+        """Capture one full training step into a HIP graph (local mode, GPU only).
+
+        Every buffer is allocated up front, so replay touches fixed pointers. The capture runs
+        on a private stream (the legacy null stream cannot be captured); replay is ordered
+        against the caller's stream with events. Capturing executes the step once for real."""
+        if self.mesh is not None or self.device.type != "cuda":
+            raise RuntimeError("graph capture is for the local GPU path")
+        cur = torch.cuda.current_stream(self.device)
+        self._stream = torch.cuda.Stream(self.device)
+        self._stream.wait_stream(cur)
+        g = native().GraphExec()
+        with torch.cuda.stream(self._stream):
+            for _ in range(warmup):
+                self.executor.run_step()
+            self._stream.synchronize()
+            g.begin_capture(self._stream.cuda_stream)
+            try:
+                self.executor.run_step()
+            finally:
+                g.end_capture()
+            g.replay(self._stream.cuda_stream)  # the captured step is not executed by capture
+        cur.wait_stream(self._stream)
+        self._graph = g
+        self.graph_nodes = g.num_nodes
+        torch.cuda.synchronize(self.device)
+
+    def release_graph(self) -> None:
+        self._graph = None
+
+    # -------------------------------------------------------------------------------------
+    def loss(self) -> Optional[float]:
+        """Mean loss of the last step (this replica's share scaled to the global batch)."""
+        if self.last is None:
+            return None
+        return self.last.loss_sum() / (self.micro_batch * self.num_micro)
+
+    def correct(self) -> Optional[int]:
+        return None if self.last is None else int(self.last.correct.item())
+
+    def load_weights(self, weights: Sequence[np.ndarray], biases: Sequence[np.ndarray]) -> None:
+        for st in self.stages:
+            st.params.load(weights[st.l0:st.l1], biases[st.l0:st.l1])
+
+    def local_weights(self) -> dict[int, tuple[np.ndarray, np.ndarray]]:
+        out = {}
+        for st in self.stages:
+            ws, bs = st.params.export()
+            for k, (w, b) in enumerate(zip(ws, bs)):
+                out[st.l0 + k] = (w, b)
+        return out
+
+    def flops_per_step(self) -> float:
+        """Model FLOPs of one global step across all ranks (padding excluded)."""
+        return float(self.spec.flops_per_sample_train()) * self.global_batch

@@ -1,7 +1,8 @@
-from .kernels import (KMAJ, MNMAJ, adam_update, colsum_partial, gemm, linear_dgrad, linear_fwd,
+from .kernels import (KMAJ, MNMAJ, adam_update, colsum_partial, dgrad_tiles, gemm, linear_dgrad, linear_fwd,
                       linear_wgrad, pack_bf16, pick_splits, pick_tiles, reduce_slabs, sgd_update,
-                      softmax_rows, softmax_xent, unpack_bf16)
+                      softmax_rows, softmax_xent, unpack_bf16, xent_blocks)
 
-__all__ = ["KMAJ", "MNMAJ", "adam_update", "colsum_partial", "gemm", "linear_dgrad",
+__all__ = ["KMAJ", "MNMAJ", "adam_update", "colsum_partial", "dgrad_tiles", "gemm", "linear_dgrad",
            "linear_fwd", "linear_wgrad", "pack_bf16", "pick_splits", "pick_tiles",
-           "reduce_slabs", "sgd_update", "softmax_rows", "softmax_xent", "unpack_bf16"]
+           "reduce_slabs", "sgd_update", "softmax_rows", "softmax_xent", "unpack_bf16",
+           "xent_blocks"]

@@ -77,13 +77,24 @@ def pick_splits(M: int, N: int, K_total: int, target_wg: int = 2 * NUM_CU) -> in
 
 
 def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=None, aux=None,
-         act=0, accumulate: bool = False, splits: int = 1, tiles: tuple[int, int] | None = None):
-    """C (+)= epilogue(A.B). See csrc/kernels/gemm.hpp for the layout/epilogue contract."""
+         act=0, accumulate: bool = False, splits: int = 1, tiles: tuple[int, int] | None = None,
+         colsum=None):
+    """C (+)= epilogue(A.B). See csrc/kernels/gemm.hpp for the layout/epilogue contract.
+
+    ``colsum`` (bf16 output only): fp32 [M/bm][>=N] receives per-row-tile column sums of the
+    stored output; requires explicit ``tiles`` so the caller knows the partial count."""
     act = _act(act)
     out_f32 = c.dtype == torch.float32
+    if colsum is not None:
+        if tiles is None or out_f32:
+            raise ValueError("colsum needs explicit tiles and a bf16 output")
+        if colsum.dtype != torch.float32 or colsum.dim() != 2 or colsum.stride(1) != 1 or \
+                colsum.shape[0] < M // tiles[0] or colsum.shape[1] < N:
+            raise ValueError(f"colsum must be fp32 [{M // tiles[0]}][>={N}] row-major")
     if not a.is_cuda:
         return ref.gemm(a, b, c, layout_a=layout_a, layout_b=layout_b, M=M, N=N, K=K, bias=bias,
-                        aux=aux, act=act, accumulate=accumulate, splits=splits)
+                        aux=aux, act=act, accumulate=accumulate, splits=splits, colsum=colsum,
+                        colsum_rows=tiles[0] if tiles else 0)
     _rows(a, "A", torch.bfloat16)
     _rows(b, "B", torch.bfloat16)
     if splits > 1:
@@ -113,7 +124,8 @@ def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=
     native().gemm_bf16(_p(a), a.stride(0), _p(b), b.stride(0), _p(c_rows), c_rows.stride(0),
                        split_stride, _p(bias), _p(aux), aux.stride(0) if aux is not None else 0,
                        M, N, K, act, int(accumulate), layout_a, layout_b, int(out_f32), bm, bn,
-                       splits, _stream(a))
+                       splits, _stream(a), _p(colsum),
+                       colsum.stride(0) if colsum is not None else 0)
     return c
 
 
@@ -126,14 +138,21 @@ def linear_fwd(x, w, bias, y, act="relu"):
     return gemm(x, w, y, layout_a=KMAJ, layout_b=KMAJ, M=M, N=N, K=K, bias=bias, act=act)
 
 
-def linear_dgrad(dz, w, dx, y_prev=None, act_prev="linear"):
-    """dx[M][Kp] = (dz[M][Np] . w[Np][Kp]) * act_prev'(y_prev) (mask fused in the epilogue)."""
+def dgrad_tiles(M: int, K: int) -> tuple[int, int]:
+    """Tile shape used by linear_dgrad for an [M][K] output (fixes the colsum partial count)."""
+    return pick_tiles(M, K, 1)
+
+
+def linear_dgrad(dz, w, dx, y_prev=None, act_prev="linear", colsum=None):
+    """dx[M][Kp] = (dz[M][Np] . w[Np][Kp]) * act_prev'(y_prev) (mask fused in the epilogue).
+    ``colsum`` [M/bm][Kp] receives the bias-gradient partials of the PREVIOUS layer (column
+    sums of dx), fused in the same epilogue."""
     M, N = dz.shape
     K = w.shape[1]
     if y_prev is None:
         act_prev = "linear"
     return gemm(dz, w, dx, layout_a=KMAJ, layout_b=MNMAJ, M=M, N=K, K=N, aux=y_prev,
-                act=act_prev)
+                act=act_prev, tiles=dgrad_tiles(M, K), colsum=colsum)
 
 
 def linear_wgrad(dz, x, slabs, splits=1, accumulate=False):
@@ -148,17 +167,35 @@ def linear_wgrad(dz, x, slabs, splits=1, accumulate=False):
 
 # ---- loss / reductions / optimizers ----------------------------------------------------------
 
-def softmax_xent(logits, labels, dz, n_cls, scale, loss_sum=None, correct=None):
+XENT_ROWS_PER_BLOCK = 64  # csrc/kernels/elementwise.hip XENT_ROWS_PER_BLOCK
+
+
+def xent_blocks(rows: int) -> int:
+    """Number of per-block loss partials softmax_xent writes for ``rows`` rows."""
+    return -(-rows // XENT_ROWS_PER_BLOCK)
+
+
+def softmax_xent(logits, labels, dz, n_cls, scale, loss_part=None, correct=None, colsum=None):
+    """dz = (softmax - onehot) * scale; per 64-row block: loss partial sum -> loss_part and
+    (optional) dz column sums -> colsum [xent_blocks(rows)][width] (bias-gradient partials)."""
     rows, width = dz.shape
+    if loss_part is not None and loss_part.numel() < xent_blocks(rows):
+        raise ValueError("loss_part needs xent_blocks(rows) entries")
+    if colsum is not None and (colsum.dtype != torch.float32 or colsum.dim() != 2 or
+                               colsum.shape[0] < xent_blocks(rows) or colsum.shape[1] < width
+                               or colsum.stride(1) != 1):
+        raise ValueError("colsum must be fp32 [xent_blocks(rows)][>=width]")
     if not logits.is_cuda:
-        return ref.softmax_xent(logits, labels, dz, n_cls, scale, loss_sum, correct)
+        return ref.softmax_xent(logits, labels, dz, n_cls, scale, loss_part, correct,
+                                XENT_ROWS_PER_BLOCK, colsum)
     _rows(logits, "logits", torch.float32)
     _rows(dz, "dz", torch.bfloat16)
     if labels.dtype != torch.int32 or labels.numel() < rows or logits.shape[0] < rows:
         raise ValueError("labels must be int32 with one entry per row")
     native().softmax_xent(_p(logits), logits.stride(0), _p(labels), _p(dz), dz.stride(0), rows,
-                          n_cls, width, float(scale), _p(loss_sum), _p(correct),
-                          _stream(logits))
+                          n_cls, width, float(scale), _p(loss_part), _p(correct),
+                          _stream(logits), _p(colsum),
+                          colsum.stride(0) if colsum is not None else 0)
 
 
 def softmax_rows(logits, out, n_cls, labels=None, pred=None, correct=None):

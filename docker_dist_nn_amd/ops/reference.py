@@ -34,8 +34,13 @@ def _logical(a, b, layout_a, layout_b, M, N, Ktot):
     return A.float(), B.float()
 
 
+def _colsum_blocks(vals, out, rows_per):
+    nb = vals.shape[0] // rows_per
+    out[:nb, :vals.shape[1]] = vals[:nb * rows_per].reshape(nb, rows_per, -1).sum(1)
+
+
 def gemm(a, b, c, *, layout_a, layout_b, M, N, K, bias=None, aux=None, act=0, accumulate=False,
-         splits=1):
+         splits=1, colsum=None, colsum_rows=0):
     A, B = _logical(a, b, layout_a, layout_b, M, N, K * splits)
     out_f32 = c.dtype == torch.float32
     for s in range(splits):
@@ -46,6 +51,8 @@ def gemm(a, b, c, *, layout_a, layout_b, M, N, K, bias=None, aux=None, act=0, ac
             dst = c[s] if c.dim() == 3 else c
             if accumulate:
                 acc = acc + dst[:M, :N]
+            else:
+                acc = act_fwd(acc, act)
             dst[:M, :N] = acc
         else:
             if aux is not None:
@@ -53,10 +60,13 @@ def gemm(a, b, c, *, layout_a, layout_b, M, N, K, bias=None, aux=None, act=0, ac
             else:
                 acc = act_fwd(acc, act)
             c[:M, :N] = acc.to(c.dtype)
+            if colsum is not None:
+                _colsum_blocks(c[:M, :N].float(), colsum, colsum_rows)
     return c
 
 
-def softmax_xent(logits, labels, dz, n_cls, scale, loss_sum=None, correct=None):
+def softmax_xent(logits, labels, dz, n_cls, scale, loss_part=None, correct=None,
+                 rows_per_block=64, colsum=None):
     rows, width = dz.shape
     lg = logits[:rows, :n_cls].float()
     lab = labels[:rows].long()
@@ -69,13 +79,21 @@ def softmax_xent(logits, labels, dz, n_cls, scale, loss_sum=None, correct=None):
     g[~valid] = 0.0
     dz.zero_()
     dz[:, :n_cls] = g.to(dz.dtype)
-    if loss_sum is not None:
+    if loss_part is not None:
         logp = torch.log_softmax(lg, dim=1)
-        nll = -logp[torch.arange(rows), safe]
-        loss_sum += nll[valid].sum().to(loss_sum.dtype)
+        nll = torch.where(valid, -logp[torch.arange(rows), safe], torch.zeros_like(lg[:, 0]))
+        nb = -(-rows // rows_per_block)
+        pad = torch.zeros(nb * rows_per_block)
+        pad[:rows] = nll
+        loss_part[:nb] = pad.view(nb, rows_per_block).sum(1).to(loss_part.dtype)
     if correct is not None:
         pred = torch.argmax(lg, dim=1)
         correct += ((pred == lab) & valid).sum().to(correct.dtype)
+    if colsum is not None:
+        nb = -(-rows // rows_per_block)
+        pad = torch.zeros(nb * rows_per_block, width)
+        pad[:rows] = dz.float()
+        colsum[:nb, :width] = pad.view(nb, rows_per_block, width).sum(1)
 
 
 def softmax_rows(logits, out, n_cls, labels=None, pred=None, correct=None):

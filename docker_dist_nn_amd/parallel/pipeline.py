@@ -1,0 +1,151 @@
+"""Executes pipeline schedules (csrc/runtime/schedule.cpp) over stages and transports.
+
+For a rank that owns one stage, the schedule's op list runs in order:
+
+  F(j): recv activation j -> stage.forward(j) -> send activation j
+  B(j): recv gradient  j -> stage.backward(j) -> send gradient j
+  W(j): stage.wgrad(j)            (W(-1): one batch-contraction GEMM per layer over all rows)
+  O   : finalize grads -> data-parallel all-reduce -> fused optimizer
+
+When the step ends with a batched W, the weight gradients are produced layer by layer from the
+last layer backwards and each layer's gradient bucket is all-reduced asynchronously (RCCL
+stream) while the next layer's wgrad GEMM runs -- the DP traffic overlaps compute.
+
+For several stages in ONE process (loopback), ops of all stages are interleaved in a
+dependency-respecting order (F(s,j) after F(s-1,j); B(s,j) after B(s+1,j)), which both runs
+S-stage pipelines on one device and checks that the schedules are deadlock-free.
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional, Sequence
+
+import torch.distributed as dist
+
+from ..utils.native import native
+
+
+def schedule_ops(kind: str, num_stages: int, num_micro: int, stage: int):
+    n = native()
+    out = []
+    for op in n.make_schedule(kind, num_stages, num_micro, stage):
+        out.append(({n.OpKind.FWD: "F", n.OpKind.BWD: "B", n.OpKind.WGRAD: "W",
+                     n.OpKind.OPT: "O"}[op.kind], op.micro))
+    return out
+
+
+class GradSync:
+    """Bucketed, asynchronous gradient all-reduce over the data-parallel group."""
+
+    def __init__(self, group, world: int):
+        self.group = group
+        self.world = world
+        self._works = []
+
+    def launch(self, flat_grad, start: int, end: int) -> None:
+        if self.world <= 1:
+            return
+        self._works.append(dist.all_reduce(flat_grad[start:end], group=self.group,
+                                           async_op=True))
+
+    def wait(self) -> None:
+        for w in self._works:
+            w.wait()
+        self._works.clear()
+
+
+class PipelineExecutor:
+    def __init__(self, stages: Sequence, pipe, kind: str, num_stages: int,
+                 stage_ids: Sequence[int], grad_sync: Optional[GradSync] = None,
+                 lr_fn: Optional[Callable[[], float]] = None):
+        self.stages = list(stages)
+        self.pipe = pipe
+        self.kind = kind
+        self.S = num_stages
+        self.stage_ids = list(stage_ids)
+        self.grad_sync = grad_sync
+        self.lr_fn = lr_fn
+        self.ops = [schedule_ops(kind, num_stages, st.nm, sid)
+                    for st, sid in zip(self.stages, self.stage_ids)]
+        self.hooks: dict[str, list[Callable]] = {"before_op": [], "after_op": []}
+
+    # ---------------------------------------------------------------------------------------
+    def _run_op(self, st, op, j, next_op=None):
+        for h in self.hooks["before_op"]:
+            h(st, op, j)
+        if op == "F":
+            self.pipe.recv_fwd(st, j)
+            st.forward(j)
+            self.pipe.send_fwd(st, j)
+        elif op == "B":
+            self.pipe.recv_bwd(st, j)
+            st.backward(j)
+            self.pipe.send_bwd(st, j)
+        elif op == "W":
+            if j < 0 and next_op == "O":
+                self._wgrad_finalize_overlapped(st)
+            else:
+                st.wgrad(j)
+        elif op == "O":
+            if not getattr(st, "_finalized", False):
+                st.finalize_grads()
+                if self.grad_sync is not None:
+                    self.grad_sync.launch(st.params.grad, 0, st.params.numel)
+            if self.grad_sync is not None:
+                self.grad_sync.wait()
+            st._finalized = False
+            st.optimizer_step(self.lr_fn() if self.lr_fn else None)
+        for h in self.hooks["after_op"]:
+            h(st, op, j)
+
+    def _wgrad_finalize_overlapped(self, st):
+        """Batched W: per layer (last first) wgrad -> reduce -> async bucket all-reduce."""
+        for i in range(len(st.geoms) - 1, -1, -1):
+            st.wgrad_layer(i)
+            st.finalize_grads([i])
+            if self.grad_sync is not None:
+                a, b = st.params.layer_grad_range(i)
+                self.grad_sync.launch(st.params.grad, a, b)
+        st._finalized = True
+
+    def run_step(self) -> None:
+        self.pipe.begin_step()
+        for st in self.stages:
+            st.begin_step()
+        if len(self.stages) == 1:
+            st, ops = self.stages[0], self.ops[0]
+            for k, (op, j) in enumerate(ops):
+                nxt = ops[k + 1][0] if k + 1 < len(ops) else None
+                self._run_op(st, op, j, nxt)
+        else:
+            self._run_interleaved()
+        self.pipe.end_step()
+
+    def _run_interleaved(self):
+        S = len(self.stages)
+        pc = [0] * S
+        fdone = [set() for _ in range(S)]
+        bdone = [set() for _ in range(S)]
+        remaining = sum(len(o) for o in self.ops)
+        while remaining:
+            progress = False
+            for s in range(S):
+                ops = self.ops[s]
+                while pc[s] < len(ops):
+                    op, j = ops[pc[s]]
+                    if op == "F" and s > 0 and j not in fdone[s - 1]:
+                        break
+                    if op == "B" and s < S - 1 and j not in bdone[s + 1]:
+                        break
+                    nxt = ops[pc[s] + 1][0] if pc[s] + 1 < len(ops) else None
+                    self._run_op(self.stages[s], op, j, nxt)
+                    if op == "F":
+                        fdone[s].add(j)
+                    elif op == "B":
+                        bdone[s].add(j)
+                    pc[s] += 1
+                    remaining -= 1
+                    progress = True
+                    if op in ("F", "B"):
+                        break  # round-robin: give the neighbours a chance
+            if not progress:
+                raise RuntimeError("pipeline schedule deadlocked (inconsistent op lists)")

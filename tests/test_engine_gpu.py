@@ -1,0 +1,78 @@
+"""End-to-end training on the GPU through the native kernels: parity with the CPU reference
+path, S-stage loopback pipelines == 1 stage, HIP-graph replay == eager execution."""
+import numpy as np
+import pytest
+import torch
+
+from docker_dist_nn_amd import MLPSpec
+from docker_dist_nn_amd.data import synthetic_mnist
+from docker_dist_nn_amd.engine import OptimConfig, Trainer
+
+pytestmark = pytest.mark.gpu
+
+
+def _batch(n, dev, seed=1):
+    x, y = synthetic_mnist(n, seed=seed)
+    xt = torch.zeros(n, 832, dtype=torch.bfloat16)
+    xt[:, :784] = torch.from_numpy(x).to(torch.bfloat16)
+    return xt.to(dev), torch.from_numpy(y).to(dev)
+
+
+def _run(spec, dev, steps, **kw):
+    tr = Trainer(spec, device=dev, optim=OptimConfig(lr=0.1), **kw)
+    x, y = _batch(kw["micro_batch"] * kw.get("num_micro", 1), dev)
+    losses = []
+    for _ in range(steps):
+        tr.set_batch(x, y)
+        tr.step()
+        losses.append(tr.loss())
+    return tr, losses
+
+
+def test_gpu_training_matches_cpu_reference(dev):
+    spec = MLPSpec.parse("784-128-64-10")
+    _, lg = _run(spec, dev, 8, micro_batch=512, num_micro=2)
+    _, lc = _run(spec, torch.device("cpu"), 8, micro_batch=512, num_micro=2)
+    assert lg[-1] < lg[0]
+    np.testing.assert_allclose(lg, lc, rtol=2e-2, atol=2e-3)
+
+
+@pytest.mark.parametrize("pp,sched", [(2, "1f1b"), (4, "gpipe"), (4, "zb"), (3, "1f1b_w")])
+def test_gpu_pipeline_equals_single_stage(dev, pp, sched):
+    spec = MLPSpec.parse("784-512-256-128-10")
+    t1, l1 = _run(spec, dev, 4, micro_batch=256, num_micro=4)
+    tp, lp = _run(spec, dev, 4, micro_batch=256, num_micro=4, pp=pp, schedule=sched)
+    np.testing.assert_allclose(lp, l1, rtol=1e-3, atol=1e-4)
+    w1, wp = t1.local_weights(), tp.local_weights()
+    for k in w1:
+        np.testing.assert_allclose(wp[k][0], w1[k][0], rtol=1e-3, atol=1e-5)
+
+
+def test_gpu_graph_replay_equals_eager(dev):
+    spec = MLPSpec.parse("784-512-256-128-10")
+    x, y = _batch(1024, dev)
+    ta = Trainer(spec, device=dev, micro_batch=1024, optim=OptimConfig(lr=0.1))
+    tb = Trainer(spec, device=dev, micro_batch=1024, optim=OptimConfig(lr=0.1))
+    ta.set_batch(x, y)
+    tb.set_batch(x, y)
+    tb.capture(warmup=0)  # capture executes one real step
+    ta.step()
+    la, lb = [ta.loss()], [tb.loss()]
+    for _ in range(5):
+        ta.set_batch(x, y)
+        ta.step()
+        tb.set_batch(x, y)
+        tb.step()
+        la.append(ta.loss())
+        lb.append(tb.loss())
+    assert la == lb
+    wa, wb = ta.local_weights(), tb.local_weights()
+    for k in wa:
+        assert np.array_equal(wa[k][0], wb[k][0])
+
+
+def test_gpu_bitwise_deterministic(dev):
+    spec = MLPSpec.parse("784-512-256-128-10")
+    _, la = _run(spec, dev, 3, micro_batch=2048)
+    _, lb = _run(spec, dev, 3, micro_batch=2048)
+    assert la == lb

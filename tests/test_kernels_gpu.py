@@ -141,14 +141,15 @@ def test_softmax_xent(dev):
     labels = torch.randint(0, ncls, (rows,), generator=gen, dtype=torch.int32)
     labels[::7] = -1  # padding rows
     dz = torch.empty(rows, width, dtype=torch.bfloat16, device=dev)
-    loss = torch.zeros(1, device=dev)
+    loss = torch.zeros(ops.xent_blocks(rows), device=dev)
     corr = torch.zeros(1, dtype=torch.int32, device=dev)
     ops.softmax_xent(logits.to(dev), labels.to(dev), dz, ncls, 1.0 / rows, loss, corr)
     dz_r = torch.empty(rows, width, dtype=torch.bfloat16)
-    loss_r = torch.zeros(1)
+    loss_r = torch.zeros(ops.xent_blocks(rows))
     corr_r = torch.zeros(1, dtype=torch.int32)
     from docker_dist_nn_amd.ops import reference as ref
     ref.softmax_xent(logits, labels, dz_r, ncls, 1.0 / rows, loss_r, corr_r)
+    assert loss.shape == loss_r.shape
     torch.testing.assert_close(dz.float().cpu(), dz_r.float(), rtol=1e-2, atol=1e-4)
     torch.testing.assert_close(loss.cpu(), loss_r, rtol=1e-5, atol=1e-3)
     assert int(corr.item()) == int(corr_r.item())
@@ -220,3 +221,41 @@ def test_pack_unpack(dev):
     back = torch.empty(100, 784, device=dev)
     ops.unpack_bf16(out, back)
     assert torch.equal(back, x.to(torch.bfloat16).float())
+
+
+@pytest.mark.parametrize("n_src", [1, 3, 8, 17, 128])
+def test_reduce_slabs_many_sources(dev, n_src):
+    gen = torch.Generator().manual_seed(n_src)
+    n = 4096 + 64
+    src = torch.randn(n_src, n, generator=gen).to(dev)
+    out = torch.ones(n, device=dev)
+    ops.reduce_slabs(src, n_src, n, n, out, scale=0.25, accumulate=True)
+    torch.testing.assert_close(out, 1 + 0.25 * src.sum(0), rtol=1e-5, atol=1e-5)
+
+
+def test_dgrad_colsum_partials(dev):
+    gen = torch.Generator().manual_seed(21)
+    M, N, K = 512, 128, 832
+    dz = torch.randn(M, N, generator=gen).to(torch.bfloat16).to(dev)
+    w = torch.randn(N, K, generator=gen).to(torch.bfloat16).to(dev)
+    y_prev = torch.randn(M, K, generator=gen).clamp_min(0).to(torch.bfloat16).to(dev)
+    dx = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
+    bm = ops.dgrad_tiles(M, K)[0]
+    part = torch.full((M // bm, K), 99.0, device=dev)
+    ops.linear_dgrad(dz, w, dx, y_prev=y_prev, act_prev="relu", colsum=part)
+    ref = dx.float().view(M // bm, bm, K).sum(1)
+    torch.testing.assert_close(part, ref, rtol=1e-5, atol=1e-4)
+
+
+def test_xent_colsum_partials(dev):
+    gen = torch.Generator().manual_seed(22)
+    rows, width, ncls = 1000, 64, 10
+    logits = (torch.randn(rows, width, generator=gen) * 2).to(dev)
+    labels = torch.randint(0, ncls, (rows,), generator=gen, dtype=torch.int32).to(dev)
+    dz = torch.empty(rows, width, dtype=torch.bfloat16, device=dev)
+    nb = ops.xent_blocks(rows)
+    part = torch.full((nb, width), 5.0, device=dev)
+    ops.softmax_xent(logits, labels, dz, ncls, 1.0, None, None, colsum=part)
+    pad = torch.zeros(nb * 64, width, device=dev)
+    pad[:rows] = dz.float()
+    torch.testing.assert_close(part, pad.view(nb, 64, width).sum(1), rtol=1e-5, atol=1e-5)
