@@ -53,6 +53,8 @@ def parse_args(argv=None):
     ap.add_argument("--micro", type=int, default=0, help="micro-batch rows (0 = planner)")
     ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--graph-copies", type=int, default=2,
+                    help="alternate between this many instantiations of the step graph")
     ap.add_argument("--seed", type=int, default=0)
     return ap.parse_args(argv)
 
@@ -101,13 +103,13 @@ def main(argv=None):
     def one_step():
         nonlocal step_i
         xb, yb = data.batch(step_i)
-        tr.set_batch(xb if tr.first else None, yb if tr.last else None)
+        tr.set_batch(xb if tr.first else None, yb if tr.last else None, zero_copy=True)
         tr.step()
         step_i += 1
 
     if use_graph:
         tr.set_batch(*data.batch(0))
-        tr.capture()
+        tr.capture(copies=a.graph_copies)
     for _ in range(a.warmup):
         one_step()
 
@@ -155,6 +157,7 @@ def main(argv=None):
             "schedule": a.schedule if plan.pp > 1 else "none",
             "optimizer": "sgd",
             "hip_graph": use_graph,
+            "graph_copies": a.graph_copies if use_graph else 0,
         },
         "model_tflops": round(spec.flops_per_sample_train() * value / 1e12, 1),
         "last_loss": None if loss is None else round(loss, 5),

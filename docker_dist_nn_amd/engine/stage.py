@@ -97,7 +97,7 @@ class StageParams:
 
     def layer_grad_range(self, i) -> tuple[int, int]:
         """Flat [start, end) of layer i's W and b gradients (a DP all-reduce bucket)."""
-        end = self.b_off[i + 1] if i + 1 < len(self.geoms) else self.numel
+        end = self.w_off[i + 1] if i + 1 < len(self.geoms) else self.numel
         return self.w_off[i], end
 
     # weights in/out -----------------------------------------------------------------------
@@ -182,7 +182,8 @@ class Stage:
         R, dev = self.rows, self.device
         bf, f32 = torch.bfloat16, torch.float32
         g0 = self.geoms[0]
-        self.x_in = torch.zeros(R, g0.kp, dtype=bf, device=dev)
+        self.x_buf = torch.zeros(R, g0.kp, dtype=bf, device=dev)
+        self.x_in = self.x_buf  # may be re-pointed at a resident dataset slice (zero-copy)
         self.acts: list[torch.Tensor] = []  # output of local layer i
         for i, g in enumerate(self.geoms):
             is_logits = self.last and i == len(self.geoms) - 1

@@ -34,7 +34,7 @@ class LoopbackPipe:
         for a, b in zip(stages, stages[1:]):
             if a.output.shape != b.x_in.shape or a.device != b.device:
                 raise ValueError("loopback stages must share device and boundary width")
-            b.x_in = a.output           # activations: producer writes the consumer's input
+            b.x_in = b.x_buf = a.output  # activations: producer writes the consumer's input
             a.dz[-1] = b.dx_send        # gradients: consumer writes the producer's dZ
 
     def begin_step(self):

@@ -1,13 +1,14 @@
+# One GPU-box session: tests, smoke, bench variants, rocprofv3 kernel stats.
 set -o pipefail
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out; mkdir -p $O
 cd $R
-timeout -k 10 600 python -m pytest tests/test_engine_gpu.py tests/test_kernels_gpu.py -q -m gpu > $O/tests.log 2>&1; rc=$?; echo "rc=$rc" >> $O/tests.log
+timeout -k 10 600 python -m pytest tests/ -q -m gpu > $O/tests.log 2>&1; rc=$?; echo "rc=$rc" >> $O/tests.log
 [ $rc -le 1 ] || exit $rc
 timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
-for b in 8192 16384 32768 65536 131072; do
-  timeout -k 10 180 python bench.py --steps 30 --warmup 5 --batch $b >> $O/bench_sweep.log 2>&1 || exit $?
+: > $O/bench_sweep.log
+for args in "--graph-copies 1" "--graph-copies 2" "--no-graph" "--batch 32768" "--batch 131072"; do
+  timeout -k 10 180 python bench.py --steps 30 --warmup 5 $args >> $O/bench_sweep.log 2>&1 || exit $?
 done
-timeout -k 10 180 python bench.py --steps 30 --warmup 5 --no-graph >> $O/bench_sweep.log 2>&1 || exit $?
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python $R/bench.py --steps 20 --warmup 3 > $O/prof.log 2>&1 || exit $?
 echo done >> $O/tests.log

@@ -134,3 +134,17 @@ def test_classification_report_matches_weighted_definition():
     # class precisions 0.5, 2/3, 1 ; recalls 0.5, 1, 2/3 ; weights 2/7, 2/7, 3/7
     prec = (2 * 0.5 + 2 * 2 / 3 + 3 * 1.0) / 7
     assert abs(r["precision"] - prec) < 1e-12
+
+
+def test_dp_buckets_partition_flat_gradient():
+    from docker_dist_nn_amd.engine.stage import StageParams
+    from docker_dist_nn_amd.models.mlp import LayerGeom
+    spec = MLPSpec.parse("784-512-256-10")
+    geoms = [LayerGeom(i, l) for i, l in enumerate(spec.layers)]
+    p = StageParams(geoms, torch.device("cpu"))
+    covered = np.zeros(p.numel, np.int32)
+    for i in range(len(geoms)):
+        a, b = p.layer_grad_range(i)
+        covered[a:b] += 1
+        assert a <= p.w_off[i] and p.b_off[i] + geoms[i].np_ <= b
+    assert (covered == 1).all()
