@@ -52,7 +52,8 @@ def parse_args(argv=None):
     ap.add_argument("--schedule", default="1f1b")
     ap.add_argument("--micro", type=int, default=0, help="micro-batch rows (0 = planner)")
     ap.add_argument("--lr", type=float, default=0.05)
-    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the step as a HIP graph (1 GPU); eager is faster at large batch")
     ap.add_argument("--graph-copies", type=int, default=2,
                     help="alternate between this many instantiations of the step graph")
     ap.add_argument("--seed", type=int, default=0)
@@ -97,7 +98,7 @@ def main(argv=None):
     x, y = synthetic_mnist(max(60000, 2 * rows), seed=a.seed + 1000 * replica)
     data = DeviceDataset(x, y, rows, dev, kp=tr.stages[0].x_in.shape[1] if tr.first else None)
 
-    use_graph = world == 1 and not a.no_graph
+    use_graph = world == 1 and a.graph
     step_i = 0
 
     def one_step():

@@ -6,7 +6,7 @@ timeout -k 10 600 python -m pytest tests/ -q -m gpu > $O/tests.log 2>&1; rc=$?; 
 [ $rc -le 1 ] || exit $rc
 timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
 : > $O/bench_sweep.log
-for args in "--graph-copies 1" "--graph-copies 2" "--no-graph" "--batch 32768" "--batch 131072"; do
+for args in "" "--graph" "--batch 32768" "--batch 131072"; do
   timeout -k 10 180 python bench.py --steps 30 --warmup 5 $args >> $O/bench_sweep.log 2>&1 || exit $?
 done
 cd /tmp && export TMPDIR=/tmp

@@ -1,0 +1,154 @@
+"""End-to-end compatibility on CPU: run_grpc_fcnn.py brings up the stages (in-process or one
+gloo rank per stage), run_grpc_inference.py talks the reference gRPC protocol to it, and the
+answers match the fp64 reference forward. Also covers the error paths (INVALID_ARGUMENT for a
+width mismatch, a failing middle stage surfacing as "Failed to forward request to ...")."""
+import json
+import os
+import socket
+import subprocess
+import sys
+import time
+
+import grpc
+import numpy as np
+import pytest
+
+from docker_dist_nn_amd.config import load_model_config
+from docker_dist_nn_amd.cpu_ref import model_forward
+from docker_dist_nn_amd.data import write_examples
+from docker_dist_nn_amd.serve.ingress import LayerClient
+from docker_dist_nn_amd.weights_io import export_model_json
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture(scope="module")
+def model_files(tmp_path_factory):
+    d = tmp_path_factory.mktemp("m")
+    rng = np.random.default_rng(0)
+    dims = [784, 64, 32, 10]
+    ws = [rng.standard_normal((dims[i + 1], dims[i])) * (2.0 / np.sqrt(dims[i])) for i in range(3)]
+    bs = [rng.standard_normal(dims[i + 1]) * 0.1 for i in range(3)]
+    cfg = d / "model.json"
+    export_model_json(str(cfg), ws, bs, ["relu", "relu", "softmax"], layer_distribution=[1, 1, 1])
+    x = rng.random((300, 784))
+    y = model_forward(load_model_config(str(cfg)).layers, x).argmax(1)  # fp64 labels
+    inp = d / "inputs.json"
+    write_examples(str(inp), x, y)
+    return cfg, inp, x, y
+
+
+def _start(cfg, inp, port, mode, tmp, extra_env=None):
+    env = dict(os.environ, PYTHONPATH=ROOT, **(extra_env or {}))
+    p = subprocess.Popen([sys.executable, os.path.join(ROOT, "src", "run_grpc_fcnn.py"),
+                          "--config", str(cfg), "--inputs", str(inp), "--port", str(port),
+                          "--mode", mode, "--device", "cpu", "--run-for", "120",
+                          "--cache-dir", str(tmp / f"cache_{mode}")],
+                         env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    t0 = time.time()
+    while time.time() - t0 < 90:
+        try:
+            socket.create_connection(("127.0.0.1", port), timeout=0.5).close()
+            return p
+        except OSError:
+            if p.poll() is not None:
+                raise RuntimeError(p.stdout.read())
+            time.sleep(0.3)
+    p.terminate()
+    raise RuntimeError("server did not come up")
+
+
+def _stop(p):
+    p.terminate()
+    try:
+        out, _ = p.communicate(timeout=30)
+    except subprocess.TimeoutExpired:
+        p.kill()
+        out, _ = p.communicate()
+    return out
+
+
+def _client(inp, port, *args):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "src", "run_grpc_inference.py"),
+                        "--inputs", str(inp), "--port", str(port), *args],
+                       capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, PYTHONPATH=ROOT))
+    return r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("mode", ["local", "ranks"])
+def test_fcnn_chain_serves_reference_protocol(model_files, tmp_path, mode):
+    cfg, inp, x, y = model_files
+    port = _port()
+    p = _start(cfg, inp, port, mode, tmp_path)
+    try:
+        log = _client(inp, port, "--batch-size", "128")
+        assert "Batch 3/3 completed" in log
+        assert "Inference process completed." in log
+        n = int(log.split("Correct predictions: ")[1].split(" ")[0])
+        assert n >= 290, log  # bf16 vs fp64 may flip a near-tie
+        c = LayerClient(f"127.0.0.1:{port}", timeout=30)
+        out = c.process(x[:5])
+        ref = model_forward(load_model_config(str(cfg)).layers, x[:5])
+        np.testing.assert_allclose(out, ref, atol=2e-2)
+        # width mismatch -> INVALID_ARGUMENT with the reference's dimension message
+        with pytest.raises(grpc.RpcError) as ei:
+            c.process(np.ones((2, 5)))
+        assert ei.value.code() == grpc.StatusCode.INVALID_ARGUMENT
+        assert "expected input dim 784, got 5" in ei.value.details()
+        # single-index mode counts one example (reference miscounted)
+        log1 = _client(inp, port, "7")
+        assert "out of 1" in log1
+        c.close()
+    finally:
+        out = _stop(p)
+    assert "Distributed FCNN setup completed in" in out
+    assert "Shutdown complete." in out
+
+
+def test_failing_middle_stage_is_reported(model_files, tmp_path):
+    cfg, inp, x, y = model_files
+    port = _port()
+    p = _start(cfg, inp, port, "ranks", tmp_path, {"DNN_FAULT_STAGE": "1"})
+    try:
+        c = LayerClient(f"127.0.0.1:{port}", timeout=30)
+        with pytest.raises(grpc.RpcError) as ei:
+            c.process(x[:4])
+        assert ei.value.code() == grpc.StatusCode.INTERNAL
+        assert "Failed to forward request to layer_container_1" in ei.value.details()
+        c.close()
+    finally:
+        _stop(p)
+
+
+def test_reference_mapping_errors_are_logged(model_files, tmp_path):
+    cfg, inp, *_ = model_files
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "src", "run_grpc_fcnn.py"),
+                        "--config", str(cfg), "--inputs", str(inp), "--no-serve",
+                        "--layer-distribution", "[1,1]", "--cache-dir", str(tmp_path / "c")],
+                       capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, PYTHONPATH=ROOT))
+    assert "Sum of layer_distribution does not match" in r.stderr + r.stdout
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "src", "run_grpc_fcnn.py"),
+                        "--config", str(tmp_path / "missing.json"), "--inputs", str(inp)],
+                       capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, PYTHONPATH=ROOT))
+    assert "Configuration file not found" in r.stderr + r.stdout
+    # stage files are written in the reference's per-stage format
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "src", "run_grpc_fcnn.py"),
+                        "--config", str(cfg), "--inputs", str(inp), "--no-serve",
+                        "--cache-dir", str(tmp_path / "c2")],
+                       capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, PYTHONPATH=ROOT))
+    f = tmp_path / "c2" / "layer_container_1_neurons_config.json"
+    doc = json.load(open(f))
+    assert list(doc) == ["layer_1"] and len(doc["layer_1"]) == 32
+    assert len(doc["layer_1"][0]["weights"]) == 64
