@@ -73,6 +73,30 @@ PYBIND11_MODULE(_native, m) {
       py::arg("layout_b"), py::arg("out_f32"), py::arg("bm"), py::arg("bn"), py::arg("splits"),
       py::arg("stream"), py::arg("colsum") = 0, py::arg("ld_colsum") = 0);
 
+  m.def(
+      "gemm_bf16_streamk",
+      [](uintptr_t a, long lda, uintptr_t b, long ldb, uintptr_t c, long ldc, int M, int N, int K,
+         int accumulate, int layout_a, int layout_b, int bm, int bn, int nwg, uintptr_t part,
+         uintptr_t stream) {
+        GemmParams p{};
+        p.A = P<const uint16_t>(a);
+        p.lda = lda;
+        p.B = P<const uint16_t>(b);
+        p.ldb = ldb;
+        p.C = P<void>(c);
+        p.ldc = ldc;
+        p.M = M;
+        p.N = N;
+        p.K = K;
+        p.accumulate = accumulate;
+        check(dnn::gemm_bf16_streamk(p, layout_a, layout_b, bm, bn, nwg, P<float>(part),
+                                     S(stream)),
+              "gemm_bf16");
+      },
+      py::arg("a"), py::arg("lda"), py::arg("b"), py::arg("ldb"), py::arg("c"), py::arg("ldc"),
+      py::arg("M"), py::arg("N"), py::arg("K"), py::arg("accumulate"), py::arg("layout_a"),
+      py::arg("layout_b"), py::arg("bm"), py::arg("bn"), py::arg("nwg"), py::arg("part"),
+      py::arg("stream"));
   m.def("softmax_xent",
         [](uintptr_t logits, long ld_logits, uintptr_t labels, uintptr_t dz, long ld_dz, int rows,
            int n_cls, int width, float scale, uintptr_t loss_part, uintptr_t correct,

@@ -100,33 +100,30 @@ struct cmax {
   static constexpr int v = A > B ? A : B;
 };
 
-template <int BM, int BN, int LA, int LB, bool OUT_F32>
-__global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmParams p, int tiles_n, int tiles_m,
-                                                        int nwg) {
-  constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
-  constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
-  constexpr int CS_LD = BN + 4;  // fp32 epilogue staging row stride (floats)
-  constexpr int SMEM = cmax<2 * STAGE, BM * CS_LD * 4>::v;
-  __shared__ __attribute__((aligned(16))) char smem[SMEM];
-  char LDS_AS* lds = (char LDS_AS*)smem;
-
-  // XCD-aware bijective remap: hardware deals block b to XCD group b%8; give each group a
-  // contiguous run of logical tiles (tile_n fastest -> neighbours share the A panel in L2).
-  const int bid = blockIdx.x;
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int tn = wgid % tiles_n;
-  const int tm = (wgid / tiles_n) % tiles_m;
-  const int split = wgid / (tiles_n * tiles_m);
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+}
 
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+template <int BM, int BN>
+struct TileCfg {
+  static constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
+  static constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
+  static constexpr int CS_LD = BN + 4;  // fp32 epilogue staging row stride (floats)
+  static constexpr int SMEM = cmax<2 * STAGE, BM * CS_LD * 4>::v;
+};
+
+// acc (+)= A[m0:m0+BM, k] . B[k, n0:n0+BN] over k-steps [kbase, kbase + 64*nk): LDS-DMA
+// double buffering, one barrier per 64-deep k-step. acc is zeroed first. Ends with every
+// wave past a barrier, so the caller may reuse the LDS.
+template <int BM, int BN, int LA, int LB>
+__device__ __forceinline__ void mma_tile(const GemmParams& p, int m0, int n0, int kbase, int nk,
+                                         char LDS_AS* lds,
+                                         f32x4_t (&acc)[TileCfg<BM, BN>::FM][TileCfg<BM, BN>::FN],
+                                         int wave, int lane) {
+  using C = TileCfg<BM, BN>;
+  constexpr int FM = C::FM, FN = C::FN, A_BYTES = C::A_BYTES, STAGE = C::STAGE;
   const int wm = wave >> 1, wn = wave & 1;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int kbase = split * p.K;
-  const int nk = p.K >> 6;
-
-  f32x4_t acc[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -163,19 +160,55 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmParams p, int tiles_
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
+}
+
+// 16x16 accumulator fragments -> fp32 [BM][CS_LD] LDS tile (C/D map: col = lane&15,
+// row = 4*(lane>>4) + r).
+template <int BM, int BN>
+__device__ __forceinline__ void acc_to_lds(
+    const f32x4_t (&acc)[TileCfg<BM, BN>::FM][TileCfg<BM, BN>::FN], float LDS_AS* cs, int wave,
+    int lane) {
+  using C = TileCfg<BM, BN>;
+  const int wm = wave >> 1, wn = wave & 1;
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * C::WM + i * 16 + (lane >> 4) * 4 + r;
+        const int col = wn * C::WN + j * 16 + (lane & 15);
+        cs[row * C::CS_LD + col] = acc[i][j][r];
+      }
+}
+
+template <int BM, int BN, int LA, int LB, bool OUT_F32>
+__global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmParams p, int tiles_n, int tiles_m,
+                                                        int nwg) {
+  using TC = TileCfg<BM, BN>;
+  constexpr int FM = TC::FM, FN = TC::FN, CS_LD = TC::CS_LD;
+  __shared__ __attribute__((aligned(16))) char smem[TC::SMEM];
+  char LDS_AS* lds = (char LDS_AS*)smem;
+
+  // XCD-aware bijective remap: hardware deals block b to XCD group b%8; give each group a
+  // contiguous run of logical tiles (tile_n fastest -> neighbours share the A panel in L2).
+  const int wgid = xcd_remap(blockIdx.x, nwg);
+  const int tn = wgid % tiles_n;
+  const int tm = (wgid / tiles_n) % tiles_m;
+  const int split = wgid / (tiles_n * tiles_m);
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kbase = split * p.K;
+  const int nk = p.K >> 6;
+
+  f32x4_t acc[FM][FN];
+  mma_tile<BM, BN, LA, LB>(p, m0, n0, kbase, nk, lds, acc, wave, lane);
 
   // ---- epilogue: accumulators -> LDS (fp32) -> 16-B row chunks to global --------------------
   float LDS_AS* cs = (float LDS_AS*)lds;
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wm * WM + i * 16 + (lane >> 4) * 4 + r;
-        const int col = wn * WN + j * 16 + (lane & 15);
-        cs[row * CS_LD + col] = acc[i][j][r];
-      }
+  acc_to_lds<BM, BN>(acc, cs, wave, lane);
   __syncthreads();
 
   constexpr int CPR = BN / 8;
@@ -248,6 +281,108 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmParams p, int tiles_
       }
     }
   }
+}
+
+// ---- stream-K (balanced split-K) for batch-contraction GEMMs ---------------------------------
+// The wgrad GEMMs have few output tiles (e.g. 52 for a 512x832 weight) and a huge contraction
+// (the batch). Classic split-K leaves the chip unevenly loaded (416 workgroups = 2 on 160 CUs,
+// 1 on 96). Here the flattened (tile, k-step) space of `total` iterations is cut into `nwg`
+// contiguous, equal shares; a workgroup walks its share, emitting one fp32 partial tile per
+// tile segment it touches (at most 2 when ipw <= k-steps per tile) into
+// part[(wg * 2 + seg)][BM][BN]. streamk_reduce then sums each tile's contributors in
+// workgroup order (deterministic) into C.
+template <int BM, int BN, int LA, int LB>
+__global__ __launch_bounds__(256) void gemm_bf16_streamk_kernel(GemmParams p, int tiles_n,
+                                                                int ksteps, int ipw, int total,
+                                                                int nwg, float* part) {
+  using TC = TileCfg<BM, BN>;
+  constexpr int FM = TC::FM, FN = TC::FN, CS_LD = TC::CS_LD;
+  __shared__ __attribute__((aligned(16))) char smem[TC::SMEM];
+  char LDS_AS* lds = (char LDS_AS*)smem;
+  const int w = xcd_remap(blockIdx.x, nwg);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  int it = w * ipw;
+  const int it_end = min(total, it + ipw);
+  for (int seg = 0; it < it_end; ++seg) {
+    const int tile = it / ksteps, k0 = it % ksteps;
+    const int k1 = min(ksteps, k0 + (it_end - it));
+    const int tn = tile % tiles_n, tm = tile / tiles_n;
+    f32x4_t acc[FM][FN];
+    mma_tile<BM, BN, LA, LB>(p, tm * BM, tn * BN, k0 * 64, k1 - k0, lds, acc, wave, lane);
+    float LDS_AS* cs = (float LDS_AS*)lds;
+    acc_to_lds<BM, BN>(acc, cs, wave, lane);
+    __syncthreads();
+    float* dst = part + ((long)w * 2 + seg) * (BM * BN);
+    constexpr int C4 = BN / 4;
+#pragma unroll 4
+    for (int idx = threadIdx.x; idx < BM * C4; idx += 256) {
+      const int row = idx / C4, col = (idx % C4) * 4;
+      *(f32x4_t*)(dst + row * BN + col) = *(const f32x4_t LDS_AS*)(cs + row * CS_LD + col);
+    }
+    __syncthreads();  // LDS is re-staged by the next segment
+    it += k1 - k0;
+  }
+}
+
+// C[tile] (+)= sum of the tile's partials; one block per (tile, 1024-float chunk).
+__global__ __launch_bounds__(256) void streamk_reduce_kernel(const float* __restrict__ part,
+                                                             float* __restrict__ C, long ldc,
+                                                             int bm, int bn, int tiles_n,
+                                                             int ksteps, int ipw,
+                                                             int accumulate) {
+  const int tile = blockIdx.y;
+  const int tn = tile % tiles_n, tm = tile / tiles_n;
+  const int tile_elems = bm * bn;
+  const int e = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (e >= tile_elems) return;
+  const long first_it = (long)tile * ksteps, last_it = first_it + ksteps - 1;
+  const int w0 = (int)(first_it / ipw), w1 = (int)(last_it / ipw);
+  f32x4_t s = {0.f, 0.f, 0.f, 0.f};
+  for (int w = w0; w <= w1; ++w) {
+    const int seg = ((long)w * ipw / ksteps == tile) ? 0 : 1;  // tile w started in -> seg 0
+    s += *(const f32x4_t*)(part + ((long)w * 2 + seg) * tile_elems + e);
+  }
+  const int row = e / bn, col = e % bn;
+  float* c = C + (long)(tm * bm + row) * ldc + tn * bn + col;
+  if (accumulate) s += *(const f32x4_t*)c;
+  *(f32x4_t*)c = s;
+}
+
+int gemm_bf16_streamk(const GemmParams& p, int layout_a, int layout_b, int bm, int bn, int nwg,
+                      float* part, hipStream_t stream) {
+  if (!((bm == 64 || bm == 128) && (bn == 64 || bn == 128))) return -1;
+  if (p.M <= 0 || p.N <= 0 || p.M % bm || p.N % bn) return -2;
+  if (p.K <= 0 || p.K % 64) return -3;
+  if ((p.lda | p.ldb | p.ldc) % 4 || p.lda % 8 || p.ldb % 8) return -4;
+  auto mis = [](const void* q) { return ((uintptr_t)q) & 15; };
+  if (mis(p.A) || mis(p.B) || mis(p.C) || mis(part)) return -5;
+  if ((layout_a != KMAJ && layout_a != MNMAJ) || (layout_b != KMAJ && layout_b != MNMAJ)) return -6;
+  const int tiles_n = p.N / bn, tiles = tiles_n * (p.M / bm), ksteps = p.K / 64;
+  const long total = (long)tiles * ksteps;
+  if (nwg < tiles) nwg = tiles;  // guarantees ipw <= ksteps -> at most 2 segments per wg
+  if (total > 0x7fffffff) return -3;
+  const int ipw = (int)((total + nwg - 1) / nwg);
+  nwg = (int)((total + ipw - 1) / ipw);
+  typedef void (*fn_t)(GemmParams, int, int, int, int, int, float*);
+  fn_t fn;
+#define DNN_SK(BM_, BN_)                                                                     \
+  fn = (layout_a == KMAJ ? (layout_b == KMAJ ? gemm_bf16_streamk_kernel<BM_, BN_, KMAJ, KMAJ>   \
+                                             : gemm_bf16_streamk_kernel<BM_, BN_, KMAJ, MNMAJ>) \
+                         : (layout_b == KMAJ ? gemm_bf16_streamk_kernel<BM_, BN_, MNMAJ, KMAJ>  \
+                                             : gemm_bf16_streamk_kernel<BM_, BN_, MNMAJ, MNMAJ>))
+  if (bm == 128 && bn == 128) DNN_SK(128, 128);
+  else if (bm == 128) DNN_SK(128, 64);
+  else if (bn == 128) DNN_SK(64, 128);
+  else DNN_SK(64, 64);
+#undef DNN_SK
+  hipLaunchKernelGGL(fn, dim3(nwg), dim3(256), 0, stream, p, tiles_n, ksteps, ipw, (int)total,
+                     nwg, part);
+  if (hipGetLastError() != hipSuccess) return -9;
+  const int chunks = (bm * bn / 4 + 255) / 256;
+  hipLaunchKernelGGL(streamk_reduce_kernel, dim3(chunks, tiles), dim3(256), 0, stream, part,
+                     (float*)p.C, p.ldc, bm, bn, tiles_n, ksteps, ipw, p.accumulate);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
 }
 
 typedef void (*gemm_fn)(GemmParams, int, int, int);

@@ -39,6 +39,13 @@ struct GemmParams {
 int gemm_bf16(const GemmParams& p, int layout_a, int layout_b, int out_f32, int bm, int bn,
               int splits, hipStream_t stream);
 
+// Stream-K form for batch-contraction (wgrad) GEMMs with few output tiles: `nwg` workgroups take
+// equal shares of the (tile, k-step) space, write fp32 partial tiles to `part`
+// (nwg * 2 * bm * bn floats), and a reduction kernel sums them in a fixed order into the fp32 C
+// (C += when p.accumulate). p.K is the FULL contraction length.
+int gemm_bf16_streamk(const GemmParams& p, int layout_a, int layout_b, int bm, int bn, int nwg,
+                      float* part, hipStream_t stream);
+
 const char* gemm_error_string(int code);
 
 }  // namespace dnn

@@ -95,7 +95,8 @@ def main(argv: Optional[list[str]] = None, script_dir: str = SCRIPT_DIR_DEFAULT)
             spec = MLPSpec.parse(a.model)
             mc = ModelConfig([LayerWeights(np.zeros((l.out_dim, l.in_dim), np.float32),
                                            np.zeros(l.out_dim, np.float32), l.activation, l.type,
-                                           l.out_dim) for l in spec.layers], None, source=a.model)
+                                           l.out_dim) for l in spec.layers],
+                             [len(spec.layers)], source=a.model)
             random_init = True
         else:
             mc = load_model_config(a.config)

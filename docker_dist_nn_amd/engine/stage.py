@@ -21,6 +21,7 @@ stage writes fp32 logits and runs the fused softmax-cross-entropy kernel.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Optional, Sequence
 
@@ -155,7 +156,7 @@ class Stage:
     def __init__(self, spec: MLPSpec, layer_start: int, layer_end: int, *, micro_batch: int,
                  num_micro: int, device: torch.device, global_batch: Optional[int] = None,
                  optim: Optional[OptimConfig] = None, wgrad: str = "batched",
-                 stage_index: int = 0, num_stages: int = 1):
+                 stage_index: int = 0, num_stages: int = 1, wgrad_algo: Optional[str] = None):
         if not 0 <= layer_start < layer_end <= len(spec.layers):
             raise ValueError("bad layer range")
         if micro_batch <= 0 or micro_batch % 64:
@@ -171,6 +172,9 @@ class Stage:
         self.device = device
         self.global_batch = global_batch or self.rows
         self.wgrad_mode = wgrad
+        self.wgrad_algo = wgrad_algo or os.environ.get("DNN_WGRAD_ALGO", "streamk")
+        if self.wgrad_algo not in ("streamk", "splitk"):
+            raise ValueError(f"wgrad_algo must be streamk | splitk, got {self.wgrad_algo!r}")
         self.geoms = [LayerGeom(i, spec.layers[i]) for i in range(layer_start, layer_end)]
         self.params = StageParams(self.geoms, device, optim)
         self.prev_act = spec.layers[layer_start - 1].activation if not self.first else "linear"
@@ -196,9 +200,15 @@ class Stage:
         self.correct = torch.zeros(1, dtype=torch.int32, device=dev)
         # wgrad geometry: batched = one GEMM over all rows; per_micro = one per micro-batch
         wrows = R if self.wgrad_mode == "batched" else self.mb
-        self.w_splits = [ops.pick_splits(g.np_, g.kp, wrows) for g in self.geoms]
-        self.slabs = [torch.zeros(s, g.np_, g.kp, dtype=f32, device=dev)
-                      for s, g in zip(self.w_splits, self.geoms)]
+        if self.wgrad_algo == "streamk":  # balanced stream-K, reduced straight into the grads
+            self.w_splits = [1] * len(self.geoms)
+            self.slabs = []
+            n = max(ops.streamk_partial_elems(g.np_, g.kp) for g in self.geoms)
+            self.sk_part = torch.zeros(n, dtype=f32, device=dev)
+        else:  # classic split-K slabs + reduce
+            self.w_splits = [ops.pick_splits(g.np_, g.kp, wrows) for g in self.geoms]
+            self.slabs = [torch.zeros(s, g.np_, g.kp, dtype=f32, device=dev)
+                          for s, g in zip(self.w_splits, self.geoms)]
         # Bias-gradient partials (column sums of dZ) come fused from whichever kernel produces
         # dZ: the dgrad epilogue of the next local layer (one partial per output row tile), the
         # softmax-CE kernel (one per 64-row block), or -- for a gradient received from the next
@@ -291,16 +301,23 @@ class Stage:
             if self.wgrad_mode == "batched":
                 raise RuntimeError("per-micro wgrad on a stage built with wgrad='batched'")
             r, accumulate = self.rows_of(j), self._w_done > 0
-        ops.linear_wgrad(self.dz[i][r], self.input_of(i)[r], self.slabs[i],
-                         splits=self.w_splits[i], accumulate=accumulate)
+        if self.wgrad_algo == "streamk":
+            g = self.geoms[i]
+            ops.linear_wgrad_streamk(self.dz[i][r], self.input_of(i)[r],
+                                     self.params.gw(i).view(g.np_, g.kp), self.sk_part,
+                                     accumulate=accumulate)
+        else:
+            ops.linear_wgrad(self.dz[i][r], self.input_of(i)[r], self.slabs[i],
+                             splits=self.w_splits[i], accumulate=accumulate)
 
     def finalize_grads(self, layers: Optional[Sequence[int]] = None) -> None:
-        """Reduce split-K slabs / bias partials into the flat gradient buffer."""
+        """Reduce bias partials (and, for split-K, weight slabs) into the flat gradient."""
         p = self.params
         for i in (range(len(self.geoms)) if layers is None else layers):
             g = self.geoms[i]
             n = g.np_ * g.kp
-            ops.reduce_slabs(self.slabs[i], self.w_splits[i], n, n, p.gw(i))
+            if self.wgrad_algo != "streamk":
+                ops.reduce_slabs(self.slabs[i], self.w_splits[i], n, n, p.gw(i))
             ops.reduce_slabs(self.bpart[i], self.bpart[i].shape[0], g.np_, g.np_, p.gb(i))
 
     def optimizer_step(self, lr: Optional[float] = None) -> None:

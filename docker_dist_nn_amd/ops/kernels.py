@@ -165,6 +165,49 @@ def linear_wgrad(dz, x, slabs, splits=1, accumulate=False):
                 accumulate=accumulate, splits=splits)
 
 
+STREAMK_WG = 2 * NUM_CU  # stream-K workgroups: two resident per CU, every CU equally loaded
+
+
+def streamk_tiles(N: int, K: int) -> tuple[int, int]:
+    """Output tile of the [N][K] weight gradient: largest tile that divides it."""
+    for t in ((128, 128), (128, 64), (64, 128), (64, 64)):
+        if N % t[0] == 0 and K % t[1] == 0:
+            return t
+    raise ValueError(f"weight shape [{N}][{K}] is not 64-aligned")
+
+
+def streamk_partial_elems(N: int, K: int, nwg: int = STREAMK_WG) -> int:
+    bm, bn = streamk_tiles(N, K)
+    tiles = (N // bm) * (K // bn)
+    return max(nwg, tiles) * 2 * bm * bn
+
+
+def linear_wgrad_streamk(dz, x, grad_w, part, accumulate=False, nwg: int = STREAMK_WG):
+    """grad_w[Np][Kp] (+)= dz^T . x over ALL rows, stream-K balanced; ``part`` is fp32 scratch
+    of streamk_partial_elems(Np, Kp) elements."""
+    R, N = dz.shape
+    K = x.shape[1]
+    if not dz.is_cuda:
+        g = dz.float().t() @ x.float()
+        if accumulate:
+            grad_w += g
+        else:
+            grad_w.copy_(g)
+        return grad_w
+    _rows(dz, "dz", torch.bfloat16)
+    _rows(x, "x", torch.bfloat16)
+    _rows(grad_w, "grad_w", torch.float32)
+    if x.shape[0] != R or grad_w.shape[0] < N or grad_w.shape[1] < K or R % 64:
+        raise ValueError("wgrad shapes do not match")
+    if part.dtype != torch.float32 or part.numel() < streamk_partial_elems(N, K, nwg):
+        raise ValueError("stream-K partial buffer too small")
+    bm, bn = streamk_tiles(N, K)
+    native().gemm_bf16_streamk(_p(dz), dz.stride(0), _p(x), x.stride(0), _p(grad_w),
+                               grad_w.stride(0), N, K, R, int(accumulate), MNMAJ, MNMAJ, bm, bn,
+                               nwg, _p(part), _stream(dz))
+    return grad_w
+
+
 # ---- loss / reductions / optimizers ----------------------------------------------------------
 
 XENT_ROWS_PER_BLOCK = 64  # csrc/kernels/elementwise.hip XENT_ROWS_PER_BLOCK

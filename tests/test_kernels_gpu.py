@@ -259,3 +259,22 @@ def test_xent_colsum_partials(dev):
     pad = torch.zeros(nb * 64, width, device=dev)
     pad[:rows] = dz.float()
     torch.testing.assert_close(part, pad.view(nb, 64, width).sum(1), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("R,N,K,nwg", [(65536, 512, 832, 512), (4096, 64, 128, 512),
+                                       (2048, 256, 512, 7), (8192, 1024, 1024, 512),
+                                       (1024, 128, 192, 3)])
+def test_wgrad_streamk(dev, R, N, K, nwg):
+    gen = torch.Generator().manual_seed(R + N)
+    dz = torch.randn(R, N, generator=gen).to(torch.bfloat16).to(dev)
+    x = torch.randn(R, K, generator=gen).to(torch.bfloat16).to(dev)
+    part = torch.empty(ops.streamk_partial_elems(N, K, nwg), device=dev)
+    g = torch.full((N, K), 3.0, device=dev)
+    ops.linear_wgrad_streamk(dz, x, g, part, accumulate=False, nwg=nwg)
+    ref = dz.float().t() @ x.float()
+    torch.testing.assert_close(g, ref, rtol=1e-4, atol=2e-3 * (R / 1024) ** 0.5)
+    ops.linear_wgrad_streamk(dz, x, g, part, accumulate=True, nwg=nwg)
+    torch.testing.assert_close(g, 2 * ref, rtol=1e-4, atol=4e-3 * (R / 1024) ** 0.5)
+    g2 = torch.empty_like(g)
+    ops.linear_wgrad_streamk(dz, x, g2, part, nwg=nwg)
+    assert torch.equal(g2, g / 2) or torch.equal(g2 * 2, g)  # deterministic
