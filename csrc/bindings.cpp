@@ -45,10 +45,17 @@ PYBIND11_MODULE(_native, m) {
       [](uintptr_t a, long lda, uintptr_t b, long ldb, uintptr_t c, long ldc, long c_split_stride,
          uintptr_t bias, uintptr_t aux, long ld_aux, int M, int N, int K, int act, int accumulate,
          int layout_a, int layout_b, int out_f32, int bm, int bn, int splits, uintptr_t stream,
-         uintptr_t colsum, long ld_colsum) {
+         uintptr_t colsum, long ld_colsum, uintptr_t xent_labels, int n_cls, float xent_scale,
+         uintptr_t loss_part, uintptr_t correct, int k_total) {
         GemmParams p{};
+        p.k_total = k_total;
         p.colsum = P<float>(colsum);
         p.ld_colsum = ld_colsum;
+        p.xent_labels = P<const int>(xent_labels);
+        p.n_cls = n_cls;
+        p.xent_scale = xent_scale;
+        p.loss_part = P<float>(loss_part);
+        p.correct = P<int>(correct);
         p.A = P<const uint16_t>(a);
         p.lda = lda;
         p.B = P<const uint16_t>(b);
@@ -71,7 +78,9 @@ PYBIND11_MODULE(_native, m) {
       py::arg("c_split_stride"), py::arg("bias"), py::arg("aux"), py::arg("ld_aux"), py::arg("M"),
       py::arg("N"), py::arg("K"), py::arg("act"), py::arg("accumulate"), py::arg("layout_a"),
       py::arg("layout_b"), py::arg("out_f32"), py::arg("bm"), py::arg("bn"), py::arg("splits"),
-      py::arg("stream"), py::arg("colsum") = 0, py::arg("ld_colsum") = 0);
+      py::arg("stream"), py::arg("colsum") = 0, py::arg("ld_colsum") = 0,
+      py::arg("xent_labels") = 0, py::arg("n_cls") = 0, py::arg("xent_scale") = 0.f,
+      py::arg("loss_part") = 0, py::arg("correct") = 0, py::arg("k_total") = 0);
 
   m.def(
       "gemm_bf16_streamk",

@@ -110,7 +110,8 @@ struct TileCfg {
   static constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
   static constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
   static constexpr int CS_LD = BN + 4;  // fp32 epilogue staging row stride (floats)
-  static constexpr int SMEM = cmax<2 * STAGE, BM * CS_LD * 4>::v;
+  static constexpr int CS_BYTES = BM * CS_LD * 4;
+  static constexpr int SMEM = cmax<2 * STAGE, CS_BYTES + 64>::v;  // +64: epilogue reductions
 };
 
 // acc (+)= A[m0:m0+BM, k] . B[k, n0:n0+BN] over k-steps [kbase, kbase + 64*nk): LDS-DMA
@@ -182,6 +183,64 @@ __device__ __forceinline__ void acc_to_lds(
       }
 }
 
+// Fused softmax cross-entropy over the fp32 logits tile in LDS (the whole padded row lives in
+// this tile: N == BN). Thread r < BM owns row r: adds the bias, finds max / argmax (lowest index,
+// np.argmax rule) / log-sum-exp over the n_cls valid columns, and overwrites the row with
+// dz = (p - onehot) * scale (0 in padding columns and for label < 0 padding rows). Block loss
+// and correct-count go to loss_part[tile_m] / *correct.
+template <int BM, int BN>
+__device__ __forceinline__ void xent_rows(const GemmParams& p, float LDS_AS* cs, int m0) {
+  constexpr int CS_LD = TileCfg<BM, BN>::CS_LD;
+  // scratch after the staging tile (all LDS lives in the kernel's single __shared__ array)
+  float LDS_AS* s_loss = cs + BM * CS_LD;
+  int LDS_AS* s_corr = (int LDS_AS*)(s_loss + 4);
+  const int r = threadIdx.x;
+  float loss = 0.f;
+  int corr = 0;
+  if (r < BM) {
+    float LDS_AS* row = cs + r * CS_LD;
+    const int label = p.xent_labels[m0 + r];
+    const int nc = p.n_cls;
+    float mx = -INFINITY;
+    int amax = 0;
+    for (int c = 0; c < nc; ++c) {
+      const float v = row[c] + p.bias[c];
+      row[c] = v;
+      if (v > mx) {
+        mx = v;
+        amax = c;
+      }
+    }
+    float se = 0.f;
+    for (int c = 0; c < nc; ++c) se += __expf(row[c] - mx);
+    const float inv = 1.f / se;
+    if (label >= 0) {
+      loss = -(row[label] - mx - __logf(se));
+      corr = amax == label;
+      for (int c = 0; c < nc; ++c)
+        row[c] = (__expf(row[c] - mx) * inv - (c == label ? 1.f : 0.f)) * p.xent_scale;
+    } else {
+      for (int c = 0; c < nc; ++c) row[c] = 0.f;
+    }
+    for (int c = nc; c < BN; ++c) row[c] = 0.f;
+  }
+  // block reduction of loss / correct (fixed order -> reproducible)
+  loss = wave_sum(loss);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) corr += __shfl_xor(corr, o, 64);
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    s_loss[wave] = loss;
+    s_corr[wave] = corr;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (p.loss_part) p.loss_part[m0 / BM] = (s_loss[0] + s_loss[1]) + (s_loss[2] + s_loss[3]);
+    const int cc = s_corr[0] + s_corr[1] + s_corr[2] + s_corr[3];
+    if (p.correct && cc) atomicAdd(p.correct, cc);
+  }
+}
+
 template <int BM, int BN, int LA, int LB, bool OUT_F32>
 __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmParams p, int tiles_n, int tiles_m,
                                                         int nwg) {
@@ -200,8 +259,16 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmParams p, int tiles_
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int m0 = tm * BM, n0 = tn * BN;
-  const int kbase = split * p.K;
-  const int nk = p.K >> 6;
+  int kbase, nk;
+  if (p.k_total > 0) {  // uneven split-K: split s takes k-steps [s*KS/S, (s+1)*KS/S)
+    const int KS = p.k_total >> 6, S = nwg / (tiles_n * tiles_m);
+    const int a = (int)((long)split * KS / S), b = (int)((long)(split + 1) * KS / S);
+    kbase = a * 64;
+    nk = b - a;
+  } else {
+    kbase = split * p.K;
+    nk = p.K >> 6;
+  }
 
   f32x4_t acc[FM][FN];
   mma_tile<BM, BN, LA, LB>(p, m0, n0, kbase, nk, lds, acc, wave, lane);
@@ -210,6 +277,15 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmParams p, int tiles_
   float LDS_AS* cs = (float LDS_AS*)lds;
   acc_to_lds<BM, BN>(acc, cs, wave, lane);
   __syncthreads();
+
+  bool xent = false;
+  if constexpr (!OUT_F32) {
+    if (p.xent_labels) {  // uniform: fused softmax-CE, one thread per row of the tile
+      xent = true;
+      xent_rows<BM, BN>(p, cs, m0);
+      __syncthreads();
+    }
+  }
 
   constexpr int CPR = BN / 8;
   constexpr int ITER = BM * CPR / 256;
@@ -223,7 +299,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmParams p, int tiles_
     const f32x4_t v1 = *(const f32x4_t LDS_AS*)(cs + row * CS_LD + col + 4);
     float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
     const long gm = m0 + row, gn = n0 + col;
-    if (p.bias) {
+    if (p.bias && !xent) {
       const f32x4_t b0 = *(const f32x4_t*)(p.bias + gn);
       const f32x4_t b1 = *(const f32x4_t*)(p.bias + gn + 4);
 #pragma unroll
@@ -246,7 +322,9 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmParams p, int tiles_
       *(f32x4_t*)c = o0;
       *(f32x4_t*)(c + 4) = o1;
     } else {
-      if (p.aux) {
+      if (xent) {
+        // dz already computed in LDS
+      } else if (p.aux) {
         const bf16x8_t y = *(const bf16x8_t*)(p.aux + gm * p.ld_aux + gn);
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = act_bwd(v[e], bf2f((u16)y[e]), p.act);
@@ -410,6 +488,7 @@ const char* gemm_error_string(int code) {
     case -8: return "leading dimension smaller than the row it stores";
     case -9: return "hip launch failed";
     case -10: return "colsum needs bf16 output and ld_colsum >= N";
+    case -11: return "fused cross-entropy needs bf16 output, N == bn, a bias and 0 < n_cls <= N";
     default: return "unknown gemm error";
   }
 }
@@ -418,7 +497,13 @@ int gemm_bf16(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, 
               hipStream_t stream) {
   if (!((bm == 64 || bm == 128) && (bn == 64 || bn == 128))) return -1;
   if (p.M <= 0 || p.N <= 0 || p.M % bm || p.N % bn) return -2;
-  if (p.K <= 0 || p.K % 64 || splits < 1) return -3;
+  if (splits < 1) return -3;
+  if (p.k_total > 0) {
+    if (p.k_total % 64 || splits > p.k_total / 64) return -3;
+  } else if (p.K <= 0 || p.K % 64) {
+    return -3;
+  }
+  const long ktot = p.k_total > 0 ? (long)p.k_total : (long)p.K * splits;
   if ((p.lda | p.ldb | p.ldc) % 8 || (p.aux && p.ld_aux % 8)) return -4;
   auto mis = [](const void* q) { return ((uintptr_t)q) & 15; };
   if (mis(p.A) || mis(p.B) || mis(p.C) || (p.aux && mis(p.aux)) || (p.bias && mis(p.bias)))
@@ -426,8 +511,11 @@ int gemm_bf16(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, 
   if ((la != KMAJ && la != MNMAJ) || (lb != KMAJ && lb != MNMAJ)) return -6;
   if (splits > 1 && !out_f32) return -7;
   if (p.colsum && (out_f32 || p.ld_colsum < p.N)) return -10;
-  const long a_row = la == KMAJ ? (long)p.K * splits : p.M;
-  const long b_row = lb == KMAJ ? (long)p.K * splits : p.N;
+  if (p.xent_labels && (out_f32 || p.N != bn || !p.bias || p.n_cls <= 0 || p.n_cls > p.N ||
+                        splits != 1 || p.aux))
+    return -11;
+  const long a_row = la == KMAJ ? ktot : p.M;
+  const long b_row = lb == KMAJ ? ktot : p.N;
   if (p.lda < a_row || p.ldb < b_row || p.ldc < p.N || (p.aux && p.ld_aux < p.N)) return -8;
 
   gemm_fn fn;

@@ -27,11 +27,21 @@ struct GemmParams {
   const float* bias;    // optional, [N] fp32, added in the epilogue
   const uint16_t* aux;  // optional, bf16 activation output used for the backward mask
   long ld_aux;
-  int M, N, K;     // K = contraction length handled by ONE split
+  int M, N, K;     // K = contraction length handled by ONE split (uniform split-K)
+  int k_total;     // > 0: uneven split-K over k_total (split s: k-steps [s*KS/S, (s+1)*KS/S))
   int act;         // Act code: forward activation, or (with aux) the activation to differentiate
   int accumulate;  // f32 output: C += result (split slab accumulation across micro-batches)
   float* colsum;   // optional (bf16 output only): colsum[tile_m][n] = sum over the tile's rows
   long ld_colsum;  //   of the stored (bf16-rounded) output -> bias-gradient partials of dgrad
+  // Fused softmax cross-entropy epilogue (bf16 output, N == bn: a row is one tile). When
+  // xent_labels is set the kernel computes logits = acc + bias, and stores
+  // dz = (softmax(logits[:n_cls]) - onehot(label)) * xent_scale instead of the logits;
+  // loss_part[tile_m] = sum of -log p[label] over the tile's rows, *correct += #argmax==label.
+  const int* xent_labels;
+  int n_cls;
+  float xent_scale;
+  float* loss_part;
+  int* correct;
 };
 
 // Returns 0 on success, a negative code when a shape/alignment precondition fails

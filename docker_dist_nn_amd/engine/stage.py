@@ -172,7 +172,7 @@ class Stage:
         self.device = device
         self.global_batch = global_batch or self.rows
         self.wgrad_mode = wgrad
-        self.wgrad_algo = wgrad_algo or os.environ.get("DNN_WGRAD_ALGO", "streamk")
+        self.wgrad_algo = wgrad_algo or os.environ.get("DNN_WGRAD_ALGO", "splitk")
         if self.wgrad_algo not in ("streamk", "splitk"):
             raise ValueError(f"wgrad_algo must be streamk | splitk, got {self.wgrad_algo!r}")
         self.geoms = [LayerGeom(i, spec.layers[i]) for i in range(layer_start, layer_end)]
@@ -188,14 +188,24 @@ class Stage:
         g0 = self.geoms[0]
         self.x_buf = torch.zeros(R, g0.kp, dtype=bf, device=dev)
         self.x_in = self.x_buf  # may be re-pointed at a resident dataset slice (zero-copy)
+        # the last layer's softmax-CE is fused into its GEMM epilogue when the padded class
+        # count is one 64/128-wide tile: logits then never exist in memory
+        gl = self.geoms[-1]
+        self.fused_xent = (self.last and gl.np_ in (64, 128) and
+                           os.environ.get("DNN_FUSED_XENT", "1") == "1")
         self.acts: list[torch.Tensor] = []  # output of local layer i
         for i, g in enumerate(self.geoms):
             is_logits = self.last and i == len(self.geoms) - 1
-            self.acts.append(torch.zeros(R, g.np_, dtype=f32 if is_logits else bf, device=dev))
+            if is_logits and self.fused_xent:
+                self.acts.append(torch.empty(0, g.np_, dtype=f32, device=dev))
+            else:
+                self.acts.append(torch.zeros(R, g.np_, dtype=f32 if is_logits else bf,
+                                             device=dev))
         self.dz = [torch.zeros(R, g.np_, dtype=bf, device=dev) for g in self.geoms]
         self.dx_send = None if self.first else torch.zeros(R, g0.kp, dtype=bf, device=dev)
         self.labels = torch.full((R,), -1, dtype=torch.int32, device=dev) if self.last else None
-        self.xent_per_micro = ops.xent_blocks(self.mb)
+        self.xent_per_micro = (self.mb // ops.xent_tiles(self.mb, gl.np_)[0] if self.fused_xent
+                               else ops.xent_blocks(self.mb))
         self.loss_part = torch.zeros(self.xent_per_micro * self.nm, dtype=f32, device=dev)
         self.correct = torch.zeros(1, dtype=torch.int32, device=dev)
         # wgrad geometry: batched = one GEMM over all rows; per_micro = one per micro-batch
@@ -219,7 +229,7 @@ class Stage:
             if i < L - 1:
                 self.bp.append(self.mb // ops.dgrad_tiles(self.mb, self.geoms[i + 1].kp)[0])
             elif self.last:
-                self.bp.append(ops.xent_blocks(self.mb))
+                self.bp.append(self.xent_per_micro)
             else:
                 self.bp.append(max(1, self.mb // 1024))
         self.bpart = [torch.zeros(self.bp[i] * self.nm, g.np_, dtype=f32, device=dev)
@@ -255,7 +265,13 @@ class Stage:
         for i, g in enumerate(self.geoms):
             x = self.input_of(i)[r]
             y = self.acts[i][r]
-            if self.last and i == len(self.geoms) - 1:
+            if self.last and i == len(self.geoms) - 1 and self.fused_xent:
+                k = j * self.xent_per_micro
+                ops.linear_fwd_xent(x, p.wbf(i), p.b32(i), self.dz[i][r], self.labels[r],
+                                    self.n_cls, 1.0 / self.global_batch,
+                                    self.loss_part[k:k + self.xent_per_micro], self.correct,
+                                    colsum=self._bpart(i, j))
+            elif self.last and i == len(self.geoms) - 1:
                 ops.linear_fwd(x, p.wbf(i), p.b32(i), y, act="linear")  # fp32 logits
                 k = j * self.xent_per_micro
                 ops.softmax_xent(y, self.labels[r], self.dz[i][r], self.n_cls,

@@ -66,23 +66,45 @@ def pick_tiles(M: int, N: int, splits: int = 1) -> tuple[int, int]:
     return best
 
 
-def pick_splits(M: int, N: int, K_total: int, target_wg: int = 2 * NUM_CU) -> int:
-    """Split-K factor for the batch-contraction (wgrad) GEMM: enough workgroups, chunks >= 256."""
-    bm, bn = pick_tiles(M, N, 1)
-    tiles = (M // bm) * (N // bn)
-    s = 1
-    while (tiles * s < target_wg and K_total % (2 * s * 64) == 0 and K_total // (2 * s) >= 256):
-        s *= 2
-    return s
+def pick_splits(M: int, N: int, K_total: int, max_splits: int = 48) -> int:
+    """Split-K factor for the batch-contraction (wgrad) GEMM.
+
+    Splits may be uneven (k-ranges differ by at most one 64-step), so any S works. Resident
+    workgroups share a CU, so time ~ ceil(tiles*S / CUs) / S tile-times (wave quantisation);
+    each extra split adds an fp32 slab of M*N to write and re-read. E.g. 52 tiles: S=8 puts 2
+    workgroups on 160 CUs and 1 on 96 (81% busy); S=14 gives 2-3 per CU (95%)."""
+    return wgrad_config(M, N, K_total, max_splits)[2]
+
+
+def wgrad_config(M: int, N: int, K_total: int, max_splits: int = 48) -> tuple[int, int, int]:
+    """Joint (bm, bn, splits) choice for the batch-contraction GEMM (see pick_splits)."""
+    ksteps = K_total // 64
+    slab_cost = 2.0 * M * N * 4 / 5.0e12 * 0.6e15 / NUM_CU  # slab bytes in tile-FLOP units
+    best, best_c = None, math.inf
+    for (bm, bn), eff in _TILE_EFF.items():
+        if M % bm or N % bn:
+            continue
+        tiles = (M // bm) * (N // bn)
+        tile_flops = 2.0 * bm * bn * K_total / eff
+        for s in range(1, min(max_splits, ksteps) + 1):
+            c = math.ceil(tiles * s / NUM_CU) / s * tile_flops + (s > 1) * s * slab_cost
+            if c < best_c * 0.995:
+                best, best_c = (bm, bn, s), c
+    if best is None:
+        raise ValueError(f"no tile divides [{M}][{N}]")
+    return best
 
 
 def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=None, aux=None,
          act=0, accumulate: bool = False, splits: int = 1, tiles: tuple[int, int] | None = None,
-         colsum=None):
+         colsum=None, k_total: int = 0):
     """C (+)= epilogue(A.B). See csrc/kernels/gemm.hpp for the layout/epilogue contract.
 
+    ``k_total`` > 0 selects uneven split-K over the full contraction length (K is ignored).
     ``colsum`` (bf16 output only): fp32 [M/bm][>=N] receives per-row-tile column sums of the
     stored output; requires explicit ``tiles`` so the caller knows the partial count."""
+    if k_total:
+        K = k_total
     act = _act(act)
     out_f32 = c.dtype == torch.float32
     if colsum is not None:
@@ -94,7 +116,7 @@ def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=
     if not a.is_cuda:
         return ref.gemm(a, b, c, layout_a=layout_a, layout_b=layout_b, M=M, N=N, K=K, bias=bias,
                         aux=aux, act=act, accumulate=accumulate, splits=splits, colsum=colsum,
-                        colsum_rows=tiles[0] if tiles else 0)
+                        colsum_rows=tiles[0] if tiles else 0, k_total=k_total)
     _rows(a, "A", torch.bfloat16)
     _rows(b, "B", torch.bfloat16)
     if splits > 1:
@@ -109,7 +131,7 @@ def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=
     if aux is not None:
         _rows(aux, "aux", torch.bfloat16)
     # shape checks against the storage the kernel will touch
-    ka = K * splits
+    ka = k_total or K * splits
     need_a = (M, ka) if layout_a == KMAJ else (ka, M)
     need_b = (N, ka) if layout_b == KMAJ else (ka, N)
     if a.shape[0] < need_a[0] or a.shape[1] < need_a[1]:
@@ -125,7 +147,7 @@ def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=
                        split_stride, _p(bias), _p(aux), aux.stride(0) if aux is not None else 0,
                        M, N, K, act, int(accumulate), layout_a, layout_b, int(out_f32), bm, bn,
                        splits, _stream(a), _p(colsum),
-                       colsum.stride(0) if colsum is not None else 0)
+                       colsum.stride(0) if colsum is not None else 0, k_total=int(k_total))
     return c
 
 
@@ -136,6 +158,48 @@ def linear_fwd(x, w, bias, y, act="relu"):
     M, K = x.shape
     N = w.shape[0]
     return gemm(x, w, y, layout_a=KMAJ, layout_b=KMAJ, M=M, N=N, K=K, bias=bias, act=act)
+
+
+def xent_tiles(M: int, N: int) -> tuple[int, int]:
+    """Tile of the fused linear+softmax-CE GEMM: the whole padded row in one tile (bn == N)."""
+    if N not in (64, 128):
+        raise ValueError(f"fused cross-entropy supports 64 or 128 padded classes, got {N}")
+    bm = 128 if M % 128 == 0 and (M // 128) * 1 >= NUM_CU // 2 else 64
+    if M % bm:
+        raise ValueError("rows must be a multiple of 64")
+    return bm, N
+
+
+def linear_fwd_xent(x, w, bias, dz, labels, n_cls, scale, loss_part=None, correct=None,
+                    colsum=None):
+    """Last layer + softmax cross-entropy in ONE kernel: dz[M][Np] = (softmax(x.w^T + b) -
+    onehot) * scale; loss_part[M/bm] per-tile loss sums; correct += #argmax == label;
+    colsum[M/bm][Np] = per-tile column sums of dz (the bias-gradient partials)."""
+    M, K = x.shape
+    N = w.shape[0]
+    bm, bn = xent_tiles(M, N)
+    if labels.dtype != torch.int32 or labels.numel() < M:
+        raise ValueError("labels must be int32 with one entry per row")
+    if loss_part is not None and loss_part.numel() < M // bm:
+        raise ValueError(f"loss_part needs {M // bm} entries")
+    if not x.is_cuda:
+        logits = torch.empty(M, N, dtype=torch.float32)
+        ref.gemm(x, w, logits, layout_a=KMAJ, layout_b=KMAJ, M=M, N=N, K=K, bias=bias)
+        ref.softmax_xent(logits, labels, dz, n_cls, scale, loss_part, correct, bm, colsum)
+        return dz
+    _rows(x, "x", torch.bfloat16)
+    _rows(w, "w", torch.bfloat16)
+    _rows(dz, "dz", torch.bfloat16)
+    if colsum is not None and (colsum.dtype != torch.float32 or colsum.shape[0] < M // bm or
+                               colsum.shape[1] < N or colsum.stride(1) != 1):
+        raise ValueError(f"colsum must be fp32 [{M // bm}][>={N}]")
+    if bias is None or bias.dtype != torch.float32 or bias.numel() < N:
+        raise ValueError("fused cross-entropy needs an fp32 bias")
+    native().gemm_bf16(_p(x), x.stride(0), _p(w), w.stride(0), _p(dz), dz.stride(0), 0,
+                       _p(bias), 0, 0, M, N, K, 0, 0, KMAJ, KMAJ, 0, bm, bn, 1, _stream(x),
+                       _p(colsum), colsum.stride(0) if colsum is not None else 0, _p(labels),
+                       int(n_cls), float(scale), _p(loss_part), _p(correct))
+    return dz
 
 
 def dgrad_tiles(M: int, K: int) -> tuple[int, int]:
@@ -159,10 +223,12 @@ def linear_wgrad(dz, x, slabs, splits=1, accumulate=False):
     """slabs[s][Np][Kp] (+)= dz[rows_s]^T . x[rows_s] over the batch rows of split s (fp32)."""
     R, N = dz.shape
     K = x.shape[1]
-    if R % splits:
-        raise ValueError("rows must divide evenly into splits")
-    return gemm(dz, x, slabs, layout_a=MNMAJ, layout_b=MNMAJ, M=N, N=K, K=R // splits,
-                accumulate=accumulate, splits=splits)
+    if R % 64 or splits > R // 64:
+        raise ValueError("rows must be a multiple of 64 with at least 64 rows per split")
+    bm, bn, s = wgrad_config(N, K, R)
+    tiles = (bm, bn) if s == splits else None
+    return gemm(dz, x, slabs, layout_a=MNMAJ, layout_b=MNMAJ, M=N, N=K, K=R, k_total=R,
+                accumulate=accumulate, splits=splits, tiles=tiles)
 
 
 STREAMK_WG = 2 * NUM_CU  # stream-K workgroups: two resident per CU, every CU equally loaded

@@ -40,11 +40,17 @@ def _colsum_blocks(vals, out, rows_per):
 
 
 def gemm(a, b, c, *, layout_a, layout_b, M, N, K, bias=None, aux=None, act=0, accumulate=False,
-         splits=1, colsum=None, colsum_rows=0):
-    A, B = _logical(a, b, layout_a, layout_b, M, N, K * splits)
+         splits=1, colsum=None, colsum_rows=0, k_total=0):
+    ktot = k_total or K * splits
+    A, B = _logical(a, b, layout_a, layout_b, M, N, ktot)
     out_f32 = c.dtype == torch.float32
+    ks = ktot // 64
     for s in range(splits):
-        acc = A[:, s * K:(s + 1) * K] @ B[s * K:(s + 1) * K, :]
+        if k_total:  # uneven split-K: same k-step ranges as the kernel
+            k0, k1 = (s * ks // splits) * 64, ((s + 1) * ks // splits) * 64
+        else:
+            k0, k1 = s * K, (s + 1) * K
+        acc = A[:, k0:k1] @ B[k0:k1, :]
         if bias is not None:
             acc = acc + bias[:N].float()
         if out_f32:

@@ -278,3 +278,50 @@ def test_wgrad_streamk(dev, R, N, K, nwg):
     g2 = torch.empty_like(g)
     ops.linear_wgrad_streamk(dz, x, g2, part, nwg=nwg)
     assert torch.equal(g2, g / 2) or torch.equal(g2 * 2, g)  # deterministic
+
+
+@pytest.mark.parametrize("R,S", [(65536 // 8, 14), (640, 3), (4096, 48)])
+def test_uneven_split_k_exact(dev, R, S):
+    gen = torch.Generator().manual_seed(S)
+    N, K = 128, 192
+    dz = torch.randint(-2, 3, (R, N), generator=gen).float().to(torch.bfloat16).to(dev)
+    x = torch.randint(-2, 3, (R, K), generator=gen).float().to(torch.bfloat16).to(dev)
+    slabs = torch.empty(S, N, K, device=dev)
+    ops.linear_wgrad(dz, x, slabs, splits=S)
+    assert torch.equal(slabs.sum(0), dz.float().t() @ x.float())
+    ks = R // 64
+    for s in (0, S - 1):
+        a, b = (s * ks // S) * 64, ((s + 1) * ks // S) * 64
+        assert torch.equal(slabs[s], dz.float()[a:b].t() @ x.float()[a:b])
+
+
+@pytest.mark.parametrize("M,Np", [(1024, 64), (256, 64), (512, 128)])
+def test_fused_linear_xent_matches_unfused(dev, M, Np):
+    gen = torch.Generator().manual_seed(M + Np)
+    K, ncls = 128, 10
+    x = torch.randn(M, K, generator=gen).to(torch.bfloat16).to(dev)
+    w = torch.zeros(Np, K)
+    w[:ncls] = torch.randn(ncls, K, generator=gen) * 0.2
+    w = w.to(torch.bfloat16).to(dev)
+    b = torch.zeros(Np)
+    b[:ncls] = torch.randn(ncls, generator=gen)
+    b = b.to(dev)
+    labels = torch.randint(0, ncls, (M,), generator=gen, dtype=torch.int32)
+    labels[::9] = -1
+    labels = labels.to(dev)
+    bm = ops.xent_tiles(M, Np)[0]
+    dz = torch.empty(M, Np, dtype=torch.bfloat16, device=dev)
+    lp = torch.zeros(M // bm, device=dev)
+    cor = torch.zeros(1, dtype=torch.int32, device=dev)
+    cs = torch.zeros(M // bm, Np, device=dev)
+    ops.linear_fwd_xent(x, w, b, dz, labels, ncls, 1.0 / M, lp, cor, colsum=cs)
+    logits = torch.empty(M, Np, device=dev)
+    ops.linear_fwd(x, w, b, logits, act="linear")
+    dz2 = torch.empty(M, Np, dtype=torch.bfloat16, device=dev)
+    lp2 = torch.zeros(ops.xent_blocks(M), device=dev)
+    cor2 = torch.zeros(1, dtype=torch.int32, device=dev)
+    ops.softmax_xent(logits, labels, dz2, ncls, 1.0 / M, lp2, cor2)
+    torch.testing.assert_close(dz.float(), dz2.float(), rtol=2e-2, atol=1e-5)
+    torch.testing.assert_close(lp.sum(), lp2.sum(), rtol=1e-4, atol=1e-3)
+    assert int(cor.item()) == int(cor2.item())
+    torch.testing.assert_close(cs, dz.float().view(M // bm, bm, Np).sum(1), rtol=1e-5, atol=1e-5)
