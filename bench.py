@@ -68,7 +68,9 @@ def main(argv=None):
     n = max(a.gpus, world)
     spec = NAMED_MODELS.get(a.model) or MLPSpec.parse(a.model)
 
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # DNN_FORCE_DEVICE / DNN_DIST_BACKEND exist only to rehearse the multi-rank path on a
+    # one-GPU box (several gloo ranks sharing cuda:0); real runs use one GPU per rank + RCCL.
+    local = int(os.environ.get("DNN_FORCE_DEVICE", os.environ.get("LOCAL_RANK", "0")))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -76,7 +78,7 @@ def main(argv=None):
     if world > 1:
         from docker_dist_nn_amd.parallel.groups import build_mesh, init_distributed
 
-        init_distributed("nccl")
+        init_distributed(os.environ.get("DNN_DIST_BACKEND", "nccl"))
     pp, dp = parse_parallelism(a.parallelism, n)
     planner = Planner()
     if pp is None:
