@@ -41,13 +41,50 @@ def _try_import():
             _err = e
 
 
+class _SyncDebug:
+    """``DNN_SYNC_DEBUG=1``: every native call is followed by a device synchronize, so an
+    asynchronous kernel fault is reported at the op that launched it (with its name) instead of
+    at some later, unrelated sync. Debug only -- it serialises host and device. Calls made while
+    a HIP graph is being captured are not synchronised (sync is illegal during capture)."""
+
+    _NO_SYNC = {"GraphExec", "device_sync"}
+
+    def __init__(self, mod):
+        self._mod = mod
+
+    def __getattr__(self, name):
+        f = getattr(self._mod, name)
+        if name in self._NO_SYNC or not callable(f):
+            return f
+
+        def call(*a, **k):
+            out = f(*a, **k)
+            if not torch.cuda.is_current_stream_capturing():
+                try:
+                    self._mod.device_sync()
+                except RuntimeError as e:
+                    raise RuntimeError(f"DNN_SYNC_DEBUG: device error after native.{name}: {e}") \
+                        from e
+            return out
+
+        return call
+
+
+_debug = None
+
+
 def native():
     """Return the native module or raise a loud error explaining why it is unavailable."""
+    global _debug
     _try_import()
     if _mod is None:
         raise RuntimeError(
             "docker_dist_nn_amd native extension is not available "
             f"({_err}); build it with `python -m docker_dist_nn_amd._build`")
+    if os.environ.get("DNN_SYNC_DEBUG", "0") == "1":
+        if _debug is None:
+            _debug = _SyncDebug(_mod)
+        return _debug
     return _mod
 
 

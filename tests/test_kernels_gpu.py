@@ -325,3 +325,23 @@ def test_fused_linear_xent_matches_unfused(dev, M, Np):
     torch.testing.assert_close(lp.sum(), lp2.sum(), rtol=1e-4, atol=1e-3)
     assert int(cor.item()) == int(cor2.item())
     torch.testing.assert_close(cs, dz.float().view(M // bm, bm, Np).sum(1), rtol=1e-5, atol=1e-5)
+
+
+def test_sync_debug_mode(dev, monkeypatch):
+    """DNN_SYNC_DEBUG=1 routes every native call through a synchronising proxy; results are
+    unchanged and host-side validation errors still surface with their message."""
+    import docker_dist_nn_amd.utils.native as nat
+
+    monkeypatch.setenv("DNN_SYNC_DEBUG", "1")
+    monkeypatch.setattr(nat, "_debug", None)
+    assert type(nat.native()).__name__ == "_SyncDebug"
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(128, 64, generator=g).to(torch.bfloat16).to(dev)
+    w = torch.randn(64, 64, generator=g).to(torch.bfloat16).to(dev)
+    b = torch.randn(64, generator=g).to(dev)
+    y = torch.empty(128, 64, dtype=torch.bfloat16, device=dev)
+    ops.linear_fwd(x, w, b, y, act="relu")
+    ref = torch.relu(x.float() @ w.float().t() + b)
+    torch.testing.assert_close(y.float(), ref, rtol=2e-2, atol=2e-2)
+    with pytest.raises((RuntimeError, ValueError)):
+        ops.gemm(x, w, y, layout_a=KMAJ, layout_b=KMAJ, M=128, N=64, K=63)
