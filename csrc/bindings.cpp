@@ -7,9 +7,12 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <tuple>
+#include <vector>
 
 #include "kernels/elementwise.hpp"
 #include "kernels/gemm.hpp"
@@ -46,7 +49,7 @@ PYBIND11_MODULE(_native, m) {
          uintptr_t bias, uintptr_t aux, long ld_aux, int M, int N, int K, int act, int accumulate,
          int layout_a, int layout_b, int out_f32, int bm, int bn, int splits, uintptr_t stream,
          uintptr_t colsum, long ld_colsum, uintptr_t xent_labels, int n_cls, float xent_scale,
-         uintptr_t loss_part, uintptr_t correct, int k_total) {
+         uintptr_t loss_part, uintptr_t correct, int k_total, int stages) {
         GemmParams p{};
         p.k_total = k_total;
         p.colsum = P<float>(colsum);
@@ -71,7 +74,7 @@ PYBIND11_MODULE(_native, m) {
         p.K = K;
         p.act = act;
         p.accumulate = accumulate;
-        check(dnn::gemm_bf16(p, layout_a, layout_b, out_f32, bm, bn, splits, S(stream)),
+        check(dnn::gemm_bf16(p, layout_a, layout_b, out_f32, bm, bn, splits, S(stream), stages),
               "gemm_bf16");
       },
       py::arg("a"), py::arg("lda"), py::arg("b"), py::arg("ldb"), py::arg("c"), py::arg("ldc"),
@@ -80,7 +83,9 @@ PYBIND11_MODULE(_native, m) {
       py::arg("layout_b"), py::arg("out_f32"), py::arg("bm"), py::arg("bn"), py::arg("splits"),
       py::arg("stream"), py::arg("colsum") = 0, py::arg("ld_colsum") = 0,
       py::arg("xent_labels") = 0, py::arg("n_cls") = 0, py::arg("xent_scale") = 0.f,
-      py::arg("loss_part") = 0, py::arg("correct") = 0, py::arg("k_total") = 0);
+      py::arg("loss_part") = 0, py::arg("correct") = 0, py::arg("k_total") = 0,
+      py::arg("stages") = 0);
+  m.def("gemm_default_stages", &dnn::default_stages);
 
   m.def(
       "gemm_bf16_streamk",
@@ -139,6 +144,21 @@ PYBIND11_MODULE(_native, m) {
     check(dnn::reduce_slabs(P<const float>(src), stride, n_src, n, scale, P<float>(out),
                             accumulate, S(stream)),
           "reduce_slabs");
+  });
+  // jobs: sequence of (src, stride, n_src, n, out, scale, accumulate); > 16 jobs -> several
+  // launches
+  m.def("reduce_multi", [](const std::vector<std::tuple<uintptr_t, long, int, long, uintptr_t,
+                                                        float, int>>& jobs,
+                           uintptr_t stream) {
+    std::vector<dnn::ReduceJob> J;
+    J.reserve(jobs.size());
+    for (const auto& t : jobs)
+      J.push_back({P<const float>(std::get<0>(t)), std::get<1>(t), std::get<3>(t),
+                   P<float>(std::get<4>(t)), std::get<2>(t), std::get<5>(t), std::get<6>(t)});
+    for (size_t k = 0; k < J.size(); k += dnn::REDUCE_MAX_JOBS) {
+      const int n = (int)std::min<size_t>(dnn::REDUCE_MAX_JOBS, J.size() - k);
+      check(dnn::reduce_multi(J.data() + k, n, S(stream)), "reduce_multi");
+    }
   });
   m.def("sgd_update", [](uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t shadow, long n,
                          float lr, float mu, float wd, uintptr_t stream) {

@@ -8,6 +8,7 @@
 //                    (/root/reference/src/run_grpc_inference.py:192-193, 208-209)
 //   colsum_partial : bias gradient partial column sums of dZ
 //   reduce_slabs   : split-K slab / partial reduction into the flat gradient buffer
+//   reduce_multi   : all of a stage's slab / partial reductions in one launch
 //   sgd / adam     : fused multi-tensor optimizer over the flat fp32 master buffer, refreshing
 //                    the bf16 shadow weights in the same pass
 //   pack_bf16      : fp32 host data -> padded bf16 device layout (and back)
@@ -22,7 +23,8 @@ namespace dnn {
 // dz = (softmax(logits) - onehot(label)) * scale in the first n_cls columns, 0 elsewhere.
 // Rows whose label is < 0 are padding: dz = 0 and no loss. The block's loss sum goes to
 // loss_part[blockIdx.x] (summed later in a fixed order: bitwise reproducible, no float
-// atomics); the correct-prediction count uses one integer atomic per block (exact).
+// atomics); the correct-prediction count likewise goes to correct[blockIdx.x] (written, not
+// accumulated, so nothing has to be zeroed per step).
 // ------------------------------------------------------------------------------------------
 constexpr int XENT_ROWS_PER_WAVE = 16;
 constexpr int XENT_ROWS_PER_BLOCK = 4 * XENT_ROWS_PER_WAVE;
@@ -119,7 +121,7 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
     const float l = (s_loss[0] + s_loss[1]) + (s_loss[2] + s_loss[3]);
     const int cc = s_corr[0] + s_corr[1] + s_corr[2] + s_corr[3];
     if (loss_part) loss_part[blockIdx.x] = l;
-    if (correct && cc) atomicAdd(correct, cc);
+    if (correct) correct[blockIdx.x] = cc;
   }
   if (colsum) {
     for (int col = threadIdx.x; col < width; col += 256)
@@ -320,6 +322,82 @@ int reduce_slabs(const float* src, long stride, int n_src, long n, float scale, 
   else
     hipLaunchKernelGGL(reduce_slabs_kernel<1>, grid(256), dim3(256), 0, stream, src, stride, n_src,
                        n4, scale, out, accumulate);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
+// ------------------------------------------------------------------------------------------
+// Multi-job reduce: every split-K weight slab set and bias-partial set of a stage in ONE
+// launch (they are small and latency-bound: one launch each cost ~5 us). The job table travels
+// by value in the kernel arguments; blocks are assigned to jobs by a prefix table, and each
+// job runs the TX x TY scheme of reduce_slabs_kernel with its own TY (same fixed summation
+// order, so results are bitwise identical to reduce_slabs).
+// ------------------------------------------------------------------------------------------
+template <int TY>
+__device__ __forceinline__ void reduce_block(const ReduceJob& jb, long blk, f32x4_t LDS_AS* red) {
+  constexpr int TX = 256 / TY;
+  const int tx = threadIdx.x % TX, ty = threadIdx.x / TX;
+  const long i = blk * TX + tx;
+  const long n4 = jb.n / 4;
+  f32x4_t a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
+  if (i < n4) {
+    const float* p = jb.src + i * 4;
+    const long stride = jb.stride;
+    const int n_src = jb.n_src;
+    int s = ty;
+    for (; s + 3 * TY < n_src; s += 4 * TY) {
+      a0 += *(const f32x4_t*)(p + (long)s * stride);
+      a1 += *(const f32x4_t*)(p + (long)(s + TY) * stride);
+      a2 += *(const f32x4_t*)(p + (long)(s + 2 * TY) * stride);
+      a3 += *(const f32x4_t*)(p + (long)(s + 3 * TY) * stride);
+    }
+    for (; s < n_src; s += TY) a0 += *(const f32x4_t*)(p + (long)s * stride);
+  }
+  red[ty * TX + tx] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (ty == 0 && i < n4) {
+    f32x4_t t = red[tx];
+#pragma unroll
+    for (int k = 1; k < TY; ++k) t += red[k * TX + tx];
+    t *= jb.scale;
+    if (jb.accumulate) t += *(const f32x4_t*)(jb.out + i * 4);
+    *(f32x4_t*)(jb.out + i * 4) = t;
+  }
+}
+
+static __host__ __device__ int reduce_ty(int n_src) { return n_src >= 16 ? 16 : n_src >= 4 ? 4 : 1; }
+
+__global__ __launch_bounds__(256) void reduce_multi_kernel(ReduceJobs jobs) {
+  __shared__ f32x4_t red_s[256];
+  f32x4_t LDS_AS* red = (f32x4_t LDS_AS*)red_s;
+  int j = 0;
+  while (j + 1 < jobs.n_jobs && (int)blockIdx.x >= jobs.block_start[j + 1]) ++j;
+  const ReduceJob& jb = jobs.job[j];
+  const long blk = (long)blockIdx.x - jobs.block_start[j];
+  switch (reduce_ty(jb.n_src)) {
+    case 16: reduce_block<16>(jb, blk, red); break;
+    case 4: reduce_block<4>(jb, blk, red); break;
+    default: reduce_block<1>(jb, blk, red); break;
+  }
+}
+
+int reduce_multi(const ReduceJob* job, int n_jobs, hipStream_t stream) {
+  if (n_jobs <= 0 || n_jobs > REDUCE_MAX_JOBS) return -1;
+  ReduceJobs J{};
+  J.n_jobs = n_jobs;
+  int blocks = 0;
+  for (int k = 0; k < n_jobs; ++k) {
+    const ReduceJob& jb = job[k];
+    if (jb.n <= 0 || jb.n % 4 || jb.n_src <= 0 || (jb.n_src > 1 && jb.stride % 4)) return -1;
+    if ((((uintptr_t)jb.src) | ((uintptr_t)jb.out)) & 15) return -5;
+    J.job[k] = jb;
+    J.block_start[k] = blocks;
+    const int tx = 256 / reduce_ty(jb.n_src);
+    const long b = (jb.n / 4 + tx - 1) / tx;
+    if (b > (1L << 30) - blocks) return -1;
+    blocks += (int)b;
+  }
+  J.block_start[n_jobs] = blocks;
+  hipLaunchKernelGGL(reduce_multi_kernel, dim3(blocks), dim3(256), 0, stream, J);
   return hipGetLastError() == hipSuccess ? 0 : -9;
 }
 

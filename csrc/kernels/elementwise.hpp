@@ -18,6 +18,24 @@ int colsum_partial(const uint16_t* x, long ld, int rows, int cols, int n_part, f
                    hipStream_t stream);
 int reduce_slabs(const float* src, long stride, int n_src, long n, float scale, float* out,
                  int accumulate, hipStream_t stream);
+// One reduction of reduce_multi: out[i] (+)= scale * sum_{s < n_src} src[s * stride + i].
+struct ReduceJob {
+  const float* src;
+  long stride;
+  long n;  // multiple of 4
+  float* out;
+  int n_src;
+  float scale;
+  int accumulate;
+};
+constexpr int REDUCE_MAX_JOBS = 16;
+struct ReduceJobs {  // passed by value as the kernel argument
+  ReduceJob job[REDUCE_MAX_JOBS];
+  int block_start[REDUCE_MAX_JOBS + 1];
+  int n_jobs;
+};
+// All jobs in one launch, each bitwise identical to reduce_slabs on the same inputs.
+int reduce_multi(const ReduceJob* job, int n_jobs, hipStream_t stream);
 int sgd_update(float* p, const float* g, float* mom, uint16_t* shadow, long n, float lr, float mu,
                float wd, hipStream_t stream);
 int adam_update(float* p, const float* g, float* m, float* v, uint16_t* shadow, long n, float lr,

@@ -32,27 +32,56 @@ __device__ __forceinline__ int k_swz(int r) { return (r >> 1) & 7; }
 
 // MNMAJ image: [64 k-rows][T cols] bf16 (T*2-byte rows). A transposed read by one 32-lane half
 // touches 8 k-rows x 32 B; the XOR (always even, so 32-B column pairs stay together) spreads the
-// 8 rows over distinct 32-B bank positions.
+// 8 rows over distinct 32-B bank positions. For T >= 128 a row spans >= one 256-B bank row, so
+// the T = 128 pattern serves T = 256 too (the XOR only flips chunk bits 1..3).
 template <int T>
-__device__ __forceinline__ int mn_swz(int r);
-template <>
-__device__ __forceinline__ int mn_swz<128>(int r) {
+__device__ __forceinline__ int mn_swz(int r) {
+  static_assert(T == 64 || T == 128 || T == 256, "MNMAJ tile width");
+  if constexpr (T == 64) return (((r >> 1) & 1) | (((r >> 3) & 1) << 1)) << 1;
   return ((r & 3) | (((r >> 3) & 1) << 2)) << 1;
 }
-template <>
-__device__ __forceinline__ int mn_swz<64>(int r) {
-  return (((r >> 1) & 1) | (((r >> 3) & 1) << 1)) << 1;
-}
+
+// ---- tile configurations ----------------------------------------------------------------------
+// BM x BN output tile computed by WM x WN waves (NT = 64*WM*WN threads), each wave owning an
+// (BM/WM) x (BN/WN) sub-tile of 16x16 MFMA fragments; NS = LDS pipeline stages (NS-1 tiles in
+// flight while one is consumed). 4-wave tiles (<= 128x128) run 2..4 per CU; the 8-wave 256-row
+// /-column tiles halve the bytes staged into LDS per FLOP (the GEMMs of this engine are bound
+// by the global->LDS fill rate, see profiles/) at one workgroup per CU.
+template <int A, int B>
+struct cmax {
+  static constexpr int v = A > B ? A : B;
+};
+
+template <int BM_, int BN_, int WM_, int WN_, int NS_>
+struct Cfg {
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, NS = NS_;
+  static constexpr int NW = WM * WN, NT = 64 * NW;
+  static constexpr int SM = BM / WM, SN = BN / WN, FM = SM / 16, FN = SN / 16;
+  static constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
+  // LDS-DMA instructions one wave issues per stage (A + B): the vmcnt unit of the pipeline
+  static constexpr int PER_STAGE = (BM + BN) / (8 * NW);
+  // epilogue: fp32 staging of EPI_ROWS rows at a time (whole tile when it fits)
+  static constexpr int CS_LD = BN + 4;
+  static constexpr int EPI_ROWS = NW == 4 ? BM : SM;
+  static constexpr int CHUNKS = BM / EPI_ROWS, WPC = EPI_ROWS / SM;  // wave-rows per chunk
+  static constexpr int CS_BYTES = EPI_ROWS * CS_LD * 4;
+  static constexpr int RED_BYTES = NT * 32;  // colsum partial staging
+  static constexpr int SMEM = cmax<cmax<NS * STAGE, CS_BYTES + 64>::v, RED_BYTES>::v;
+  static_assert(FM >= 1 && FN >= 1 && SM % 16 == 0 && SN % 16 == 0, "wave sub-tile");
+  static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "LDS-DMA pieces per wave");
+  static_assert(NT % (BN / 8) == 0 && (EPI_ROWS * (BN / 8)) % NT == 0, "epilogue mapping");
+  static_assert(SMEM <= 160 * 1024, "LDS budget");
+};
 
 // Stage one operand tile (T entries of the M/N dim x 64 of K) into LDS with LDS-DMA.
-// Tile bytes = T*128 = T/8 KiB pieces; each of the 4 waves issues T/32 of them.
-template <int L, int T>
+// Tile bytes = T*128 = T/8 KiB pieces; each of the NW waves issues T/(8*NW) of them.
+template <int L, int T, int NW>
 __device__ __forceinline__ void stage_tile(const u16* __restrict__ g, long ld, int mn0, int k0,
                                            char LDS_AS* dst, int wave, int lane) {
-  constexpr int NI = T / 32;
+  constexpr int NI = T / (8 * NW);
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
-    const int piece = i * 4 + wave;
+    const int piece = i * NW + wave;
     const int chunk = piece * 64 + lane;
     const u16* src;
     if constexpr (L == KMAJ) {
@@ -95,102 +124,129 @@ __device__ __forceinline__ bf16x8_t load_frag(const char LDS_AS* tile, int blk, 
   }
 }
 
-template <int A, int B>
-struct cmax {
-  static constexpr int v = A > B ? A : B;
-};
-
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
 }
 
-template <int BM, int BN>
-struct TileCfg {
-  static constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
-  static constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
-  static constexpr int CS_LD = BN + 4;  // fp32 epilogue staging row stride (floats)
-  static constexpr int CS_BYTES = BM * CS_LD * 4;
-  static constexpr int SMEM = cmax<2 * STAGE, CS_BYTES + 64>::v;  // +64: epilogue reductions
-};
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 
-// acc (+)= A[m0:m0+BM, k] . B[k, n0:n0+BN] over k-steps [kbase, kbase + 64*nk): LDS-DMA
-// double buffering, one barrier per 64-deep k-step. acc is zeroed first. Ends with every
-// wave past a barrier, so the caller may reuse the LDS.
-template <int BM, int BN, int LA, int LB>
+// Workgroup barrier WITHOUT the release fence of __syncthreads(): that fence waits for
+// vmcnt(0), i.e. for every LDS-DMA load in flight, which would serialise the pipeline. LDS
+// hazards are handled explicitly instead: own ds_reads done (lgkmcnt(0)) + own LDS-DMA tile
+// landed (wait_stage) before the barrier. The "memory" clobber keeps the compiler from moving
+// LDS accesses across it.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Wait until at most `after` (0 .. NS-2, runtime) later stages are still in flight.
+template <int NS, int PS>
+__device__ __forceinline__ void wait_stage(int after) {
+  if constexpr (NS >= 4) {
+    if (after >= 2) {
+      wait_vmcnt<2 * PS>();
+      return;
+    }
+  }
+  if constexpr (NS >= 3) {
+    if (after >= 1) {
+      wait_vmcnt<PS>();
+      return;
+    }
+  }
+  wait_vmcnt<0>();
+}
+
+// acc (+)= A[m0:m0+BM, k] . B[k, n0:n0+BN] over k-steps [kbase, kbase + 64*nk) with an
+// NS-deep LDS-DMA ring and ONE barrier per 64-deep k-step:
+//   top of step kt: own loads of tile kt landed (vmcnt) -> barrier (everyone's landed, and
+//   everyone finished step kt-1, so its buffer is free) -> issue tile kt+NS-1 into that
+//   buffer -> MFMA on tile kt.
+// acc is zeroed first; ends with every wave past a barrier, so the caller may reuse the LDS.
+template <class C, int LA, int LB>
 __device__ __forceinline__ void mma_tile(const GemmParams& p, int m0, int n0, int kbase, int nk,
-                                         char LDS_AS* lds,
-                                         f32x4_t (&acc)[TileCfg<BM, BN>::FM][TileCfg<BM, BN>::FN],
+                                         char LDS_AS* lds, f32x4_t (&acc)[C::FM][C::FN],
                                          int wave, int lane) {
-  using C = TileCfg<BM, BN>;
-  constexpr int FM = C::FM, FN = C::FN, A_BYTES = C::A_BYTES, STAGE = C::STAGE;
-  const int wm = wave >> 1, wn = wave & 1;
+  constexpr int FM = C::FM, FN = C::FN, A_BYTES = C::A_BYTES, STAGE = C::STAGE, NS = C::NS;
+  const int wm = wave / C::WN, wn = wave % C::WN;
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  stage_tile<LA, BM>(p.A, p.lda, m0, kbase, lds, wave, lane);
-  stage_tile<LB, BN>(p.B, p.ldb, n0, kbase, lds + A_BYTES, wave, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) {
-      char LDS_AS* nxt = lds + (buf ^ 1) * STAGE;
-      const int k0 = kbase + (kt + 1) * 64;
-      stage_tile<LA, BM>(p.A, p.lda, m0, k0, nxt, wave, lane);
-      stage_tile<LB, BN>(p.B, p.ldb, n0, k0, nxt + A_BYTES, wave, lane);
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s) {
+    if (s < nk) {
+      stage_tile<LA, C::BM, C::NW>(p.A, p.lda, m0, kbase + s * 64, lds + s * STAGE, wave, lane);
+      stage_tile<LB, C::BN, C::NW>(p.B, p.ldb, n0, kbase + s * 64, lds + s * STAGE + A_BYTES,
+                                   wave, lane);
     }
-    const char LDS_AS* sa = lds + buf * STAGE;
+  }
+  int rd = 0, wr = NS - 1;  // ring slots of tile kt and of tile kt + NS - 1
+  for (int kt = 0; kt < nk; ++kt) {
+    wait_stage<NS, C::PER_STAGE>(min(nk - 1 - kt, NS - 2));
+    lds_barrier();
+    if (kt + NS - 1 < nk) {
+      char LDS_AS* nxt = lds + wr * STAGE;
+      const int k0 = kbase + (kt + NS - 1) * 64;
+      stage_tile<LA, C::BM, C::NW>(p.A, p.lda, m0, k0, nxt, wave, lane);
+      stage_tile<LB, C::BN, C::NW>(p.B, p.ldb, n0, k0, nxt + A_BYTES, wave, lane);
+    }
+    const char LDS_AS* sa = lds + rd * STAGE;
     const char LDS_AS* sb = sa + A_BYTES;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       bf16x8_t a[FM], b[FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i) a[i] = load_frag<LA, BM>(sa, wm * FM + i, s, lane);
+      for (int i = 0; i < FM; ++i) a[i] = load_frag<LA, C::BM>(sa, wm * FM + i, s, lane);
 #pragma unroll
-      for (int j = 0; j < FN; ++j) b[j] = load_frag<LB, BN>(sb, wn * FN + j, s, lane);
+      for (int j = 0; j < FN; ++j) b[j] = load_frag<LB, C::BN>(sb, wn * FN + j, s, lane);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    rd = rd + 1 == NS ? 0 : rd + 1;
+    wr = wr + 1 == NS ? 0 : wr + 1;
   }
+  __syncthreads();
 }
 
-// 16x16 accumulator fragments -> fp32 [BM][CS_LD] LDS tile (C/D map: col = lane&15,
-// row = 4*(lane>>4) + r).
-template <int BM, int BN>
-__device__ __forceinline__ void acc_to_lds(
-    const f32x4_t (&acc)[TileCfg<BM, BN>::FM][TileCfg<BM, BN>::FN], float LDS_AS* cs, int wave,
-    int lane) {
-  using C = TileCfg<BM, BN>;
-  const int wm = wave >> 1, wn = wave & 1;
+// Accumulator fragments of the waves in epilogue chunk `chunk` -> fp32 [EPI_ROWS][CS_LD] LDS
+// tile (C/D map: col = lane&15, row = 4*(lane>>4) + r).
+template <class C>
+__device__ __forceinline__ void acc_to_lds(const f32x4_t (&acc)[C::FM][C::FN],
+                                           float LDS_AS* cs, int chunk, int wave, int lane) {
+  const int wm = wave / C::WN, wn = wave % C::WN;
+  if (wm / C::WPC != chunk) return;
+  const int rbase = (wm % C::WPC) * C::SM;
 #pragma unroll
   for (int i = 0; i < C::FM; ++i)
 #pragma unroll
     for (int j = 0; j < C::FN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = wm * C::WM + i * 16 + (lane >> 4) * 4 + r;
-        const int col = wn * C::WN + j * 16 + (lane & 15);
+        const int row = rbase + i * 16 + (lane >> 4) * 4 + r;
+        const int col = wn * C::SN + j * 16 + (lane & 15);
         cs[row * C::CS_LD + col] = acc[i][j][r];
       }
 }
 
 // Fused softmax cross-entropy over the fp32 logits tile in LDS (the whole padded row lives in
-// this tile: N == BN). Thread r < BM owns row r: adds the bias, finds max / argmax (lowest index,
-// np.argmax rule) / log-sum-exp over the n_cls valid columns, and overwrites the row with
-// dz = (p - onehot) * scale (0 in padding columns and for label < 0 padding rows). Block loss
-// and correct-count go to loss_part[tile_m] / *correct.
-template <int BM, int BN>
+// this tile: N == BN; 4-wave tiles, one epilogue chunk). Thread r < BM owns row r: adds the
+// bias, finds max / argmax (lowest index, np.argmax rule) / log-sum-exp over the n_cls valid
+// columns, and overwrites the row with dz = (p - onehot) * scale (0 in padding columns and for
+// label < 0 padding rows). Block loss and correct-count go to loss_part[tile_m] /
+// correct[tile_m].
+template <class C>
 __device__ __forceinline__ void xent_rows(const GemmParams& p, float LDS_AS* cs, int m0) {
-  constexpr int CS_LD = TileCfg<BM, BN>::CS_LD;
+  static_assert(C::NW == 4 && C::CHUNKS == 1, "fused cross-entropy runs on 4-wave tiles");
+  constexpr int BM = C::BM, BN = C::BN, CS_LD = C::CS_LD;
   // scratch after the staging tile (all LDS lives in the kernel's single __shared__ array)
   float LDS_AS* s_loss = cs + BM * CS_LD;
   int LDS_AS* s_corr = (int LDS_AS*)(s_loss + 4);
@@ -237,16 +293,15 @@ __device__ __forceinline__ void xent_rows(const GemmParams& p, float LDS_AS* cs,
   if (threadIdx.x == 0) {
     if (p.loss_part) p.loss_part[m0 / BM] = (s_loss[0] + s_loss[1]) + (s_loss[2] + s_loss[3]);
     const int cc = s_corr[0] + s_corr[1] + s_corr[2] + s_corr[3];
-    if (p.correct && cc) atomicAdd(p.correct, cc);
+    if (p.correct) p.correct[m0 / BM] = cc;
   }
 }
 
-template <int BM, int BN, int LA, int LB, bool OUT_F32>
-__global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmParams p, int tiles_n, int tiles_m,
-                                                        int nwg) {
-  using TC = TileCfg<BM, BN>;
-  constexpr int FM = TC::FM, FN = TC::FN, CS_LD = TC::CS_LD;
-  __shared__ __attribute__((aligned(16))) char smem[TC::SMEM];
+template <class C, int LA, int LB, bool OUT_F32>
+__global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(GemmParams p, int tiles_n, int tiles_m,
+                                                          int nwg) {
+  constexpr int BM = C::BM, BN = C::BN, NT = C::NT, CS_LD = C::CS_LD;
+  __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
   char LDS_AS* lds = (char LDS_AS*)smem;
 
   // XCD-aware bijective remap: hardware deals block b to XCD group b%8; give each group a
@@ -270,76 +325,80 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmParams p, int tiles_
     nk = p.K >> 6;
   }
 
-  f32x4_t acc[FM][FN];
-  mma_tile<BM, BN, LA, LB>(p, m0, n0, kbase, nk, lds, acc, wave, lane);
+  f32x4_t acc[C::FM][C::FN];
+  mma_tile<C, LA, LB>(p, m0, n0, kbase, nk, lds, acc, wave, lane);
 
-  // ---- epilogue: accumulators -> LDS (fp32) -> 16-B row chunks to global --------------------
+  // ---- epilogue: accumulators -> LDS (fp32, EPI_ROWS at a time) -> 16-B row chunks -----------
   float LDS_AS* cs = (float LDS_AS*)lds;
-  acc_to_lds<BM, BN>(acc, cs, wave, lane);
-  __syncthreads();
-
-  bool xent = false;
-  if constexpr (!OUT_F32) {
-    if (p.xent_labels) {  // uniform: fused softmax-CE, one thread per row of the tile
-      xent = true;
-      xent_rows<BM, BN>(p, cs, m0);
-      __syncthreads();
-    }
-  }
-
   constexpr int CPR = BN / 8;
-  constexpr int ITER = BM * CPR / 256;
+  constexpr int ITER = C::EPI_ROWS * CPR / NT;
   float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // this thread's column chunk is
-                                                            // fixed: 256 % CPR == 0
-#pragma unroll 2
-  for (int it = 0; it < ITER; ++it) {
-    const int idx = threadIdx.x + it * 256;
-    const int row = idx / CPR, col = (idx % CPR) * 8;
-    const f32x4_t v0 = *(const f32x4_t LDS_AS*)(cs + row * CS_LD + col);
-    const f32x4_t v1 = *(const f32x4_t LDS_AS*)(cs + row * CS_LD + col + 4);
-    float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-    const long gm = m0 + row, gn = n0 + col;
-    if (p.bias && !xent) {
-      const f32x4_t b0 = *(const f32x4_t*)(p.bias + gn);
-      const f32x4_t b1 = *(const f32x4_t*)(p.bias + gn + 4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] += b0[e];
-        v[e + 4] += b1[e];
+                                                            // fixed: NT % CPR == 0
+#pragma unroll 1
+  for (int chunk = 0; chunk < C::CHUNKS; ++chunk) {
+    if (chunk) __syncthreads();  // previous chunk's stores have read the staging tile
+    acc_to_lds<C>(acc, cs, chunk, wave, lane);
+    __syncthreads();
+
+    bool xent = false;
+    if constexpr (!OUT_F32 && C::NW == 4) {
+      if (p.xent_labels) {  // uniform: fused softmax-CE, one thread per row of the tile
+        xent = true;
+        xent_rows<C>(p, cs, m0);
+        __syncthreads();
       }
     }
-    if constexpr (OUT_F32) {
-      float* c = (float*)p.C + (long)split * p.c_split_stride + gm * p.ldc + gn;
-      if (!p.accumulate && p.act != ACT_LINEAR) {
+    const int r0 = chunk * C::EPI_ROWS;
+#pragma unroll 2
+    for (int it = 0; it < ITER; ++it) {
+      const int idx = threadIdx.x + it * NT;
+      const int row = idx / CPR, col = (idx % CPR) * 8;
+      const f32x4_t v0 = *(const f32x4_t LDS_AS*)(cs + row * CS_LD + col);
+      const f32x4_t v1 = *(const f32x4_t LDS_AS*)(cs + row * CS_LD + col + 4);
+      float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      const long gm = m0 + r0 + row, gn = n0 + col;
+      if (p.bias && !xent) {
+        const f32x4_t b0 = *(const f32x4_t*)(p.bias + gn);
+        const f32x4_t b1 = *(const f32x4_t*)(p.bias + gn + 4);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = act_fwd(v[e], p.act);
+        for (int e = 0; e < 4; ++e) {
+          v[e] += b0[e];
+          v[e + 4] += b1[e];
+        }
       }
-      f32x4_t o0 = {v[0], v[1], v[2], v[3]}, o1 = {v[4], v[5], v[6], v[7]};
-      if (p.accumulate) {
-        o0 += *(const f32x4_t*)c;
-        o1 += *(const f32x4_t*)(c + 4);
-      }
-      *(f32x4_t*)c = o0;
-      *(f32x4_t*)(c + 4) = o1;
-    } else {
-      if (xent) {
-        // dz already computed in LDS
-      } else if (p.aux) {
-        const bf16x8_t y = *(const bf16x8_t*)(p.aux + gm * p.ld_aux + gn);
+      if constexpr (OUT_F32) {
+        float* c = (float*)p.C + (long)split * p.c_split_stride + gm * p.ldc + gn;
+        if (!p.accumulate && p.act != ACT_LINEAR) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = act_bwd(v[e], bf2f((u16)y[e]), p.act);
+          for (int e = 0; e < 8; ++e) v[e] = act_fwd(v[e], p.act);
+        }
+        f32x4_t o0 = {v[0], v[1], v[2], v[3]}, o1 = {v[4], v[5], v[6], v[7]};
+        if (p.accumulate) {
+          o0 += *(const f32x4_t*)c;
+          o1 += *(const f32x4_t*)(c + 4);
+        }
+        *(f32x4_t*)c = o0;
+        *(f32x4_t*)(c + 4) = o1;
       } else {
+        if (xent) {
+          // dz already computed in LDS
+        } else if (p.aux) {
+          const bf16x8_t y = *(const bf16x8_t*)(p.aux + gm * p.ld_aux + gn);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = act_fwd(v[e], p.act);
-      }
-      bf16x8_t o;
+          for (int e = 0; e < 8; ++e) v[e] = act_bwd(v[e], bf2f((u16)y[e]), p.act);
+        } else {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const u16 h = f2bf(v[e]);
-        o[e] = (short)h;
-        csum[e] += bf2f(h);
+          for (int e = 0; e < 8; ++e) v[e] = act_fwd(v[e], p.act);
+        }
+        bf16x8_t o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const u16 h = f2bf(v[e]);
+          o[e] = (short)h;
+          csum[e] += bf2f(h);
+        }
+        *(bf16x8_t*)((u16*)p.C + gm * p.ldc + gn) = o;
       }
-      *(bf16x8_t*)((u16*)p.C + gm * p.ldc + gn) = o;
     }
   }
   if constexpr (!OUT_F32) {
@@ -354,7 +413,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemmParams p, int tiles_
         const float LDS_AS* rf = (const float LDS_AS*)lds;
         float t = 0.f;
 #pragma unroll 4
-        for (int r = 0; r < 256 / CPR; ++r) t += rf[(r * CPR + cc) * 8 + e];
+        for (int r = 0; r < NT / CPR; ++r) t += rf[(r * CPR + cc) * 8 + e];
         p.colsum[(long)tm * p.ld_colsum + n0 + col] = t;
       }
     }
@@ -373,7 +432,7 @@ template <int BM, int BN, int LA, int LB>
 __global__ __launch_bounds__(256) void gemm_bf16_streamk_kernel(GemmParams p, int tiles_n,
                                                                 int ksteps, int ipw, int total,
                                                                 int nwg, float* part) {
-  using TC = TileCfg<BM, BN>;
+  using TC = Cfg<BM, BN, 2, 2, 2>;
   constexpr int FM = TC::FM, FN = TC::FN, CS_LD = TC::CS_LD;
   __shared__ __attribute__((aligned(16))) char smem[TC::SMEM];
   char LDS_AS* lds = (char LDS_AS*)smem;
@@ -387,9 +446,9 @@ __global__ __launch_bounds__(256) void gemm_bf16_streamk_kernel(GemmParams p, in
     const int k1 = min(ksteps, k0 + (it_end - it));
     const int tn = tile % tiles_n, tm = tile / tiles_n;
     f32x4_t acc[FM][FN];
-    mma_tile<BM, BN, LA, LB>(p, tm * BM, tn * BN, k0 * 64, k1 - k0, lds, acc, wave, lane);
+    mma_tile<TC, LA, LB>(p, tm * BM, tn * BN, k0 * 64, k1 - k0, lds, acc, wave, lane);
     float LDS_AS* cs = (float LDS_AS*)lds;
-    acc_to_lds<BM, BN>(acc, cs, wave, lane);
+    acc_to_lds<TC>(acc, cs, 0, wave, lane);
     __syncthreads();
     float* dst = part + ((long)w * 2 + seg) * (BM * BN);
     constexpr int C4 = BN / 4;
@@ -465,9 +524,9 @@ int gemm_bf16_streamk(const GemmParams& p, int layout_a, int layout_b, int bm, i
 
 typedef void (*gemm_fn)(GemmParams, int, int, int);
 
-template <int BM, int BN>
+template <class C>
 static gemm_fn pick_layout(int la, int lb, int f32) {
-#define DNN_G(LA, LB, F) gemm_bf16_kernel<BM, BN, LA, LB, F>
+#define DNN_G(LA, LB, F) gemm_bf16_kernel<C, LA, LB, F>
   if (la == KMAJ && lb == KMAJ) return f32 ? DNN_G(KMAJ, KMAJ, true) : DNN_G(KMAJ, KMAJ, false);
   if (la == KMAJ && lb == MNMAJ) return f32 ? DNN_G(KMAJ, MNMAJ, true) : DNN_G(KMAJ, MNMAJ, false);
   if (la == MNMAJ && lb == KMAJ) return f32 ? DNN_G(MNMAJ, KMAJ, true) : DNN_G(MNMAJ, KMAJ, false);
@@ -475,10 +534,26 @@ static gemm_fn pick_layout(int la, int lb, int f32) {
 #undef DNN_G
 }
 
+// 4-wave tiles: any NS in 2..4; 8-wave tiles: NS = 2 (a third 64-KiB stage does not fit)
+template <int BM, int BN>
+static gemm_fn pick4(int ns, int la, int lb, int f32) {
+  return ns == 2   ? pick_layout<Cfg<BM, BN, 2, 2, 2>>(la, lb, f32)
+         : ns == 3 ? pick_layout<Cfg<BM, BN, 2, 2, 3>>(la, lb, f32)
+                   : pick_layout<Cfg<BM, BN, 2, 2, 4>>(la, lb, f32);
+}
+
+bool gemm_tile_supported(int bm, int bn) {
+  const bool small = (bm == 64 || bm == 128) && (bn == 64 || bn == 128);
+  const bool big = (bm == 256 && (bn == 64 || bn == 128 || bn == 256)) || (bm == 128 && bn == 256);
+  return small || big;
+}
+
+int gemm_tile_threads(int bm, int bn) { return bm == 256 || bn == 256 ? 512 : 256; }
+
 const char* gemm_error_string(int code) {
   switch (code) {
     case 0: return "ok";
-    case -1: return "unsupported tile size (bm, bn must be 64 or 128)";
+    case -1: return "unsupported tile (64|128 x 64|128, 256 x 64|128|256, 128 x 256)";
     case -2: return "M must be a multiple of bm and N a multiple of bn";
     case -3: return "per-split K must be a positive multiple of 64";
     case -4: return "leading dimensions must be multiples of 8 elements (16-byte rows)";
@@ -488,14 +563,21 @@ const char* gemm_error_string(int code) {
     case -8: return "leading dimension smaller than the row it stores";
     case -9: return "hip launch failed";
     case -10: return "colsum needs bf16 output and ld_colsum >= N";
-    case -11: return "fused cross-entropy needs bf16 output, N == bn, a bias and 0 < n_cls <= N";
+    case -11: return "fused cross-entropy needs bf16 output, N == bn <= 128, a bias and 0 < n_cls <= N";
+    case -12: return "pipeline stages must be 2, 3 or 4 (2 for 8-wave tiles > 128x128)";
     default: return "unknown gemm error";
   }
 }
 
+int default_stages(int bm, int bn) {
+  (void)bm;
+  (void)bn;
+  return 2;
+}
+
 int gemm_bf16(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, int splits,
-              hipStream_t stream) {
-  if (!((bm == 64 || bm == 128) && (bn == 64 || bn == 128))) return -1;
+              hipStream_t stream, int stages) {
+  if (!gemm_tile_supported(bm, bn)) return -1;
   if (p.M <= 0 || p.N <= 0 || p.M % bm || p.N % bn) return -2;
   if (splits < 1) return -3;
   if (p.k_total > 0) {
@@ -511,22 +593,29 @@ int gemm_bf16(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, 
   if ((la != KMAJ && la != MNMAJ) || (lb != KMAJ && lb != MNMAJ)) return -6;
   if (splits > 1 && !out_f32) return -7;
   if (p.colsum && (out_f32 || p.ld_colsum < p.N)) return -10;
-  if (p.xent_labels && (out_f32 || p.N != bn || !p.bias || p.n_cls <= 0 || p.n_cls > p.N ||
-                        splits != 1 || p.aux))
+  if (p.xent_labels && (out_f32 || p.N != bn || bn > 128 || bm > 128 || !p.bias ||
+                        p.n_cls <= 0 || p.n_cls > p.N || splits != 1 || p.aux))
     return -11;
   const long a_row = la == KMAJ ? ktot : p.M;
   const long b_row = lb == KMAJ ? ktot : p.N;
   if (p.lda < a_row || p.ldb < b_row || p.ldc < p.N || (p.aux && p.ld_aux < p.N)) return -8;
 
+  const int nt = gemm_tile_threads(bm, bn);
+  const int ns = stages ? stages : default_stages(bm, bn);
+  if (ns < 2 || ns > 4 || (nt == 512 && ns != 2)) return -12;
   gemm_fn fn;
-  if (bm == 128 && bn == 128) fn = pick_layout<128, 128>(la, lb, out_f32);
-  else if (bm == 128) fn = pick_layout<128, 64>(la, lb, out_f32);
-  else if (bn == 128) fn = pick_layout<64, 128>(la, lb, out_f32);
-  else fn = pick_layout<64, 64>(la, lb, out_f32);
+  if (bm == 128 && bn == 128) fn = pick4<128, 128>(ns, la, lb, out_f32);
+  else if (bm == 128 && bn == 64) fn = pick4<128, 64>(ns, la, lb, out_f32);
+  else if (bm == 64 && bn == 128) fn = pick4<64, 128>(ns, la, lb, out_f32);
+  else if (bm == 64 && bn == 64) fn = pick4<64, 64>(ns, la, lb, out_f32);
+  else if (bm == 256 && bn == 256) fn = pick_layout<Cfg<256, 256, 4, 2, 2>>(la, lb, out_f32);
+  else if (bm == 256 && bn == 128) fn = pick_layout<Cfg<256, 128, 4, 2, 2>>(la, lb, out_f32);
+  else if (bm == 256 && bn == 64) fn = pick_layout<Cfg<256, 64, 4, 2, 2>>(la, lb, out_f32);
+  else fn = pick_layout<Cfg<128, 256, 2, 4, 2>>(la, lb, out_f32);
 
   const int tiles_n = p.N / bn, tiles_m = p.M / bm;
   const int nwg = tiles_n * tiles_m * splits;
-  hipLaunchKernelGGL(fn, dim3(nwg), dim3(256), 0, stream, p, tiles_n, tiles_m, nwg);
+  hipLaunchKernelGGL(fn, dim3(nwg), dim3(nt), 0, stream, p, tiles_n, tiles_m, nwg);
   return hipGetLastError() == hipSuccess ? 0 : -9;
 }
 

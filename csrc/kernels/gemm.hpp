@@ -36,7 +36,8 @@ struct GemmParams {
   // Fused softmax cross-entropy epilogue (bf16 output, N == bn: a row is one tile). When
   // xent_labels is set the kernel computes logits = acc + bias, and stores
   // dz = (softmax(logits[:n_cls]) - onehot(label)) * xent_scale instead of the logits;
-  // loss_part[tile_m] = sum of -log p[label] over the tile's rows, *correct += #argmax==label.
+  // loss_part[tile_m] = sum of -log p[label] over the tile's rows, correct[tile_m] = #argmax==label
+  // (per-tile partials, written not accumulated: no per-step zeroing, fixed-order host sum).
   const int* xent_labels;
   int n_cls;
   float xent_scale;
@@ -46,8 +47,13 @@ struct GemmParams {
 
 // Returns 0 on success, a negative code when a shape/alignment precondition fails
 // (nothing is launched then).
+// stages: LDS pipeline depth 2..4 (0 = default_stages(bm, bn)).
 int gemm_bf16(const GemmParams& p, int layout_a, int layout_b, int out_f32, int bm, int bn,
-              int splits, hipStream_t stream);
+              int splits, hipStream_t stream, int stages = 0);
+int default_stages(int bm, int bn);
+// Tiles: 64|128 x 64|128 (4 waves, 256 threads) and 256 x 64|128|256, 128 x 256 (8 waves).
+bool gemm_tile_supported(int bm, int bn);
+int gemm_tile_threads(int bm, int bn);
 
 // Stream-K form for batch-contraction (wgrad) GEMMs with few output tiles: `nwg` workgroups take
 // equal shares of the (tile, k-step) space, write fp32 partial tiles to `part`

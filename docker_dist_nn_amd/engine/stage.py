@@ -204,10 +204,12 @@ class Stage:
         self.dz = [torch.zeros(R, g.np_, dtype=bf, device=dev) for g in self.geoms]
         self.dx_send = None if self.first else torch.zeros(R, g0.kp, dtype=bf, device=dev)
         self.labels = torch.full((R,), -1, dtype=torch.int32, device=dev) if self.last else None
+        self.labels_buf = self.labels  # owned buffer; ``labels`` may alias a dataset slice
         self.xent_per_micro = (self.mb // ops.xent_tiles(self.mb, gl.np_)[0] if self.fused_xent
                                else ops.xent_blocks(self.mb))
         self.loss_part = torch.zeros(self.xent_per_micro * self.nm, dtype=f32, device=dev)
-        self.correct = torch.zeros(1, dtype=torch.int32, device=dev)
+        # per-block correct counts, written (not accumulated) by the loss kernels
+        self.correct = torch.zeros(self.xent_per_micro * self.nm, dtype=torch.int32, device=dev)
         # wgrad geometry: batched = one GEMM over all rows; per_micro = one per micro-batch
         wrows = R if self.wgrad_mode == "batched" else self.mb
         if self.wgrad_algo == "streamk":  # balanced stream-K, reduced straight into the grads
@@ -227,7 +229,8 @@ class Stage:
         L = len(self.geoms)
         for i in range(L):
             if i < L - 1:
-                self.bp.append(self.mb // ops.dgrad_tiles(self.mb, self.geoms[i + 1].kp)[0])
+                g1 = self.geoms[i + 1]
+                self.bp.append(self.mb // ops.dgrad_tiles(self.mb, g1.kp, g1.np_)[0])
             elif self.last:
                 self.bp.append(self.xent_per_micro)
             else:
@@ -235,6 +238,7 @@ class Stage:
         self.bpart = [torch.zeros(self.bp[i] * self.nm, g.np_, dtype=f32, device=dev)
                       for i, g in enumerate(self.geoms)]
         self._w_done = 0
+        self._reduce_jobs: dict = {}
 
     def rows_of(self, j: int) -> slice:
         if not 0 <= j < self.nm:
@@ -256,7 +260,6 @@ class Stage:
 
     # -------------------------------------------------------------------------------------
     def begin_step(self) -> None:
-        self.correct.zero_()
         self._w_done = 0
 
     def forward(self, j: int) -> None:
@@ -269,14 +272,16 @@ class Stage:
                 k = j * self.xent_per_micro
                 ops.linear_fwd_xent(x, p.wbf(i), p.b32(i), self.dz[i][r], self.labels[r],
                                     self.n_cls, 1.0 / self.global_batch,
-                                    self.loss_part[k:k + self.xent_per_micro], self.correct,
+                                    self.loss_part[k:k + self.xent_per_micro],
+                                    self.correct[k:k + self.xent_per_micro],
                                     colsum=self._bpart(i, j))
             elif self.last and i == len(self.geoms) - 1:
                 ops.linear_fwd(x, p.wbf(i), p.b32(i), y, act="linear")  # fp32 logits
                 k = j * self.xent_per_micro
                 ops.softmax_xent(y, self.labels[r], self.dz[i][r], self.n_cls,
                                  1.0 / self.global_batch,
-                                 self.loss_part[k:k + self.xent_per_micro], self.correct,
+                                 self.loss_part[k:k + self.xent_per_micro],
+                                 self.correct[k:k + self.xent_per_micro],
                                  colsum=self._bpart(i, j))
             else:
                 ops.linear_fwd(x, p.wbf(i), p.b32(i), y, act=g.spec.activation)
@@ -328,21 +333,30 @@ class Stage:
 
     def finalize_grads(self, layers: Optional[Sequence[int]] = None) -> None:
         """Reduce bias partials (and, for split-K, weight slabs) into the flat gradient."""
-        p = self.params
-        for i in (range(len(self.geoms)) if layers is None else layers):
-            g = self.geoms[i]
-            n = g.np_ * g.kp
-            if self.wgrad_algo != "streamk":
-                ops.reduce_slabs(self.slabs[i], self.w_splits[i], n, n, p.gw(i))
-            ops.reduce_slabs(self.bpart[i], self.bpart[i].shape[0], g.np_, g.np_, p.gb(i))
+        key = tuple(range(len(self.geoms))) if layers is None else tuple(layers)
+        jobs = self._reduce_jobs.get(key)
+        if jobs is None:  # buffers are fixed for the stage's lifetime: build the table once
+            p = self.params
+            jobs = []
+            for i in key:
+                g = self.geoms[i]
+                n = g.np_ * g.kp
+                if self.wgrad_algo != "streamk":
+                    jobs.append((self.slabs[i], self.w_splits[i], n, n, p.gw(i), 1.0, False))
+                jobs.append((self.bpart[i], self.bpart[i].shape[0], g.np_, g.np_, p.gb(i), 1.0,
+                             False))
+            self._reduce_jobs[key] = jobs
+        ops.reduce_multi(jobs)  # one launch for every slab set and bias-partial set
 
     def optimizer_step(self, lr: Optional[float] = None) -> None:
         self.params.optimizer_step(lr)
 
     # convenience: a whole step when this stage holds the entire model ----------------------
     def set_batch(self, x: torch.Tensor, labels: torch.Tensor) -> None:
+        self.x_in = self.x_buf  # never write through an alias of the caller's dataset
         self.x_in.copy_(x)
         if self.labels is not None:
+            self.labels = self.labels_buf
             self.labels.copy_(labels)
 
     def loss_sum(self) -> float:

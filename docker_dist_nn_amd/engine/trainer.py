@@ -110,13 +110,19 @@ class Trainer:
                     x.stride(1) == 1 and x.data_ptr() % 16 == 0 and len(self.stages) == 1:
                 st.x_in = x
             else:
-                if zero_copy and st.x_in.data_ptr() != st.x_buf.data_ptr():
-                    st.x_in = st.x_buf
+                st.x_in = st.x_buf  # never write through an alias of a previous batch
                 st.x_in.copy_(x)
         if self.last is not None:
             if labels is None:
                 raise ValueError("last stage needs labels")
-            self.last.labels.copy_(labels)
+            st = self.last
+            if zero_copy and self._graph is None and labels.shape == st.labels.shape and \
+                    labels.dtype == st.labels.dtype and labels.device == st.labels.device and \
+                    labels.is_contiguous():
+                st.labels = labels
+            else:
+                st.labels = st.labels_buf
+                st.labels.copy_(labels)
 
     def step(self) -> None:
         if self._graph is not None:
@@ -176,7 +182,7 @@ class Trainer:
         return self.last.loss_sum() / (self.micro_batch * self.num_micro)
 
     def correct(self) -> Optional[int]:
-        return None if self.last is None else int(self.last.correct.item())
+        return None if self.last is None else int(self.last.correct.sum().item())
 
     def load_weights(self, weights: Sequence[np.ndarray], biases: Sequence[np.ndarray]) -> None:
         for st in self.stages:

@@ -1,9 +1,11 @@
-from .kernels import (STREAMK_WG, linear_fwd_xent, xent_tiles, linear_wgrad_streamk, streamk_partial_elems, streamk_tiles,
-                      KMAJ, MNMAJ, adam_update, colsum_partial, dgrad_tiles, gemm, linear_dgrad, linear_fwd,
-                      linear_wgrad, pack_bf16, pick_splits, pick_tiles, reduce_slabs, sgd_update,
-                      softmax_rows, softmax_xent, unpack_bf16, xent_blocks)
+from .kernels import (KMAJ, MNMAJ, STREAMK_WG, adam_update, colsum_partial, dgrad_tiles, gemm,
+                      linear_dgrad, linear_fwd, linear_fwd_xent, linear_wgrad,
+                      linear_wgrad_streamk, pack_bf16, pick_splits, pick_tiles, reduce_multi,
+                      reduce_slabs, sgd_update, softmax_rows, softmax_xent, streamk_partial_elems,
+                      streamk_tiles, unpack_bf16, wgrad_config, xent_blocks, xent_tiles)
 
-__all__ = ["STREAMK_WG", "linear_fwd_xent", "xent_tiles", "linear_wgrad_streamk", "streamk_partial_elems", "streamk_tiles", "KMAJ", "MNMAJ", "adam_update", "colsum_partial", "dgrad_tiles", "gemm", "linear_dgrad",
-           "linear_fwd", "linear_wgrad", "pack_bf16", "pick_splits", "pick_tiles",
-           "reduce_slabs", "sgd_update", "softmax_rows", "softmax_xent", "unpack_bf16",
-           "xent_blocks"]
+__all__ = ["KMAJ", "MNMAJ", "STREAMK_WG", "adam_update", "colsum_partial", "dgrad_tiles", "gemm",
+           "linear_dgrad", "linear_fwd", "linear_fwd_xent", "linear_wgrad",
+           "linear_wgrad_streamk", "pack_bf16", "pick_splits", "pick_tiles", "reduce_multi",
+           "reduce_slabs", "sgd_update", "softmax_rows", "softmax_xent", "streamk_partial_elems",
+           "streamk_tiles", "unpack_bf16", "wgrad_config", "xent_blocks", "xent_tiles"]

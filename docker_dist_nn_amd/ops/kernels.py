@@ -13,14 +13,37 @@ graph replays with fixed pointers) and dispatches on the device of its inputs:
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
 from ..models.mlp import ACT_CODE
 from ..utils.native import native
 from . import reference as ref
+from . import tuning
 
 KMAJ, MNMAJ = 0, 1
+
+
+def _parse_stages(spec: str) -> dict:
+    """DNN_GEMM_STAGES: "3" (every GEMM) or "fwd=3,dgrad=2,wgrad=4,xent=2"; 0 = kernel
+    default."""
+    out = {"fwd": 0, "dgrad": 0, "wgrad": 0, "xent": 0}
+    spec = spec.strip()
+    if not spec:
+        return out
+    if "=" not in spec:
+        return {k: int(spec) for k in out}
+    for part in spec.split(","):
+        k, v = part.split("=")
+        if k.strip() not in out:
+            raise ValueError(f"DNN_GEMM_STAGES: unknown GEMM kind {k!r}")
+        out[k.strip()] = int(v)
+    return out
+
+
+# LDS pipeline depth (2..4) per GEMM kind; see mma_tile in csrc/kernels/gemm.hip.
+STAGES = _parse_stages(os.environ.get("DNN_GEMM_STAGES", ""))
 
 
 def _stream(t: torch.Tensor) -> int:
@@ -44,16 +67,29 @@ def _act(act) -> int:
 
 
 # Residency model for tile choice: LDS/regs admit 2 (128x128), 3 (128x64 / 64x128) or
-# 4 (64x64) workgroups per CU; relative per-CU throughput of the tile shapes.
-_TILE_OCC = {(128, 128): 2, (128, 64): 3, (64, 128): 3, (64, 64): 4}
+# 4 (64x64) 4-wave workgroups per CU, and one 8-wave workgroup of the 256-row/-column tiles;
+# relative per-CU throughput of the tile shapes.
+_TILE_OCC = {(128, 128): 2, (128, 64): 3, (64, 128): 3, (64, 64): 4,
+             (256, 256): 1, (256, 128): 1, (128, 256): 1, (256, 64): 1}
 _TILE_EFF = {(128, 128): 1.0, (128, 64): 0.82, (64, 128): 0.82, (64, 64): 0.62}
+BIG_TILES = [(256, 256), (256, 128), (128, 256), (256, 64)]
 NUM_CU = 256
 
 
 def pick_tiles(M: int, N: int, splits: int = 1) -> tuple[int, int]:
-    """Tile shape minimising modelled time = rounds of resident tiles x per-tile cost."""
+    """Tile for a [M][N] output (fwd / dgrad, M = batch rows).
+
+    The 8-wave 256-row tiles stage half the LDS bytes per FLOP of the 128x128 tile and win
+    whenever they still give >= 2 workgroups per CU (bench/stage_sweep.py on MI355X): 256x256
+    for outputs >= 1024 wide, 256x64 for 128..1023. Otherwise: the 4-wave tile minimising
+    modelled time = rounds of resident tiles x per-tile cost."""
+    if splits == 1 and M % 256 == 0:
+        if N % 256 == 0 and N >= 1024 and (M // 256) * (N // 256) >= 2 * NUM_CU:
+            return 256, 256
+        if N % 64 == 0 and N >= 128 and (M // 256) * (N // 64) >= 2 * NUM_CU:
+            return 256, 64
     best, best_t = None, math.inf
-    for (bm, bn) in _TILE_OCC:
+    for (bm, bn) in _TILE_EFF:  # calibrated tiles only
         if M % bm or N % bn:
             continue
         tiles = (M // bm) * (N // bn) * splits
@@ -77,7 +113,11 @@ def pick_splits(M: int, N: int, K_total: int, max_splits: int = 48) -> int:
 
 
 def wgrad_config(M: int, N: int, K_total: int, max_splits: int = 48) -> tuple[int, int, int]:
-    """Joint (bm, bn, splits) choice for the batch-contraction GEMM (see pick_splits)."""
+    """Joint (bm, bn, splits) choice for the batch-contraction GEMM (see pick_splits): the
+    tuned table's measured optimum when it has the shape, else the model below."""
+    t = tuning.lookup("wgrad", M, N, K_total)
+    if t is not None:
+        return t["tile"][0], t["tile"][1], t["splits"]
     ksteps = K_total // 64
     slab_cost = 2.0 * M * N * 4 / 5.0e12 * 0.6e15 / NUM_CU  # slab bytes in tile-FLOP units
     best, best_c = None, math.inf
@@ -97,7 +137,7 @@ def wgrad_config(M: int, N: int, K_total: int, max_splits: int = 48) -> tuple[in
 
 def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=None, aux=None,
          act=0, accumulate: bool = False, splits: int = 1, tiles: tuple[int, int] | None = None,
-         colsum=None, k_total: int = 0):
+         colsum=None, k_total: int = 0, stages: int = 0):
     """C (+)= epilogue(A.B). See csrc/kernels/gemm.hpp for the layout/epilogue contract.
 
     ``k_total`` > 0 selects uneven split-K over the full contraction length (K is ignored).
@@ -147,7 +187,8 @@ def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=
                        split_stride, _p(bias), _p(aux), aux.stride(0) if aux is not None else 0,
                        M, N, K, act, int(accumulate), layout_a, layout_b, int(out_f32), bm, bn,
                        splits, _stream(a), _p(colsum),
-                       colsum.stride(0) if colsum is not None else 0, k_total=int(k_total))
+                       colsum.stride(0) if colsum is not None else 0, k_total=int(k_total),
+                       stages=int(stages))
     return c
 
 
@@ -157,7 +198,10 @@ def linear_fwd(x, w, bias, y, act="relu"):
     """y[M][Np] = act(x[M][Kp] . w[Np][Kp]^T + bias). y bf16 (activation) or fp32 (logits)."""
     M, K = x.shape
     N = w.shape[0]
-    return gemm(x, w, y, layout_a=KMAJ, layout_b=KMAJ, M=M, N=N, K=K, bias=bias, act=act)
+    t = tuning.lookup("fwd", M, N, K)
+    tiles = tuple(t["tile"]) if t else pick_tiles(M, N)
+    return gemm(x, w, y, layout_a=KMAJ, layout_b=KMAJ, M=M, N=N, K=K, bias=bias, act=act,
+                tiles=tiles, stages=STAGES["fwd"] or (t or {}).get("stages", 0))
 
 
 def xent_tiles(M: int, N: int) -> tuple[int, int]:
@@ -173,7 +217,7 @@ def xent_tiles(M: int, N: int) -> tuple[int, int]:
 def linear_fwd_xent(x, w, bias, dz, labels, n_cls, scale, loss_part=None, correct=None,
                     colsum=None):
     """Last layer + softmax cross-entropy in ONE kernel: dz[M][Np] = (softmax(x.w^T + b) -
-    onehot) * scale; loss_part[M/bm] per-tile loss sums; correct += #argmax == label;
+    onehot) * scale; loss_part[M/bm] per-tile loss sums; correct[M/bm] per-tile #argmax==label;
     colsum[M/bm][Np] = per-tile column sums of dz (the bias-gradient partials)."""
     M, K = x.shape
     N = w.shape[0]
@@ -182,6 +226,8 @@ def linear_fwd_xent(x, w, bias, dz, labels, n_cls, scale, loss_part=None, correc
         raise ValueError("labels must be int32 with one entry per row")
     if loss_part is not None and loss_part.numel() < M // bm:
         raise ValueError(f"loss_part needs {M // bm} entries")
+    if correct is not None and (correct.dtype != torch.int32 or correct.numel() < M // bm):
+        raise ValueError(f"correct needs {M // bm} int32 entries")
     if not x.is_cuda:
         logits = torch.empty(M, N, dtype=torch.float32)
         ref.gemm(x, w, logits, layout_a=KMAJ, layout_b=KMAJ, M=M, N=N, K=K, bias=bias)
@@ -198,13 +244,16 @@ def linear_fwd_xent(x, w, bias, dz, labels, n_cls, scale, loss_part=None, correc
     native().gemm_bf16(_p(x), x.stride(0), _p(w), w.stride(0), _p(dz), dz.stride(0), 0,
                        _p(bias), 0, 0, M, N, K, 0, 0, KMAJ, KMAJ, 0, bm, bn, 1, _stream(x),
                        _p(colsum), colsum.stride(0) if colsum is not None else 0, _p(labels),
-                       int(n_cls), float(scale), _p(loss_part), _p(correct))
+                       int(n_cls), float(scale), _p(loss_part), _p(correct),
+                       stages=STAGES["xent"])
     return dz
 
 
-def dgrad_tiles(M: int, K: int) -> tuple[int, int]:
-    """Tile shape used by linear_dgrad for an [M][K] output (fixes the colsum partial count)."""
-    return pick_tiles(M, K, 1)
+def dgrad_tiles(M: int, K: int, N: int = 0) -> tuple[int, int]:
+    """Tile shape used by linear_dgrad for an [M][K] output from an [M][N] gradient (fixes
+    the colsum partial count)."""
+    t = tuning.lookup("dgrad", M, K, N) if N else None
+    return tuple(t["tile"]) if t else pick_tiles(M, K, 1)
 
 
 def linear_dgrad(dz, w, dx, y_prev=None, act_prev="linear", colsum=None):
@@ -216,7 +265,8 @@ def linear_dgrad(dz, w, dx, y_prev=None, act_prev="linear", colsum=None):
     if y_prev is None:
         act_prev = "linear"
     return gemm(dz, w, dx, layout_a=KMAJ, layout_b=MNMAJ, M=M, N=K, K=N, aux=y_prev,
-                act=act_prev, tiles=dgrad_tiles(M, K), colsum=colsum)
+                act=act_prev, tiles=dgrad_tiles(M, K, N), colsum=colsum,
+                stages=STAGES["dgrad"])
 
 
 def linear_wgrad(dz, x, slabs, splits=1, accumulate=False):
@@ -226,9 +276,9 @@ def linear_wgrad(dz, x, slabs, splits=1, accumulate=False):
     if R % 64 or splits > R // 64:
         raise ValueError("rows must be a multiple of 64 with at least 64 rows per split")
     bm, bn, s = wgrad_config(N, K, R)
-    tiles = (bm, bn) if s == splits else None
+    tiles = (bm, bn) if s == splits else pick_tiles(N, K, splits)
     return gemm(dz, x, slabs, layout_a=MNMAJ, layout_b=MNMAJ, M=N, N=K, K=R, k_total=R,
-                accumulate=accumulate, splits=splits, tiles=tiles)
+                accumulate=accumulate, splits=splits, tiles=tiles, stages=STAGES["wgrad"])
 
 
 STREAMK_WG = 2 * NUM_CU  # stream-K workgroups: two resident per CU, every CU equally loaded
@@ -285,11 +335,15 @@ def xent_blocks(rows: int) -> int:
 
 
 def softmax_xent(logits, labels, dz, n_cls, scale, loss_part=None, correct=None, colsum=None):
-    """dz = (softmax - onehot) * scale; per 64-row block: loss partial sum -> loss_part and
-    (optional) dz column sums -> colsum [xent_blocks(rows)][width] (bias-gradient partials)."""
+    """dz = (softmax - onehot) * scale; per 64-row block: loss partial sum -> loss_part,
+    #argmax==label -> correct (int32), and (optional) dz column sums -> colsum
+    [xent_blocks(rows)][width] (bias-gradient partials)."""
     rows, width = dz.shape
     if loss_part is not None and loss_part.numel() < xent_blocks(rows):
         raise ValueError("loss_part needs xent_blocks(rows) entries")
+    if correct is not None and (correct.dtype != torch.int32 or
+                                correct.numel() < xent_blocks(rows)):
+        raise ValueError("correct needs xent_blocks(rows) int32 entries")
     if colsum is not None and (colsum.dtype != torch.float32 or colsum.dim() != 2 or
                                colsum.shape[0] < xent_blocks(rows) or colsum.shape[1] < width
                                or colsum.stride(1) != 1):
@@ -343,6 +397,30 @@ def reduce_slabs(src, n_src, stride, n, out, scale=1.0, accumulate=False):
         raise ValueError("reduce_slabs range out of bounds")
     native().reduce_slabs(_p(src), stride, n_src, n, float(scale), _p(out), int(accumulate),
                           _stream(src))
+
+
+def reduce_multi(jobs):
+    """Several reduce_slabs in ONE launch. jobs: iterable of
+    (src, n_src, stride, n, out, scale, accumulate) with reduce_slabs' meaning; the results are
+    bitwise identical to running reduce_slabs on each job."""
+    jobs = list(jobs)
+    if not jobs:
+        return
+    if not jobs[0][0].is_cuda:
+        for (src, n_src, stride, n, out, scale, acc) in jobs:
+            ref.reduce_slabs(src, n_src, stride, n, out, scale, acc)
+        return
+    packed = []
+    for (src, n_src, stride, n, out, scale, acc) in jobs:
+        if src.dtype != torch.float32 or out.dtype != torch.float32:
+            raise TypeError("reduce_multi works on fp32")
+        if not (src.is_contiguous() and out.is_contiguous()):
+            raise ValueError("reduce_multi needs contiguous buffers")
+        if (n_src - 1) * stride + n > src.numel() or out.numel() < n:
+            raise ValueError("reduce_multi range out of bounds")
+        packed.append((_p(src), int(stride), int(n_src), int(n), _p(out), float(scale),
+                       int(acc)))
+    native().reduce_multi(packed, _stream(jobs[0][0]))
 
 
 def sgd_update(p, g, mom=None, shadow=None, lr=0.01, momentum=0.0, weight_decay=0.0):

@@ -92,9 +92,12 @@ def softmax_xent(logits, labels, dz, n_cls, scale, loss_part=None, correct=None,
         pad = torch.zeros(nb * rows_per_block)
         pad[:rows] = nll
         loss_part[:nb] = pad.view(nb, rows_per_block).sum(1).to(loss_part.dtype)
-    if correct is not None:
+    if correct is not None:  # per-block partial counts (written, not accumulated)
         pred = torch.argmax(lg, dim=1)
-        correct += ((pred == lab) & valid).sum().to(correct.dtype)
+        nb = -(-rows // rows_per_block)
+        hit = torch.zeros(nb * rows_per_block, dtype=torch.int64)
+        hit[:rows] = ((pred == lab) & valid).long()
+        correct[:nb] = hit.view(nb, rows_per_block).sum(1).to(correct.dtype)
     if colsum is not None:
         nb = -(-rows // rows_per_block)
         pad = torch.zeros(nb * rows_per_block, width)

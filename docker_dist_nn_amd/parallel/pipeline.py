@@ -98,7 +98,14 @@ class PipelineExecutor:
             h(st, op, j)
 
     def _wgrad_finalize_overlapped(self, st):
-        """Batched W: per layer (last first) wgrad -> reduce -> async bucket all-reduce."""
+        """Batched W: per layer (last first) wgrad -> reduce -> async bucket all-reduce. Without
+        a DP group there is nothing to overlap: all wgrads, then ONE reduce launch."""
+        if self.grad_sync is None or self.grad_sync.world <= 1:
+            for i in range(len(st.geoms) - 1, -1, -1):
+                st.wgrad_layer(i)
+            st.finalize_grads()
+            st._finalized = True
+            return
         for i in range(len(st.geoms) - 1, -1, -1):
             st.wgrad_layer(i)
             st.finalize_grads([i])
