@@ -79,14 +79,16 @@ def main(argv=None):
         from docker_dist_nn_amd.parallel.groups import build_mesh, init_distributed
 
         init_distributed(os.environ.get("DNN_DIST_BACKEND", "nccl"))
-    pp, dp = parse_parallelism(a.parallelism, n)
+    pp, dp = parse_parallelism(a.parallelism, n, loopback=world == 1)
     planner = Planner()
+    gpus_per_replica = 1 if world == 1 else None  # loopback: every stage on the one GPU
     if pp is None:
         plan = planner.best(spec, n, a.batch)
     else:
-        plan = planner.evaluate(spec, pp, dp, a.batch * pp)
+        plan = planner.evaluate(spec, pp, dp, a.batch * (gpus_per_replica or pp))
     mb = a.micro or plan.micro_batch
-    rows = a.batch * plan.pp  # rows per replica per step (weak scaling: batch rows per GPU)
+    # rows per replica per step (weak scaling: `batch` rows per GPU)
+    rows = a.batch * (gpus_per_replica or plan.pp)
     nm = max(1, rows // mb)
     if mb * nm != rows or mb % 64:
         raise SystemExit(f"batch {rows} must split into micro-batches of a multiple of 64")
@@ -153,7 +155,8 @@ def main(argv=None):
             "model": MODEL_LABEL.get(a.model, spec.describe()),
             "global_batch": global_batch,
             "seq_len": None,
-            "parallelism": plan.parallelism,
+            "parallelism": plan.parallelism + ("-loopback" if world == 1 and plan.pp > 1
+                                               else ""),
             "layer_distribution": plan.distribution,
             "micro_batch": mb,
             "num_micro": nm,

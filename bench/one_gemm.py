@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--stages", type=int, default=2)
     ap.add_argument("--splits", type=int, default=8)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--group-m", type=int, default=0)
     a = ap.parse_args()
     bm, bn = map(int, a.tile.split("x"))
     dev = torch.device("cuda")
@@ -36,15 +37,15 @@ def main():
     if a.op == "fwd":
         y = torch.empty(R, N, device=dev, dtype=torch.bfloat16)
         fn = lambda: ops.gemm(x, w, y, layout_a=KMAJ, layout_b=KMAJ, M=R, N=N, K=K, bias=b,  # noqa: E731,E501
-                              act="relu", tiles=(bm, bn), stages=a.stages)
+                              act="relu", tiles=(bm, bn), stages=a.stages, group_m=a.group_m)
     elif a.op == "dgrad":
         dx = torch.empty(R, K, device=dev, dtype=torch.bfloat16)
         fn = lambda: ops.gemm(dz, w, dx, layout_a=KMAJ, layout_b=MNMAJ, M=R, N=K, K=N, aux=x,  # noqa: E731,E501
-                              act="relu", tiles=(bm, bn), stages=a.stages)
+                              act="relu", tiles=(bm, bn), stages=a.stages, group_m=a.group_m)
     else:
         slabs = torch.empty(a.splits, N, K, device=dev)
         fn = lambda: ops.gemm(dz, x, slabs, layout_a=MNMAJ, layout_b=MNMAJ, M=N, N=K, K=R,  # noqa: E731,E501
-                              k_total=R, splits=a.splits, tiles=(bm, bn), stages=a.stages)
+                              k_total=R, splits=a.splits, tiles=(bm, bn), stages=a.stages, group_m=a.group_m)
     for _ in range(a.iters):
         fn()
     torch.cuda.synchronize()

@@ -53,15 +53,15 @@ def signatures(spec, R):
             if op == "wgrad":
                 cands = []
                 for (bm, bn) in TILES:
-                    if M % bm or N % bn:
+                    if M % bm or N % 64:  # N % bn != 0 runs as bulk + 64-wide remainder
                         continue
-                    nt = (M // bm) * (N // bn)
+                    nt = (M // bm) * -(-N // bn)
                     for k in (1, 2, 3, 4, 6, 8):
                         s = max(1, min(K // 64, round(k * 256 / nt)))
                         if ((bm, bn), s) not in cands:
                             cands.append(((bm, bn), s))
             else:
-                cands = [((bm, bn), 1) for (bm, bn) in TILES if M % bm == 0 and N % bn == 0]
+                cands = [((bm, bn), 1) for (bm, bn) in TILES if M % bm == 0 and N % 64 == 0]
             out.append((op, M, N, K, cands))
     return out
 
@@ -85,7 +85,7 @@ def step_ms(spec, R, x, y, dev, steps, reps):
     return statistics.median(times)
 
 
-def tune_config(R, model, dev, table, steps, reps, log):
+def tune_config(R, model, dev, table, steps, reps, log, only=None, verbose=False):
     spec = NAMED_MODELS.get(model) or MLPSpec.parse(model)
     kp0 = (spec.layers[0].in_dim + 63) // 64 * 64
     xs, ys = synthetic_mnist(min(R, 65536), seed=3)
@@ -99,12 +99,17 @@ def tune_config(R, model, dev, table, steps, reps, log):
     log({"rows": R, "model": model, "start_ms": round(base, 4)})
     for (op, M, N, K, cands) in sigs:
         k = tuning.key(op, M, N, K)
+        if only and k not in only:
+            continue
         prev = table.get(k)
         res = []
         for (tile, s) in cands:
             table[k] = {"tile": list(tile), "splits": s, "stages": 2}
             try:
                 res.append((step_ms(spec, R, x, y, dev, steps, reps), tile, s))
+                if verbose:
+                    log({"cand": k, "tile": list(tile), "splits": s,
+                         "step_ms": round(res[-1][0], 4)})
             except (ValueError, RuntimeError) as e:
                 log({"skip": k, "tile": tile, "splits": s, "err": str(e)[:80]})
         ms, tile, s = min(res)
@@ -127,6 +132,9 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--out", default=tuning.TABLE_PATH)
+    ap.add_argument("--only", default="", help="comma list of signatures, e.g. "
+                    "wgrad:512x832x65536")
+    ap.add_argument("--verbose", action="store_true", help="log every candidate")
     a = ap.parse_args()
     dev = torch.device("cuda")
     doc = {"device": torch.cuda.get_device_name(0), "generated_by": "bench/tune.py",
@@ -145,7 +153,8 @@ def main():
 
     for cfg in a.configs.split(","):
         rows, model = cfg.split(":")
-        tune_config(int(rows), model, dev, table, a.steps, a.reps, log)
+        tune_config(int(rows), model, dev, table, a.steps, a.reps, log,
+                    only=set(a.only.split(",")) if a.only else None, verbose=a.verbose)
         doc["entries"] = dict(table)
         with open(a.out, "w") as f:
             json.dump(doc, f, indent=1, sort_keys=True)

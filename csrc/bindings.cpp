@@ -49,8 +49,9 @@ PYBIND11_MODULE(_native, m) {
          uintptr_t bias, uintptr_t aux, long ld_aux, int M, int N, int K, int act, int accumulate,
          int layout_a, int layout_b, int out_f32, int bm, int bn, int splits, uintptr_t stream,
          uintptr_t colsum, long ld_colsum, uintptr_t xent_labels, int n_cls, float xent_scale,
-         uintptr_t loss_part, uintptr_t correct, int k_total, int stages) {
+         uintptr_t loss_part, uintptr_t correct, int k_total, int stages, int group_m) {
         GemmParams p{};
+        p.group_m = group_m;
         p.k_total = k_total;
         p.colsum = P<float>(colsum);
         p.ld_colsum = ld_colsum;
@@ -84,7 +85,7 @@ PYBIND11_MODULE(_native, m) {
       py::arg("stream"), py::arg("colsum") = 0, py::arg("ld_colsum") = 0,
       py::arg("xent_labels") = 0, py::arg("n_cls") = 0, py::arg("xent_scale") = 0.f,
       py::arg("loss_part") = 0, py::arg("correct") = 0, py::arg("k_total") = 0,
-      py::arg("stages") = 0);
+      py::arg("stages") = 0, py::arg("group_m") = 0);
   m.def("gemm_default_stages", &dnn::default_stages);
 
   m.def(

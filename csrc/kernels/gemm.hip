@@ -198,6 +198,9 @@ __device__ __forceinline__ void mma_tile(const GemmParams& p, int m0, int n0, in
     }
     const char LDS_AS* sa = lds + rd * STAGE;
     const char LDS_AS* sb = sa + A_BYTES;
+    // (Reading both 32-deep halves' fragments up front behind a sched_barrier was measured:
+    // +8 % on 128x128 big GEMMs, -35 % on 256x256 dgrad whose 40 transposed reads exceed what
+    // lgkmcnt can count -- the compiler's own interleaving is kept.)
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       bf16x8_t a[FM], b[FN];
@@ -305,11 +308,21 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(GemmParams p, int tile
   char LDS_AS* lds = (char LDS_AS*)smem;
 
   // XCD-aware bijective remap: hardware deals block b to XCD group b%8; give each group a
-  // contiguous run of logical tiles (tile_n fastest -> neighbours share the A panel in L2).
+  // contiguous run of logical tiles. Within a split, tiles are walked in groups of
+  // group_m row-tiles (column-major inside a group), so the ~32 workgroups an XCD holds at
+  // once cover e.g. 4 row x 8 column tiles: 12 operand k-slices shared through its L2
+  // instead of 33 for a 1 x 32 strip (guide §5.5 T1 + grouped raster order).
   const int wgid = xcd_remap(blockIdx.x, nwg);
-  const int tn = wgid % tiles_n;
-  const int tm = (wgid / tiles_n) % tiles_m;
-  const int split = wgid / (tiles_n * tiles_m);
+  const int per_split = tiles_n * tiles_m;
+  const int split = wgid / per_split;
+  const int t = wgid - split * per_split;
+  const int gm_full = p.group_m > 1 ? p.group_m : 1;
+  const int per_group = gm_full * tiles_n;
+  const int grp = t / per_group, first_m = grp * gm_full;
+  const int gm = min(tiles_m - first_m, gm_full);
+  const int tin = t - grp * per_group;
+  const int tm = first_m + tin % gm;
+  const int tn = tin / gm;
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -564,7 +577,7 @@ const char* gemm_error_string(int code) {
     case -9: return "hip launch failed";
     case -10: return "colsum needs bf16 output and ld_colsum >= N";
     case -11: return "fused cross-entropy needs bf16 output, N == bn <= 128, a bias and 0 < n_cls <= N";
-    case -12: return "pipeline stages must be 2, 3 or 4 (2 for 8-wave tiles > 128x128)";
+    case -12: return "pipeline stages must be 2..4 (8-wave tiles: 2..3, 256x256: 2)";
     default: return "unknown gemm error";
   }
 }
@@ -602,20 +615,32 @@ int gemm_bf16(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, 
 
   const int nt = gemm_tile_threads(bm, bn);
   const int ns = stages ? stages : default_stages(bm, bn);
-  if (ns < 2 || ns > 4 || (nt == 512 && ns != 2)) return -12;
+  // 8-wave tiles: NS = 3 where three stages fit (not 256x256)
+  if (ns < 2 || ns > 4 || (nt == 512 && (ns > 3 || (ns == 3 && bm == 256 && bn == 256))))
+    return -12;
   gemm_fn fn;
   if (bm == 128 && bn == 128) fn = pick4<128, 128>(ns, la, lb, out_f32);
   else if (bm == 128 && bn == 64) fn = pick4<128, 64>(ns, la, lb, out_f32);
   else if (bm == 64 && bn == 128) fn = pick4<64, 128>(ns, la, lb, out_f32);
   else if (bm == 64 && bn == 64) fn = pick4<64, 64>(ns, la, lb, out_f32);
   else if (bm == 256 && bn == 256) fn = pick_layout<Cfg<256, 256, 4, 2, 2>>(la, lb, out_f32);
-  else if (bm == 256 && bn == 128) fn = pick_layout<Cfg<256, 128, 4, 2, 2>>(la, lb, out_f32);
-  else if (bm == 256 && bn == 64) fn = pick_layout<Cfg<256, 64, 4, 2, 2>>(la, lb, out_f32);
-  else fn = pick_layout<Cfg<128, 256, 2, 4, 2>>(la, lb, out_f32);
+  else if (bm == 256 && bn == 128)
+    fn = ns == 2 ? pick_layout<Cfg<256, 128, 4, 2, 2>>(la, lb, out_f32)
+                 : pick_layout<Cfg<256, 128, 4, 2, 3>>(la, lb, out_f32);
+  else if (bm == 256 && bn == 64)
+    fn = ns == 2 ? pick_layout<Cfg<256, 64, 4, 2, 2>>(la, lb, out_f32)
+                 : pick_layout<Cfg<256, 64, 4, 2, 3>>(la, lb, out_f32);
+  else
+    fn = ns == 2 ? pick_layout<Cfg<128, 256, 2, 4, 2>>(la, lb, out_f32)
+                 : pick_layout<Cfg<128, 256, 2, 4, 3>>(la, lb, out_f32);
 
   const int tiles_n = p.N / bn, tiles_m = p.M / bm;
   const int nwg = tiles_n * tiles_m * splits;
-  hipLaunchKernelGGL(fn, dim3(nwg), dim3(nt), 0, stream, p, tiles_n, tiles_m, nwg);
+  GemmParams q = p;
+  // grouped raster (see the kernel): worth it once a row of column tiles outgrows what one
+  // XCD holds at a time; a caller-provided group_m wins
+  if (q.group_m <= 0) q.group_m = tiles_n >= 8 ? 4 : 1;
+  hipLaunchKernelGGL(fn, dim3(nwg), dim3(nt), 0, stream, q, tiles_n, tiles_m, nwg);
   return hipGetLastError() == hipSuccess ? 0 : -9;
 }
 

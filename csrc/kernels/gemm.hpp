@@ -43,6 +43,8 @@ struct GemmParams {
   float xent_scale;
   float* loss_part;
   int* correct;
+  // raster order: row-tiles per group (<= 0: launcher default, 1 = row-major tiles)
+  int group_m;
 };
 
 // Returns 0 on success, a negative code when a shape/alignment precondition fails

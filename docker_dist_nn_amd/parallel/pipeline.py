@@ -106,7 +106,11 @@ class PipelineExecutor:
             st.finalize_grads()
             st._finalized = True
             return
-        for i in range(len(st.geoms) - 1, -1, -1):
+        # Largest gradient first: its all-reduce (the longest on the xGMI ring) then overlaps
+        # the wgrad GEMMs of every other layer, and only the smallest bucket is exposed at the
+        # end (last-layer-first would leave the big first-layer bucket exposed).
+        order = sorted(range(len(st.geoms)), key=lambda i: -st.geoms[i].np_ * st.geoms[i].kp)
+        for i in order:
             st.wgrad_layer(i)
             st.finalize_grads([i])
             if self.grad_sync is not None:

@@ -94,8 +94,11 @@ class Planner:
         return max(cands, key=lambda p: p.samples_per_s)
 
 
-def parse_parallelism(text: str, n_gpus: int) -> tuple[Optional[int], Optional[int]]:
-    """'auto' -> (None, None); 'pp4' / 'dp8' / 'pp2dp4' -> explicit degrees."""
+def parse_parallelism(text: str, n_gpus: int,
+                      loopback: bool = False) -> tuple[Optional[int], Optional[int]]:
+    """'auto' -> (None, None); 'pp4' / 'dp8' / 'pp2dp4' -> explicit degrees. With
+    ``loopback`` (one process), 'ppS' may exceed the GPU count: all S stages then run in the
+    one process (loopback channels) -- the pipeline engine without the interconnect."""
     if text == "auto":
         return None, None
     import re
@@ -108,7 +111,9 @@ def parse_parallelism(text: str, n_gpus: int) -> tuple[Optional[int], Optional[i
     if pp is None:
         pp = n_gpus // dp
     if dp is None:
-        dp = n_gpus // pp
+        dp = 1 if loopback and n_gpus == 1 else n_gpus // pp
+    if loopback and n_gpus == 1 and dp == 1:
+        return pp, 1
     if pp * dp != n_gpus:
         raise ValueError(f"--parallelism {text} does not use {n_gpus} GPUs")
     return pp, dp

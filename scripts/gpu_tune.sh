@@ -1,13 +1,12 @@
-# GPU tests, GEMM tuning table, bench with rules-only and with the table, step kernel trace.
+# GPU tests, in-situ GEMM tuning (starting from the committed table), bench, step kernel trace.
 set -o pipefail
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out; mkdir -p $O
 cd $R
 timeout -k 10 600 python -m pytest tests/ -q -m gpu -x > $O/tests.log 2>&1; rc=$?; echo "rc=$rc" >> $O/tests.log
 [ $rc -eq 0 ] || exit 1
-rm -f docker_dist_nn_amd/ops/tuned_gfx950.json
-DNN_TUNED=0 timeout -k 10 300 python bench.py --steps 50 --warmup 10 > $O/bench_rules.log 2>&1 || exit $?
-timeout -k 10 1000 python bench/tune.py --out $O/tuned_gfx950.json > $O/tune.log 2>&1 || exit $?
-cp $O/tuned_gfx950.json docker_dist_nn_amd/ops/tuned_gfx950.json
+timeout -k 10 300 python bench.py --steps 50 --warmup 10 > $O/bench_before.log 2>&1 || exit $?
+timeout -k 10 1000 python bench/tune.py ${TUNE_ARGS} > $O/tune.log 2>&1 || exit $?
+cp docker_dist_nn_amd/ops/tuned_gfx950.json $O/tuned_gfx950.json
 timeout -k 10 300 python bench.py --steps 50 --warmup 10 > $O/bench_tuned.log 2>&1 || exit $?
 timeout -k 10 300 python bench.py --steps 50 --warmup 10 --batch 131072 >> $O/bench_tuned.log 2>&1 || exit $?
 export TMPDIR=/tmp

@@ -81,6 +81,30 @@ def test_gemm_exact_integer_8wave(dev, la, lb, bm, bn):
     assert torch.equal(slabs.sum(0), ref)
 
 
+@pytest.mark.parametrize("la,lb", LAYOUTS)
+@pytest.mark.parametrize("bm,bn", [(256, 256), (128, 128), (256, 128)])
+def test_gemm_n_split_remainder(dev, la, lb, bm, bn):
+    """N not a multiple of bn: bulk on (bm, bn) + remainder on (bm, 64) -- exact on integer
+    data for bf16 output (+bias, relu, colsum) and split-K slabs."""
+    gen = torch.Generator().manual_seed(5 + bm + bn + 3 * la + lb)
+    M, N, K = 2 * bm, 832, 320
+    a = _storage(la, M, K, gen, dev, True)
+    b = _storage(lb, N, K, gen, dev, True)
+    ref = _logical(a, la, M, K) @ _logical(b, lb, N, K).t()
+    bias = torch.randint(-4, 5, (N,), generator=gen).float().to(dev)
+    y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    cs = torch.full((M // bm, N), 3.0, device=dev)
+    ops.gemm(a, b, y, layout_a=la, layout_b=lb, M=M, N=N, K=K, bias=bias, act="relu",
+             tiles=(bm, bn), colsum=cs)
+    yr = (ref + bias).clamp_min(0).to(torch.bfloat16)
+    assert torch.equal(y, yr)
+    torch.testing.assert_close(cs, yr.float().view(M // bm, bm, N).sum(1), rtol=1e-5, atol=1e-2)
+    slabs = torch.empty(3, M, N, device=dev)
+    ops.gemm(a, b, slabs, layout_a=la, layout_b=lb, M=M, N=N, K=K, k_total=K, splits=3,
+             tiles=(bm, bn))
+    assert torch.equal(slabs.sum(0), ref)
+
+
 def test_gemm_identity_asymmetric(dev):
     M = N = K = 128
     eye = torch.eye(M, dtype=torch.bfloat16, device=dev)
