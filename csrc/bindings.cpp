@@ -19,6 +19,7 @@
 #include "runtime/graph.hpp"
 #include "runtime/json_weights.hpp"
 #include "runtime/matrix_codec.hpp"
+#include "runtime/program.hpp"
 #include "runtime/schedule.hpp"
 
 namespace py = pybind11;
@@ -30,10 +31,23 @@ static T* P(uintptr_t p) {
   return reinterpret_cast<T*>(p);
 }
 
+static void check(int rc, const char* what);
+
+// Launch now, or append to the Program recording on this thread (see runtime/program.hpp).
+template <class F>
+static void launch(const char* what, F f, uintptr_t stream) {
+  if (dnn::Program* pr = dnn::recording_program()) {
+    pr->add(what, dnn::Program::Launch(std::move(f)));
+    return;
+  }
+  static const dnn::Program identity;  // no regions: fix() is the identity
+  check(f(S(stream), identity), what);
+}
+
 static void check(int rc, const char* what) {
   if (rc != 0) {
     std::string msg = std::string(what) + " failed: ";
-    if (std::string(what) == "gemm_bf16") msg += dnn::gemm_error_string(rc);
+    if (std::string(what).rfind("gemm_bf16", 0) == 0) msg += dnn::gemm_error_string(rc);
     else msg += "precondition/launch error code " + std::to_string(rc);
     if (rc == -9) msg += std::string(" (") + hipGetErrorString(hipGetLastError()) + ")";
     throw std::invalid_argument(msg);
@@ -43,6 +57,9 @@ static void check(int rc, const char* what) {
 PYBIND11_MODULE(_native, m) {
   m.doc() = "docker_dist_nn_amd native runtime + gfx950 HIP kernels";
 
+  // Every kernel binding goes through launch(): it launches now, or -- while a Program is
+  // recording on this thread -- appends the launch (pointers routed through Program::fix so
+  // they can be relocated at replay; stream chosen at replay).
   m.def(
       "gemm_bf16",
       [](uintptr_t a, long lda, uintptr_t b, long ldb, uintptr_t c, long ldc, long c_split_stride,
@@ -75,8 +92,22 @@ PYBIND11_MODULE(_native, m) {
         p.K = K;
         p.act = act;
         p.accumulate = accumulate;
-        check(dnn::gemm_bf16(p, layout_a, layout_b, out_f32, bm, bn, splits, S(stream), stages),
-              "gemm_bf16");
+        launch(
+            "gemm_bf16",
+            [=](hipStream_t s, const dnn::Program& R) {
+              GemmParams q = p;
+              q.A = R.fix(q.A);
+              q.B = R.fix(q.B);
+              q.C = R.fix(q.C);
+              q.bias = R.fix(q.bias);
+              q.aux = R.fix(q.aux);
+              q.colsum = R.fix(q.colsum);
+              q.xent_labels = R.fix(q.xent_labels);
+              q.loss_part = R.fix(q.loss_part);
+              q.correct = R.fix(q.correct);
+              return dnn::gemm_bf16(q, layout_a, layout_b, out_f32, bm, bn, splits, s, stages);
+            },
+            stream);
       },
       py::arg("a"), py::arg("lda"), py::arg("b"), py::arg("ldb"), py::arg("c"), py::arg("ldc"),
       py::arg("c_split_stride"), py::arg("bias"), py::arg("aux"), py::arg("ld_aux"), py::arg("M"),
@@ -104,9 +135,17 @@ PYBIND11_MODULE(_native, m) {
         p.N = N;
         p.K = K;
         p.accumulate = accumulate;
-        check(dnn::gemm_bf16_streamk(p, layout_a, layout_b, bm, bn, nwg, P<float>(part),
-                                     S(stream)),
-              "gemm_bf16");
+        launch(
+            "gemm_bf16_streamk",
+            [=](hipStream_t s, const dnn::Program& R) {
+              GemmParams q = p;
+              q.A = R.fix(q.A);
+              q.B = R.fix(q.B);
+              q.C = R.fix(q.C);
+              return dnn::gemm_bf16_streamk(q, layout_a, layout_b, bm, bn, nwg,
+                                            R.fix(P<float>(part)), s);
+            },
+            stream);
       },
       py::arg("a"), py::arg("lda"), py::arg("b"), py::arg("ldb"), py::arg("c"), py::arg("ldc"),
       py::arg("M"), py::arg("N"), py::arg("K"), py::arg("accumulate"), py::arg("layout_a"),
@@ -116,11 +155,16 @@ PYBIND11_MODULE(_native, m) {
         [](uintptr_t logits, long ld_logits, uintptr_t labels, uintptr_t dz, long ld_dz, int rows,
            int n_cls, int width, float scale, uintptr_t loss_part, uintptr_t correct,
            uintptr_t stream, uintptr_t colsum, long ld_colsum) {
-          check(dnn::softmax_xent(P<const float>(logits), ld_logits, P<const int>(labels),
-                                  P<uint16_t>(dz), ld_dz, rows, n_cls, width, scale,
-                                  P<float>(loss_part), P<int>(correct), P<float>(colsum),
-                                  ld_colsum, S(stream)),
-                "softmax_xent");
+          launch(
+              "softmax_xent",
+              [=](hipStream_t s, const dnn::Program& R) {
+                return dnn::softmax_xent(R.fix(P<const float>(logits)), ld_logits,
+                                         R.fix(P<const int>(labels)), R.fix(P<uint16_t>(dz)),
+                                         ld_dz, rows, n_cls, width, scale,
+                                         R.fix(P<float>(loss_part)), R.fix(P<int>(correct)),
+                                         R.fix(P<float>(colsum)), ld_colsum, s);
+              },
+              stream);
         },
         py::arg("logits"), py::arg("ld_logits"), py::arg("labels"), py::arg("dz"),
         py::arg("ld_dz"), py::arg("rows"), py::arg("n_cls"), py::arg("width"), py::arg("scale"),
@@ -130,21 +174,34 @@ PYBIND11_MODULE(_native, m) {
   m.def("softmax_rows", [](uintptr_t logits, long ld_in, uintptr_t out, long ld_out, int rows,
                            int n_cls, uintptr_t labels, uintptr_t pred, uintptr_t correct,
                            uintptr_t stream) {
-    check(dnn::softmax_rows(P<const float>(logits), ld_in, P<float>(out), ld_out, rows, n_cls,
-                            P<const int>(labels), P<int>(pred), P<int>(correct), S(stream)),
-          "softmax_rows");
+    launch(
+        "softmax_rows",
+        [=](hipStream_t s, const dnn::Program& R) {
+          return dnn::softmax_rows(R.fix(P<const float>(logits)), ld_in, R.fix(P<float>(out)),
+                                   ld_out, rows, n_cls, R.fix(P<const int>(labels)),
+                                   R.fix(P<int>(pred)), R.fix(P<int>(correct)), s);
+        },
+        stream);
   });
   m.def("colsum_partial", [](uintptr_t x, long ld, int rows, int cols, int n_part, uintptr_t part,
                              uintptr_t stream) {
-    check(dnn::colsum_partial(P<const uint16_t>(x), ld, rows, cols, n_part, P<float>(part),
-                              S(stream)),
-          "colsum_partial");
+    launch(
+        "colsum_partial",
+        [=](hipStream_t s, const dnn::Program& R) {
+          return dnn::colsum_partial(R.fix(P<const uint16_t>(x)), ld, rows, cols, n_part,
+                                     R.fix(P<float>(part)), s);
+        },
+        stream);
   });
   m.def("reduce_slabs", [](uintptr_t src, long stride, int n_src, long n, float scale,
                            uintptr_t out, int accumulate, uintptr_t stream) {
-    check(dnn::reduce_slabs(P<const float>(src), stride, n_src, n, scale, P<float>(out),
-                            accumulate, S(stream)),
-          "reduce_slabs");
+    launch(
+        "reduce_slabs",
+        [=](hipStream_t s, const dnn::Program& R) {
+          return dnn::reduce_slabs(R.fix(P<const float>(src)), stride, n_src, n, scale,
+                                   R.fix(P<float>(out)), accumulate, s);
+        },
+        stream);
   });
   // jobs: sequence of (src, stride, n_src, n, out, scale, accumulate); > 16 jobs -> several
   // launches
@@ -158,36 +215,103 @@ PYBIND11_MODULE(_native, m) {
                    P<float>(std::get<4>(t)), std::get<2>(t), std::get<5>(t), std::get<6>(t)});
     for (size_t k = 0; k < J.size(); k += dnn::REDUCE_MAX_JOBS) {
       const int n = (int)std::min<size_t>(dnn::REDUCE_MAX_JOBS, J.size() - k);
-      check(dnn::reduce_multi(J.data() + k, n, S(stream)), "reduce_multi");
+      std::vector<dnn::ReduceJob> part(J.begin() + k, J.begin() + k + n);
+      launch(
+          "reduce_multi",
+          [part](hipStream_t s, const dnn::Program& R) mutable {
+            std::vector<dnn::ReduceJob> q = part;
+            for (auto& j : q) {
+              j.src = R.fix(j.src);
+              j.out = R.fix(j.out);
+            }
+            return dnn::reduce_multi(q.data(), (int)q.size(), s);
+          },
+          stream);
     }
   });
   m.def("sgd_update", [](uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t shadow, long n,
                          float lr, float mu, float wd, uintptr_t stream) {
-    check(dnn::sgd_update(P<float>(p), P<const float>(g), P<float>(mom), P<uint16_t>(shadow), n,
-                          lr, mu, wd, S(stream)),
-          "sgd_update");
+    launch(
+        "sgd_update",
+        [=](hipStream_t s, const dnn::Program& R) {
+          return dnn::sgd_update(R.fix(P<float>(p)), R.fix(P<const float>(g)),
+                                 R.fix(P<float>(mom)), R.fix(P<uint16_t>(shadow)), n, lr, mu, wd,
+                                 s);
+        },
+        stream);
   });
   m.def("adam_update",
         [](uintptr_t p, uintptr_t g, uintptr_t mm, uintptr_t vv, uintptr_t shadow, long n,
            float lr, float b1, float b2, float eps, float wd, int decoupled, float bc1, float bc2,
            uintptr_t stream) {
-          check(dnn::adam_update(P<float>(p), P<const float>(g), P<float>(mm), P<float>(vv),
-                                 P<uint16_t>(shadow), n, lr, b1, b2, eps, wd, decoupled, bc1, bc2,
-                                 S(stream)),
-                "adam_update");
+          launch(
+              "adam_update",
+              [=](hipStream_t s, const dnn::Program& R) {
+                return dnn::adam_update(R.fix(P<float>(p)), R.fix(P<const float>(g)),
+                                        R.fix(P<float>(mm)), R.fix(P<float>(vv)),
+                                        R.fix(P<uint16_t>(shadow)), n, lr, b1, b2, eps, wd,
+                                        decoupled, bc1, bc2, s);
+              },
+              stream);
         });
   m.def("pack_bf16", [](uintptr_t in, long ld_in, int rows, int cols, uintptr_t out, long ld_out,
                         int rows_p, int cols_p, uintptr_t stream) {
-    check(dnn::pack_bf16(P<const float>(in), ld_in, rows, cols, P<uint16_t>(out), ld_out, rows_p,
-                         cols_p, S(stream)),
-          "pack_bf16");
+    launch(
+        "pack_bf16",
+        [=](hipStream_t s, const dnn::Program& R) {
+          return dnn::pack_bf16(R.fix(P<const float>(in)), ld_in, rows, cols,
+                                R.fix(P<uint16_t>(out)), ld_out, rows_p, cols_p, s);
+        },
+        stream);
   });
   m.def("unpack_bf16", [](uintptr_t in, long ld_in, int rows, int cols, uintptr_t out,
                           long ld_out, uintptr_t stream) {
-    check(dnn::unpack_bf16(P<const uint16_t>(in), ld_in, rows, cols, P<float>(out), ld_out,
-                           S(stream)),
-          "unpack_bf16");
+    launch(
+        "unpack_bf16",
+        [=](hipStream_t s, const dnn::Program& R) {
+          return dnn::unpack_bf16(R.fix(P<const uint16_t>(in)), ld_in, rows, cols,
+                                  R.fix(P<float>(out)), ld_out, s);
+        },
+        stream);
   });
+
+  // ---- runtime: native step executor (recorded launch programs) ---------------------------
+  py::class_<dnn::Program>(m, "Program",
+                           "Recorded kernel launches in named segments, replayed from C++.")
+      .def(py::init<>())
+      .def("mark", &dnn::Program::mark, py::arg("name"))
+      .def("close", &dnn::Program::close)
+      .def("region", &dnn::Program::region, py::arg("base"), py::arg("size"))
+      .def("rebase", &dnn::Program::rebase, py::arg("id"), py::arg("new_base"))
+      .def(
+          "run",
+          [](const dnn::Program& pr, const std::vector<std::string>& names, uintptr_t stream) {
+            py::gil_scoped_release nogil;
+            pr.run(names, S(stream));
+          },
+          py::arg("names"), py::arg("stream"))
+      .def(
+          "run_all",
+          [](const dnn::Program& pr, uintptr_t stream) {
+            py::gil_scoped_release nogil;
+            pr.run_all(S(stream));
+          },
+          py::arg("stream"))
+      .def_property_readonly("size", &dnn::Program::size)
+      .def("segments", &dnn::Program::segments)
+      .def("segment_size", &dnn::Program::segment_size)
+      .def("clear", &dnn::Program::clear);
+  m.def("record_begin", [](dnn::Program& pr) {
+    if (dnn::recording_program()) throw std::runtime_error("already recording a Program");
+    dnn::recording_program() = &pr;
+  });
+  m.def("record_end", []() {
+    if (dnn::recording_program()) dnn::recording_program()->close();
+    dnn::recording_program() = nullptr;
+  });
+  m.def("is_recording", []() { return dnn::recording_program() != nullptr; });
+  m.def("roctx_push", [](const std::string& n) { dnn::roctx_push(n.c_str()); });
+  m.def("roctx_pop", []() { dnn::roctx_pop(); });
 
   // ---- runtime: pipeline schedules -------------------------------------------------------
   py::enum_<dnn::OpKind>(m, "OpKind")

@@ -30,6 +30,7 @@ import torch
 
 from .. import ops
 from ..models.mlp import LayerGeom, MLPSpec, round_up
+from ..utils.native import native
 
 _ALIGN = 64  # elements; keeps every layer's region 256-B aligned
 
@@ -239,6 +240,11 @@ class Stage:
                       for i, g in enumerate(self.geoms)]
         self._w_done = 0
         self._reduce_jobs: dict = {}
+        self._prog = None  # native Program once compile_native() ran
+        self._recording = False
+        self._has_w = False
+        self._o_lr: Optional[float] = None
+        self._rx = self._rl = None
 
     def rows_of(self, j: int) -> slice:
         if not 0 <= j < self.nm:
@@ -263,6 +269,8 @@ class Stage:
         self._w_done = 0
 
     def forward(self, j: int) -> None:
+        if self._prog is not None and not self._recording:
+            return self._replay(f"F{j}")
         r = self.rows_of(j)
         p = self.params
         for i, g in enumerate(self.geoms):
@@ -288,6 +296,8 @@ class Stage:
 
     def backward(self, j: int) -> None:
         """dgrad chain of micro-batch j; dZ of the last local layer must already be present."""
+        if self._prog is not None and not self._recording:
+            return self._replay(f"B{j}")
         r = self.rows_of(j)
         p = self.params
         if not self.last:  # dZ of our last layer arrived from the next stage
@@ -307,6 +317,10 @@ class Stage:
 
     def wgrad(self, j: int = -1) -> None:
         """Weight/bias gradients for micro-batch j (slab-accumulated) or all rows (j = -1)."""
+        if j < 0 and self._prog is not None and not self._recording and self._has_w:
+            self._replay("W")
+            self._w_done += 1
+            return
         for i in range(len(self.geoms)):
             self.wgrad_layer(i, j)
         self._w_done += 1
@@ -316,6 +330,8 @@ class Stage:
 
     def wgrad_layer(self, i: int, j: int = -1) -> None:
         """Weight gradient GEMM of local layer i (bias partials were produced with dZ)."""
+        if j < 0 and self._prog is not None and not self._recording and self._has_w:
+            return self._replay(f"W{i}")
         if j < 0:
             r, accumulate = slice(0, self.rows), False
         else:
@@ -333,6 +349,11 @@ class Stage:
 
     def finalize_grads(self, layers: Optional[Sequence[int]] = None) -> None:
         """Reduce bias partials (and, for split-K, weight slabs) into the flat gradient."""
+        if self._prog is not None and not self._recording:
+            if layers is None:
+                return self._replay("FIN")
+            if len(layers) == 1:
+                return self._replay(f"FIN{layers[0]}")
         key = tuple(range(len(self.geoms))) if layers is None else tuple(layers)
         jobs = self._reduce_jobs.get(key)
         if jobs is None:  # buffers are fixed for the stage's lifetime: build the table once
@@ -349,14 +370,84 @@ class Stage:
         ops.reduce_multi(jobs)  # one launch for every slab set and bias-partial set
 
     def optimizer_step(self, lr: Optional[float] = None) -> None:
+        if self._prog is not None and self._o_lr is not None and (lr is None or lr == self._o_lr):
+            self.params.step_count += 1
+            return self._replay("O")
         self.params.optimizer_step(lr)
+
+    # ---- native replay (csrc/runtime/program.{hpp,cpp}) ---------------------------------
+    def compile_native(self) -> None:
+        """Record every per-op kernel sequence of this stage ONCE into a native Program:
+        F{j} / B{j} per micro-batch, W{i} / W (batched wgrad), FIN{i} / FIN (gradient
+        reduction) and O (SGD update). Afterwards forward/backward/... replay their segment
+        from C++ (one Python call per schedule op instead of one per kernel). The first
+        stage's input and the last stage's labels are relocatable regions, so zero-copy
+        batches (bind_input / bind_labels) work without re-recording. The Python bodies stay
+        the reference path (CPU, per-micro wgrad, Adam)."""
+        nat = native()
+        prog = nat.Program()
+        self.x_in = self.x_buf
+        if self.labels is not None:
+            self.labels = self.labels_buf
+        self._rx = (prog.region(self.x_buf.data_ptr(), self.x_buf.numel() * 2)
+                    if self.first else None)
+        self._rl = (prog.region(self.labels_buf.data_ptr(), self.labels_buf.numel() * 4)
+                    if self.labels is not None else None)
+        self._recording = True
+        nat.record_begin(prog)
+        try:
+            for j in range(self.nm):
+                prog.mark(f"F{j}")
+                self.forward(j)
+            for j in range(self.nm):
+                prog.mark(f"B{j}")
+                self.backward(j)
+            self._has_w = self.wgrad_mode == "batched"
+            if self._has_w:
+                for i in range(len(self.geoms)):
+                    prog.mark(f"W{i}")
+                    self.wgrad_layer(i)
+                prog.mark("W")
+                for i in range(len(self.geoms)):
+                    self.wgrad_layer(i)
+            for i in range(len(self.geoms)):
+                prog.mark(f"FIN{i}")
+                self.finalize_grads([i])
+            prog.mark("FIN")
+            self.finalize_grads()
+            o = self.params.optim
+            if o.name == "sgd":
+                prog.mark("O")
+                ops.sgd_update(self.params.master, self.params.grad,
+                               self.params.state[0] if self.params.state else None,
+                               self.params.shadow, lr=o.lr, momentum=o.momentum,
+                               weight_decay=o.weight_decay)
+                self._o_lr = o.lr
+        finally:
+            nat.record_end()
+            self._recording = False
+        self._prog = prog
+
+    def _replay(self, seg: str) -> None:
+        self._prog.run([seg], torch.cuda.current_stream(self.device).cuda_stream)
+
+    def bind_input(self, x: torch.Tensor) -> None:
+        """First stage reads ``x`` in place (zero-copy) from now on."""
+        self.x_in = x
+        if self._prog is not None and self._rx is not None:
+            self._prog.rebase(self._rx, x.data_ptr())
+
+    def bind_labels(self, y: torch.Tensor) -> None:
+        self.labels = y
+        if self._prog is not None and self._rl is not None:
+            self._prog.rebase(self._rl, y.data_ptr())
 
     # convenience: a whole step when this stage holds the entire model ----------------------
     def set_batch(self, x: torch.Tensor, labels: torch.Tensor) -> None:
-        self.x_in = self.x_buf  # never write through an alias of the caller's dataset
+        self.bind_input(self.x_buf)  # never write through an alias of the caller's dataset
         self.x_in.copy_(x)
         if self.labels is not None:
-            self.labels = self.labels_buf
+            self.bind_labels(self.labels_buf)
             self.labels.copy_(labels)
 
     def loss_sum(self) -> float:

@@ -17,6 +17,8 @@ backward -> optimizer step) distributed over the stages.
 """
 from __future__ import annotations
 
+import os
+
 from typing import Optional, Sequence
 
 import numpy as np
@@ -41,7 +43,8 @@ class Trainer:
                  dp: int = 1, distribution: Optional[Sequence[int]] = None,
                  schedule: str = "1f1b", optim: Optional[OptimConfig] = None,
                  device: Optional[torch.device] = None, seed: int = 0,
-                 mesh: Optional[Mesh] = None, wgrad: Optional[str] = None):
+                 mesh: Optional[Mesh] = None, wgrad: Optional[str] = None,
+                 native_exec: Optional[bool] = None):
         self.spec = spec
         self.mesh = mesh
         self.device = device or (torch.device("cuda", torch.cuda.current_device())
@@ -81,6 +84,15 @@ class Trainer:
             ids = [mesh.stage]
             sync = GradSync(mesh.dp_group, mesh.dp) if mesh.dp > 1 else None
         self.executor = PipelineExecutor(self.stages, self.pipe, schedule, pp, ids, sync)
+        # native step executor: record each stage's launches once, replay from C++ (after the
+        # pipe has aliased loopback buffers, so the recorded pointers are the final ones)
+        if native_exec is None:
+            native_exec = (self.device.type == "cuda" and
+                           os.environ.get("DNN_NATIVE_EXEC", "1") != "0")
+        self.native_exec = bool(native_exec)
+        if self.native_exec:
+            for st in self.stages:
+                st.compile_native()
         self._graph = None
         self._stream = None
         self.graph_nodes = 0
@@ -105,23 +117,23 @@ class Trainer:
             if x is None:
                 raise ValueError("first stage needs inputs")
             st = self.first
-            if zero_copy and self._graph is None and x.shape == st.x_in.shape and \
-                    x.dtype == st.x_in.dtype and x.device == st.x_in.device and \
+            if zero_copy and self._graph is None and x.shape == st.x_buf.shape and \
+                    x.dtype == st.x_buf.dtype and x.device == st.x_buf.device and \
                     x.stride(1) == 1 and x.data_ptr() % 16 == 0 and len(self.stages) == 1:
-                st.x_in = x
+                st.bind_input(x)
             else:
-                st.x_in = st.x_buf  # never write through an alias of a previous batch
+                st.bind_input(st.x_buf)  # never write through an alias of a previous batch
                 st.x_in.copy_(x)
         if self.last is not None:
             if labels is None:
                 raise ValueError("last stage needs labels")
             st = self.last
-            if zero_copy and self._graph is None and labels.shape == st.labels.shape and \
-                    labels.dtype == st.labels.dtype and labels.device == st.labels.device and \
-                    labels.is_contiguous():
-                st.labels = labels
+            if zero_copy and self._graph is None and labels.shape == st.labels_buf.shape and \
+                    labels.dtype == st.labels_buf.dtype and \
+                    labels.device == st.labels_buf.device and labels.is_contiguous():
+                st.bind_labels(labels)
             else:
-                st.labels = st.labels_buf
+                st.bind_labels(st.labels_buf)
                 st.labels.copy_(labels)
 
     def step(self) -> None:
