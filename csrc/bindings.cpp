@@ -301,6 +301,19 @@ PYBIND11_MODULE(_native, m) {
       .def("segments", &dnn::Program::segments)
       .def("segment_size", &dnn::Program::segment_size)
       .def("clear", &dnn::Program::clear);
+  // A whole step of a single-process (loopback) pipeline: (program, segment) pairs in
+  // schedule order, one call, GIL released.
+  m.def(
+      "run_plan",
+      [](const std::vector<std::pair<const dnn::Program*, std::string>>& plan, uintptr_t stream) {
+        py::gil_scoped_release nogil;
+        std::vector<std::string> one(1);
+        for (const auto& [pr, seg] : plan) {
+          one[0] = seg;
+          pr->run(one, S(stream));
+        }
+      },
+      py::arg("plan"), py::arg("stream"));
   m.def("record_begin", [](dnn::Program& pr) {
     if (dnn::recording_program()) throw std::runtime_error("already recording a Program");
     dnn::recording_program() = &pr;

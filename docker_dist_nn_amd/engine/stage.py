@@ -235,11 +235,15 @@ class Stage:
             elif self.last:
                 self.bp.append(self.xent_per_micro)
             else:
-                self.bp.append(max(1, self.mb // 1024))
+                # one partial per 128 rows: enough workgroups to fill the chip (1024-row
+                # partitions left a 4096-row boundary colsum at 32 workgroups, 12 us)
+                self.bp.append(max(1, self.mb // 128))
         self.bpart = [torch.zeros(self.bp[i] * self.nm, g.np_, dtype=f32, device=dev)
                       for i, g in enumerate(self.geoms)]
         self._w_done = 0
         self._reduce_jobs: dict = {}
+        self._colsum_by = None  # loopback: the next stage computes our boundary colsum
+        self._colsum_for = None  # ... and this is the stage we compute it for
         self._prog = None  # native Program once compile_native() ran
         self._recording = False
         self._has_w = False
@@ -300,8 +304,8 @@ class Stage:
             return self._replay(f"B{j}")
         r = self.rows_of(j)
         p = self.params
-        if not self.last:  # dZ of our last layer arrived from the next stage
-            L = len(self.geoms) - 1
+        if not self.last and self._colsum_by is None:  # dZ of our last layer arrived from
+            L = len(self.geoms) - 1                       # the next stage
             ops.colsum_partial(self.dz[L][r], self._bpart(L, j), self.bp[L])
         for i in range(len(self.geoms) - 1, -1, -1):
             if i > 0:
@@ -312,8 +316,10 @@ class Stage:
             elif not self.first:
                 # gradient for the previous stage, already multiplied by the derivative of its
                 # last layer's activation (its output is our input x_in)
+                up = self._colsum_for
                 ops.linear_dgrad(self.dz[0][r], p.wbf(0), self.dx_send[r], y_prev=self.x_in[r],
-                                 act_prev=self.prev_act)
+                                 act_prev=self.prev_act,
+                                 colsum=None if up is None else up._bpart(len(up.geoms) - 1, j))
 
     def wgrad(self, j: int = -1) -> None:
         """Weight/bias gradients for micro-batch j (slab-accumulated) or all rows (j = -1)."""
@@ -374,6 +380,21 @@ class Stage:
             self.params.step_count += 1
             return self._replay("O")
         self.params.optimizer_step(lr)
+
+    def fuse_boundary_colsum(self, consumer: "Stage") -> None:
+        """Same-process pipeline: ``consumer`` (the next stage) writes our last layer's
+        bias-gradient partials from its input-gradient dgrad epilogue (loopback only)."""
+        if consumer.mb != self.mb or consumer.nm != self.nm:
+            raise ValueError("loopback stages must share the micro-batch layout")
+        L = len(self.geoms) - 1
+        g0 = consumer.geoms[0]
+        bm = ops.dgrad_tiles(consumer.mb, g0.kp, g0.np_)[0]
+        self.bp[L] = self.mb // bm
+        self.bpart[L] = torch.zeros(self.bp[L] * self.nm, self.geoms[L].np_,
+                                    dtype=torch.float32, device=self.device)
+        self._reduce_jobs.clear()
+        self._colsum_by = consumer
+        consumer._colsum_for = self
 
     # ---- native replay (csrc/runtime/program.{hpp,cpp}) ---------------------------------
     def compile_native(self) -> None:

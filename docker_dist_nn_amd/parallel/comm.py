@@ -36,6 +36,9 @@ class LoopbackPipe:
                 raise ValueError("loopback stages must share device and boundary width")
             b.x_in = b.x_buf = a.output  # activations: producer writes the consumer's input
             a.dz[-1] = b.dx_send        # gradients: consumer writes the producer's dZ
+            # ... and the consumer's first dgrad epilogue emits the producer's bias-gradient
+            # partials (column sums of that dZ): no boundary colsum kernel per micro-batch
+            a.fuse_boundary_colsum(b)
 
     def begin_step(self):
         pass

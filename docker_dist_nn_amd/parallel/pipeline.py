@@ -19,6 +19,7 @@ from __future__ import annotations
 
 from typing import Callable, Optional, Sequence
 
+import torch
 import torch.distributed as dist
 
 from ..utils.native import native
@@ -118,10 +119,56 @@ class PipelineExecutor:
                 self.grad_sync.launch(st.params.grad, a, b)
         st._finalized = True
 
+    def _native_plan(self):
+        """For an all-native loopback step (one process, no DP, batched wgrad, SGD): the
+        schedule's op order as (stage, segment) pairs, computed once by a dry traversal of
+        the same dispatch rules as _run_op. None when any op needs the Python path."""
+        if getattr(self, "_plan", False) is not False:
+            return self._plan
+        from .comm import LoopbackPipe
+
+        self._plan = None
+        if not isinstance(self.pipe, LoopbackPipe) or self.grad_sync is not None or \
+                self.hooks["before_op"] or self.hooks["after_op"] or self.lr_fn is not None:
+            return None
+        if any(st._prog is None or not st._has_w or st._o_lr is None for st in self.stages):
+            return None
+        order = []
+        self._traverse(lambda s, op, j, nxt: order.append((s, op, j, nxt)))
+        plan = []
+        for s, op, j, nxt in order:
+            st = self.stages[s]
+            if op in ("F", "B"):
+                plan.append((st, f"{op}{j}"))
+            elif op == "W":
+                if j >= 0:
+                    return None
+                if nxt == "O":  # as _wgrad_finalize_overlapped without a DP group
+                    plan += [(st, f"W{i}") for i in range(len(st.geoms) - 1, -1, -1)]
+                    plan.append((st, "FIN"))
+                    plan.append((st, "#finalized"))
+                else:
+                    plan.append((st, "W"))
+            elif op == "O":
+                if (st, "#finalized") not in plan:
+                    plan.append((st, "FIN"))
+                plan.append((st, "O"))
+        self._plan = [(st, seg) for st, seg in plan if not seg.startswith("#")]
+        return self._plan
+
     def run_step(self) -> None:
         self.pipe.begin_step()
         for st in self.stages:
             st.begin_step()
+        plan = self._native_plan()
+        if plan is not None:
+            dev = self.stages[0].device
+            native().run_plan([(st._prog, seg) for st, seg in plan],
+                              torch.cuda.current_stream(dev).cuda_stream)
+            for st in self.stages:
+                st.params.step_count += 1
+            self.pipe.end_step()
+            return
         if len(self.stages) == 1:
             st, ops = self.stages[0], self.ops[0]
             for k, (op, j) in enumerate(ops):
@@ -132,6 +179,11 @@ class PipelineExecutor:
         self.pipe.end_step()
 
     def _run_interleaved(self):
+        self._traverse(lambda s, op, j, nxt: self._run_op(self.stages[s], op, j, nxt))
+
+    def _traverse(self, visit):
+        """Walk every stage's op list in a dependency-respecting round-robin order (a
+        micro-batch's F after the previous stage's F, its B after the next stage's B)."""
         S = len(self.stages)
         pc = [0] * S
         fdone = [set() for _ in range(S)]
@@ -148,7 +200,7 @@ class PipelineExecutor:
                     if op == "B" and s < S - 1 and j not in bdone[s + 1]:
                         break
                     nxt = ops[pc[s] + 1][0] if pc[s] + 1 < len(ops) else None
-                    self._run_op(self.stages[s], op, j, nxt)
+                    visit(s, op, j, nxt)
                     if op == "F":
                         fdone[s].add(j)
                     elif op == "B":

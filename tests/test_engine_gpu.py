@@ -96,6 +96,8 @@ def test_native_executor_equals_python(dev, pp, sched):
             tr.set_batch(xs, ys, zero_copy=True)
             tr.step()
             losses.append(tr.loss())
+        # all-native loopback steps run as ONE C++ call over a precomputed segment plan
+        assert (tr.executor._native_plan() is not None) == native_exec
         out.append((losses, tr.local_weights(), tr.correct()))
     (l0, w0, c0), (l1, w1, c1) = out
     assert l0 == l1 and c0 == c1
