@@ -303,17 +303,36 @@ PYBIND11_MODULE(_native, m) {
       .def("clear", &dnn::Program::clear);
   // A whole step of a single-process (loopback) pipeline: (program, segment) pairs in
   // schedule order, one call, GIL released.
+  // A whole step of a single-process (loopback) pipeline: (program, segment, stream) triples
+  // in schedule order, one call, GIL released. stream 0 = `stream`, 1 = `side`; the pseudo
+  // segments "@fork" (side waits for main) and "@join" (main waits for side) order the two.
   m.def(
       "run_plan",
-      [](const std::vector<std::pair<const dnn::Program*, std::string>>& plan, uintptr_t stream) {
+      [](const std::vector<std::tuple<const dnn::Program*, std::string, int>>& plan,
+         uintptr_t stream, uintptr_t side) {
         py::gil_scoped_release nogil;
+        static thread_local hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+        if (!ev_fork) {
+          if (hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming) != hipSuccess ||
+              hipEventCreateWithFlags(&ev_join, hipEventDisableTiming) != hipSuccess)
+            throw std::runtime_error("run_plan: hipEventCreate failed");
+        }
         std::vector<std::string> one(1);
-        for (const auto& [pr, seg] : plan) {
+        for (const auto& [pr, seg, si] : plan) {
+          if (seg == "@fork" || seg == "@join") {
+            if (!side) throw std::invalid_argument("run_plan: fork/join without a side stream");
+            hipEvent_t ev = seg == "@fork" ? ev_fork : ev_join;
+            hipStream_t from = seg == "@fork" ? S(stream) : S(side);
+            hipStream_t to = seg == "@fork" ? S(side) : S(stream);
+            if (hipEventRecord(ev, from) != hipSuccess || hipStreamWaitEvent(to, ev, 0) != hipSuccess)
+              throw std::runtime_error("run_plan: event fork/join failed");
+            continue;
+          }
           one[0] = seg;
-          pr->run(one, S(stream));
+          pr->run(one, si ? S(side) : S(stream));
         }
       },
-      py::arg("plan"), py::arg("stream"));
+      py::arg("plan"), py::arg("stream"), py::arg("side") = 0);
   m.def("record_begin", [](dnn::Program& pr) {
     if (dnn::recording_program()) throw std::runtime_error("already recording a Program");
     dnn::recording_program() = &pr;

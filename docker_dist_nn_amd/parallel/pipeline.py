@@ -17,6 +17,7 @@ S-stage pipelines on one device and checks that the schedules are deadlock-free.
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, Optional, Sequence
 
 import torch
@@ -68,6 +69,9 @@ class PipelineExecutor:
         self.ops = [schedule_ops(kind, num_stages, st.nm, sid)
                     for st, sid in zip(self.stages, self.stage_ids)]
         self.hooks: dict[str, list[Callable]] = {"before_op": [], "after_op": []}
+        # concurrent wgrad streams in native single-process plans (DNN_WGRAD_STREAMS)
+        self.wgrad_streams = int(os.environ.get("DNN_WGRAD_STREAMS", "1"))
+        self._side = None
 
     # ---------------------------------------------------------------------------------------
     def _run_op(self, st, op, j, next_op=None):
@@ -144,7 +148,18 @@ class PipelineExecutor:
                 if j >= 0:
                     return None
                 if nxt == "O":  # as _wgrad_finalize_overlapped without a DP group
-                    plan += [(st, f"W{i}") for i in range(len(st.geoms) - 1, -1, -1)]
+                    L = len(st.geoms)
+                    if self.wgrad_streams > 1 and L > 1:
+                        # the biggest layer's wgrad on the main stream, the rest concurrently
+                        # on the side stream (independent GEMMs; small ones alone leave the
+                        # chip idle), joined before the one reduction launch
+                        big = max(range(L), key=lambda i: st.geoms[i].np_ * st.geoms[i].kp)
+                        plan.append((None, "@fork"))
+                        plan += [(st, f"W{i}", 1) for i in range(L - 1, -1, -1) if i != big]
+                        plan.append((st, f"W{big}"))
+                        plan.append((None, "@join"))
+                    else:
+                        plan += [(st, f"W{i}") for i in range(L - 1, -1, -1)]
                     plan.append((st, "FIN"))
                     plan.append((st, "#finalized"))
                 else:
@@ -153,7 +168,8 @@ class PipelineExecutor:
                 if (st, "#finalized") not in plan:
                     plan.append((st, "FIN"))
                 plan.append((st, "O"))
-        self._plan = [(st, seg) for st, seg in plan if not seg.startswith("#")]
+        self._plan = [(e[0], e[1], e[2] if len(e) > 2 else 0) for e in plan
+                      if not e[1].startswith("#")]
         return self._plan
 
     def run_step(self) -> None:
@@ -163,8 +179,12 @@ class PipelineExecutor:
         plan = self._native_plan()
         if plan is not None:
             dev = self.stages[0].device
-            native().run_plan([(st._prog, seg) for st, seg in plan],
-                              torch.cuda.current_stream(dev).cuda_stream)
+            if self._side is None and self.wgrad_streams > 1:
+                self._side = torch.cuda.Stream(dev)
+            native().run_plan([(st._prog if st is not None else None, seg, si)
+                               for st, seg, si in plan],
+                              torch.cuda.current_stream(dev).cuda_stream,
+                              self._side.cuda_stream if self._side is not None else 0)
             for st in self.stages:
                 st.params.step_count += 1
             self.pipe.end_step()

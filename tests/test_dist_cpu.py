@@ -59,7 +59,8 @@ def _worker(rank, world, port, pp, dp, mb, nm, sched, steps, out_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("pp,dp,sched", [(2, 2, "1f1b"), (4, 1, "zb"), (1, 2, "1f1b")])
+@pytest.mark.parametrize("pp,dp,sched", [(2, 2, "1f1b"), (4, 1, "zb"), (1, 2, "1f1b"),
+                                         (2, 4, "1f1b"), (1, 8, "1f1b")])
 def test_distributed_matches_single_process(pp, dp, sched):
     mb, nm, steps = 128, 4, 3
     world = pp * dp
