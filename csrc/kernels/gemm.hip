@@ -62,7 +62,7 @@ struct Cfg {
   static constexpr int PER_STAGE = (BM + BN) / (8 * NW);
   // epilogue: fp32 staging of EPI_ROWS rows at a time (whole tile when it fits)
   static constexpr int CS_LD = BN + 4;
-  static constexpr int EPI_ROWS = NW == 4 ? BM : SM;
+  static constexpr int EPI_ROWS = (NW == 4 && BM <= 128) ? BM : SM;
   static constexpr int CHUNKS = BM / EPI_ROWS, WPC = EPI_ROWS / SM;  // wave-rows per chunk
   static constexpr int CS_BYTES = EPI_ROWS * CS_LD * 4;
   static constexpr int RED_BYTES = NT * 32;  // colsum partial staging
@@ -345,40 +345,68 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(GemmParams p, int tile
   float LDS_AS* cs = (float LDS_AS*)lds;
   constexpr int CPR = BN / 8;
   constexpr int ITER = C::EPI_ROWS * CPR / NT;
-  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // this thread's column chunk is
-                                                            // fixed: NT % CPR == 0
+  constexpr int RSTEP = NT / CPR;  // rows between a thread's consecutive iterations
+  // A thread's 8-column chunk is the same in every iteration and chunk (NT % CPR == 0): its
+  // bias is loaded ONCE, and the per-row global reads of a chunk (activation for the dgrad
+  // mask, previous slab for split-K accumulation) are all issued before the first is used --
+  // one L2 round trip per chunk instead of one per row (the per-row form serialised ~16
+  // round trips per 256x256 tile: half the tile's time at K = 832).
+  const int ccol = (threadIdx.x % CPR) * 8, crow = threadIdx.x / CPR;
+  const long gn = n0 + ccol;
+  bool xent = false;
+  if constexpr (!OUT_F32 && C::NW == 4 && C::CHUNKS == 1)
+    xent = p.xent_labels != nullptr;  // uniform
+  float bias_r[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (p.bias && !xent) {
+    const f32x4_t b0 = *(const f32x4_t*)(p.bias + gn);
+    const f32x4_t b1 = *(const f32x4_t*)(p.bias + gn + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      bias_r[e] = b0[e];
+      bias_r[e + 4] = b1[e];
+    }
+  }
+  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
   for (int chunk = 0; chunk < C::CHUNKS; ++chunk) {
     if (chunk) __syncthreads();  // previous chunk's stores have read the staging tile
     acc_to_lds<C>(acc, cs, chunk, wave, lane);
     __syncthreads();
-
-    bool xent = false;
-    if constexpr (!OUT_F32 && C::NW == 4) {
-      if (p.xent_labels) {  // uniform: fused softmax-CE, one thread per row of the tile
-        xent = true;
+    if constexpr (!OUT_F32 && C::NW == 4 && C::CHUNKS == 1) {
+      if (xent) {  // fused softmax-CE, one thread per row of the tile
         xent_rows<C>(p, cs, m0);
         __syncthreads();
       }
     }
-    const int r0 = chunk * C::EPI_ROWS;
-#pragma unroll 2
-    for (int it = 0; it < ITER; ++it) {
-      const int idx = threadIdx.x + it * NT;
-      const int row = idx / CPR, col = (idx % CPR) * 8;
-      const f32x4_t v0 = *(const f32x4_t LDS_AS*)(cs + row * CS_LD + col);
-      const f32x4_t v1 = *(const f32x4_t LDS_AS*)(cs + row * CS_LD + col + 4);
-      float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-      const long gm = m0 + r0 + row, gn = n0 + col;
-      if (p.bias && !xent) {
-        const f32x4_t b0 = *(const f32x4_t*)(p.bias + gn);
-        const f32x4_t b1 = *(const f32x4_t*)(p.bias + gn + 4);
+    const long gm0 = m0 + chunk * C::EPI_ROWS + crow;
+    [[maybe_unused]] bf16x8_t yv[ITER];
+    [[maybe_unused]] f32x4_t cp0[ITER], cp1[ITER];
+    if constexpr (OUT_F32) {
+      if (p.accumulate) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          v[e] += b0[e];
-          v[e + 4] += b1[e];
+        for (int it = 0; it < ITER; ++it) {
+          const float* c = (const float*)p.C + (long)split * p.c_split_stride +
+                           (gm0 + it * RSTEP) * p.ldc + gn;
+          cp0[it] = *(const f32x4_t*)c;
+          cp1[it] = *(const f32x4_t*)(c + 4);
         }
       }
+    } else {
+      if (p.aux && !xent) {
+#pragma unroll
+        for (int it = 0; it < ITER; ++it)
+          yv[it] = *(const bf16x8_t*)(p.aux + (gm0 + it * RSTEP) * p.ld_aux + gn);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int row = crow + it * RSTEP;
+      const f32x4_t v0 = *(const f32x4_t LDS_AS*)(cs + row * CS_LD + ccol);
+      const f32x4_t v1 = *(const f32x4_t LDS_AS*)(cs + row * CS_LD + ccol + 4);
+      float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      const long gm = gm0 + it * RSTEP;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += bias_r[e];
       if constexpr (OUT_F32) {
         float* c = (float*)p.C + (long)split * p.c_split_stride + gm * p.ldc + gn;
         if (!p.accumulate && p.act != ACT_LINEAR) {
@@ -387,8 +415,8 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(GemmParams p, int tile
         }
         f32x4_t o0 = {v[0], v[1], v[2], v[3]}, o1 = {v[4], v[5], v[6], v[7]};
         if (p.accumulate) {
-          o0 += *(const f32x4_t*)c;
-          o1 += *(const f32x4_t*)(c + 4);
+          o0 += cp0[it];
+          o1 += cp1[it];
         }
         *(f32x4_t*)c = o0;
         *(f32x4_t*)(c + 4) = o1;
@@ -396,9 +424,8 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(GemmParams p, int tile
         if (xent) {
           // dz already computed in LDS
         } else if (p.aux) {
-          const bf16x8_t y = *(const bf16x8_t*)(p.aux + gm * p.ld_aux + gn);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = act_bwd(v[e], bf2f((u16)y[e]), p.act);
+          for (int e = 0; e < 8; ++e) v[e] = act_bwd(v[e], bf2f((u16)yv[it][e]), p.act);
         } else {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = act_fwd(v[e], p.act);
@@ -613,6 +640,10 @@ int gemm_bf16(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, 
   const long b_row = lb == KMAJ ? ktot : p.N;
   if (p.lda < a_row || p.ldb < b_row || p.ldc < p.N || (p.aux && p.ld_aux < p.N)) return -8;
 
+  // (A 4-wave 256x256 form -- 128x128 per wave, one wave per SIMD, accumulators in AGPRs,
+  // hipBLASLt's MT256x256 MIWT8_8 shape -- was built and measured: 7 % slower on 8192^3 fwd,
+  // 20 % on K = 832, 3-4x on dgrad (spills); without hand-scheduled intra-wave pipelining one
+  // wave per SIMD cannot hide LDS latency, so the 8-wave form is the 256x256 tile.)
   const int nt = gemm_tile_threads(bm, bn);
   const int ns = stages ? stages : default_stages(bm, bn);
   // 8-wave tiles: NS = 3 where three stages fit (not 256x256)

@@ -459,3 +459,4 @@ def test_pipeline_depth_rejects_bad_stages(dev):
     c = torch.zeros(128, 128, device=dev)
     with pytest.raises(ValueError, match="stages"):
         ops.gemm(a, a, c, layout_a=KMAJ, layout_b=KMAJ, M=128, N=128, K=64, stages=5)
+
