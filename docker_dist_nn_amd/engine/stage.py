@@ -358,8 +358,11 @@ class Stage:
         if self._prog is not None and not self._recording:
             if layers is None:
                 return self._replay("FIN")
-            if len(layers) == 1:
-                return self._replay(f"FIN{layers[0]}")
+            ls = list(layers)
+            if len(ls) == 1:
+                return self._replay(f"FIN{ls[0]}")
+            if ls == list(range(ls[0], ls[-1] + 1)):
+                return self._replay(f"FIN{ls[0]}-{ls[-1]}")
         key = tuple(range(len(self.geoms))) if layers is None else tuple(layers)
         jobs = self._reduce_jobs.get(key)
         if jobs is None:  # buffers are fixed for the stage's lifetime: build the table once
@@ -431,9 +434,11 @@ class Stage:
                 prog.mark("W")
                 for i in range(len(self.geoms)):
                     self.wgrad_layer(i)
-            for i in range(len(self.geoms)):
-                prog.mark(f"FIN{i}")
-                self.finalize_grads([i])
+            L = len(self.geoms)
+            for a in range(L):  # every contiguous layer range: one reduce launch per DP bucket
+                for b in range(a, L):
+                    prog.mark(f"FIN{a}" if a == b else f"FIN{a}-{b}")
+                    self.finalize_grads(list(range(a, b + 1)))
             prog.mark("FIN")
             self.finalize_grads()
             o = self.params.optim

@@ -55,6 +55,34 @@ class GradSync:
         self._works.clear()
 
 
+def dp_buckets(st, cap_bytes: int = 4 << 20) -> list[list[int]]:
+    """Data-parallel gradient buckets of a stage, in launch order.
+
+    The largest layer's gradient goes first and alone: its all-reduce -- the longest on the
+    xGMI ring -- then overlaps every other layer's wgrad GEMM. The remaining layers are merged
+    into runs of consecutive layer indices (a contiguous range of the flat gradient, so one
+    RCCL call and one reduce launch each), last layers first, up to ``cap_bytes`` of fp32
+    gradient per bucket: few, larger collectives instead of one latency-bound call per layer.
+    """
+    L = len(st.geoms)
+    size = [4 * (st.geoms[i].np_ * st.geoms[i].kp + st.geoms[i].np_) for i in range(L)]
+    big = max(range(L), key=lambda i: size[i])
+    out = [[big]]
+    run: list[int] = []
+    for i in range(L - 1, -1, -1):
+        if i == big or (run and (run[0] - 1 != i or sum(size[j] for j in run) + size[i] >
+                                 cap_bytes)):
+            if run:
+                out.append(sorted(run))
+            run = []
+            if i == big:
+                continue
+        run.insert(0, i)
+    if run:
+        out.append(sorted(run))
+    return out
+
+
 class PipelineExecutor:
     def __init__(self, stages: Sequence, pipe, kind: str, num_stages: int,
                  stage_ids: Sequence[int], grad_sync: Optional[GradSync] = None,
@@ -111,16 +139,13 @@ class PipelineExecutor:
             st.finalize_grads()
             st._finalized = True
             return
-        # Largest gradient first: its all-reduce (the longest on the xGMI ring) then overlaps
-        # the wgrad GEMMs of every other layer, and only the smallest bucket is exposed at the
-        # end (last-layer-first would leave the big first-layer bucket exposed).
-        order = sorted(range(len(st.geoms)), key=lambda i: -st.geoms[i].np_ * st.geoms[i].kp)
-        for i in order:
-            st.wgrad_layer(i)
-            st.finalize_grads([i])
-            if self.grad_sync is not None:
-                a, b = st.params.layer_grad_range(i)
-                self.grad_sync.launch(st.params.grad, a, b)
+        for bucket in dp_buckets(st):
+            for i in bucket:
+                st.wgrad_layer(i)
+            st.finalize_grads(bucket)  # one reduce launch per bucket
+            a, _ = st.params.layer_grad_range(bucket[0])
+            _, b = st.params.layer_grad_range(bucket[-1])
+            self.grad_sync.launch(st.params.grad, a, b)  # contiguous flat range
         st._finalized = True
 
     def _native_plan(self):

@@ -84,3 +84,23 @@ def test_distributed_matches_single_process(pp, dp, sched):
         # per-replica loss is the mean over that replica's shard; their mean is the global one
         lr_ = np.mean([np.load(os.path.join(d, f"loss_r{r}.npy")) for r in range(dp)], axis=0)
         np.testing.assert_allclose(lr_, ref_losses, rtol=1e-4)
+
+
+def test_dp_buckets_cover_every_layer_once_in_contiguous_runs():
+    from types import SimpleNamespace as NS
+
+    from docker_dist_nn_amd.parallel.pipeline import dp_buckets
+
+    def stage(dims):
+        pad = lambda d: (d + 63) // 64 * 64  # noqa: E731
+        return NS(geoms=[NS(kp=pad(a), np_=pad(b)) for a, b in zip(dims, dims[1:])])
+
+    for dims, first in [([784, 512, 256, 128, 10], 0), ([784, 8192, 8192, 10], 1),
+                        ([784] + [1024] * 7 + [10], 1), ([784, 10], 0)]:
+        b = dp_buckets(stage(dims))
+        assert b[0] == [first]  # the largest gradient is all-reduced first, alone
+        flat = sorted(i for bk in b for i in bk)
+        assert flat == list(range(len(dims) - 1))
+        for bk in b:
+            assert bk == list(range(bk[0], bk[-1] + 1))  # one contiguous flat range each
+    assert dp_buckets(stage([784, 512, 256, 128, 10])) == [[0], [1, 2, 3]]
