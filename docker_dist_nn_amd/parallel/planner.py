@@ -45,8 +45,12 @@ class Plan:
 
 
 class Planner:
-    def __init__(self, tflops: float = 450.0, link_gbps: float = 55.0, hop_latency_us: float = 25.0,
-                 allreduce_gbps: float = 120.0, step_overhead_us: float = 60.0):
+    # Defaults calibrated on MI355X: measured training steps run at 565 (784-512-256-128-10),
+    # 730 (784-1024x7-10) and 935 (784-8192-8192-10) model TFLOP/s with no launch gaps
+    # (profiles/r1_tiles/configs_vs_torch.jsonl); xGMI P2P and all-reduce rates are
+    # conservative estimates (not measurable on the 1-GPU test pool).
+    def __init__(self, tflops: float = 700.0, link_gbps: float = 55.0, hop_latency_us: float = 25.0,
+                 allreduce_gbps: float = 120.0, step_overhead_us: float = 20.0):
         self.rate = tflops * 1e12
         self.link = link_gbps * 1e9
         self.lat = hop_latency_us * 1e-6
