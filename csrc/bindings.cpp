@@ -16,6 +16,7 @@
 
 #include "kernels/elementwise.hpp"
 #include "kernels/gemm.hpp"
+#include "kernels/gemv.hpp"
 #include "runtime/graph.hpp"
 #include "runtime/json_weights.hpp"
 #include "runtime/matrix_codec.hpp"
@@ -119,6 +120,23 @@ PYBIND11_MODULE(_native, m) {
       py::arg("stages") = 0, py::arg("group_m") = 0);
   m.def("gemm_default_stages", &dnn::default_stages);
 
+  m.def("gemv_max_rows", []() { return dnn::GEMV_MAX_ROWS; });
+  m.def(
+      "gemv_bf16",
+      [](uintptr_t x, long ldx, uintptr_t w, long ldw, uintptr_t bias, uintptr_t y, long ldy,
+         int M, int N, int K, int act, int out_f32, uintptr_t stream) {
+        launch(
+            "gemv_bf16",
+            [=](hipStream_t s, const dnn::Program& R) {
+              return dnn::gemv_bf16(R.fix(P<const uint16_t>(x)), ldx,
+                                    R.fix(P<const uint16_t>(w)), ldw, R.fix(P<const float>(bias)),
+                                    R.fix(P<void>(y)), ldy, M, N, K, act, out_f32, s);
+            },
+            stream);
+      },
+      py::arg("x"), py::arg("ldx"), py::arg("w"), py::arg("ldw"), py::arg("bias"), py::arg("y"),
+      py::arg("ldy"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("act"),
+      py::arg("out_f32"), py::arg("stream"));
   m.def(
       "gemm_bf16_streamk",
       [](uintptr_t a, long lda, uintptr_t b, long ldb, uintptr_t c, long ldc, int M, int N, int K,

@@ -215,10 +215,37 @@ def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=
 
 # ---- the three GEMMs of a Linear layer -----------------------------------------------------
 
-def linear_fwd(x, w, bias, y, act="relu"):
-    """y[M][Np] = act(x[M][Kp] . w[Np][Kp]^T + bias). y bf16 (activation) or fp32 (logits)."""
+GEMV_MAX_ROWS = 8
+
+
+def gemv(x, w, bias, y, act="relu"):
+    """Serving-size layer (1..8 rows): y[m][n] = act(x[m] . w[n] + bias[n]), one wave per
+    output neuron (csrc/kernels/gemv.hip). y bf16 or fp32."""
     M, K = x.shape
     N = w.shape[0]
+    if not x.is_cuda:
+        return ref.gemm(x, w, y, layout_a=KMAJ, layout_b=KMAJ, M=M, N=N, K=K, bias=bias,
+                        act=_act(act))
+    if M > GEMV_MAX_ROWS or K % 8:
+        raise ValueError(f"gemv takes <= {GEMV_MAX_ROWS} rows and K % 8 == 0")
+    _rows(x, "x", torch.bfloat16)
+    _rows(w, "w", torch.bfloat16)
+    if w.shape[1] < K or y.shape[0] < M or y.shape[1] < N or y.stride(1) != 1:
+        raise ValueError("gemv operand shapes do not match")
+    if bias is not None and (bias.dtype != torch.float32 or bias.numel() < N):
+        raise ValueError("bias must be fp32 with >= N entries")
+    native().gemv_bf16(_p(x), x.stride(0), _p(w), w.stride(0), _p(bias), _p(y), y.stride(0),
+                       M, N, K, _act(act), int(y.dtype == torch.float32), _stream(x))
+    return y
+
+
+def linear_fwd(x, w, bias, y, act="relu"):
+    """y[M][Np] = act(x[M][Kp] . w[Np][Kp]^T + bias). y bf16 (activation) or fp32 (logits).
+    M <= 8 rows (serving) runs the GEMV kernel; otherwise the MFMA GEMM."""
+    M, K = x.shape
+    N = w.shape[0]
+    if x.is_cuda and M <= GEMV_MAX_ROWS:
+        return gemv(x, w, bias, y, act)
     t = tuning.lookup("fwd", M, N, K)
     tiles = tuple(t["tile"]) if t else pick_tiles(M, N)
     return gemm(x, w, y, layout_a=KMAJ, layout_b=KMAJ, M=M, N=N, K=K, bias=bias, act=act,

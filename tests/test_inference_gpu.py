@@ -23,7 +23,7 @@ def _layers(dims, acts, seed=0):
                          rng.standard_normal(dims[i + 1]) * 0.1, acts[i]) for i in range(len(acts))]
 
 
-@pytest.mark.parametrize("rows", [1, 63, 64, 500, 4096])
+@pytest.mark.parametrize("rows", [1, 3, 8, 63, 64, 500, 4096])
 def test_engine_matches_fp64(dev, rows):
     L = _layers([784, 512, 256, 128, 10], ["relu", "sigmoid", "relu", "softmax"])
     eng = InferenceEngine([L[:2], L[2:]], dev, expected_input=784)
@@ -37,8 +37,9 @@ def test_engine_matches_fp64(dev, rows):
 def test_hidden_softmax_and_linear_output(dev):
     L = _layers([100, 64, 32], ["softmax", "linear"])
     eng = InferenceEngine([L], dev, expected_input=100)
-    x = np.random.default_rng(1).random((70, 100))
-    np.testing.assert_allclose(eng.predict(x), model_forward(L, x), rtol=2e-2, atol=2e-2)
+    for rows in (70, 2):  # MFMA path and the serving-size GEMV path
+        x = np.random.default_rng(rows).random((rows, 100))
+        np.testing.assert_allclose(eng.predict(x), model_forward(L, x), rtol=2e-2, atol=2e-2)
 
 
 def test_batch1_latency_8_stage_chain(dev):

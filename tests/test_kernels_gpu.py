@@ -460,3 +460,23 @@ def test_pipeline_depth_rejects_bad_stages(dev):
     with pytest.raises(ValueError, match="stages"):
         ops.gemm(a, a, c, layout_a=KMAJ, layout_b=KMAJ, M=128, N=128, K=64, stages=5)
 
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("N,K", [(10, 832), (1024, 1024), (64, 8192), (300, 4104)])
+def test_gemv_matches_fp32(dev, M, N, K):
+    """Serving-size layer kernel vs torch fp32: all row counts 1..8 (rows beyond M untouched),
+    K tails past the 4x512 unroll, bias + activation, bf16 and fp32 outputs."""
+    gen = torch.Generator().manual_seed(M * 1000 + N + K)
+    x = torch.randn(M, K, generator=gen).to(torch.bfloat16).to(dev)
+    w = (torch.randn(N, K, generator=gen) / K ** 0.5).to(torch.bfloat16).to(dev)
+    b = torch.randn(N, generator=gen).to(dev)
+    ref = x.float() @ w.float().t() + b
+    for act, fn in (("relu", torch.relu), ("sigmoid", torch.sigmoid), ("linear", lambda t: t)):
+        y = torch.full((M + 1, N), 7.0, device=dev)
+        ops.gemv(x, w, b, y, act=act)
+        torch.testing.assert_close(y[:M], fn(ref), rtol=1e-3, atol=1e-3)
+        assert torch.all(y[M] == 7.0)  # row beyond M untouched
+    yb = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    ops.linear_fwd(x, w, b, yb, act="relu")  # dispatches to gemv for <= 8 rows
+    torch.testing.assert_close(yb.float(), torch.relu(ref), rtol=1.6e-2, atol=1e-2)
