@@ -244,7 +244,9 @@ def linear_fwd(x, w, bias, y, act="relu"):
     M <= 8 rows (serving) runs the GEMV kernel; otherwise the MFMA GEMM."""
     M, K = x.shape
     N = w.shape[0]
-    if x.is_cuda and M <= GEMV_MAX_ROWS:
+    if not x.is_cuda:  # CPU reference: any row count
+        return gemm(x, w, y, layout_a=KMAJ, layout_b=KMAJ, M=M, N=N, K=K, bias=bias, act=act)
+    if M <= GEMV_MAX_ROWS:
         return gemv(x, w, bias, y, act)
     t = tuning.lookup("fwd", M, N, K)
     tiles = tuple(t["tile"]) if t else pick_tiles(M, N)

@@ -43,6 +43,10 @@ _CODES = {ST_VALUE: grpc.StatusCode.INVALID_ARGUMENT, ST_INTERNAL: grpc.StatusCo
 
 
 def bucket(rows: int) -> int:
+    """Row bucket of a request: serving sizes (<= ops.GEMV_MAX_ROWS) travel and run unpadded
+    (GEMV path, csrc/kernels/gemv.hip), larger batches pad to a power of two >= 64."""
+    if rows <= ops.GEMV_MAX_ROWS:
+        return rows
     b = 64
     while b < rows:
         b *= 2
