@@ -75,9 +75,11 @@ struct Cfg {
 
 // Stage one operand tile (T entries of the M/N dim x 64 of K) into LDS with LDS-DMA.
 // Tile bytes = T*128 = T/8 KiB pieces; each of the NW waves issues T/(8*NW) of them.
+// Rows / columns at or past `mn_lim` (a partial edge tile) are clamped onto the last valid
+// row / 8-column chunk: the loads stay in bounds, and the outputs they feed are never stored.
 template <int L, int T, int NW>
 __device__ __forceinline__ void stage_tile(const u16* __restrict__ g, long ld, int mn0, int k0,
-                                           char LDS_AS* dst, int wave, int lane) {
+                                           char LDS_AS* dst, int wave, int lane, int mn_lim) {
   constexpr int NI = T / (8 * NW);
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
@@ -87,12 +89,12 @@ __device__ __forceinline__ void stage_tile(const u16* __restrict__ g, long ld, i
     if constexpr (L == KMAJ) {
       const int r = chunk >> 3, ph = chunk & 7;
       const int c = ph ^ k_swz(r);
-      src = g + (long)(mn0 + r) * ld + k0 + c * 8;
+      src = g + (long)min(mn0 + r, mn_lim - 1) * ld + k0 + c * 8;
     } else {
       constexpr int CPR = T / 8;
       const int r = chunk / CPR, ph = chunk % CPR;
       const int c = ph ^ mn_swz<T>(r);
-      src = g + (long)(k0 + r) * ld + mn0 + c * 8;
+      src = g + (long)(k0 + r) * ld + min(mn0 + c * 8, mn_lim - 8);
     }
     __builtin_amdgcn_global_load_lds((const void*)src, (void LDS_AS*)(dst + piece * 1024), 16, 0, 0);
   }
@@ -181,9 +183,10 @@ __device__ __forceinline__ void mma_tile(const GemmParams& p, int m0, int n0, in
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s) {
     if (s < nk) {
-      stage_tile<LA, C::BM, C::NW>(p.A, p.lda, m0, kbase + s * 64, lds + s * STAGE, wave, lane);
+      stage_tile<LA, C::BM, C::NW>(p.A, p.lda, m0, kbase + s * 64, lds + s * STAGE, wave, lane,
+                                   p.M);
       stage_tile<LB, C::BN, C::NW>(p.B, p.ldb, n0, kbase + s * 64, lds + s * STAGE + A_BYTES,
-                                   wave, lane);
+                                   wave, lane, p.N);
     }
   }
   int rd = 0, wr = NS - 1;  // ring slots of tile kt and of tile kt + NS - 1
@@ -193,8 +196,8 @@ __device__ __forceinline__ void mma_tile(const GemmParams& p, int m0, int n0, in
     if (kt + NS - 1 < nk) {
       char LDS_AS* nxt = lds + wr * STAGE;
       const int k0 = kbase + (kt + NS - 1) * 64;
-      stage_tile<LA, C::BM, C::NW>(p.A, p.lda, m0, k0, nxt, wave, lane);
-      stage_tile<LB, C::BN, C::NW>(p.B, p.ldb, n0, k0, nxt + A_BYTES, wave, lane);
+      stage_tile<LA, C::BM, C::NW>(p.A, p.lda, m0, k0, nxt, wave, lane, p.M);
+      stage_tile<LB, C::BN, C::NW>(p.B, p.ldb, n0, k0, nxt + A_BYTES, wave, lane, p.N);
     }
     const char LDS_AS* sa = lds + rd * STAGE;
     const char LDS_AS* sb = sa + A_BYTES;
@@ -356,8 +359,9 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(GemmParams p, int tile
   bool xent = false;
   if constexpr (!OUT_F32 && C::NW == 4 && C::CHUNKS == 1)
     xent = p.xent_labels != nullptr;  // uniform
+  const bool col_ok = gn < p.N;  // partial edge tile: this thread's columns may be past N
   float bias_r[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (p.bias && !xent) {
+  if (p.bias && !xent && col_ok) {
     const f32x4_t b0 = *(const f32x4_t*)(p.bias + gn);
     const f32x4_t b1 = *(const f32x4_t*)(p.bias + gn + 4);
 #pragma unroll
@@ -385,6 +389,7 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(GemmParams p, int tile
       if (p.accumulate) {
 #pragma unroll
         for (int it = 0; it < ITER; ++it) {
+          if (!col_ok || gm0 + it * RSTEP >= p.M) continue;
           const float* c = (const float*)p.C + (long)split * p.c_split_stride +
                            (gm0 + it * RSTEP) * p.ldc + gn;
           cp0[it] = *(const f32x4_t*)c;
@@ -395,7 +400,8 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(GemmParams p, int tile
       if (p.aux && !xent) {
 #pragma unroll
         for (int it = 0; it < ITER; ++it)
-          yv[it] = *(const bf16x8_t*)(p.aux + (gm0 + it * RSTEP) * p.ld_aux + gn);
+          if (col_ok && gm0 + it * RSTEP < p.M)
+            yv[it] = *(const bf16x8_t*)(p.aux + (gm0 + it * RSTEP) * p.ld_aux + gn);
       }
     }
 #pragma unroll
@@ -405,6 +411,7 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(GemmParams p, int tile
       const f32x4_t v1 = *(const f32x4_t LDS_AS*)(cs + row * CS_LD + ccol + 4);
       float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
       const long gm = gm0 + it * RSTEP;
+      if (!col_ok || gm >= p.M) continue;  // outside a partial edge tile: not stored
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] += bias_r[e];
       if constexpr (OUT_F32) {
@@ -454,7 +461,7 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(GemmParams p, int tile
         float t = 0.f;
 #pragma unroll 4
         for (int r = 0; r < NT / CPR; ++r) t += rf[(r * CPR + cc) * 8 + e];
-        p.colsum[(long)tm * p.ld_colsum + n0 + col] = t;
+        if (n0 + col < p.N) p.colsum[(long)tm * p.ld_colsum + n0 + col] = t;
       }
     }
   }
@@ -594,7 +601,7 @@ const char* gemm_error_string(int code) {
   switch (code) {
     case 0: return "ok";
     case -1: return "unsupported tile (64|128 x 64|128, 256 x 64|128|256, 128 x 256)";
-    case -2: return "M must be a multiple of bm and N a multiple of bn";
+    case -2: return "M and N must be positive multiples of 8 (edge tiles are partial)";
     case -3: return "per-split K must be a positive multiple of 64";
     case -4: return "leading dimensions must be multiples of 8 elements (16-byte rows)";
     case -5: return "pointers must be 16-byte aligned";
@@ -618,7 +625,8 @@ int default_stages(int bm, int bn) {
 int gemm_bf16(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, int splits,
               hipStream_t stream, int stages) {
   if (!gemm_tile_supported(bm, bn)) return -1;
-  if (p.M <= 0 || p.N <= 0 || p.M % bm || p.N % bn) return -2;
+  // partial edge tiles: M and N need only be multiples of 8 (16-byte rows / chunks)
+  if (p.M <= 0 || p.N <= 0 || p.M % 8 || p.N % 8) return -2;
   if (splits < 1) return -3;
   if (p.k_total > 0) {
     if (p.k_total % 64 || splits > p.k_total / 64) return -3;
@@ -633,7 +641,7 @@ int gemm_bf16(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, 
   if ((la != KMAJ && la != MNMAJ) || (lb != KMAJ && lb != MNMAJ)) return -6;
   if (splits > 1 && !out_f32) return -7;
   if (p.colsum && (out_f32 || p.ld_colsum < p.N)) return -10;
-  if (p.xent_labels && (out_f32 || p.N != bn || bn > 128 || bm > 128 || !p.bias ||
+  if (p.xent_labels && (out_f32 || p.N != bn || bn > 128 || bm > 128 || p.M % bm || !p.bias ||
                         p.n_cls <= 0 || p.n_cls > p.N || splits != 1 || p.aux))
     return -11;
   const long a_row = la == KMAJ ? ktot : p.M;
@@ -665,7 +673,7 @@ int gemm_bf16(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, 
     fn = ns == 2 ? pick_layout<Cfg<128, 256, 2, 4, 2>>(la, lb, out_f32)
                  : pick_layout<Cfg<128, 256, 2, 4, 3>>(la, lb, out_f32);
 
-  const int tiles_n = p.N / bn, tiles_m = p.M / bm;
+  const int tiles_n = (p.N + bn - 1) / bn, tiles_m = (p.M + bm - 1) / bm;
   const int nwg = tiles_n * tiles_m * splits;
   GemmParams q = p;
   // grouped raster (see the kernel): worth it once a row of column tiles outgrows what one

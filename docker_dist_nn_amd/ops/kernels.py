@@ -151,8 +151,8 @@ def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=
         if tiles is None or out_f32:
             raise ValueError("colsum needs explicit tiles and a bf16 output")
         if colsum.dtype != torch.float32 or colsum.dim() != 2 or colsum.stride(1) != 1 or \
-                colsum.shape[0] < M // tiles[0] or colsum.shape[1] < N:
-            raise ValueError(f"colsum must be fp32 [{M // tiles[0]}][>={N}] row-major")
+                colsum.shape[0] < -(-M // tiles[0]) or colsum.shape[1] < N:
+            raise ValueError(f"colsum must be fp32 [{-(-M // tiles[0])}][>={N}] row-major")
     if not a.is_cuda:
         return ref.gemm(a, b, c, layout_a=layout_a, layout_b=layout_b, M=M, N=N, K=K, bias=bias,
                         aux=aux, act=act, accumulate=accumulate, splits=splits, colsum=colsum,
@@ -183,33 +183,14 @@ def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=
     if aux is not None and (aux.shape[0] < M or aux.shape[1] < N):
         raise ValueError("aux storage too small")
     bm, bn = tiles or pick_tiles(M, N, splits)
-    cel = c_rows.element_size()
-    st = _stream(a)
-
-    def launch(n0: int, n: int, tbn: int) -> None:
-        # columns [n0, n0 + n) of C: offset B's output-dim, C, bias, aux and colsum pointers
-        boff = n0 * (b.stride(0) if layout_b == KMAJ else 1) * 2
-        native().gemm_bf16(_p(a), a.stride(0), _p(b) + boff, b.stride(0),
-                           _p(c_rows) + n0 * cel, c_rows.stride(0), split_stride,
-                           _p(bias) + 4 * n0 if bias is not None else 0,
-                           _p(aux) + 2 * n0 if aux is not None else 0,
-                           aux.stride(0) if aux is not None else 0,
-                           M, n, K, act, int(accumulate), layout_a, layout_b, int(out_f32), bm,
-                           tbn, splits, st, _p(colsum) + 4 * n0 if colsum is not None else 0,
-                           colsum.stride(0) if colsum is not None else 0, k_total=int(k_total),
-                           stages=int(stages) if tbn == bn else 0, group_m=int(group_m))
-
-    rem = N % bn
-    if rem and N % 64 == 0 and bn > 64:
-        # N-split: the bulk on the requested (wide) tile, the remainder columns on a 64-wide
-        # tile of the same height (same split-K, so slabs / colsum partials line up). E.g. a
-        # 512x832 weight gradient runs 768 columns on 256x256 tiles + 64 on 256x64, instead of
-        # all 13 column tiles at 64 wide (which re-stages dZ 13 times).
-        if N - rem:
-            launch(0, N - rem, bn)
-        launch(N - rem, rem, 64)
-    else:
-        launch(0, N, bn)
+    # M or N not a multiple of the tile runs as partial edge tiles in the same launch:
+    # out-of-range operand rows/columns are clamped on load and never stored (gemm.hip)
+    native().gemm_bf16(_p(a), a.stride(0), _p(b), b.stride(0), _p(c_rows), c_rows.stride(0),
+                       split_stride, _p(bias), _p(aux), aux.stride(0) if aux is not None else 0,
+                       M, N, K, act, int(accumulate), layout_a, layout_b, int(out_f32), bm, bn,
+                       splits, _stream(a), _p(colsum),
+                       colsum.stride(0) if colsum is not None else 0, k_total=int(k_total),
+                       stages=int(stages), group_m=int(group_m))
     return c
 
 

@@ -83,9 +83,10 @@ def test_gemm_exact_integer_8wave(dev, la, lb, bm, bn):
 
 @pytest.mark.parametrize("la,lb", LAYOUTS)
 @pytest.mark.parametrize("bm,bn", [(256, 256), (128, 128), (256, 128)])
-def test_gemm_n_split_remainder(dev, la, lb, bm, bn):
-    """N not a multiple of bn: bulk on (bm, bn) + remainder on (bm, 64) -- exact on integer
-    data for bf16 output (+bias, relu, colsum) and split-K slabs."""
+def test_gemm_partial_edge_tiles(dev, la, lb, bm, bn):
+    """N (and M) not a multiple of the tile: partial edge tiles in one launch (clamped loads,
+    masked stores) -- exact on integer data for bf16 output (+bias, relu, colsum) and split-K
+    slabs; storage past N/M is never written."""
     gen = torch.Generator().manual_seed(5 + bm + bn + 3 * la + lb)
     M, N, K = 2 * bm, 832, 320
     a = _storage(la, M, K, gen, dev, True)
@@ -103,6 +104,12 @@ def test_gemm_n_split_remainder(dev, la, lb, bm, bn):
     ops.gemm(a, b, slabs, layout_a=la, layout_b=lb, M=M, N=N, K=K, k_total=K, splits=3,
              tiles=(bm, bn))
     assert torch.equal(slabs.sum(0), ref)
+    # partial rows too (M = bm + 40), into a wider buffer whose extra rows/cols must stay
+    Mp = bm + 40
+    big = torch.full((Mp + 8, N + 8), -1.0, device=dev)
+    ops.gemm(a, b, big, layout_a=la, layout_b=lb, M=Mp, N=N, K=K, tiles=(bm, bn))
+    assert torch.equal(big[:Mp, :N], ref[:Mp])
+    assert torch.all(big[Mp:] == -1.0) and torch.all(big[:, N:] == -1.0)
 
 
 def test_gemm_identity_asymmetric(dev):
