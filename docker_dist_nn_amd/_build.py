@@ -63,7 +63,10 @@ def _header_digest() -> str:
 
 def _flags(sanitize: bool) -> tuple[list[str], list[str]]:
     common = ["-O3", "-std=c++17", "-fPIC", f"-I{CSRC}", "-Wall", "-Wno-unused-function"]
-    dev = [_hipcc(), f"--offload-arch={ARCH}", *common, "-Wno-unused-result"]
+    # DNN_HIP_DEFINES: extra device-compile defines for A/B experiments (e.g.
+    # "-DDNN_GEMM_SETPRIO=1"); they are part of the object-directory tag below
+    dev = [_hipcc(), f"--offload-arch={ARCH}", *common, "-Wno-unused-result",
+           *os.environ.get("DNN_HIP_DEFINES", "").split()]
     host = [_host_cxx(), *common, f"-I{ROCM / 'include'}", "-D__HIP_PLATFORM_AMD__",
             *_pybind_includes(), "-fvisibility=hidden"]
     if sanitize:
@@ -81,6 +84,9 @@ def build(force: bool = False, jobs: int | None = None, sanitize: bool = False,
     """Compile (incrementally) and link the extension; returns the path of the .so."""
     dev_src, host_src = _sources()
     tag = "asan" if sanitize else "rel"
+    extra = os.environ.get("DNN_HIP_DEFINES", "")
+    if extra:
+        tag += "-" + hashlib.sha1(extra.encode()).hexdigest()[:8]
     obj_dir = ROOT / "build" / f"native-{tag}-{_header_digest()}"
     obj_dir.mkdir(parents=True, exist_ok=True)
     dev_cmd, host_cmd = _flags(sanitize)
