@@ -247,31 +247,48 @@ PYBIND11_MODULE(_native, m) {
           stream);
     }
   });
-  m.def("sgd_update", [](uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t shadow, long n,
-                         float lr, float mu, float wd, uintptr_t stream) {
+  m.def(
+      "sgd_update",
+      [](uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t shadow, long n, float lr, float mu,
+         float wd, uintptr_t stream, uintptr_t lr_dev) {
+        launch(
+            "sgd_update",
+            [=](hipStream_t s, const dnn::Program& R) {
+              return dnn::sgd_update(R.fix(P<float>(p)), R.fix(P<const float>(g)),
+                                     R.fix(P<float>(mom)), R.fix(P<uint16_t>(shadow)), n, lr, mu,
+                                     wd, s, P<const float>(lr_dev));
+            },
+            stream);
+      },
+      py::arg("p"), py::arg("g"), py::arg("mom"), py::arg("shadow"), py::arg("n"), py::arg("lr"),
+      py::arg("mu"), py::arg("wd"), py::arg("stream"), py::arg("lr_dev") = 0);
+  m.def(
+      "adam_update",
+      [](uintptr_t p, uintptr_t g, uintptr_t mm, uintptr_t vv, uintptr_t shadow, long n, float lr,
+         float b1, float b2, float eps, float wd, int decoupled, float bc1, float bc2,
+         uintptr_t stream, uintptr_t lr_dev, uintptr_t step_dev, double db1, double db2) {
+        launch(
+            "adam_update",
+            [=](hipStream_t s, const dnn::Program& R) {
+              return dnn::adam_update(R.fix(P<float>(p)), R.fix(P<const float>(g)),
+                                      R.fix(P<float>(mm)), R.fix(P<float>(vv)),
+                                      R.fix(P<uint16_t>(shadow)), n, lr, b1, b2, eps, wd,
+                                      decoupled, bc1, bc2, s, P<const float>(lr_dev),
+                                      P<const int>(step_dev), db1, db2);
+            },
+            stream);
+      },
+      py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("shadow"), py::arg("n"),
+      py::arg("lr"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"),
+      py::arg("decoupled"), py::arg("bc1"), py::arg("bc2"), py::arg("stream"),
+      py::arg("lr_dev") = 0, py::arg("step_dev") = 0, py::arg("db1") = 0.9,
+      py::arg("db2") = 0.999);
+  m.def("step_advance", [](uintptr_t step, uintptr_t stream) {
     launch(
-        "sgd_update",
-        [=](hipStream_t s, const dnn::Program& R) {
-          return dnn::sgd_update(R.fix(P<float>(p)), R.fix(P<const float>(g)),
-                                 R.fix(P<float>(mom)), R.fix(P<uint16_t>(shadow)), n, lr, mu, wd,
-                                 s);
-        },
+        "step_advance",
+        [=](hipStream_t s, const dnn::Program&) { return dnn::step_advance(P<int>(step), s); },
         stream);
   });
-  m.def("adam_update",
-        [](uintptr_t p, uintptr_t g, uintptr_t mm, uintptr_t vv, uintptr_t shadow, long n,
-           float lr, float b1, float b2, float eps, float wd, int decoupled, float bc1, float bc2,
-           uintptr_t stream) {
-          launch(
-              "adam_update",
-              [=](hipStream_t s, const dnn::Program& R) {
-                return dnn::adam_update(R.fix(P<float>(p)), R.fix(P<const float>(g)),
-                                        R.fix(P<float>(mm)), R.fix(P<float>(vv)),
-                                        R.fix(P<uint16_t>(shadow)), n, lr, b1, b2, eps, wd,
-                                        decoupled, bc1, bc2, s);
-              },
-              stream);
-        });
   m.def("pack_bf16", [](uintptr_t in, long ld_in, int rows, int cols, uintptr_t out, long ld_out,
                         int rows_p, int cols_p, uintptr_t stream) {
     launch(

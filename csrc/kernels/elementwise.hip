@@ -405,9 +405,13 @@ int reduce_multi(const ReduceJob* job, int n_jobs, hipStream_t stream) {
 // Fused SGD (+momentum, +decoupled-from-nothing L2 weight decay like torch.optim.SGD):
 //   g' = g + wd * p ; v = mu * v + g' (if mu != 0) ; p -= lr * (v or g') ; shadow = bf16(p)
 // ------------------------------------------------------------------------------------------
+// lr_dev (optional): learning rate read from device memory, so a recorded/replayed update
+// follows an LR schedule without re-recording.
 __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                   float* __restrict__ mom, u16* __restrict__ shadow,
-                                                  long n4, float lr, float mu, float wd) {
+                                                  long n4, float lr, float mu, float wd,
+                                                  const float* __restrict__ lr_dev) {
+  if (lr_dev) lr = *lr_dev;
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
     f32x4_t pv = *(const f32x4_t*)(p + i * 4);
     f32x4_t gv = *(const f32x4_t*)(g + i * 4);
@@ -430,19 +434,31 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
 }
 
 int sgd_update(float* p, const float* g, float* mom, uint16_t* shadow, long n, float lr, float mu,
-               float wd, hipStream_t stream) {
+               float wd, hipStream_t stream, const float* lr_dev) {
   if (n <= 0 || n % 4) return -1;
   hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n / 4)), dim3(256), 0, stream, p, g, mom, shadow,
-                     n / 4, lr, mu, wd);
+                     n / 4, lr, mu, wd, lr_dev);
   return hipGetLastError() == hipSuccess ? 0 : -9;
 }
 
-// Adam / AdamW (torch.optim semantics; bc1 = 1/(1-b1^t), bc2 = 1/(1-b2^t) computed on the host).
+// Adam / AdamW (torch.optim semantics; bc1 = 1/(1-b1^t), bc2 = 1/(1-b2^t)). The corrections
+// come from the host, or -- with step_dev -- are computed here in double from the device step
+// counter (t = *step_dev + 1; the same double arithmetic as the host path, so both paths
+// agree bit for bit) and lr from lr_dev: a recorded update then needs no per-step host values.
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    u16* __restrict__ shadow, long n4, float lr,
                                                    float b1, float b2, float eps, float wd,
-                                                   int decoupled, float bc1, float bc2) {
+                                                   int decoupled, float bc1, float bc2,
+                                                   const float* __restrict__ lr_dev,
+                                                   const int* __restrict__ step_dev, double db1,
+                                                   double db2) {
+  if (lr_dev) lr = *lr_dev;
+  if (step_dev) {
+    const double t = (double)(*step_dev + 1);
+    bc1 = (float)(1.0 / (1.0 - pow(db1, t)));
+    bc2 = (float)(1.0 / (1.0 - pow(db2, t)));
+  }
   for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
     f32x4_t pv = *(const f32x4_t*)(p + i * 4);
     f32x4_t gv = *(const f32x4_t*)(g + i * 4);
@@ -468,10 +484,19 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
 
 int adam_update(float* p, const float* g, float* m, float* v, uint16_t* shadow, long n, float lr,
                 float b1, float b2, float eps, float wd, int decoupled, float bc1, float bc2,
-                hipStream_t stream) {
+                hipStream_t stream, const float* lr_dev, const int* step_dev, double db1,
+                double db2) {
   if (n <= 0 || n % 4) return -1;
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4)), dim3(256), 0, stream, p, g, m, v, shadow,
-                     n / 4, lr, b1, b2, eps, wd, decoupled, bc1, bc2);
+                     n / 4, lr, b1, b2, eps, wd, decoupled, bc1, bc2, lr_dev, step_dev, db1, db2);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
+__global__ void step_advance_kernel(int* step) { *step += 1; }
+
+int step_advance(int* step, hipStream_t stream) {
+  if (!step) return -1;
+  hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(1), 0, stream, step);
   return hipGetLastError() == hipSuccess ? 0 : -9;
 }
 

@@ -36,11 +36,15 @@ struct ReduceJobs {  // passed by value as the kernel argument
 };
 // All jobs in one launch, each bitwise identical to reduce_slabs on the same inputs.
 int reduce_multi(const ReduceJob* job, int n_jobs, hipStream_t stream);
+// lr_dev / step_dev (optional, device memory): see the kernels in elementwise.hip.
 int sgd_update(float* p, const float* g, float* mom, uint16_t* shadow, long n, float lr, float mu,
-               float wd, hipStream_t stream);
+               float wd, hipStream_t stream, const float* lr_dev = nullptr);
 int adam_update(float* p, const float* g, float* m, float* v, uint16_t* shadow, long n, float lr,
                 float b1, float b2, float eps, float wd, int decoupled, float bc1, float bc2,
-                hipStream_t stream);
+                hipStream_t stream, const float* lr_dev = nullptr, const int* step_dev = nullptr,
+                double db1 = 0.9, double db2 = 0.999);
+// *step += 1 (one thread): advances a device-side optimizer step counter.
+int step_advance(int* step, hipStream_t stream);
 int pack_bf16(const float* in, long ld_in, int rows, int cols, uint16_t* out, long ld_out,
               int rows_p, int cols_p, hipStream_t stream);
 int unpack_bf16(const uint16_t* in, long ld_in, int rows, int cols, float* out, long ld_out,

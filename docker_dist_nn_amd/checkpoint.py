@@ -74,7 +74,7 @@ def load_stage(d: str, stage) -> int:
     for k, s in enumerate(p.state):
         if f"state{k}" in t:
             s.copy_(t[f"state{k}"].to(s.device))
-    p.step_count = int(md.get("opt_steps", 0))
+    p.set_step(int(md.get("opt_steps", 0)))
     p.refresh_shadow()
     return int(md["step"])
 

@@ -138,9 +138,54 @@ class StageParams:
         return ws, bs
 
     # optimizer ----------------------------------------------------------------------------
+    def _device_scalars(self) -> None:
+        if getattr(self, "lr_dev", None) is None:
+            self.lr_dev = torch.full((1,), float(self.optim.lr), dtype=torch.float32,
+                                     device=self.device)
+            self.step_dev = torch.full((1,), int(self.step_count), dtype=torch.int32,
+                                       device=self.device)
+            self._lr_cur = float(self.optim.lr)
+
+    def set_lr(self, lr: float) -> None:
+        """Learning rate of the device-scalar (recorded) update path."""
+        self._device_scalars()
+        if float(lr) != self._lr_cur:
+            self.lr_dev.fill_(float(lr))
+            self._lr_cur = float(lr)
+
+    def set_step(self, n: int) -> None:
+        """Number of updates done (checkpoint resume): host counter and device counter."""
+        self.step_count = int(n)
+        if getattr(self, "step_dev", None) is not None:
+            self.step_dev.fill_(int(n))
+
+    def record_update(self) -> None:
+        """The launches of one optimizer update reading lr / step from device memory (for
+        recording into a native Program: no per-step host values)."""
+        self._device_scalars()
+        o = self.optim
+        if o.name == "sgd":
+            ops.sgd_update(self.master, self.grad, self.state[0] if self.state else None,
+                           self.shadow, lr=o.lr, momentum=o.momentum,
+                           weight_decay=o.weight_decay, lr_dev=self.lr_dev)
+        else:
+            ops.adam_update(self.master, self.grad, self.state[0], self.state[1], self.shadow,
+                            lr=o.lr, betas=o.betas, eps=o.eps, weight_decay=o.weight_decay,
+                            decoupled=o.decoupled or o.name == "adamw", lr_dev=self.lr_dev,
+                            step_dev=self.step_dev)
+            ops.step_advance(self.step_dev)
+
     def optimizer_step(self, lr: Optional[float] = None) -> None:
         o = self.optim
         lr = o.lr if lr is None else lr
+        if self.device.type == "cuda":
+            # GPU: lr and step always come from device memory, so the same launches are valid
+            # eagerly, recorded into a native Program, or captured in a HIP graph (by-value
+            # Adam bias corrections would be frozen by a capture)
+            self.set_lr(lr)
+            self.record_update()
+            self.step_count += 1
+            return
         self.step_count += 1
         if o.name == "sgd":
             ops.sgd_update(self.master, self.grad, self.state[0] if self.state else None,
@@ -247,7 +292,7 @@ class Stage:
         self._prog = None  # native Program once compile_native() ran
         self._recording = False
         self._has_w = False
-        self._o_lr: Optional[float] = None
+        self._o_native = False  # "O" recorded (device-side lr / step)
         self._rx = self._rl = None
 
     def rows_of(self, j: int) -> slice:
@@ -379,7 +424,8 @@ class Stage:
         ops.reduce_multi(jobs)  # one launch for every slab set and bias-partial set
 
     def optimizer_step(self, lr: Optional[float] = None) -> None:
-        if self._prog is not None and self._o_lr is not None and (lr is None or lr == self._o_lr):
+        if self._prog is not None and self._o_native and not self._recording:
+            self.params.set_lr(self.params.optim.lr if lr is None else lr)
             self.params.step_count += 1
             return self._replay("O")
         self.params.optimizer_step(lr)
@@ -441,14 +487,9 @@ class Stage:
                     self.finalize_grads(list(range(a, b + 1)))
             prog.mark("FIN")
             self.finalize_grads()
-            o = self.params.optim
-            if o.name == "sgd":
-                prog.mark("O")
-                ops.sgd_update(self.params.master, self.params.grad,
-                               self.params.state[0] if self.params.state else None,
-                               self.params.shadow, lr=o.lr, momentum=o.momentum,
-                               weight_decay=o.weight_decay)
-                self._o_lr = o.lr
+            prog.mark("O")
+            self.params.record_update()
+            self._o_native = True
         finally:
             nat.record_end()
             self._recording = False

@@ -139,12 +139,16 @@ class Trainer:
     def step(self) -> None:
         if self._graph is not None:
             cur = torch.cuda.current_stream(self.device)
-            self._stream.wait_stream(cur)  # inputs written on the caller's stream
+            for st in self.stages:  # the captured update reads the learning rate from device
+                st.params.set_lr(st.params.optim.lr)
+            self._stream.wait_stream(cur)  # inputs (and lr) written on the caller's stream
             # alternate between identical instantiations: relaunching the SAME exec before its
             # previous launch retired makes the host wait (measured ~130 us idle per step)
             g = self._graphs[self.steps_done % len(self._graphs)]
             g.replay(self._stream.cuda_stream)
             cur.wait_stream(self._stream)
+            for st in self.stages:  # the captured update advanced the device step counter
+                st.params.step_count += 1
         else:
             self.executor.run_step()
         self.steps_done += 1
@@ -167,6 +171,7 @@ class Trainer:
             for _ in range(warmup):
                 self.executor.run_step()
             self._stream.synchronize()
+            counts = [st.params.step_count for st in self.stages]
             for _ in range(max(1, copies)):
                 g = native().GraphExec()
                 g.begin_capture(self._stream.cuda_stream)
@@ -176,6 +181,8 @@ class Trainer:
                     g.end_capture()
                 graphs.append(g)
             graphs[0].replay(self._stream.cuda_stream)  # capture itself executes nothing
+        for st, c in zip(self.stages, counts):  # `copies` captures, ONE executed step
+            st.params.step_count = c + 1
         cur.wait_stream(self._stream)
         self._graphs = graphs
         self._graph = graphs[0]

@@ -454,31 +454,55 @@ def reduce_multi(jobs):
     native().reduce_multi(packed, _stream(jobs[0][0]))
 
 
-def sgd_update(p, g, mom=None, shadow=None, lr=0.01, momentum=0.0, weight_decay=0.0):
+def sgd_update(p, g, mom=None, shadow=None, lr=0.01, momentum=0.0, weight_decay=0.0,
+               lr_dev=None):
+    """Fused SGD over flat buffers. ``lr_dev`` (fp32 [1] device tensor): read the learning
+    rate from device memory instead (replayable under an LR schedule)."""
     if not p.is_cuda:
+        if lr_dev is not None:
+            lr = float(lr_dev[0])
         return ref.sgd_update(p, g, mom, shadow, lr, momentum, weight_decay)
     n = p.numel()
     if g.numel() != n or (mom is not None and mom.numel() != n) or (
             shadow is not None and shadow.numel() != n):
         raise ValueError("sgd buffers must have equal sizes")
     native().sgd_update(_p(p), _p(g), _p(mom if momentum else None), _p(shadow), n, float(lr),
-                        float(momentum), float(weight_decay), _stream(p))
+                        float(momentum), float(weight_decay), _stream(p), lr_dev=_p(lr_dev))
 
 
 def adam_update(p, g, m, v, shadow=None, lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
-                weight_decay=0.0, decoupled=False, step=1):
+                weight_decay=0.0, decoupled=False, step=1, lr_dev=None, step_dev=None):
+    """Fused Adam/AdamW. ``step`` is the 1-based step of this update; with ``step_dev`` (int32
+    [1] device tensor holding the number of PREVIOUS updates) and ``lr_dev`` the bias
+    corrections and learning rate are taken from device memory (replayable); advance the
+    counter with :func:`step_advance` after the update."""
     b1, b2 = betas
+    if not p.is_cuda:
+        if lr_dev is not None:
+            lr = float(lr_dev[0])
+        if step_dev is not None:
+            step = int(step_dev[0]) + 1
+        return ref.adam_update(p, g, m, v, shadow, lr, b1, b2, eps, weight_decay, decoupled,
+                               1.0 / (1.0 - b1 ** step), 1.0 / (1.0 - b2 ** step))
     bc1 = 1.0 / (1.0 - b1 ** step)
     bc2 = 1.0 / (1.0 - b2 ** step)
-    if not p.is_cuda:
-        return ref.adam_update(p, g, m, v, shadow, lr, b1, b2, eps, weight_decay, decoupled, bc1,
-                               bc2)
     n = p.numel()
     if any(t.numel() != n for t in (g, m, v)):
         raise ValueError("adam buffers must have equal sizes")
+    if step_dev is not None and step_dev.dtype != torch.int32:
+        raise TypeError("step_dev must be int32")
     native().adam_update(_p(p), _p(g), _p(m), _p(v), _p(shadow), n, float(lr), float(b1),
                          float(b2), float(eps), float(weight_decay), int(decoupled), float(bc1),
-                         float(bc2), _stream(p))
+                         float(bc2), _stream(p), lr_dev=_p(lr_dev), step_dev=_p(step_dev),
+                         db1=float(b1), db2=float(b2))
+
+
+def step_advance(step_dev):
+    """step_dev += 1 on the device (after a device-step optimizer update)."""
+    if not step_dev.is_cuda:
+        step_dev += 1
+        return
+    native().step_advance(_p(step_dev), _stream(step_dev))
 
 
 def pack_bf16(src, out):

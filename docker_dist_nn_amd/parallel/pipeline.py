@@ -160,7 +160,7 @@ class PipelineExecutor:
         if not isinstance(self.pipe, LoopbackPipe) or self.grad_sync is not None or \
                 self.hooks["before_op"] or self.hooks["after_op"] or self.lr_fn is not None:
             return None
-        if any(st._prog is None or not st._has_w or st._o_lr is None for st in self.stages):
+        if any(st._prog is None or not st._has_w or not st._o_native for st in self.stages):
             return None
         order = []
         self._traverse(lambda s, op, j, nxt: order.append((s, op, j, nxt)))
@@ -204,6 +204,8 @@ class PipelineExecutor:
         plan = self._native_plan()
         if plan is not None:
             dev = self.stages[0].device
+            for st in self.stages:
+                st.params.set_lr(st.params.optim.lr)
             if self._side is None and self.wgrad_streams > 1:
                 self._side = torch.cuda.Stream(dev)
             native().run_plan([(st._prog if st is not None else None, seg, si)
