@@ -52,6 +52,7 @@ def parse_args(argv=None):
     ap.add_argument("--schedule", default="1f1b")
     ap.add_argument("--micro", type=int, default=0, help="micro-batch rows (0 = planner)")
     ap.add_argument("--lr", type=float, default=0.05)
+    ap.add_argument("--optimizer", default="sgd", choices=["sgd", "adam", "adamw"])
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as a HIP graph (1 GPU); eager is faster at large batch")
     ap.add_argument("--graph-copies", type=int, default=2,
@@ -96,7 +97,8 @@ def main(argv=None):
         mesh = build_mesh(plan.pp, plan.dp)
 
     tr = Trainer(spec, micro_batch=mb, num_micro=nm, distribution=plan.distribution,
-                 pp=plan.pp, dp=plan.dp, schedule=a.schedule, optim=OptimConfig(lr=a.lr),
+                 pp=plan.pp, dp=plan.dp, schedule=a.schedule,
+                 optim=OptimConfig(name=a.optimizer, lr=a.lr),
                  device=dev, seed=a.seed, mesh=mesh)
     replica = mesh.replica if mesh else 0
     x, y = synthetic_mnist(max(60000, 2 * rows), seed=a.seed + 1000 * replica)
@@ -161,7 +163,7 @@ def main(argv=None):
             "micro_batch": mb,
             "num_micro": nm,
             "schedule": a.schedule if plan.pp > 1 else "none",
-            "optimizer": "sgd",
+            "optimizer": a.optimizer,
             "hip_graph": use_graph,
             "graph_copies": a.graph_copies if use_graph else 0,
         },

@@ -33,17 +33,18 @@ def build(spec, dtype, dev):
     return nn.Sequential(*layers).to(dev, dtype)
 
 
-def run(variant, spec, batch, steps, warmup, dev):
+def run(variant, spec, batch, steps, warmup, dev, optimizer="sgd"):
     torch.manual_seed(0)
     pdtype = torch.bfloat16 if variant == "eager-bf16" else torch.float32
     model = build(spec, pdtype, dev)
-    opt = torch.optim.SGD(model.parameters(), lr=0.05)
+    opt = (torch.optim.Adam(model.parameters(), lr=1e-3, capturable=variant == "graph")
+           if optimizer == "adam" else torch.optim.SGD(model.parameters(), lr=0.05))
     x = torch.randn(batch, spec.layers[0].in_dim, device=dev).to(pdtype)
     y = torch.randint(0, spec.layers[-1].out_dim, (batch,), device=dev)
     lossf = nn.CrossEntropyLoss()
 
     def step():
-        opt.zero_grad(set_to_none=False)
+        opt.zero_grad(set_to_none=False)  # (graph capture needs persistent .grad tensors)
         if variant == "eager-bf16":
             loss = lossf(model(x).float(), y)
         else:
@@ -85,11 +86,14 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--variants", default="eager-bf16,amp,graph")
+    ap.add_argument("--optimizer", default="sgd", choices=["sgd", "adam"])
     a = ap.parse_args()
     spec = NAMED_MODELS.get(a.model) or MLPSpec.parse(a.model)
     dev = torch.device("cuda")
     for v in a.variants.split(","):
-        print(json.dumps(run(v, spec, a.batch, a.steps, a.warmup, dev)), flush=True)
+        r = run(v, spec, a.batch, a.steps, a.warmup, dev, a.optimizer)
+        r["optimizer"] = a.optimizer
+        print(json.dumps(r), flush=True)
 
 
 if __name__ == "__main__":
