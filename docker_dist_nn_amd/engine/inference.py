@@ -15,6 +15,7 @@ stage is a slice of layers on one GPU:
 """
 from __future__ import annotations
 
+import os
 import threading
 from typing import Optional, Sequence
 
@@ -131,6 +132,9 @@ class InferenceEngine:
         self._stream = torch.cuda.Stream(device) if device.type == "cuda" else None
         self.n_out = self.stages[-1].out_dim
         self._stage_bufs: dict = {}
+        # per-bucket replay: "graph" (HIP graph) or "native" (recorded launch Program)
+        self.replay = os.environ.get("DNN_SERVE_REPLAY", "graph")
+        self._programs: dict[int, tuple] = {}
 
     @property
     def input_dim(self) -> int:
@@ -161,6 +165,22 @@ class InferenceEngine:
     def _forward_padded(self, rows: int) -> torch.Tensor:
         if not self.use_graphs:
             return self._run(rows)
+        if self.replay == "native":  # recorded launches replayed from C++ (no graph launch)
+            entry = self._programs.get(rows)
+            if entry is None:
+                with torch.cuda.stream(self._stream):
+                    self._run(rows)  # allocate buffers
+                    prog = native().Program()
+                    native().record_begin(prog)
+                    try:
+                        prog.mark("fwd")
+                        out = self._run(rows)
+                    finally:
+                        native().record_end()
+                entry = self._programs[rows] = (prog, out)
+            prog, out = entry
+            prog.run(["fwd"], self._stream.cuda_stream)
+            return out
         entry = self._graphs.get(rows)
         if entry is None:
             with torch.cuda.stream(self._stream):
