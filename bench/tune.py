@@ -7,7 +7,8 @@ inputs resident in the 256-MiB Infinity Cache and its split-K slabs hot, which m
 signature of the step (fwd / dgrad / wgrad of each layer) the candidates -- every tile that
 divides the output, and for wgrad tiles x split-K counts -- are tried one at a time inside the
 real step (coordinate descent, others held at their current best), each timed over whole steps
-with HIP events. The winners go into the table with the step time they produced.
+with HIP events; every candidate runs in both GEMM forms (one tile per workgroup / persistent
+workgroups, ``--persist``). The winners go into the table with the step time they produced.
 
 Usage: python bench/tune.py [--configs 65536:mnist-fcnn,...] [--out PATH]"""
 from __future__ import annotations
@@ -85,7 +86,8 @@ def step_ms(spec, R, x, y, dev, steps, reps):
     return statistics.median(times)
 
 
-def tune_config(R, model, dev, table, steps, reps, log, only=None, verbose=False):
+def tune_config(R, model, dev, table, steps, reps, log, only=None, verbose=False,
+                persist_opts=(0,)):
     spec = NAMED_MODELS.get(model) or MLPSpec.parse(model)
     kp0 = (spec.layers[0].in_dim + 63) // 64 * 64
     xs, ys = synthetic_mnist(min(R, 65536), seed=3)
@@ -104,23 +106,26 @@ def tune_config(R, model, dev, table, steps, reps, log, only=None, verbose=False
         prev = table.get(k)
         res = []
         for (tile, s) in cands:
-            table[k] = {"tile": list(tile), "splits": s, "stages": 2}
-            try:
-                res.append((step_ms(spec, R, x, y, dev, steps, reps), tile, s))
-                if verbose:
-                    log({"cand": k, "tile": list(tile), "splits": s,
-                         "step_ms": round(res[-1][0], 4)})
-            except (ValueError, RuntimeError) as e:
-                log({"skip": k, "tile": tile, "splits": s, "err": str(e)[:80]})
-        ms, tile, s = min(res)
+            for pers in persist_opts:
+                table[k] = {"tile": list(tile), "splits": s, "stages": 2, "persist": pers}
+                try:
+                    res.append((step_ms(spec, R, x, y, dev, steps, reps), tile, s, pers))
+                    if verbose:
+                        log({"cand": k, "tile": list(tile), "splits": s, "persist": pers,
+                             "step_ms": round(res[-1][0], 4)})
+                except (ValueError, RuntimeError) as e:
+                    log({"skip": k, "tile": tile, "splits": s, "persist": pers,
+                         "err": str(e)[:80]})
+        ms, tile, s, pers = min(res)
         # keep the incumbent unless the challenger wins by more than noise (0.5 %)
         if prev is not None:
-            inc = [r for r in res if list(r[1]) == prev["tile"] and r[2] == prev["splits"]]
+            inc = [r for r in res if list(r[1]) == prev["tile"] and r[2] == prev["splits"]
+                   and r[3] == prev.get("persist", 0)]
             if inc and inc[0][0] <= ms * 1.005:
-                ms, tile, s = inc[0]
-        table[k] = {"tile": list(tile), "splits": s, "stages": 2, "step_ms": round(ms, 4),
-                    "model": model}
-        log({"sig": k, "best": [list(tile), s], "step_ms": round(ms, 4),
+                ms, tile, s, pers = inc[0]
+        table[k] = {"tile": list(tile), "splits": s, "stages": 2, "persist": pers,
+                    "step_ms": round(ms, 4), "model": model}
+        log({"sig": k, "best": [list(tile), s, pers], "step_ms": round(ms, 4),
              "worst_ms": round(max(r[0] for r in res), 4), "n": len(res)})
     final = step_ms(spec, R, x, y, dev, steps, reps)
     log({"rows": R, "model": model, "start_ms": round(base, 4), "final_ms": round(final, 4)})
@@ -135,6 +140,9 @@ def main():
     ap.add_argument("--only", default="", help="comma list of signatures, e.g. "
                     "wgrad:512x832x65536")
     ap.add_argument("--verbose", action="store_true", help="log every candidate")
+    ap.add_argument("--persist", default="0,1",
+                    help="GEMM forms to try: 0 = one tile per workgroup (gemm.hip), 1 = "
+                    "persistent workgroups (gemm_persist.hip)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     doc = {"device": torch.cuda.get_device_name(0), "generated_by": "bench/tune.py",
@@ -154,7 +162,8 @@ def main():
     for cfg in a.configs.split(","):
         rows, model = cfg.split(":")
         tune_config(int(rows), model, dev, table, a.steps, a.reps, log,
-                    only=set(a.only.split(",")) if a.only else None, verbose=a.verbose)
+                    only=set(a.only.split(",")) if a.only else None, verbose=a.verbose,
+                    persist_opts=tuple(int(v) for v in a.persist.split(",")))
         doc["entries"] = dict(table)
         with open(a.out, "w") as f:
             json.dump(doc, f, indent=1, sort_keys=True)

@@ -67,7 +67,8 @@ PYBIND11_MODULE(_native, m) {
          uintptr_t bias, uintptr_t aux, long ld_aux, int M, int N, int K, int act, int accumulate,
          int layout_a, int layout_b, int out_f32, int bm, int bn, int splits, uintptr_t stream,
          uintptr_t colsum, long ld_colsum, uintptr_t xent_labels, int n_cls, float xent_scale,
-         uintptr_t loss_part, uintptr_t correct, int k_total, int stages, int group_m) {
+         uintptr_t loss_part, uintptr_t correct, int k_total, int stages, int group_m,
+         int persist) {
         GemmParams p{};
         p.group_m = group_m;
         p.k_total = k_total;
@@ -106,7 +107,8 @@ PYBIND11_MODULE(_native, m) {
               q.xent_labels = R.fix(q.xent_labels);
               q.loss_part = R.fix(q.loss_part);
               q.correct = R.fix(q.correct);
-              return dnn::gemm_bf16(q, layout_a, layout_b, out_f32, bm, bn, splits, s, stages);
+              return dnn::gemm_bf16(q, layout_a, layout_b, out_f32, bm, bn, splits, s, stages,
+                                    persist);
             },
             stream);
       },
@@ -117,7 +119,7 @@ PYBIND11_MODULE(_native, m) {
       py::arg("stream"), py::arg("colsum") = 0, py::arg("ld_colsum") = 0,
       py::arg("xent_labels") = 0, py::arg("n_cls") = 0, py::arg("xent_scale") = 0.f,
       py::arg("loss_part") = 0, py::arg("correct") = 0, py::arg("k_total") = 0,
-      py::arg("stages") = 0, py::arg("group_m") = 0);
+      py::arg("stages") = 0, py::arg("group_m") = 0, py::arg("persist") = 0);
   m.def("gemm_default_stages", &dnn::default_stages);
 
   m.def("gemv_max_rows", []() { return dnn::GEMV_MAX_ROWS; });

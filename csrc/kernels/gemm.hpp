@@ -50,8 +50,13 @@ struct GemmParams {
 // Returns 0 on success, a negative code when a shape/alignment precondition fails
 // (nothing is launched then).
 // stages: LDS pipeline depth 2..4 (0 = default_stages(bm, bn)).
+// persist: 0 = one tile per workgroup (gemm.hip); != 0 = persistent workgroups walking tile
+// runs with a register-direct epilogue (gemm_persist.hip): > 0 workgroup count, < 0 one round
+// of resident workgroups. The fused cross-entropy always runs the one-tile form.
 int gemm_bf16(const GemmParams& p, int layout_a, int layout_b, int out_f32, int bm, int bn,
-              int splits, hipStream_t stream, int stages = 0);
+              int splits, hipStream_t stream, int stages = 0, int persist = 0);
+int gemm_persist_launch(const GemmParams& q, int la, int lb, int out_f32, int bm, int bn,
+                        int splits, int ns, int persist, hipStream_t stream);
 int default_stages(int bm, int bn);
 // Tiles: 64|128 x 64|128 (4 waves, 256 threads) and 256 x 64|128|256, 128 x 256 (8 waves).
 bool gemm_tile_supported(int bm, int bn);

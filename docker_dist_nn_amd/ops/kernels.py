@@ -46,6 +46,36 @@ def _parse_stages(spec: str) -> dict:
 STAGES = _parse_stages(os.environ.get("DNN_GEMM_STAGES", ""))
 
 
+def _parse_persist(spec: str) -> dict:
+    """DNN_GEMM_PERSIST: "" (tuned table decides), "0"/"1" (every GEMM off/on), or
+    "fwd=1,dgrad=0,wgrad=1"; a value > 1 is an explicit workgroup count. None = table."""
+    out = {"fwd": None, "dgrad": None, "wgrad": None}
+    spec = spec.strip()
+    if not spec:
+        return out
+    if "=" not in spec:
+        return {k: int(spec) for k in out}
+    for part in spec.split(","):
+        k, v = part.split("=")
+        if k.strip() not in out:
+            raise ValueError(f"DNN_GEMM_PERSIST: unknown GEMM kind {k!r}")
+        out[k.strip()] = int(v)
+    return out
+
+
+# Persistent-workgroup GEMM form (csrc/kernels/gemm_persist.hip) per GEMM kind.
+PERSIST = _parse_persist(os.environ.get("DNN_GEMM_PERSIST", ""))
+
+
+def _persist(kind: str, entry) -> int:
+    """Native `persist` argument: 0 = one tile per workgroup, -1 = one resident round of
+    persistent workgroups, > 1 = that many workgroups."""
+    v = PERSIST[kind]
+    if v is None:
+        v = (entry or {}).get("persist", 0)
+    return -1 if v == 1 else int(v)
+
+
 def _stream(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 
@@ -137,8 +167,11 @@ def wgrad_config(M: int, N: int, K_total: int, max_splits: int = 48) -> tuple[in
 
 def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=None, aux=None,
          act=0, accumulate: bool = False, splits: int = 1, tiles: tuple[int, int] | None = None,
-         colsum=None, k_total: int = 0, stages: int = 0, group_m: int = 0):
+         colsum=None, k_total: int = 0, stages: int = 0, group_m: int = 0, persist: int = 0):
     """C (+)= epilogue(A.B). See csrc/kernels/gemm.hpp for the layout/epilogue contract.
+
+    ``persist`` != 0 runs the persistent-workgroup form with the register-direct epilogue
+    (csrc/kernels/gemm_persist.hip): -1 = one resident round, > 0 = workgroup count.
 
     ``k_total`` > 0 selects uneven split-K over the full contraction length (K is ignored).
     ``colsum`` (bf16 output only): fp32 [M/bm][>=N] receives per-row-tile column sums of the
@@ -190,7 +223,7 @@ def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=
                        M, N, K, act, int(accumulate), layout_a, layout_b, int(out_f32), bm, bn,
                        splits, _stream(a), _p(colsum),
                        colsum.stride(0) if colsum is not None else 0, k_total=int(k_total),
-                       stages=int(stages), group_m=int(group_m))
+                       stages=int(stages), group_m=int(group_m), persist=int(persist))
     return c
 
 
@@ -232,7 +265,8 @@ def linear_fwd(x, w, bias, y, act="relu"):
     t = tuning.lookup("fwd", M, N, K)
     tiles = tuple(t["tile"]) if t else pick_tiles(M, N)
     return gemm(x, w, y, layout_a=KMAJ, layout_b=KMAJ, M=M, N=N, K=K, bias=bias, act=act,
-                tiles=tiles, stages=STAGES["fwd"] or (t or {}).get("stages", 0))
+                tiles=tiles, stages=STAGES["fwd"] or (t or {}).get("stages", 0),
+                persist=_persist("fwd", t))
 
 
 def xent_tiles(M: int, N: int) -> tuple[int, int]:
@@ -295,9 +329,10 @@ def linear_dgrad(dz, w, dx, y_prev=None, act_prev="linear", colsum=None):
     K = w.shape[1]
     if y_prev is None:
         act_prev = "linear"
+    t = tuning.lookup("dgrad", M, K, N)
     return gemm(dz, w, dx, layout_a=KMAJ, layout_b=MNMAJ, M=M, N=K, K=N, aux=y_prev,
                 act=act_prev, tiles=dgrad_tiles(M, K, N), colsum=colsum,
-                stages=STAGES["dgrad"])
+                stages=STAGES["dgrad"], persist=_persist("dgrad", t))
 
 
 def linear_wgrad(dz, x, slabs, splits=1, accumulate=False):
@@ -308,8 +343,10 @@ def linear_wgrad(dz, x, slabs, splits=1, accumulate=False):
         raise ValueError("rows must be a multiple of 64 with at least 64 rows per split")
     bm, bn, s = wgrad_config(N, K, R)
     tiles = (bm, bn) if s == splits else pick_tiles(N, K, splits)
+    t = tuning.lookup("wgrad", N, K, R) if s == splits else None
     return gemm(dz, x, slabs, layout_a=MNMAJ, layout_b=MNMAJ, M=N, N=K, K=R, k_total=R,
-                accumulate=accumulate, splits=splits, tiles=tiles, stages=STAGES["wgrad"])
+                accumulate=accumulate, splits=splits, tiles=tiles, stages=STAGES["wgrad"],
+                persist=_persist("wgrad", t))
 
 
 STREAMK_WG = 2 * NUM_CU  # stream-K workgroups: two resident per CU, every CU equally loaded
