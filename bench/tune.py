@@ -106,26 +106,30 @@ def tune_config(R, model, dev, table, steps, reps, log, only=None, verbose=False
         prev = table.get(k)
         res = []
         for (tile, s) in cands:
-            for pers in persist_opts:
-                table[k] = {"tile": list(tile), "splits": s, "stages": 2, "persist": pers}
+            # 256x256 tiles also run the ping-pong form (stages 8, gemm_pp.hip)
+            forms = [(2, pers) for pers in persist_opts]
+            if tuple(tile) == (256, 256):
+                forms.append((8, 0))
+            for ns, pers in forms:
+                table[k] = {"tile": list(tile), "splits": s, "stages": ns, "persist": pers}
                 try:
-                    res.append((step_ms(spec, R, x, y, dev, steps, reps), tile, s, pers))
+                    res.append((step_ms(spec, R, x, y, dev, steps, reps), tile, s, pers, ns))
                     if verbose:
                         log({"cand": k, "tile": list(tile), "splits": s, "persist": pers,
-                             "step_ms": round(res[-1][0], 4)})
+                             "stages": ns, "step_ms": round(res[-1][0], 4)})
                 except (ValueError, RuntimeError) as e:
-                    log({"skip": k, "tile": tile, "splits": s, "persist": pers,
+                    log({"skip": k, "tile": tile, "splits": s, "persist": pers, "stages": ns,
                          "err": str(e)[:80]})
-        ms, tile, s, pers = min(res)
+        ms, tile, s, pers, ns = min(res)
         # keep the incumbent unless the challenger wins by more than noise (0.5 %)
         if prev is not None:
             inc = [r for r in res if list(r[1]) == prev["tile"] and r[2] == prev["splits"]
-                   and r[3] == prev.get("persist", 0)]
+                   and r[3] == prev.get("persist", 0) and r[4] == prev.get("stages", 2)]
             if inc and inc[0][0] <= ms * 1.005:
-                ms, tile, s, pers = inc[0]
-        table[k] = {"tile": list(tile), "splits": s, "stages": 2, "persist": pers,
+                ms, tile, s, pers, ns = inc[0]
+        table[k] = {"tile": list(tile), "splits": s, "stages": ns, "persist": pers,
                     "step_ms": round(ms, 4), "model": model}
-        log({"sig": k, "best": [list(tile), s, pers], "step_ms": round(ms, 4),
+        log({"sig": k, "best": [list(tile), s, pers, ns], "step_ms": round(ms, 4),
              "worst_ms": round(max(r[0] for r in res), 4), "n": len(res)})
     final = step_ms(spec, R, x, y, dev, steps, reps)
     log({"rows": R, "model": model, "start_ms": round(base, 4), "final_ms": round(final, 4)})

@@ -24,86 +24,6 @@
 
 namespace dnn {
 
-// Accumulator fragments of the waves in epilogue chunk `chunk` -> fp32 [EPI_ROWS][CS_LD] LDS
-// tile (C/D map: col = lane&15, row = 4*(lane>>4) + r).
-template <class C>
-__device__ __forceinline__ void acc_to_lds(const f32x4_t (&acc)[C::FM][C::FN],
-                                           float LDS_AS* cs, int chunk, int wave, int lane) {
-  const int wm = wave / C::WN, wn = wave % C::WN;
-  if (wm / C::WPC != chunk) return;
-  const int rbase = (wm % C::WPC) * C::SM;
-#pragma unroll
-  for (int i = 0; i < C::FM; ++i)
-#pragma unroll
-    for (int j = 0; j < C::FN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = rbase + i * 16 + (lane >> 4) * 4 + r;
-        const int col = wn * C::SN + j * 16 + (lane & 15);
-        cs[row * C::CS_LD + col] = acc[i][j][r];
-      }
-}
-
-// Fused softmax cross-entropy over the fp32 logits tile in LDS (the whole padded row lives in
-// this tile: N == BN; 4-wave tiles, one epilogue chunk). Thread r < BM owns row r: adds the
-// bias, finds max / argmax (lowest index, np.argmax rule) / log-sum-exp over the n_cls valid
-// columns, and overwrites the row with dz = (p - onehot) * scale (0 in padding columns and for
-// label < 0 padding rows). Block loss and correct-count go to loss_part[tile_m] /
-// correct[tile_m].
-template <class C>
-__device__ __forceinline__ void xent_rows(const GemmParams& p, float LDS_AS* cs, int m0) {
-  static_assert(C::NW == 4 && C::CHUNKS == 1, "fused cross-entropy runs on 4-wave tiles");
-  constexpr int BM = C::BM, BN = C::BN, CS_LD = C::CS_LD;
-  // scratch after the staging tile (all LDS lives in the kernel's single __shared__ array)
-  float LDS_AS* s_loss = cs + BM * CS_LD;
-  int LDS_AS* s_corr = (int LDS_AS*)(s_loss + 4);
-  const int r = threadIdx.x;
-  float loss = 0.f;
-  int corr = 0;
-  if (r < BM) {
-    float LDS_AS* row = cs + r * CS_LD;
-    const int label = p.xent_labels[m0 + r];
-    const int nc = p.n_cls;
-    float mx = -INFINITY;
-    int amax = 0;
-    for (int c = 0; c < nc; ++c) {
-      const float v = row[c] + p.bias[c];
-      row[c] = v;
-      if (v > mx) {
-        mx = v;
-        amax = c;
-      }
-    }
-    float se = 0.f;
-    for (int c = 0; c < nc; ++c) se += __expf(row[c] - mx);
-    const float inv = 1.f / se;
-    if (label >= 0) {
-      loss = -(row[label] - mx - __logf(se));
-      corr = amax == label;
-      for (int c = 0; c < nc; ++c)
-        row[c] = (__expf(row[c] - mx) * inv - (c == label ? 1.f : 0.f)) * p.xent_scale;
-    } else {
-      for (int c = 0; c < nc; ++c) row[c] = 0.f;
-    }
-    for (int c = nc; c < BN; ++c) row[c] = 0.f;
-  }
-  // block reduction of loss / correct (fixed order -> reproducible)
-  loss = wave_sum(loss);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) corr += __shfl_xor(corr, o, 64);
-  const int wave = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) {
-    s_loss[wave] = loss;
-    s_corr[wave] = corr;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    if (p.loss_part) p.loss_part[m0 / BM] = (s_loss[0] + s_loss[1]) + (s_loss[2] + s_loss[3]);
-    const int cc = s_corr[0] + s_corr[1] + s_corr[2] + s_corr[3];
-    if (p.correct) p.correct[m0 / BM] = cc;
-  }
-}
-
 template <class C, int LA, int LB, bool OUT_F32>
 __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(GemmParams p, int tiles_n, int tiles_m,
                                                           int nwg) {
@@ -145,127 +65,7 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(GemmParams p, int tile
   f32x4_t acc[C::FM][C::FN];
   mma_tile<C, LA, LB>(p, m0, n0, kbase, nk, lds, acc, wave, lane);
 
-  // ---- epilogue: accumulators -> LDS (fp32, EPI_ROWS at a time) -> 16-B row chunks -----------
-  float LDS_AS* cs = (float LDS_AS*)lds;
-  constexpr int CPR = BN / 8;
-  constexpr int ITER = C::EPI_ROWS * CPR / NT;
-  constexpr int RSTEP = NT / CPR;  // rows between a thread's consecutive iterations
-  // A thread's 8-column chunk is the same in every iteration and chunk (NT % CPR == 0): its
-  // bias is loaded ONCE, and the per-row global reads of a chunk (activation for the dgrad
-  // mask, previous slab for split-K accumulation) are all issued before the first is used --
-  // one L2 round trip per chunk instead of one per row (the per-row form serialised ~16
-  // round trips per 256x256 tile: half the tile's time at K = 832).
-  const int ccol = (threadIdx.x % CPR) * 8, crow = threadIdx.x / CPR;
-  const long gn = n0 + ccol;
-  bool xent = false;
-  if constexpr (!OUT_F32 && C::NW == 4 && C::CHUNKS == 1)
-    xent = p.xent_labels != nullptr;  // uniform
-  const bool col_ok = gn < p.N;  // partial edge tile: this thread's columns may be past N
-  float bias_r[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  if (p.bias && !xent && col_ok) {
-    const f32x4_t b0 = *(const f32x4_t*)(p.bias + gn);
-    const f32x4_t b1 = *(const f32x4_t*)(p.bias + gn + 4);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      bias_r[e] = b0[e];
-      bias_r[e + 4] = b1[e];
-    }
-  }
-  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-  for (int chunk = 0; chunk < C::CHUNKS; ++chunk) {
-    if (chunk) __syncthreads();  // previous chunk's stores have read the staging tile
-    acc_to_lds<C>(acc, cs, chunk, wave, lane);
-    __syncthreads();
-    if constexpr (!OUT_F32 && C::NW == 4 && C::CHUNKS == 1) {
-      if (xent) {  // fused softmax-CE, one thread per row of the tile
-        xent_rows<C>(p, cs, m0);
-        __syncthreads();
-      }
-    }
-    const long gm0 = m0 + chunk * C::EPI_ROWS + crow;
-    [[maybe_unused]] bf16x8_t yv[ITER];
-    [[maybe_unused]] f32x4_t cp0[ITER], cp1[ITER];
-    if constexpr (OUT_F32) {
-      if (p.accumulate) {
-#pragma unroll
-        for (int it = 0; it < ITER; ++it) {
-          if (!col_ok || gm0 + it * RSTEP >= p.M) continue;
-          const float* c = (const float*)p.C + (long)split * p.c_split_stride +
-                           (gm0 + it * RSTEP) * p.ldc + gn;
-          cp0[it] = *(const f32x4_t*)c;
-          cp1[it] = *(const f32x4_t*)(c + 4);
-        }
-      }
-    } else {
-      if (p.aux && !xent) {
-#pragma unroll
-        for (int it = 0; it < ITER; ++it)
-          if (col_ok && gm0 + it * RSTEP < p.M)
-            yv[it] = *(const bf16x8_t*)(p.aux + (gm0 + it * RSTEP) * p.ld_aux + gn);
-      }
-    }
-#pragma unroll
-    for (int it = 0; it < ITER; ++it) {
-      const int row = crow + it * RSTEP;
-      const f32x4_t v0 = *(const f32x4_t LDS_AS*)(cs + row * CS_LD + ccol);
-      const f32x4_t v1 = *(const f32x4_t LDS_AS*)(cs + row * CS_LD + ccol + 4);
-      float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-      const long gm = gm0 + it * RSTEP;
-      if (!col_ok || gm >= p.M) continue;  // outside a partial edge tile: not stored
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += bias_r[e];
-      if constexpr (OUT_F32) {
-        float* c = (float*)p.C + (long)split * p.c_split_stride + gm * p.ldc + gn;
-        if (!p.accumulate && p.act != ACT_LINEAR) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = act_fwd(v[e], p.act);
-        }
-        f32x4_t o0 = {v[0], v[1], v[2], v[3]}, o1 = {v[4], v[5], v[6], v[7]};
-        if (p.accumulate) {
-          o0 += cp0[it];
-          o1 += cp1[it];
-        }
-        *(f32x4_t*)c = o0;
-        *(f32x4_t*)(c + 4) = o1;
-      } else {
-        if (xent) {
-          // dz already computed in LDS
-        } else if (p.aux) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = act_bwd(v[e], bf2f((u16)yv[it][e]), p.act);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = act_fwd(v[e], p.act);
-        }
-        bf16x8_t o;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const u16 h = f2bf(v[e]);
-          o[e] = (short)h;
-          csum[e] += bf2f(h);
-        }
-        *(bf16x8_t*)((u16*)p.C + gm * p.ldc + gn) = o;
-      }
-    }
-  }
-  if constexpr (!OUT_F32) {
-    if (p.colsum) {  // uniform across the block
-      __syncthreads();  // all reads of the staging tile are done
-      f32x4_t LDS_AS* red = (f32x4_t LDS_AS*)lds;
-      red[2 * threadIdx.x] = f32x4_t{csum[0], csum[1], csum[2], csum[3]};
-      red[2 * threadIdx.x + 1] = f32x4_t{csum[4], csum[5], csum[6], csum[7]};
-      __syncthreads();
-      if ((int)threadIdx.x < BN) {
-        const int col = threadIdx.x, cc = col >> 3, e = col & 7;
-        const float LDS_AS* rf = (const float LDS_AS*)lds;
-        float t = 0.f;
-#pragma unroll 4
-        for (int r = 0; r < NT / CPR; ++r) t += rf[(r * CPR + cc) * 8 + e];
-        if (n0 + col < p.N) p.colsum[(long)tm * p.ld_colsum + n0 + col] = t;
-      }
-    }
-  }
+  epilogue_staged<C, OUT_F32>(p, acc, lds, m0, n0, tm, split, wave, lane);
 }
 
 // ---- stream-K (balanced split-K) for batch-contraction GEMMs ---------------------------------
@@ -412,7 +212,7 @@ const char* gemm_error_string(int code) {
     case -9: return "hip launch failed";
     case -10: return "colsum needs bf16 output and ld_colsum >= N";
     case -11: return "fused cross-entropy needs bf16 output, N == bn <= 128, a bias and 0 < n_cls <= N";
-    case -12: return "pipeline stages must be 2..4 (8-wave tiles: 2..3, 256x256: 2)";
+    case -12: return "pipeline stages must be 2..4 (8-wave tiles: 2..3, 256x256: 2 or 8 = ping-pong)";
     default: return "unknown gemm error";
   }
 }
@@ -453,6 +253,13 @@ int gemm_bf16(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, 
   // hipBLASLt's MT256x256 MIWT8_8 shape -- was built and measured: 7 % slower on 8192^3 fwd,
   // 20 % on K = 832, 3-4x on dgrad (spills); without hand-scheduled intra-wave pipelining one
   // wave per SIMD cannot hide LDS latency, so the 8-wave form is the 256x256 tile.)
+  if (stages == 8) {  // ping-pong half-tile-streamed form (gemm_pp.hip)
+    if (bm != 256 || bn != 256) return -12;
+    if (p.xent_labels) return -11;
+    GemmParams q = p;
+    if (q.group_m <= 0) q.group_m = ((p.N + 255) / 256) >= 8 ? 4 : 1;
+    return gemm_pp_launch(q, la, lb, out_f32, splits, stream);
+  }
   const int nt = gemm_tile_threads(bm, bn);
   const int ns = stages ? stages : default_stages(bm, bn);
   // 8-wave tiles: NS = 3 where three stages fit (not 256x256)

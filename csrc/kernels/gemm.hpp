@@ -55,6 +55,9 @@ struct GemmParams {
 // of resident workgroups. The fused cross-entropy always runs the one-tile form.
 int gemm_bf16(const GemmParams& p, int layout_a, int layout_b, int out_f32, int bm, int bn,
               int splits, hipStream_t stream, int stages = 0, int persist = 0);
+// stages == 8 with 256x256 tiles: the ping-pong, half-tile-streamed main loop (gemm_pp.hip).
+int gemm_pp_launch(const GemmParams& q, int la, int lb, int out_f32, int splits,
+                   hipStream_t stream);
 int gemm_persist_launch(const GemmParams& q, int la, int lb, int out_f32, int bm, int bn,
                         int splits, int ns, int persist, hipStream_t stream);
 int default_stages(int bm, int bn);

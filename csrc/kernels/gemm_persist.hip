@@ -64,23 +64,6 @@ __device__ __forceinline__ TileCoord decode_tile(const GemmParams& p, int t, int
   return c;
 }
 
-// Sum over the 16 lanes of a DPP row (lanes 16r .. 16r+15) in a fixed butterfly order.
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float x) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
-}
-__device__ __forceinline__ float row16_sum(float v) {
-  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
-  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
-  v += dpp_f<0x141>(v);  // row_half_mirror
-  v += dpp_f<0x140>(v);  // row_mirror
-  return v;
-}
-
-__device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
-  return (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
-}
-
 template <class C, int LA, int LB, bool OUT_F32>
 __global__ __launch_bounds__(C::NT) void gemm_persist_kernel(GemmParams p, int tiles_n,
                                                              int tiles_m, int splits, int nwg) {
@@ -122,7 +105,6 @@ __global__ __launch_bounds__(C::NT) void gemm_persist_kernel(GemmParams p, int t
     if (lt < t_end) issue(lds + s * STAGE);
   int rd = 0, wr = NS - 1;
 
-  const int frow = lane & 15, fg = lane >> 4;  // fragment row / 4-column group of this lane
   for (int t = t_begin; t < t_end; t += nwg) {
     const TileCoord cc = decode_tile(p, t, tiles_n, tiles_m, splits);
     f32x4_t acc[FM][FN];
@@ -157,135 +139,8 @@ __global__ __launch_bounds__(C::NT) void gemm_persist_kernel(GemmParams p, int t
       wr = wr + 1 == NS ? 0 : wr + 1;
     }
 
-    // ---- epilogue straight from the accumulators ------------------------------------------
-    // acc[i][j][e] = C[row0 + 16 i][col0 + 16 j + e]
-    const int row0 = cc.tm * BM + wm * C::SM + frow;
-    const int col0 = cc.tn * BN + wn * C::SN + 4 * fg;
-    if constexpr (OUT_F32) {
-      float* cbase = (float*)p.C + (long)cc.split * p.c_split_stride + col0;
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int row = row0 + 16 * i;
-        if (row >= p.M) continue;
-        float* crow = cbase + (long)row * p.ldc;  // columns 16 j: immediate offsets
-        f32x4_t v[FN];
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          v[j] = acc[i][j];
-          if (p.accumulate && col0 + 16 * j < p.N) v[j] += *(const f32x4_t*)(crow + 16 * j);
-        }
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          if (col0 + 16 * j >= p.N) continue;
-          if (p.bias) v[j] += *(const f32x4_t*)(p.bias + col0 + 16 * j);
-          if (!p.accumulate && p.act != ACT_LINEAR) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[j][e] = act_fwd(v[j][e], p.act);
-          }
-          *(f32x4_t*)(crow + 16 * j) = v[j];
-        }
-      }
-    } else {
-      const bool want_sum = p.colsum != nullptr;  // uniform
-      // store column after the 16-lane swap: even groups keep an 8-column half of fragment j,
-      // odd groups take one of fragment j+1 (see below)
-      const int scol0 = cc.tn * BN + wn * C::SN + 16 * (fg & 1) + 8 * (fg >> 1);
-      // [WM][BN] colsum partials in the slot of the last consumed stage: no DMA targets it
-      // before the next k-step's barrier; wait until every wave has finished reading it
-      float LDS_AS* red = (float LDS_AS*)(lds + (rd == 0 ? NS - 1 : rd - 1) * STAGE);
-      if (want_sum) lds_barrier();
-#pragma unroll
-      for (int j = 0; j < FN; j += 2) {
-        const int c0 = col0 + 16 * j, c1 = c0 + 16;
-        f32x4_t b0 = {0.f, 0.f, 0.f, 0.f}, b1 = {0.f, 0.f, 0.f, 0.f};
-        if (p.bias) {
-          if (c0 < p.N) b0 = *(const f32x4_t*)(p.bias + c0);
-          if (c1 < p.N) b1 = *(const f32x4_t*)(p.bias + c1);
-        }
-        // activation values for the derivative, all issued before the first use
-        uint2 y0[FM], y1[FM];
-        if (p.aux) {
-          const u16* ya = p.aux + min(c0, p.N - 4);
-          const u16* yb = p.aux + min(c1, p.N - 4);
-#pragma unroll
-          for (int i = 0; i < FM; ++i) {
-            const long r = min(row0 + 16 * i, p.M - 1) * p.ld_aux;
-            y0[i] = *(const uint2*)(ya + r);
-            y1[i] = *(const uint2*)(yb + r);
-          }
-        }
-        float cs0[4] = {0.f, 0.f, 0.f, 0.f}, cs1[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int i = 0; i < FM; ++i) {
-          const int row = row0 + 16 * i;
-          float v0[4], v1[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            v0[e] = acc[i][j][e] + b0[e];
-            v1[e] = acc[i][j + 1][e] + b1[e];
-          }
-          if (p.aux) {
-            const unsigned ya[2] = {y0[i].x, y0[i].y}, yb[2] = {y1[i].x, y1[i].y};
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const unsigned sh = (e & 1) ? 0u : 16u;
-              v0[e] = act_bwd(v0[e], __uint_as_float((ya[e >> 1] << sh) & 0xffff0000u), p.act);
-              v1[e] = act_bwd(v1[e], __uint_as_float((yb[e >> 1] << sh) & 0xffff0000u), p.act);
-            }
-          } else {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              v0[e] = act_fwd(v0[e], p.act);
-              v1[e] = act_fwd(v1[e], p.act);
-            }
-          }
-          const unsigned x0 = pack_bf16x2(v0[0], v0[1]), x1 = pack_bf16x2(v0[2], v0[3]);
-          const unsigned z0 = pack_bf16x2(v1[0], v1[1]), z1 = pack_bf16x2(v1[2], v1[3]);
-          if (want_sum && row < p.M) {  // sums of the STORED (bf16-rounded) values
-            cs0[0] += __uint_as_float(x0 << 16);
-            cs0[1] += __uint_as_float(x0 & 0xffff0000u);
-            cs0[2] += __uint_as_float(x1 << 16);
-            cs0[3] += __uint_as_float(x1 & 0xffff0000u);
-            cs1[0] += __uint_as_float(z0 << 16);
-            cs1[1] += __uint_as_float(z0 & 0xffff0000u);
-            cs1[2] += __uint_as_float(z1 << 16);
-            cs1[3] += __uint_as_float(z1 & 0xffff0000u);
-          }
-          // 16-lane half exchange (odd DPP rows of x <-> even rows of z). Afterwards group 0
-          // holds cols 0..7 of fragment j, group 1 cols 0..7 of j+1, group 2 cols 8..15 of j,
-          // group 3 cols 8..15 of j+1; in every group [0] = the chunk's low 4 columns.
-          const auto s0 = __builtin_amdgcn_permlane16_swap(x0, z0, false, false);
-          const auto s1 = __builtin_amdgcn_permlane16_swap(x1, z1, false, false);
-          const int scol = scol0 + 16 * j;
-          if (row < p.M && scol < p.N)
-            *(uint4*)((u16*)p.C + (long)row * p.ldc + scol) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
-        }
-        if (want_sum) {  // this pair's column sums over the wave's rows -> LDS [wm][col]
-          f32x4_t r0, r1;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            r0[e] = row16_sum(cs0[e]);
-            r1[e] = row16_sum(cs1[e]);
-          }
-          if (frow == 0) {
-            float LDS_AS* d = red + wm * BN + wn * C::SN + 16 * j + 4 * fg;
-            *(f32x4_t LDS_AS*)d = r0;
-            *(f32x4_t LDS_AS*)(d + 16) = r1;
-          }
-        }
-      }
-      if (want_sum) {
-        lds_barrier();
-        if ((int)threadIdx.x < BN) {
-          const int col = threadIdx.x;
-          float tsum = 0.f;
-#pragma unroll
-          for (int r = 0; r < C::WM; ++r) tsum += red[r * BN + col];
-          if (cc.tn * BN + col < p.N) p.colsum[(long)cc.tm * p.ld_colsum + cc.tn * BN + col] = tsum;
-        }
-        // the slot is restaged only after the next k-step's barrier
-      }
-    }
+    epilogue_direct<C::FM, C::FN, BN, C::SN, C::WM, NS, STAGE, OUT_F32>(
+        p, acc, lds, rd, cc.tm, cc.tn, cc.split, wm, wn, lane, true);
   }
 }
 

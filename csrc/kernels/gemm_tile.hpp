@@ -205,4 +205,381 @@ __device__ __forceinline__ void mma_tile(const GemmParams& p, int m0, int n0, in
   __syncthreads();
 }
 
+// Accumulator fragments of the waves in epilogue chunk `chunk` -> fp32 [EPI_ROWS][CS_LD] LDS
+// tile (C/D map: col = lane&15, row = 4*(lane>>4) + r).
+template <class C>
+__device__ __forceinline__ void acc_to_lds(const f32x4_t (&acc)[C::FM][C::FN],
+                                           float LDS_AS* cs, int chunk, int wave, int lane) {
+  const int wm = wave / C::WN, wn = wave % C::WN;
+  if (wm / C::WPC != chunk) return;
+  const int rbase = (wm % C::WPC) * C::SM;
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = rbase + i * 16 + (lane >> 4) * 4 + r;
+        const int col = wn * C::SN + j * 16 + (lane & 15);
+        cs[row * C::CS_LD + col] = acc[i][j][r];
+      }
+}
+
+// Fused softmax cross-entropy over the fp32 logits tile in LDS (the whole padded row lives in
+// this tile: N == BN; 4-wave tiles, one epilogue chunk). Thread r < BM owns row r: adds the
+// bias, finds max / argmax (lowest index, np.argmax rule) / log-sum-exp over the n_cls valid
+// columns, and overwrites the row with dz = (p - onehot) * scale (0 in padding columns and for
+// label < 0 padding rows). Block loss and correct-count go to loss_part[tile_m] /
+// correct[tile_m].
+template <class C>
+__device__ __forceinline__ void xent_rows(const GemmParams& p, float LDS_AS* cs, int m0) {
+  static_assert(C::NW == 4 && C::CHUNKS == 1, "fused cross-entropy runs on 4-wave tiles");
+  constexpr int BM = C::BM, BN = C::BN, CS_LD = C::CS_LD;
+  // scratch after the staging tile (all LDS lives in the kernel's single __shared__ array)
+  float LDS_AS* s_loss = cs + BM * CS_LD;
+  int LDS_AS* s_corr = (int LDS_AS*)(s_loss + 4);
+  const int r = threadIdx.x;
+  float loss = 0.f;
+  int corr = 0;
+  if (r < BM) {
+    float LDS_AS* row = cs + r * CS_LD;
+    const int label = p.xent_labels[m0 + r];
+    const int nc = p.n_cls;
+    float mx = -INFINITY;
+    int amax = 0;
+    for (int c = 0; c < nc; ++c) {
+      const float v = row[c] + p.bias[c];
+      row[c] = v;
+      if (v > mx) {
+        mx = v;
+        amax = c;
+      }
+    }
+    float se = 0.f;
+    for (int c = 0; c < nc; ++c) se += __expf(row[c] - mx);
+    const float inv = 1.f / se;
+    if (label >= 0) {
+      loss = -(row[label] - mx - __logf(se));
+      corr = amax == label;
+      for (int c = 0; c < nc; ++c)
+        row[c] = (__expf(row[c] - mx) * inv - (c == label ? 1.f : 0.f)) * p.xent_scale;
+    } else {
+      for (int c = 0; c < nc; ++c) row[c] = 0.f;
+    }
+    for (int c = nc; c < BN; ++c) row[c] = 0.f;
+  }
+  // block reduction of loss / correct (fixed order -> reproducible)
+  loss = wave_sum(loss);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) corr += __shfl_xor(corr, o, 64);
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    s_loss[wave] = loss;
+    s_corr[wave] = corr;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (p.loss_part) p.loss_part[m0 / BM] = (s_loss[0] + s_loss[1]) + (s_loss[2] + s_loss[3]);
+    const int cc = s_corr[0] + s_corr[1] + s_corr[2] + s_corr[3];
+    if (p.correct) p.correct[m0 / BM] = cc;
+  }
+}
+
+// Staged epilogue shared by the one-tile-per-workgroup kernels (gemm.hip, gemm_pp.hip):
+// accumulators (C/D map: col = lane&15, row = 4*(lane>>4) + r) -> fp32 LDS tile (EPI_ROWS rows at
+// a time) -> 16-byte row chunks with the fused bias / activation / activation-derivative /
+// split-K accumulation / colsum / softmax-CE work. The caller's LDS (>= C::CS_BYTES + 64) must be
+// free: every wave is past the main loop's last barrier.
+template <class C, bool OUT_F32>
+__device__ __forceinline__ void epilogue_staged(const GemmParams& p,
+                                                const f32x4_t (&acc)[C::FM][C::FN],
+                                                char LDS_AS* lds, int m0, int n0, int tm,
+                                                int split, int wave, int lane) {
+  constexpr int BM = C::BM, BN = C::BN, NT = C::NT, CS_LD = C::CS_LD;
+  (void)BM;
+  // ---- epilogue: accumulators -> LDS (fp32, EPI_ROWS at a time) -> 16-B row chunks -----------
+  float LDS_AS* cs = (float LDS_AS*)lds;
+  constexpr int CPR = BN / 8;
+  constexpr int ITER = C::EPI_ROWS * CPR / NT;
+  constexpr int RSTEP = NT / CPR;  // rows between a thread's consecutive iterations
+  // A thread's 8-column chunk is the same in every iteration and chunk (NT % CPR == 0): its
+  // bias is loaded ONCE, and the per-row global reads of a chunk (activation for the dgrad
+  // mask, previous slab for split-K accumulation) are all issued before the first is used --
+  // one L2 round trip per chunk instead of one per row (the per-row form serialised ~16
+  // round trips per 256x256 tile: half the tile's time at K = 832).
+  const int ccol = (threadIdx.x % CPR) * 8, crow = threadIdx.x / CPR;
+  const long gn = n0 + ccol;
+  bool xent = false;
+  if constexpr (!OUT_F32 && C::NW == 4 && C::CHUNKS == 1)
+    xent = p.xent_labels != nullptr;  // uniform
+  const bool col_ok = gn < p.N;  // partial edge tile: this thread's columns may be past N
+  float bias_r[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (p.bias && !xent && col_ok) {
+    const f32x4_t b0 = *(const f32x4_t*)(p.bias + gn);
+    const f32x4_t b1 = *(const f32x4_t*)(p.bias + gn + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      bias_r[e] = b0[e];
+      bias_r[e + 4] = b1[e];
+    }
+  }
+  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int chunk = 0; chunk < C::CHUNKS; ++chunk) {
+    if (chunk) __syncthreads();  // previous chunk's stores have read the staging tile
+    acc_to_lds<C>(acc, cs, chunk, wave, lane);
+    __syncthreads();
+    if constexpr (!OUT_F32 && C::NW == 4 && C::CHUNKS == 1) {
+      if (xent) {  // fused softmax-CE, one thread per row of the tile
+        xent_rows<C>(p, cs, m0);
+        __syncthreads();
+      }
+    }
+    const long gm0 = m0 + chunk * C::EPI_ROWS + crow;
+    [[maybe_unused]] bf16x8_t yv[ITER];
+    [[maybe_unused]] f32x4_t cp0[ITER], cp1[ITER];
+    if constexpr (OUT_F32) {
+      if (p.accumulate) {
+#pragma unroll
+        for (int it = 0; it < ITER; ++it) {
+          if (!col_ok || gm0 + it * RSTEP >= p.M) continue;
+          const float* c = (const float*)p.C + (long)split * p.c_split_stride +
+                           (gm0 + it * RSTEP) * p.ldc + gn;
+          cp0[it] = *(const f32x4_t*)c;
+          cp1[it] = *(const f32x4_t*)(c + 4);
+        }
+      }
+    } else {
+      if (p.aux && !xent) {
+#pragma unroll
+        for (int it = 0; it < ITER; ++it)
+          if (col_ok && gm0 + it * RSTEP < p.M)
+            yv[it] = *(const bf16x8_t*)(p.aux + (gm0 + it * RSTEP) * p.ld_aux + gn);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int row = crow + it * RSTEP;
+      const f32x4_t v0 = *(const f32x4_t LDS_AS*)(cs + row * CS_LD + ccol);
+      const f32x4_t v1 = *(const f32x4_t LDS_AS*)(cs + row * CS_LD + ccol + 4);
+      float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      const long gm = gm0 + it * RSTEP;
+      if (!col_ok || gm >= p.M) continue;  // outside a partial edge tile: not stored
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += bias_r[e];
+      if constexpr (OUT_F32) {
+        float* c = (float*)p.C + (long)split * p.c_split_stride + gm * p.ldc + gn;
+        if (!p.accumulate && p.act != ACT_LINEAR) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = act_fwd(v[e], p.act);
+        }
+        f32x4_t o0 = {v[0], v[1], v[2], v[3]}, o1 = {v[4], v[5], v[6], v[7]};
+        if (p.accumulate) {
+          o0 += cp0[it];
+          o1 += cp1[it];
+        }
+        *(f32x4_t*)c = o0;
+        *(f32x4_t*)(c + 4) = o1;
+      } else {
+        if (xent) {
+          // dz already computed in LDS
+        } else if (p.aux) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = act_bwd(v[e], bf2f((u16)yv[it][e]), p.act);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = act_fwd(v[e], p.act);
+        }
+        bf16x8_t o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const u16 h = f2bf(v[e]);
+          o[e] = (short)h;
+          csum[e] += bf2f(h);
+        }
+        *(bf16x8_t*)((u16*)p.C + gm * p.ldc + gn) = o;
+      }
+    }
+  }
+  if constexpr (!OUT_F32) {
+    if (p.colsum) {  // uniform across the block
+      __syncthreads();  // all reads of the staging tile are done
+      f32x4_t LDS_AS* red = (f32x4_t LDS_AS*)lds;
+      red[2 * threadIdx.x] = f32x4_t{csum[0], csum[1], csum[2], csum[3]};
+      red[2 * threadIdx.x + 1] = f32x4_t{csum[4], csum[5], csum[6], csum[7]};
+      __syncthreads();
+      if ((int)threadIdx.x < BN) {
+        const int col = threadIdx.x, cc = col >> 3, e = col & 7;
+        const float LDS_AS* rf = (const float LDS_AS*)lds;
+        float t = 0.f;
+#pragma unroll 4
+        for (int r = 0; r < NT / CPR; ++r) t += rf[(r * CPR + cc) * 8 + e];
+        if (n0 + col < p.N) p.colsum[(long)tm * p.ld_colsum + n0 + col] = t;
+      }
+    }
+  }
+}
+
+// Sum over the 16 lanes of a DPP row (lanes 16r .. 16r+15) in a fixed butterfly order.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);  // row_half_mirror
+  v += dpp_f<0x140>(v);  // row_mirror
+  return v;
+}
+
+__device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
+  return (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
+}
+
+// Register-direct epilogue for SWAPPED-operand accumulators (mfma(b, a): a lane's fragment
+// holds 4 consecutive output columns of one row): acc[i][j][e] = C[row0 + 16 i][col0 + 16 j + e]
+// with row0 = tile row + wave row offset + (lane & 15), col0 = ... + 4 * (lane >> 4). bf16
+// output pairs fragments j, j+1 with v_permlane16_swap into one 16-byte chunk per lane; fp32
+// output stores each fragment's 16 bytes. with_colsum: the bias-gradient column sums are
+// reduced across the WM wave rows in the ring slot the last k-step consumed (`rd` is the ring
+// read cursor after the loop) -- callers whose waves are not in lock step pass false.
+template <int FM, int FN, int BN, int SN, int WM, int NS, int STAGE, bool OUT_F32>
+__device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&acc)[FM][FN],
+                                                char LDS_AS* lds, int rd, int tm, int tn,
+                                                int split, int wm, int wn, int lane,
+                                                bool with_colsum) {
+  static_assert(FN % 2 == 0, "fragment pairs for the 16-byte epilogue stores");
+  const int frow = lane & 15, fg = lane >> 4;
+    // ---- epilogue straight from the accumulators ------------------------------------------
+    // acc[i][j][e] = C[row0 + 16 i][col0 + 16 j + e]
+    const int row0 = tm * (WM * 16 * FM) + wm * 16 * FM + frow;
+    const int col0 = tn * BN + wn * SN + 4 * fg;
+    if constexpr (OUT_F32) {
+      float* cbase = (float*)p.C + (long)split * p.c_split_stride + col0;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int row = row0 + 16 * i;
+        if (row >= p.M) continue;
+        float* crow = cbase + (long)row * p.ldc;  // columns 16 j: immediate offsets
+        f32x4_t v[FN];
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          v[j] = acc[i][j];
+          if (p.accumulate && col0 + 16 * j < p.N) v[j] += *(const f32x4_t*)(crow + 16 * j);
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          if (col0 + 16 * j >= p.N) continue;
+          if (p.bias) v[j] += *(const f32x4_t*)(p.bias + col0 + 16 * j);
+          if (!p.accumulate && p.act != ACT_LINEAR) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[j][e] = act_fwd(v[j][e], p.act);
+          }
+          *(f32x4_t*)(crow + 16 * j) = v[j];
+        }
+      }
+    } else {
+      const bool want_sum = with_colsum && p.colsum != nullptr;  // uniform
+      // store column after the 16-lane swap: even groups keep an 8-column half of fragment j,
+      // odd groups take one of fragment j+1 (see below)
+      const int scol0 = tn * BN + wn * SN + 16 * (fg & 1) + 8 * (fg >> 1);
+      // [WM][BN] colsum partials in the slot of the last consumed stage: no DMA targets it
+      // before the next k-step's barrier; wait until every wave has finished reading it
+      float LDS_AS* red = (float LDS_AS*)(lds + (rd == 0 ? NS - 1 : rd - 1) * STAGE);
+      if (want_sum) lds_barrier();
+#pragma unroll
+      for (int j = 0; j < FN; j += 2) {
+        const int c0 = col0 + 16 * j, c1 = c0 + 16;
+        f32x4_t b0 = {0.f, 0.f, 0.f, 0.f}, b1 = {0.f, 0.f, 0.f, 0.f};
+        if (p.bias) {
+          if (c0 < p.N) b0 = *(const f32x4_t*)(p.bias + c0);
+          if (c1 < p.N) b1 = *(const f32x4_t*)(p.bias + c1);
+        }
+        // activation values for the derivative, all issued before the first use
+        uint2 y0[FM], y1[FM];
+        if (p.aux) {
+          const u16* ya = p.aux + min(c0, p.N - 4);
+          const u16* yb = p.aux + min(c1, p.N - 4);
+#pragma unroll
+          for (int i = 0; i < FM; ++i) {
+            const long r = min(row0 + 16 * i, p.M - 1) * p.ld_aux;
+            y0[i] = *(const uint2*)(ya + r);
+            y1[i] = *(const uint2*)(yb + r);
+          }
+        }
+        float cs0[4] = {0.f, 0.f, 0.f, 0.f}, cs1[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int row = row0 + 16 * i;
+          float v0[4], v1[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v0[e] = acc[i][j][e] + b0[e];
+            v1[e] = acc[i][j + 1][e] + b1[e];
+          }
+          if (p.aux) {
+            const unsigned ya[2] = {y0[i].x, y0[i].y}, yb[2] = {y1[i].x, y1[i].y};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const unsigned sh = (e & 1) ? 0u : 16u;
+              v0[e] = act_bwd(v0[e], __uint_as_float((ya[e >> 1] << sh) & 0xffff0000u), p.act);
+              v1[e] = act_bwd(v1[e], __uint_as_float((yb[e >> 1] << sh) & 0xffff0000u), p.act);
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              v0[e] = act_fwd(v0[e], p.act);
+              v1[e] = act_fwd(v1[e], p.act);
+            }
+          }
+          const unsigned x0 = pack_bf16x2(v0[0], v0[1]), x1 = pack_bf16x2(v0[2], v0[3]);
+          const unsigned z0 = pack_bf16x2(v1[0], v1[1]), z1 = pack_bf16x2(v1[2], v1[3]);
+          if (want_sum && row < p.M) {  // sums of the STORED (bf16-rounded) values
+            cs0[0] += __uint_as_float(x0 << 16);
+            cs0[1] += __uint_as_float(x0 & 0xffff0000u);
+            cs0[2] += __uint_as_float(x1 << 16);
+            cs0[3] += __uint_as_float(x1 & 0xffff0000u);
+            cs1[0] += __uint_as_float(z0 << 16);
+            cs1[1] += __uint_as_float(z0 & 0xffff0000u);
+            cs1[2] += __uint_as_float(z1 << 16);
+            cs1[3] += __uint_as_float(z1 & 0xffff0000u);
+          }
+          // 16-lane half exchange (odd DPP rows of x <-> even rows of z). Afterwards group 0
+          // holds cols 0..7 of fragment j, group 1 cols 0..7 of j+1, group 2 cols 8..15 of j,
+          // group 3 cols 8..15 of j+1; in every group [0] = the chunk's low 4 columns.
+          const auto s0 = __builtin_amdgcn_permlane16_swap(x0, z0, false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(x1, z1, false, false);
+          const int scol = scol0 + 16 * j;
+          if (row < p.M && scol < p.N)
+            *(uint4*)((u16*)p.C + (long)row * p.ldc + scol) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+        }
+        if (want_sum) {  // this pair's column sums over the wave's rows -> LDS [wm][col]
+          f32x4_t r0, r1;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            r0[e] = row16_sum(cs0[e]);
+            r1[e] = row16_sum(cs1[e]);
+          }
+          if (frow == 0) {
+            float LDS_AS* d = red + wm * BN + wn * SN + 16 * j + 4 * fg;
+            *(f32x4_t LDS_AS*)d = r0;
+            *(f32x4_t LDS_AS*)(d + 16) = r1;
+          }
+        }
+      }
+      if (want_sum) {
+        lds_barrier();
+        if ((int)threadIdx.x < BN) {
+          const int col = threadIdx.x;
+          float tsum = 0.f;
+#pragma unroll
+          for (int r = 0; r < WM; ++r) tsum += red[r * BN + col];
+          if (tn * BN + col < p.N) p.colsum[(long)tm * p.ld_colsum + tn * BN + col] = tsum;
+        }
+        // the slot is restaged only after the next k-step's barrier
+      }
+    }
+}
+
 }  // namespace dnn

@@ -42,7 +42,8 @@ def _parse_stages(spec: str) -> dict:
     return out
 
 
-# LDS pipeline depth (2..4) per GEMM kind; see mma_tile in csrc/kernels/gemm.hip.
+# LDS pipeline depth (2..4) per GEMM kind; see mma_tile in csrc/kernels/gemm.hip. 8 selects the
+# ping-pong half-tile-streamed form of the 256x256 tile (csrc/kernels/gemm_pp.hip).
 STAGES = _parse_stages(os.environ.get("DNN_GEMM_STAGES", ""))
 
 
@@ -332,7 +333,8 @@ def linear_dgrad(dz, w, dx, y_prev=None, act_prev="linear", colsum=None):
     t = tuning.lookup("dgrad", M, K, N)
     return gemm(dz, w, dx, layout_a=KMAJ, layout_b=MNMAJ, M=M, N=K, K=N, aux=y_prev,
                 act=act_prev, tiles=dgrad_tiles(M, K, N), colsum=colsum,
-                stages=STAGES["dgrad"], persist=_persist("dgrad", t))
+                stages=STAGES["dgrad"] or (t or {}).get("stages", 0),
+                persist=_persist("dgrad", t))
 
 
 def linear_wgrad(dz, x, slabs, splits=1, accumulate=False):
@@ -345,7 +347,8 @@ def linear_wgrad(dz, x, slabs, splits=1, accumulate=False):
     tiles = (bm, bn) if s == splits else pick_tiles(N, K, splits)
     t = tuning.lookup("wgrad", N, K, R) if s == splits else None
     return gemm(dz, x, slabs, layout_a=MNMAJ, layout_b=MNMAJ, M=N, N=K, K=R, k_total=R,
-                accumulate=accumulate, splits=splits, tiles=tiles, stages=STAGES["wgrad"],
+                accumulate=accumulate, splits=splits, tiles=tiles,
+                stages=STAGES["wgrad"] or (t or {}).get("stages", 0),
                 persist=_persist("wgrad", t))
 
 
