@@ -129,6 +129,7 @@ def main(argv=None):
     t0 = time.perf_counter()
     for _ in range(a.steps):
         one_step()
+    tr.flush()  # the last step's deferred DP update belongs to the timed region
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:

@@ -225,6 +225,7 @@ def main(argv: Optional[list[str]] = None) -> int:
                          samples_per_s=(step - start_step) * rows * dp / (time.time() - t0))
             if a.checkpoint_dir and a.checkpoint_every and step % a.checkpoint_every == 0 \
                     and replica == 0:
+                tr.flush()  # deferred DP update of the last step
                 for st in tr.stages:
                     ckpt.save_stage(a.checkpoint_dir, st, step, spec, dist_)
             if a.steps and step >= a.steps:
@@ -242,6 +243,7 @@ def main(argv: Optional[list[str]] = None) -> int:
     if a.trace and prof.steps:
         prof.chrome_trace(a.trace.format(rank=rank))
         log.info(f"step profile: {StepProfiler.summarize(prof.steps[-1])}")
+    tr.flush()
     if a.checkpoint_dir and replica == 0:
         for st in tr.stages:
             ckpt.save_stage(a.checkpoint_dir, st, step, spec, dist_)

@@ -175,6 +175,53 @@ class StageParams:
                             step_dev=self.step_dev)
             ops.step_advance(self.step_dev)
 
+    def record_update_range(self, a: int, b: int, advance: bool) -> None:
+        """record_update over the flat element range [a, b) only (a DP bucket of whole layers);
+        the device step counter advances only when ``advance`` (once per step: the last range
+        of a split update)."""
+        self._device_scalars()
+        o = self.optim
+        sl = slice(a, b)
+        if o.name == "sgd":
+            ops.sgd_update(self.master[sl], self.grad[sl], self.state[0][sl] if self.state else None,
+                           self.shadow[sl], lr=o.lr, momentum=o.momentum,
+                           weight_decay=o.weight_decay, lr_dev=self.lr_dev)
+        else:
+            ops.adam_update(self.master[sl], self.grad[sl], self.state[0][sl], self.state[1][sl],
+                            self.shadow[sl], lr=o.lr, betas=o.betas, eps=o.eps,
+                            weight_decay=o.weight_decay,
+                            decoupled=o.decoupled or o.name == "adamw", lr_dev=self.lr_dev,
+                            step_dev=self.step_dev)
+        if advance and o.name != "sgd":
+            ops.step_advance(self.step_dev)
+
+    def update_range(self, a: int, b: int, lr: Optional[float], advance: bool) -> None:
+        """Optimizer update of the flat range [a, b) (see record_update_range); the host step
+        counter counts whole steps (advance=True)."""
+        o = self.optim
+        lr = o.lr if lr is None else lr
+        if self.device.type == "cuda":
+            self.set_lr(lr)
+            self.record_update_range(a, b, advance)
+        else:
+            sl = slice(a, b)
+            step = self.step_count + 1
+            if o.name == "sgd":
+                ops.sgd_update(self.master[sl], self.grad[sl],
+                               self.state[0][sl] if self.state else None, self.shadow[sl],
+                               lr=lr, momentum=o.momentum, weight_decay=o.weight_decay)
+            else:
+                ops.adam_update(self.master[sl], self.grad[sl], self.state[0][sl],
+                                self.state[1][sl], self.shadow[sl], lr=lr, betas=o.betas,
+                                eps=o.eps, weight_decay=o.weight_decay,
+                                decoupled=o.decoupled or o.name == "adamw", step=step)
+        if advance:
+            self.step_count += 1
+
+    def layers_range(self, a: int, b: int) -> tuple[int, int]:
+        """Flat [start, end) of layers a..b-1 (weights, biases and alignment padding)."""
+        return self.w_off[a], (self.w_off[b] if b < len(self.geoms) else self.numel)
+
     def optimizer_step(self, lr: Optional[float] = None) -> None:
         o = self.optim
         lr = o.lr if lr is None else lr
@@ -320,28 +367,42 @@ class Stage:
     def forward(self, j: int) -> None:
         if self._prog is not None and not self._recording:
             return self._replay(f"F{j}")
+        for i in range(len(self.geoms)):
+            self._forward_layer(j, i)
+
+    def forward_layers(self, j: int, i0: int, i1: int) -> None:
+        """Forward of micro-batch j through local layers [i0, i1) only (a DP step whose
+        update of later layers is deferred runs the earlier layers first)."""
+        if self._prog is not None and not self._recording:
+            self._prog.run([f"F{j}.L{i}" for i in range(i0, i1)],
+                           torch.cuda.current_stream(self.device).cuda_stream)
+            return
+        for i in range(i0, i1):
+            self._forward_layer(j, i)
+
+    def _forward_layer(self, j: int, i: int) -> None:
         r = self.rows_of(j)
         p = self.params
-        for i, g in enumerate(self.geoms):
-            x = self.input_of(i)[r]
-            y = self.acts[i][r]
-            if self.last and i == len(self.geoms) - 1 and self.fused_xent:
-                k = j * self.xent_per_micro
-                ops.linear_fwd_xent(x, p.wbf(i), p.b32(i), self.dz[i][r], self.labels[r],
-                                    self.n_cls, 1.0 / self.global_batch,
-                                    self.loss_part[k:k + self.xent_per_micro],
-                                    self.correct[k:k + self.xent_per_micro],
-                                    colsum=self._bpart(i, j))
-            elif self.last and i == len(self.geoms) - 1:
-                ops.linear_fwd(x, p.wbf(i), p.b32(i), y, act="linear")  # fp32 logits
-                k = j * self.xent_per_micro
-                ops.softmax_xent(y, self.labels[r], self.dz[i][r], self.n_cls,
-                                 1.0 / self.global_batch,
-                                 self.loss_part[k:k + self.xent_per_micro],
-                                 self.correct[k:k + self.xent_per_micro],
-                                 colsum=self._bpart(i, j))
-            else:
-                ops.linear_fwd(x, p.wbf(i), p.b32(i), y, act=g.spec.activation)
+        g = self.geoms[i]
+        x = self.input_of(i)[r]
+        y = self.acts[i][r]
+        if self.last and i == len(self.geoms) - 1 and self.fused_xent:
+            k = j * self.xent_per_micro
+            ops.linear_fwd_xent(x, p.wbf(i), p.b32(i), self.dz[i][r], self.labels[r],
+                                self.n_cls, 1.0 / self.global_batch,
+                                self.loss_part[k:k + self.xent_per_micro],
+                                self.correct[k:k + self.xent_per_micro],
+                                colsum=self._bpart(i, j))
+        elif self.last and i == len(self.geoms) - 1:
+            ops.linear_fwd(x, p.wbf(i), p.b32(i), y, act="linear")  # fp32 logits
+            k = j * self.xent_per_micro
+            ops.softmax_xent(y, self.labels[r], self.dz[i][r], self.n_cls,
+                             1.0 / self.global_batch,
+                             self.loss_part[k:k + self.xent_per_micro],
+                             self.correct[k:k + self.xent_per_micro],
+                             colsum=self._bpart(i, j))
+        else:
+            ops.linear_fwd(x, p.wbf(i), p.b32(i), y, act=g.spec.activation)
 
     def backward(self, j: int) -> None:
         """dgrad chain of micro-batch j; dZ of the last local layer must already be present."""
@@ -423,6 +484,21 @@ class Stage:
             self._reduce_jobs[key] = jobs
         ops.reduce_multi(jobs)  # one launch for every slab set and bias-partial set
 
+    def update_layers(self, a: int, b: int, lr: Optional[float] = None,
+                      advance: bool = True) -> None:
+        """Optimizer update of local layers [a, b) only (``advance``: this completes the
+        step's update -- Adam's step counter moves once per step)."""
+        if self._prog is not None and self._o_native and not self._recording:
+            p = self.params
+            p.set_lr(p.optim.lr if lr is None else lr)
+            segs = [f"O{a}-{b}"] + (["OADV"] if advance else [])
+            self._prog.run(segs, torch.cuda.current_stream(self.device).cuda_stream)
+            if advance:
+                p.step_count += 1
+            return
+        e0, e1 = self.params.layers_range(a, b)
+        self.params.update_range(e0, e1, lr, advance)
+
     def optimizer_step(self, lr: Optional[float] = None) -> None:
         if self._prog is not None and self._o_native and not self._recording:
             self.params.set_lr(self.params.optim.lr if lr is None else lr)
@@ -469,6 +545,10 @@ class Stage:
             for j in range(self.nm):
                 prog.mark(f"F{j}")
                 self.forward(j)
+            for j in range(self.nm):  # per-layer forward segments (deferred DP updates)
+                for i in range(len(self.geoms)):
+                    prog.mark(f"F{j}.L{i}")
+                    self._forward_layer(j, i)
             for j in range(self.nm):
                 prog.mark(f"B{j}")
                 self.backward(j)
@@ -489,6 +569,14 @@ class Stage:
             self.finalize_grads()
             prog.mark("O")
             self.params.record_update()
+            for a in range(L):  # split updates: every contiguous layer range, no step advance
+                for b in range(a + 1, L + 1):
+                    prog.mark(f"O{a}-{b}")
+                    e0, e1 = self.params.layers_range(a, b)
+                    self.params.record_update_range(e0, e1, advance=False)
+            prog.mark("OADV")
+            if self.params.optim.name != "sgd":
+                ops.step_advance(self.params.step_dev)
             self._o_native = True
         finally:
             nat.record_end()

@@ -207,7 +207,13 @@ class Trainer:
         for st in self.stages:
             st.params.load(weights[st.l0:st.l1], biases[st.l0:st.l1])
 
+    def flush(self) -> None:
+        """Complete every deferred data-parallel update (parallel/pipeline.dp_split): call
+        before reading weights or ending a timed region; training steps need not."""
+        self.executor.flush()
+
     def local_weights(self) -> dict[int, tuple[np.ndarray, np.ndarray]]:
+        self.flush()
         out = {}
         for st in self.stages:
             ws, bs = st.params.export()

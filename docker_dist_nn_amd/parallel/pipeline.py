@@ -43,16 +43,43 @@ class GradSync:
         self.world = world
         self._works = []
 
-    def launch(self, flat_grad, start: int, end: int) -> None:
+    def launch(self, flat_grad, start: int, end: int):
+        """Async all-reduce of flat_grad[start:end]; returns the work handle (also kept for
+        wait())."""
         if self.world <= 1:
-            return
-        self._works.append(dist.all_reduce(flat_grad[start:end], group=self.group,
-                                           async_op=True))
+            return None
+        w = dist.all_reduce(flat_grad[start:end], group=self.group, async_op=True)
+        self._works.append(w)
+        return w
 
     def wait(self) -> None:
         for w in self._works:
             w.wait()
         self._works.clear()
+
+    def wait_one(self, w) -> None:
+        """Order the current stream after one bucket's all-reduce (others stay in flight)."""
+        if w is not None:
+            w.wait()
+            self._works = [x for x in self._works if x is not w]
+
+
+def dp_split(st) -> int:
+    """Layer split s of a stage for the deferred data-parallel update: layers [0, s) are
+    all-reduced and updated at the end of the step; layers [s, L) are all-reduced behind the
+    NEXT step's forward of [0, s) and updated just before that forward reaches layer s. The
+    split puts about half the gradient bytes on each side (first layer range holding >= 50 %);
+    0 = no split (one layer)."""
+    L = len(st.geoms)
+    if L < 2:
+        return 0
+    size = [st.geoms[i].np_ * st.geoms[i].kp + st.geoms[i].np_ for i in range(L)]
+    tot, cum = sum(size), 0
+    for i in range(L - 1):
+        cum += size[i]
+        if 2 * cum >= tot:
+            return i + 1
+    return L - 1
 
 
 def dp_buckets(st, cap_bytes: int = 4 << 20) -> list[list[int]]:
@@ -100,6 +127,12 @@ class PipelineExecutor:
         # concurrent wgrad streams in native single-process plans (DNN_WGRAD_STREAMS)
         self.wgrad_streams = int(os.environ.get("DNN_WGRAD_STREAMS", "1"))
         self._side = None
+        # deferred data-parallel update (DNN_DP_DEFER=0 disables): see dp_split
+        self.defer = (grad_sync is not None and grad_sync.world > 1 and
+                      os.environ.get("DNN_DP_DEFER", "1") != "0")
+        self._split = {id(st): (dp_split(st) if self.defer else 0) for st in self.stages}
+        self._pending = {}  # id(stage) -> (work of layers [s, L), s)
+        self._works = {}    # id(stage) -> [work of [0, s), work of [s, L)] this step
 
     # ---------------------------------------------------------------------------------------
     def _run_op(self, st, op, j, next_op=None):
@@ -107,7 +140,16 @@ class PipelineExecutor:
             h(st, op, j)
         if op == "F":
             self.pipe.recv_fwd(st, j)
-            st.forward(j)
+            pend = self._pending.pop(id(st), None)
+            if pend is not None:  # first forward of the step: finish last step's update
+                work, sp = pend
+                L = len(st.geoms)
+                st.forward_layers(j, 0, sp)
+                self.grad_sync.wait_one(work)
+                st.update_layers(sp, L, self.lr_fn() if self.lr_fn else None, advance=True)
+                st.forward_layers(j, sp, L)
+            else:
+                st.forward(j)
             self.pipe.send_fwd(st, j)
         elif op == "B":
             self.pipe.recv_bwd(st, j)
@@ -119,6 +161,10 @@ class PipelineExecutor:
             else:
                 st.wgrad(j)
         elif op == "O":
+            sp = self._split.get(id(st), 0)
+            if sp:
+                self._optimizer_deferred(st, sp)
+                return self._after(st, op, j)
             if not getattr(st, "_finalized", False):
                 st.finalize_grads()
                 if self.grad_sync is not None:
@@ -127,8 +173,37 @@ class PipelineExecutor:
                 self.grad_sync.wait()
             st._finalized = False
             st.optimizer_step(self.lr_fn() if self.lr_fn else None)
+        self._after(st, op, j)
+
+    def _after(self, st, op, j):
         for h in self.hooks["after_op"]:
             h(st, op, j)
+
+    def _optimizer_deferred(self, st, sp: int) -> None:
+        """O with a deferred split: all-reduce [0, sp) must be done -> update it now; the
+        [sp, L) all-reduce stays in flight until the next step's first forward (or flush)."""
+        L = len(st.geoms)
+        works = self._works.pop(id(st), None)
+        if works is None or not getattr(st, "_finalized", False):  # per-micro W schedules
+            st.finalize_grads()
+            a0, a1 = st.params.layers_range(0, sp)
+            b0, b1 = st.params.layers_range(sp, L)
+            works = [self.grad_sync.launch(st.params.grad, a0, a1),
+                     self.grad_sync.launch(st.params.grad, b0, b1)]
+        st._finalized = False
+        self.grad_sync.wait_one(works[0])
+        st.update_layers(0, sp, self.lr_fn() if self.lr_fn else None, advance=False)
+        self._pending[id(st)] = (works[1], sp)
+
+    def flush(self) -> None:
+        """Apply every deferred update now (end of training / before reading weights)."""
+        for st in self.stages:
+            pend = self._pending.pop(id(st), None)
+            if pend is not None:
+                work, sp = pend
+                self.grad_sync.wait_one(work)
+                st.update_layers(sp, len(st.geoms), self.lr_fn() if self.lr_fn else None,
+                                 advance=True)
 
     def _wgrad_finalize_overlapped(self, st):
         """Batched W: per layer (last first) wgrad -> reduce -> async bucket all-reduce. Without
@@ -137,6 +212,20 @@ class PipelineExecutor:
             for i in range(len(st.geoms) - 1, -1, -1):
                 st.wgrad_layer(i)
             st.finalize_grads()
+            st._finalized = True
+            return
+        sp = self._split.get(id(st), 0)
+        if sp:  # deferred update: [0, sp) first (needed at O), then [sp, L)
+            L = len(st.geoms)
+            works = []
+            for a, b in ((0, sp), (sp, L)):
+                layers = list(range(a, b))
+                for i in reversed(layers):
+                    st.wgrad_layer(i)
+                st.finalize_grads(layers)
+                e0, e1 = st.params.layers_range(a, b)
+                works.append(self.grad_sync.launch(st.params.grad, e0, e1))
+            self._works[id(st)] = works
             st._finalized = True
             return
         for bucket in dp_buckets(st):

@@ -59,9 +59,14 @@ def _worker(rank, world, port, pp, dp, mb, nm, sched, steps, out_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("pp,dp,sched", [(2, 2, "1f1b"), (4, 1, "zb"), (1, 2, "1f1b"),
-                                         (2, 4, "1f1b"), (1, 8, "1f1b")])
-def test_distributed_matches_single_process(pp, dp, sched):
+@pytest.mark.parametrize("pp,dp,sched,defer", [(2, 2, "1f1b", "1"), (4, 1, "zb", "1"),
+                                               (1, 2, "1f1b", "1"), (1, 2, "1f1b", "0"),
+                                               (2, 2, "zb", "1"), (2, 4, "1f1b", "1"),
+                                               (1, 8, "1f1b", "1")])
+def test_distributed_matches_single_process(pp, dp, sched, defer, monkeypatch):
+    """defer = DNN_DP_DEFER: the data-parallel update of the later layers is applied behind
+    the next step's forward (parallel/pipeline.dp_split) or at the end of the step."""
+    monkeypatch.setenv("DNN_DP_DEFER", defer)
     mb, nm, steps = 128, 4, 3
     world = pp * dp
     with tempfile.TemporaryDirectory() as d:
@@ -104,3 +109,18 @@ def test_dp_buckets_cover_every_layer_once_in_contiguous_runs():
         for bk in b:
             assert bk == list(range(bk[0], bk[-1] + 1))  # one contiguous flat range each
     assert dp_buckets(stage([784, 512, 256, 128, 10])) == [[0], [1, 2, 3]]
+
+
+def test_dp_split_balances_gradient_bytes():
+    from types import SimpleNamespace as NS
+
+    from docker_dist_nn_amd.parallel.pipeline import dp_split
+
+    def stage(dims):
+        pad = lambda d: (d + 63) // 64 * 64  # noqa: E731
+        return NS(geoms=[NS(kp=pad(a), np_=pad(b)) for a, b in zip(dims, dims[1:])])
+
+    assert dp_split(stage([784, 512, 256, 128, 10])) == 1  # layer 0 holds 71 %
+    assert dp_split(stage([784] + [1024] * 7 + [10])) == 4
+    assert dp_split(stage([784, 8192, 8192, 10])) == 2
+    assert dp_split(stage([784, 10])) == 0  # one layer: nothing to defer
