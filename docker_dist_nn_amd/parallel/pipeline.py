@@ -246,6 +246,8 @@ class PipelineExecutor:
         from .comm import LoopbackPipe
 
         self._plan = None
+        if os.environ.get("DNN_NATIVE_PLAN", "1") == "0":  # per-op replay (A/B, host cost)
+            return None
         if not isinstance(self.pipe, LoopbackPipe) or self.grad_sync is not None or \
                 self.hooks["before_op"] or self.hooks["after_op"] or self.lr_fn is not None:
             return None
