@@ -68,9 +68,12 @@ PYBIND11_MODULE(_native, m) {
          int layout_a, int layout_b, int out_f32, int bm, int bn, int splits, uintptr_t stream,
          uintptr_t colsum, long ld_colsum, uintptr_t xent_labels, int n_cls, float xent_scale,
          uintptr_t loss_part, uintptr_t correct, int k_total, int stages, int group_m,
-         int persist) {
+         int persist, uintptr_t mask_out, uintptr_t mask_in, long ld_mask) {
         GemmParams p{};
         p.group_m = group_m;
+        p.mask_out = P<unsigned char>(mask_out);
+        p.mask_in = P<const unsigned char>(mask_in);
+        p.ld_mask = ld_mask;
         p.k_total = k_total;
         p.colsum = P<float>(colsum);
         p.ld_colsum = ld_colsum;
@@ -107,6 +110,8 @@ PYBIND11_MODULE(_native, m) {
               q.xent_labels = R.fix(q.xent_labels);
               q.loss_part = R.fix(q.loss_part);
               q.correct = R.fix(q.correct);
+              q.mask_out = R.fix(q.mask_out);
+              q.mask_in = R.fix(q.mask_in);
               return dnn::gemm_bf16(q, layout_a, layout_b, out_f32, bm, bn, splits, s, stages,
                                     persist);
             },
@@ -119,7 +124,8 @@ PYBIND11_MODULE(_native, m) {
       py::arg("stream"), py::arg("colsum") = 0, py::arg("ld_colsum") = 0,
       py::arg("xent_labels") = 0, py::arg("n_cls") = 0, py::arg("xent_scale") = 0.f,
       py::arg("loss_part") = 0, py::arg("correct") = 0, py::arg("k_total") = 0,
-      py::arg("stages") = 0, py::arg("group_m") = 0, py::arg("persist") = 0);
+      py::arg("stages") = 0, py::arg("group_m") = 0, py::arg("persist") = 0,
+      py::arg("mask_out") = 0, py::arg("mask_in") = 0, py::arg("ld_mask") = 0);
   m.def("gemm_default_stages", &dnn::default_stages);
 
   m.def("gemv_max_rows", []() { return dnn::GEMV_MAX_ROWS; });

@@ -45,6 +45,12 @@ struct GemmParams {
   int* correct;
   // raster order: row-tiles per group (<= 0: launcher default, 1 = row-major tiles)
   int group_m;
+  // 1-bit ReLU masks, [M][ld_mask] bytes, bit e of byte c = column 8c + e (bf16 output only):
+  // mask_out (forward, act = relu): bit = stored bf16 output > 0; mask_in (dgrad, act = relu,
+  // replaces aux): the derivative reads 1 bit per element instead of the 16-bit activation.
+  unsigned char* mask_out;
+  const unsigned char* mask_in;
+  long ld_mask;
 };
 
 // Returns 0 on success, a negative code when a shape/alignment precondition fails

@@ -337,6 +337,7 @@ __device__ __forceinline__ void epilogue_staged(const GemmParams& p,
     }
     const long gm0 = m0 + chunk * C::EPI_ROWS + crow;
     [[maybe_unused]] bf16x8_t yv[ITER];
+    [[maybe_unused]] unsigned mk[ITER];
     [[maybe_unused]] f32x4_t cp0[ITER], cp1[ITER];
     if constexpr (OUT_F32) {
       if (p.accumulate) {
@@ -355,6 +356,11 @@ __device__ __forceinline__ void epilogue_staged(const GemmParams& p,
         for (int it = 0; it < ITER; ++it)
           if (col_ok && gm0 + it * RSTEP < p.M)
             yv[it] = *(const bf16x8_t*)(p.aux + (gm0 + it * RSTEP) * p.ld_aux + gn);
+      } else if (p.mask_in) {
+#pragma unroll
+        for (int it = 0; it < ITER; ++it)
+          if (col_ok && gm0 + it * RSTEP < p.M)
+            mk[it] = p.mask_in[(gm0 + it * RSTEP) * p.ld_mask + (gn >> 3)];
       }
     }
 #pragma unroll
@@ -386,18 +392,24 @@ __device__ __forceinline__ void epilogue_staged(const GemmParams& p,
         } else if (p.aux) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = act_bwd(v[e], bf2f((u16)yv[it][e]), p.act);
+        } else if (p.mask_in) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = (mk[it] >> e) & 1u ? v[e] : 0.f;
         } else {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = act_fwd(v[e], p.act);
         }
         bf16x8_t o;
+        unsigned bits = 0;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const u16 h = f2bf(v[e]);
           o[e] = (short)h;
           csum[e] += bf2f(h);
+          bits |= (bf2f(h) > 0.f ? 1u : 0u) << e;
         }
         *(bf16x8_t*)((u16*)p.C + gm * p.ldc + gn) = o;
+        if (p.mask_out) p.mask_out[gm * p.ld_mask + (gn >> 3)] = (unsigned char)bits;
       }
     }
   }

@@ -168,11 +168,14 @@ def wgrad_config(M: int, N: int, K_total: int, max_splits: int = 48) -> tuple[in
 
 def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=None, aux=None,
          act=0, accumulate: bool = False, splits: int = 1, tiles: tuple[int, int] | None = None,
-         colsum=None, k_total: int = 0, stages: int = 0, group_m: int = 0, persist: int = 0):
+         colsum=None, k_total: int = 0, stages: int = 0, group_m: int = 0, persist: int = 0,
+         mask_out=None, mask_in=None):
     """C (+)= epilogue(A.B). See csrc/kernels/gemm.hpp for the layout/epilogue contract.
 
     ``persist`` != 0 runs the persistent-workgroup form with the register-direct epilogue
     (csrc/kernels/gemm_persist.hip): -1 = one resident round, > 0 = workgroup count.
+    ``mask_out`` / ``mask_in`` (uint8 [M][>= N/8], act = relu, GPU only): the forward writes the
+    1-bit ReLU mask of its stored output; a dgrad reads it instead of ``aux``.
 
     ``k_total`` > 0 selects uneven split-K over the full contraction length (K is ignored).
     ``colsum`` (bf16 output only): fp32 [M/bm][>=N] receives per-row-tile column sums of the
@@ -187,6 +190,12 @@ def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=
         if colsum.dtype != torch.float32 or colsum.dim() != 2 or colsum.stride(1) != 1 or \
                 colsum.shape[0] < -(-M // tiles[0]) or colsum.shape[1] < N:
             raise ValueError(f"colsum must be fp32 [{-(-M // tiles[0])}][>={N}] row-major")
+    if (mask_out is not None or mask_in is not None) and not a.is_cuda:
+        raise ValueError("relu bit masks are a GPU-path format (CPU uses aux)")
+    for m in (mask_out, mask_in):
+        if m is not None and (m.dtype != torch.uint8 or m.dim() != 2 or m.stride(1) != 1 or
+                              m.shape[0] < M or m.shape[1] < -(-N // 8)):
+            raise ValueError(f"relu mask must be uint8 [{M}][>={-(-N // 8)}] row-major")
     if not a.is_cuda:
         return ref.gemm(a, b, c, layout_a=layout_a, layout_b=layout_b, M=M, N=N, K=K, bias=bias,
                         aux=aux, act=act, accumulate=accumulate, splits=splits, colsum=colsum,
@@ -224,7 +233,10 @@ def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=
                        M, N, K, act, int(accumulate), layout_a, layout_b, int(out_f32), bm, bn,
                        splits, _stream(a), _p(colsum),
                        colsum.stride(0) if colsum is not None else 0, k_total=int(k_total),
-                       stages=int(stages), group_m=int(group_m), persist=int(persist))
+                       stages=int(stages), group_m=int(group_m), persist=int(persist),
+                       mask_out=_p(mask_out), mask_in=_p(mask_in),
+                       ld_mask=(mask_out if mask_out is not None else mask_in).stride(0)
+                       if (mask_out is not None or mask_in is not None) else 0)
     return c
 
 
@@ -254,9 +266,10 @@ def gemv(x, w, bias, y, act="relu"):
     return y
 
 
-def linear_fwd(x, w, bias, y, act="relu"):
+def linear_fwd(x, w, bias, y, act="relu", mask=None):
     """y[M][Np] = act(x[M][Kp] . w[Np][Kp]^T + bias). y bf16 (activation) or fp32 (logits).
-    M <= 8 rows (serving) runs the GEMV kernel; otherwise the MFMA GEMM."""
+    M <= 8 rows (serving) runs the GEMV kernel; otherwise the MFMA GEMM. ``mask`` (GPU, relu):
+    also write the 1-bit mask of y for the next dgrad."""
     M, K = x.shape
     N = w.shape[0]
     if not x.is_cuda:  # CPU reference: any row count
@@ -267,7 +280,7 @@ def linear_fwd(x, w, bias, y, act="relu"):
     tiles = tuple(t["tile"]) if t else pick_tiles(M, N)
     return gemm(x, w, y, layout_a=KMAJ, layout_b=KMAJ, M=M, N=N, K=K, bias=bias, act=act,
                 tiles=tiles, stages=STAGES["fwd"] or (t or {}).get("stages", 0),
-                persist=_persist("fwd", t))
+                persist=0 if mask is not None else _persist("fwd", t), mask_out=mask)
 
 
 def xent_tiles(M: int, N: int) -> tuple[int, int]:
@@ -322,19 +335,22 @@ def dgrad_tiles(M: int, K: int, N: int = 0) -> tuple[int, int]:
     return tuple(t["tile"]) if t else pick_tiles(M, K, 1)
 
 
-def linear_dgrad(dz, w, dx, y_prev=None, act_prev="linear", colsum=None):
+def linear_dgrad(dz, w, dx, y_prev=None, act_prev="linear", colsum=None, mask_prev=None):
     """dx[M][Kp] = (dz[M][Np] . w[Np][Kp]) * act_prev'(y_prev) (mask fused in the epilogue).
     ``colsum`` [M/bm][Kp] receives the bias-gradient partials of the PREVIOUS layer (column
     sums of dx), fused in the same epilogue."""
     M, N = dz.shape
     K = w.shape[1]
-    if y_prev is None:
+    if mask_prev is not None:  # relu derivative from the forward's 1-bit mask
+        y_prev, act_prev = None, "relu"
+    elif y_prev is None:
         act_prev = "linear"
     t = tuning.lookup("dgrad", M, K, N)
     return gemm(dz, w, dx, layout_a=KMAJ, layout_b=MNMAJ, M=M, N=K, K=N, aux=y_prev,
                 act=act_prev, tiles=dgrad_tiles(M, K, N), colsum=colsum,
                 stages=STAGES["dgrad"] or (t or {}).get("stages", 0),
-                persist=_persist("dgrad", t))
+                persist=0 if mask_prev is not None else _persist("dgrad", t),
+                mask_in=mask_prev)
 
 
 def linear_wgrad(dz, x, slabs, splits=1, accumulate=False):
