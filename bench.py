@@ -95,6 +95,13 @@ def main(argv=None):
         raise SystemExit(f"batch {rows} must split into micro-batches of a multiple of 64")
     if world > 1:
         mesh = build_mesh(plan.pp, plan.dp)
+        # communicator set-up (RCCL rings/channels) happens at a group's first collective:
+        # do it here, outside the W warm-up steps and the timed region
+        t = torch.ones(1024, device=dev)
+        if mesh.dp_group is not None:
+            torch.distributed.all_reduce(t, group=mesh.dp_group)
+        torch.distributed.all_reduce(t)
+        torch.cuda.synchronize(dev)
 
     tr = Trainer(spec, micro_batch=mb, num_micro=nm, distribution=plan.distribution,
                  pp=plan.pp, dp=plan.dp, schedule=a.schedule,
