@@ -490,13 +490,19 @@ PYBIND11_MODULE(_native, m) {
         char* buf;
         py::ssize_t n;
         PYBIND11_BYTES_AS_STRING_AND_SIZE(b.ptr(), &buf, &n);
-        dnn::DecodedMatrix M;
+        const uint8_t* u = reinterpret_cast<const uint8_t*>(buf);
+        long rows = 0, cols = 0;
         {
           py::gil_scoped_release nogil;
-          M = dnn::decode_matrix(reinterpret_cast<const uint8_t*>(buf), (size_t)n);
+          dnn::scan_matrix(u, (size_t)n, &rows, &cols);
         }
-        py::array_t<double> a({(py::ssize_t)M.rows, (py::ssize_t)M.cols});
-        if (!M.data.empty()) std::memcpy(a.mutable_data(), M.data.data(), M.data.size() * 8);
+        // decode straight into the numpy array: no intermediate vector, one copy of the data
+        py::array_t<double> a({(py::ssize_t)rows, (py::ssize_t)cols});
+        double* out = a.mutable_data();
+        if (rows && cols) {
+          py::gil_scoped_release nogil;
+          dnn::fill_matrix(u, (size_t)n, out, cols);
+        }
         return a;
       },
       py::arg("data"), "Matrix wire bytes -> float64 [rows][cols]");
@@ -504,12 +510,17 @@ PYBIND11_MODULE(_native, m) {
       "encode_matrix",
       [](py::array_t<double, py::array::c_style | py::array::forcecast> a) {
         if (a.ndim() != 2) throw std::invalid_argument("encode_matrix needs a 2-D array");
-        std::string s;
+        const long rows = (long)a.shape(0), cols = (long)a.shape(1);
+        const size_t sz = dnn::encoded_size(rows, cols);
+        // the bytes object is the output buffer: the wire bytes are written once
+        PyObject* o = PyBytes_FromStringAndSize(nullptr, (py::ssize_t)sz);
+        if (!o) throw py::error_already_set();
+        char* dst = PyBytes_AS_STRING(o);
         {
           py::gil_scoped_release nogil;
-          s = dnn::encode_matrix(a.data(), (long)a.shape(0), (long)a.shape(1));
+          dnn::encode_matrix_into(a.data(), rows, cols, dst);
         }
-        return py::bytes(s);
+        return py::reinterpret_steal<py::bytes>(o);
       },
       py::arg("array"), "float64 [rows][cols] -> Matrix wire bytes");
 

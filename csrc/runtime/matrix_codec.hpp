@@ -23,6 +23,15 @@ struct DecodedMatrix {
 
 DecodedMatrix decode_matrix(const uint8_t* buf, size_t n);
 std::string encode_matrix(const double* data, long rows, long cols);
+
+// Zero-intermediate forms (the bindings write straight into the numpy array / bytes object):
+// scan_matrix validates the wire bytes and returns the shape (ragged rows throw
+// std::invalid_argument); fill_matrix then copies the values of the same bytes into
+// out[rows][cols]. encoded_size + encode_matrix_into write the wire bytes into a caller buffer.
+void scan_matrix(const uint8_t* buf, size_t n, long* rows, long* cols);
+void fill_matrix(const uint8_t* buf, size_t n, double* out, long cols);
+size_t encoded_size(long rows, long cols);
+void encode_matrix_into(const double* data, long rows, long cols, char* dst);
 std::string encode_matrix_f32(const float* data, long rows, long cols, long ld);
 
 }  // namespace dnn
