@@ -20,6 +20,7 @@
 #include "runtime/graph.hpp"
 #include "runtime/json_weights.hpp"
 #include "runtime/matrix_codec.hpp"
+#include "runtime/p2p.hpp"
 #include "runtime/program.hpp"
 #include "runtime/schedule.hpp"
 
@@ -533,6 +534,40 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("captured", &dnn::GraphExec::captured)
       .def_property_readonly("num_nodes", &dnn::GraphExec::num_nodes)
       .def("reset", &dnn::GraphExec::reset);
+  // ---- runtime: xGMI peer-to-peer pipeline transport (csrc/runtime/p2p.hpp) ---------------
+  m.def(
+      "ipc_export",
+      [](uintptr_t ptr) {
+        auto r = dnn::ipc_export(reinterpret_cast<void*>(ptr));
+        return py::make_tuple(py::bytes(r.first), r.second);
+      },
+      py::arg("ptr"), "device pointer -> (IPC handle bytes, offset in its allocation)");
+  m.def(
+      "ipc_import",
+      [](py::bytes h, uint64_t off) {
+        return reinterpret_cast<uintptr_t>(dnn::ipc_import(std::string(h), off));
+      },
+      py::arg("handle"), py::arg("offset"));
+  m.def("ipc_close_all", &dnn::ipc_close_all);
+  m.def(
+      "copy_async",
+      [](uintptr_t dst, uintptr_t src, size_t n, uintptr_t s) {
+        dnn::copy_async(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), n,
+                        S(s));
+      },
+      py::arg("dst"), py::arg("src"), py::arg("nbytes"), py::arg("stream"));
+  m.def(
+      "signal_u32",
+      [](uintptr_t s, uintptr_t flag, uint32_t v) {
+        dnn::signal_u32(S(s), reinterpret_cast<void*>(flag), v);
+      },
+      py::arg("stream"), py::arg("flag"), py::arg("value"));
+  m.def(
+      "wait_geq_u32",
+      [](uintptr_t s, uintptr_t flag, uint32_t v) {
+        dnn::wait_geq_u32(S(s), reinterpret_cast<void*>(flag), v);
+      },
+      py::arg("stream"), py::arg("flag"), py::arg("value"));
   m.def("device_sync", []() {
     hipError_t e = hipDeviceSynchronize();
     if (e != hipSuccess) throw std::runtime_error(hipGetErrorString(e));

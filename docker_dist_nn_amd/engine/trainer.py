@@ -25,7 +25,7 @@ import numpy as np
 import torch
 
 from ..models.mlp import MLPSpec
-from ..parallel.comm import DistPipe, LoopbackPipe
+from ..parallel.comm import DistPipe, IpcPipe, LoopbackPipe
 from ..parallel.groups import Mesh
 from ..parallel.pipeline import GradSync, PipelineExecutor
 from ..partition import balanced_distribution, plan_stages
@@ -80,7 +80,10 @@ class Trainer:
             st = mk(self.plans[mesh.stage])
             st.params.init_default(seed)
             self.stages = [st]
-            self.pipe = DistPipe(mesh, st)
+            # DNN_PIPE=ipc: xGMI peer writes into IPC-mapped buffers instead of RCCL P2P
+            use_ipc = (os.environ.get("DNN_PIPE", "rccl") == "ipc" and
+                       self.device.type == "cuda" and mesh.pp > 1)
+            self.pipe = IpcPipe(mesh, st) if use_ipc else DistPipe(mesh, st)
             ids = [mesh.stage]
             sync = GradSync(mesh.dp_group, mesh.dp) if mesh.dp > 1 else None
         self.executor = PipelineExecutor(self.stages, self.pipe, schedule, pp, ids, sync)

@@ -12,6 +12,11 @@ pre-allocated step buffer, moved by:
   groups.py), so data lands as soon as the producer sends it. With ``gloo`` it runs on CPU
   tensors (tests) or stages GPU tensors through host memory (``staged=True``, one-GPU
   multi-rank rehearsals).
+* :class:`IpcPipe` -- xGMI peer writes (``DNN_PIPE=ipc``): each rank maps its neighbours'
+  receive buffers and flag words through IPC handles (csrc/runtime/p2p.cpp). A hop is one
+  device-to-device copy straight into the consumer's input rows plus a stream-ordered flag
+  write; the consumer's stream waits on the flag (hipStreamWaitValue32) -- no RCCL kernel, no
+  host round trip.
 * :class:`LoopbackPipe` -- all stages in one process on one device: the next stage's input
   buffer IS the previous stage's output buffer (and likewise for gradients), so a hop costs
   nothing; used to run/verify S-stage pipelines on a single GPU or CPU.
@@ -136,3 +141,108 @@ class DistPipe:
         self._sends.clear()
         if self._recv_f or self._recv_b:
             raise RuntimeError("step ended with unconsumed pipeline receives")
+
+
+class IpcPipe:
+    """Pipeline hops as direct writes into IPC-mapped peer buffers (one stage per rank).
+
+    Per rank, a small int32 flag block: ``f[j]`` (activation j of step s has landed in my
+    input rows), ``b[j]`` (gradient j has landed in my grad_out rows), ``ack_f`` / ``ack_b``
+    (my consumer / producer finished reading the buffers I write into, for step s). Flags
+    carry the step sequence number s = 1, 2, ... so nothing is ever reset:
+
+      send_fwd(j): wait ack_f >= s-1 (consumer done with step s-1) -> copy output rows j into
+                   the consumer's x_in rows j -> consumer.f[j] = s
+      recv_fwd(j): wait f[j] >= s
+      send_bwd / recv_bwd: the same with dx_send -> producer's grad_out and b[j]
+      end_step:   producer.ack_f... i.e. tell the previous rank its writes into my x_in may
+                  resume (prev.ack_f = s) and the next rank likewise (next.ack_b = s)
+
+    All waits/signals are stream-ordered on the compute stream: the signal follows the copy,
+    the acks follow every kernel of the step that reads the buffers (wgrad included)."""
+
+    def __init__(self, mesh: Mesh, stage):
+        import torch.distributed as dist
+
+        from ..utils.native import native
+
+        if stage.device.type != "cuda":
+            raise ValueError("IpcPipe needs GPU stages")
+        self.n = native()
+        self.mesh = mesh
+        self.stage = stage
+        nm = stage.nm
+        self.nm = nm
+        # flag block: [f[0..nm), b[0..nm), ack_f, ack_b]
+        self.flags = torch.zeros(2 * nm + 2, dtype=torch.int32, device=stage.device)
+        torch.cuda.synchronize(stage.device)
+        mine = {"x_in": self.n.ipc_export(stage.x_in.data_ptr()),
+                "grad_out": self.n.ipc_export(stage.grad_out.data_ptr()),
+                "flags": self.n.ipc_export(self.flags.data_ptr())}
+        everyone = [None] * dist.get_world_size()
+        dist.all_gather_object(everyone, mine)
+        self.seq = 0
+        self.prev = self._peer(everyone, mesh.prev_rank)
+        self.next = self._peer(everyone, mesh.next_rank)
+        # destination rows have the source's width: my output == the consumer's input, my
+        # dx_send == the producer's grad_out
+        self.row_bytes_f = stage.output.stride(0) * stage.output.element_size()
+        self.row_bytes_b = (stage.dx_send.stride(0) * stage.dx_send.element_size()
+                            if stage.dx_send is not None else 0)
+
+    def _peer(self, everyone, rank):
+        if rank is None:
+            return None
+        d = everyone[rank]
+        imp = lambda k: self.n.ipc_import(*d[k])  # noqa: E731
+        return {"x_in": imp("x_in"), "grad_out": imp("grad_out"), "flags": imp("flags")}
+
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.stage.device).cuda_stream
+
+    def _flag(self, base: int, i: int) -> int:
+        return base + 4 * i
+
+    def begin_step(self):
+        self.seq += 1
+
+    def recv_fwd(self, stage, j):
+        if self.prev is not None:
+            self.n.wait_geq_u32(self._stream(), self._flag(self.flags.data_ptr(), j), self.seq)
+
+    def send_fwd(self, stage, j):
+        if self.next is None:
+            return
+        s, nm = self._stream(), self.nm
+        if j == 0:  # the consumer finished every read of its x_in for the previous step
+            self.n.wait_geq_u32(s, self._flag(self.flags.data_ptr(), 2 * nm), self.seq - 1)
+        r = stage.rows_of(j)
+        src = stage.output[r]
+        off = r.start * self.row_bytes_f
+        self.n.copy_async(self.next["x_in"] + off, src.data_ptr(), src.numel() * src.element_size(), s)
+        self.n.signal_u32(s, self._flag(self.next["flags"], j), self.seq)
+
+    def recv_bwd(self, stage, j):
+        if self.next is not None:
+            self.n.wait_geq_u32(self._stream(), self._flag(self.flags.data_ptr(), self.nm + j),
+                                self.seq)
+
+    def send_bwd(self, stage, j):
+        if self.prev is None:
+            return
+        s, nm = self._stream(), self.nm
+        if j == 0:
+            self.n.wait_geq_u32(s, self._flag(self.flags.data_ptr(), 2 * nm + 1), self.seq - 1)
+        r = stage.rows_of(j)
+        src = stage.dx_send[r]
+        off = r.start * self.row_bytes_b
+        self.n.copy_async(self.prev["grad_out"] + off, src.data_ptr(),
+                          src.numel() * src.element_size(), s)
+        self.n.signal_u32(s, self._flag(self.prev["flags"], nm + j), self.seq)
+
+    def end_step(self):
+        s, nm = self._stream(), self.nm
+        if self.prev is not None:  # my x_in is free for the previous rank's next step
+            self.n.signal_u32(s, self._flag(self.prev["flags"], 2 * nm), self.seq)
+        if self.next is not None:  # my grad_out is free for the next rank's next step
+            self.n.signal_u32(s, self._flag(self.next["flags"], 2 * nm + 1), self.seq)
