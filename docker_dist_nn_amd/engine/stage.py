@@ -498,6 +498,35 @@ class Stage:
             self._reduce_jobs[key] = jobs
         ops.reduce_multi(jobs)  # one launch for every slab set and bias-partial set
 
+    def update_then_forward(self, j: int, s: int, lr: Optional[float] = None) -> None:
+        """Deferred DP update of layers [s, L) (completing the step: advance) followed by the
+        forward of micro-batch j through [s, L) -- ONE native call when recorded."""
+        L = len(self.geoms)
+        if self._prog is not None and self._o_native and not self._recording:
+            p = self.params
+            p.set_lr(p.optim.lr if lr is None else lr)
+            self._prog.run([f"O{s}-{L}", "OADV"] + [f"F{j}.L{i}" for i in range(s, L)],
+                           torch.cuda.current_stream(self.device).cuda_stream)
+            p.step_count += 1
+            return
+        self.update_layers(s, L, lr, advance=True)
+        self.forward_layers(j, s, L)
+
+    def wgrad_finalize(self, layers: Sequence[int]) -> None:
+        """Batched wgrad of ``layers`` (in the given order) + their gradient reduction: one
+        native call when recorded (a DP bucket)."""
+        ls = list(layers)
+        lo, hi = min(ls), max(ls)
+        if (self._prog is not None and not self._recording and self._has_w and
+                sorted(ls) == list(range(lo, hi + 1))):
+            fin = f"FIN{lo}" if lo == hi else f"FIN{lo}-{hi}"
+            self._prog.run([f"W{i}" for i in ls] + [fin],
+                           torch.cuda.current_stream(self.device).cuda_stream)
+            return
+        for i in ls:
+            self.wgrad_layer(i)
+        self.finalize_grads(sorted(ls))
+
     def update_layers(self, a: int, b: int, lr: Optional[float] = None,
                       advance: bool = True) -> None:
         """Optimizer update of local layers [a, b) only (``advance``: this completes the

@@ -143,11 +143,9 @@ class PipelineExecutor:
             pend = self._pending.pop(id(st), None)
             if pend is not None:  # first forward of the step: finish last step's update
                 work, sp = pend
-                L = len(st.geoms)
                 st.forward_layers(j, 0, sp)
                 self.grad_sync.wait_one(work)
-                st.update_layers(sp, L, self.lr_fn() if self.lr_fn else None, advance=True)
-                st.forward_layers(j, sp, L)
+                st.update_then_forward(j, sp, self.lr_fn() if self.lr_fn else None)
             else:
                 st.forward(j)
             self.pipe.send_fwd(st, j)
@@ -219,10 +217,7 @@ class PipelineExecutor:
             L = len(st.geoms)
             works = []
             for a, b in ((0, sp), (sp, L)):
-                layers = list(range(a, b))
-                for i in reversed(layers):
-                    st.wgrad_layer(i)
-                st.finalize_grads(layers)
+                st.wgrad_finalize(list(reversed(range(a, b))))  # one native call per bucket
                 e0, e1 = st.params.layers_range(a, b)
                 works.append(self.grad_sync.launch(st.params.grad, e0, e1))
             self._works[id(st)] = works
