@@ -234,28 +234,40 @@ PYBIND11_MODULE(_native, m) {
   // launches
   m.def("reduce_multi", [](const std::vector<std::tuple<uintptr_t, long, int, long, uintptr_t,
                                                         float, int>>& jobs,
-                           uintptr_t stream) {
+                           uintptr_t stream, uintptr_t grad_base, uintptr_t master,
+                           uintptr_t mom, uintptr_t shadow, float lr, float mu, float wd,
+                           uintptr_t lr_dev) {
     std::vector<dnn::ReduceJob> J;
     J.reserve(jobs.size());
     for (const auto& t : jobs)
       J.push_back({P<const float>(std::get<0>(t)), std::get<1>(t), std::get<3>(t),
                    P<float>(std::get<4>(t)), std::get<2>(t), std::get<5>(t), std::get<6>(t)});
+    const bool fused = master != 0;
+    dnn::FusedSgd sg{P<const float>(grad_base), P<float>(master), P<float>(mom),
+                     P<uint16_t>(shadow), lr, mu, wd, P<const float>(lr_dev)};
     for (size_t k = 0; k < J.size(); k += dnn::REDUCE_MAX_JOBS) {
       const int n = (int)std::min<size_t>(dnn::REDUCE_MAX_JOBS, J.size() - k);
       std::vector<dnn::ReduceJob> part(J.begin() + k, J.begin() + k + n);
       launch(
           "reduce_multi",
-          [part](hipStream_t s, const dnn::Program& R) mutable {
+          [part, fused, sg](hipStream_t s, const dnn::Program& R) mutable {
             std::vector<dnn::ReduceJob> q = part;
             for (auto& j : q) {
               j.src = R.fix(j.src);
               j.out = R.fix(j.out);
             }
-            return dnn::reduce_multi(q.data(), (int)q.size(), s);
+            dnn::FusedSgd f = sg;
+            f.grad_base = R.fix(f.grad_base);
+            f.master = R.fix(f.master);
+            f.mom = R.fix(f.mom);
+            f.shadow = R.fix(f.shadow);
+            return dnn::reduce_multi(q.data(), (int)q.size(), s, fused ? &f : nullptr);
           },
           stream);
     }
-  });
+  }, py::arg("jobs"), py::arg("stream"), py::arg("grad_base") = 0, py::arg("master") = 0,
+     py::arg("mom") = 0, py::arg("shadow") = 0, py::arg("lr") = 0.f, py::arg("mu") = 0.f,
+     py::arg("wd") = 0.f, py::arg("lr_dev") = 0);
   m.def(
       "sgd_update",
       [](uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t shadow, long n, float lr, float mu,

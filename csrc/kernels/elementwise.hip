@@ -332,8 +332,30 @@ int reduce_slabs(const float* src, long stride, int n_src, long n, float scale, 
 // job runs the TX x TY scheme of reduce_slabs_kernel with its own TY (same fixed summation
 // order, so results are bitwise identical to reduce_slabs).
 // ------------------------------------------------------------------------------------------
+// One SGD step on 4 consecutive parameters (shared by sgd_kernel and the fused reduce).
+__device__ __forceinline__ void sgd4(float* __restrict__ p, f32x4_t gv, float* __restrict__ mom,
+                                     u16* __restrict__ shadow, float lr, float mu, float wd) {
+  f32x4_t pv = *(const f32x4_t*)p;
+  gv += wd * pv;
+  if (mom) {
+    f32x4_t m = *(const f32x4_t*)mom;
+    m = mu * m + gv;
+    *(f32x4_t*)mom = m;
+    gv = m;
+  }
+  pv -= lr * gv;
+  *(f32x4_t*)p = pv;
+  if (shadow) {
+    bf16x4_t o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (short)f2bf(pv[e]);
+    *(bf16x4_t*)shadow = o;
+  }
+}
+
 template <int TY>
-__device__ __forceinline__ void reduce_block(const ReduceJob& jb, long blk, f32x4_t LDS_AS* red) {
+__device__ __forceinline__ void reduce_block(const ReduceJob& jb, long blk, f32x4_t LDS_AS* red,
+                                             const FusedSgd& sg) {
   constexpr int TX = 256 / TY;
   const int tx = threadIdx.x % TX, ty = threadIdx.x / TX;
   const long i = blk * TX + tx;
@@ -361,12 +383,18 @@ __device__ __forceinline__ void reduce_block(const ReduceJob& jb, long blk, f32x
     t *= jb.scale;
     if (jb.accumulate) t += *(const f32x4_t*)(jb.out + i * 4);
     *(f32x4_t*)(jb.out + i * 4) = t;
+    if (sg.master) {
+      const long off = (jb.out + i * 4) - sg.grad_base;
+      const float lr = sg.lr_dev ? *sg.lr_dev : sg.lr;
+      sgd4(sg.master + off, t, sg.mom ? sg.mom + off : nullptr,
+           sg.shadow ? sg.shadow + off : nullptr, lr, sg.mu, sg.wd);
+    }
   }
 }
 
 static __host__ __device__ int reduce_ty(int n_src) { return n_src >= 16 ? 16 : n_src >= 4 ? 4 : 1; }
 
-__global__ __launch_bounds__(256) void reduce_multi_kernel(ReduceJobs jobs) {
+__global__ __launch_bounds__(256) void reduce_multi_kernel(ReduceJobs jobs, FusedSgd sg) {
   __shared__ f32x4_t red_s[256];
   f32x4_t LDS_AS* red = (f32x4_t LDS_AS*)red_s;
   int j = 0;
@@ -374,13 +402,13 @@ __global__ __launch_bounds__(256) void reduce_multi_kernel(ReduceJobs jobs) {
   const ReduceJob& jb = jobs.job[j];
   const long blk = (long)blockIdx.x - jobs.block_start[j];
   switch (reduce_ty(jb.n_src)) {
-    case 16: reduce_block<16>(jb, blk, red); break;
-    case 4: reduce_block<4>(jb, blk, red); break;
-    default: reduce_block<1>(jb, blk, red); break;
+    case 16: reduce_block<16>(jb, blk, red, sg); break;
+    case 4: reduce_block<4>(jb, blk, red, sg); break;
+    default: reduce_block<1>(jb, blk, red, sg); break;
   }
 }
 
-int reduce_multi(const ReduceJob* job, int n_jobs, hipStream_t stream) {
+int reduce_multi(const ReduceJob* job, int n_jobs, hipStream_t stream, const FusedSgd* sgd) {
   if (n_jobs <= 0 || n_jobs > REDUCE_MAX_JOBS) return -1;
   ReduceJobs J{};
   J.n_jobs = n_jobs;
@@ -397,7 +425,13 @@ int reduce_multi(const ReduceJob* job, int n_jobs, hipStream_t stream) {
     blocks += (int)b;
   }
   J.block_start[n_jobs] = blocks;
-  hipLaunchKernelGGL(reduce_multi_kernel, dim3(blocks), dim3(256), 0, stream, J);
+  FusedSgd sg{};
+  if (sgd) {
+    sg = *sgd;
+    for (int k = 0; k < n_jobs; ++k)  // every output must lie in the flat gradient, 16-B aligned
+      if (job[k].out < sg.grad_base || ((job[k].out - sg.grad_base) & 3)) return -1;
+  }
+  hipLaunchKernelGGL(reduce_multi_kernel, dim3(blocks), dim3(256), 0, stream, J, sg);
   return hipGetLastError() == hipSuccess ? 0 : -9;
 }
 
@@ -412,25 +446,9 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
                                                   long n4, float lr, float mu, float wd,
                                                   const float* __restrict__ lr_dev) {
   if (lr_dev) lr = *lr_dev;
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
-    f32x4_t pv = *(const f32x4_t*)(p + i * 4);
-    f32x4_t gv = *(const f32x4_t*)(g + i * 4);
-    gv += wd * pv;
-    if (mom) {
-      f32x4_t m = *(const f32x4_t*)(mom + i * 4);
-      m = mu * m + gv;
-      *(f32x4_t*)(mom + i * 4) = m;
-      gv = m;
-    }
-    pv -= lr * gv;
-    *(f32x4_t*)(p + i * 4) = pv;
-    if (shadow) {
-      bf16x4_t o;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = (short)f2bf(pv[e]);
-      *(bf16x4_t*)(shadow + i * 4) = o;
-    }
-  }
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256)
+    sgd4(p + i * 4, *(const f32x4_t*)(g + i * 4), mom ? mom + i * 4 : nullptr,
+         shadow ? shadow + i * 4 : nullptr, lr, mu, wd);
 }
 
 int sgd_update(float* p, const float* g, float* mom, uint16_t* shadow, long n, float lr, float mu,

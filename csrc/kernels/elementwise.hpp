@@ -34,8 +34,21 @@ struct ReduceJobs {  // passed by value as the kernel argument
   int block_start[REDUCE_MAX_JOBS + 1];
   int n_jobs;
 };
+// Optional SGD fused into reduce_multi: every reduced gradient element out[k] (an element of
+// the flat gradient starting at grad_base) also updates master / momentum / bf16 shadow at the
+// same flat offset -- bitwise identical to reduce_multi followed by sgd_update over the
+// covered elements (one launch and one gradient round trip fewer per step).
+struct FusedSgd {
+  const float* grad_base;
+  float* master;
+  float* mom;        // nullptr: no momentum
+  uint16_t* shadow;  // nullptr: no bf16 refresh
+  float lr, mu, wd;
+  const float* lr_dev;  // optional device-resident learning rate
+};
 // All jobs in one launch, each bitwise identical to reduce_slabs on the same inputs.
-int reduce_multi(const ReduceJob* job, int n_jobs, hipStream_t stream);
+int reduce_multi(const ReduceJob* job, int n_jobs, hipStream_t stream,
+                 const FusedSgd* sgd = nullptr);
 // lr_dev / step_dev (optional, device memory): see the kernels in elementwise.hip.
 int sgd_update(float* p, const float* g, float* mom, uint16_t* shadow, long n, float lr, float mu,
                float wd, hipStream_t stream, const float* lr_dev = nullptr);

@@ -484,8 +484,13 @@ class Stage:
             if ls == list(range(ls[0], ls[-1] + 1)):
                 return self._replay(f"FIN{ls[0]}-{ls[-1]}")
         key = tuple(range(len(self.geoms))) if layers is None else tuple(layers)
+        ops.reduce_multi(self._jobs(key))  # one launch for every slab set and bias-partial set
+
+    def _jobs(self, key: tuple) -> list:
+        """reduce_multi job table of the layers in ``key`` (buffers are fixed for the stage's
+        lifetime: built once)."""
         jobs = self._reduce_jobs.get(key)
-        if jobs is None:  # buffers are fixed for the stage's lifetime: build the table once
+        if jobs is None:
             p = self.params
             jobs = []
             for i in key:
@@ -496,7 +501,25 @@ class Stage:
                 jobs.append((self.bpart[i], self.bpart[i].shape[0], g.np_, g.np_, p.gb(i), 1.0,
                              False))
             self._reduce_jobs[key] = jobs
-        ops.reduce_multi(jobs)  # one launch for every slab set and bias-partial set
+        return jobs
+
+    def fused_fin_sgd_ok(self) -> bool:
+        """FIN + SGD as one launch: every gradient element must come out of a reduce job
+        (not stream-K wgrad, which writes weight gradients directly) and the optimizer is SGD."""
+        return (self.params.optim.name == "sgd" and self.wgrad_algo != "streamk" and
+                self.device.type == "cuda" and os.environ.get("DNN_FUSE_FIN_SGD", "1") == "1")
+
+    def _record_fin_sgd(self) -> None:
+        """Record the whole-stage gradient reduction with the SGD update fused in (segment
+        FINO; lr from device memory like record_update)."""
+        p = self.params
+        p._device_scalars()
+        o = p.optim
+        jobs = self._jobs(tuple(range(len(self.geoms))))
+        ops.reduce_multi(jobs, sgd=dict(grad=p.grad, master=p.master,
+                                        mom=p.state[0] if p.state else None, shadow=p.shadow,
+                                        lr=o.lr, momentum=o.momentum,
+                                        weight_decay=o.weight_decay, lr_dev=p.lr_dev))
 
     def update_then_forward(self, j: int, s: int, lr: Optional[float] = None) -> None:
         """Deferred DP update of layers [s, L) (completing the step: advance) followed by the
@@ -610,6 +633,9 @@ class Stage:
                     self.finalize_grads(list(range(a, b + 1)))
             prog.mark("FIN")
             self.finalize_grads()
+            if self.fused_fin_sgd_ok():
+                prog.mark("FINO")
+                self._record_fin_sgd()
             prog.mark("O")
             self.params.record_update()
             for a in range(L):  # split updates: every contiguous layer range, no step advance

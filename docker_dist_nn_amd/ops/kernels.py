@@ -486,16 +486,24 @@ def reduce_slabs(src, n_src, stride, n, out, scale=1.0, accumulate=False):
                           _stream(src))
 
 
-def reduce_multi(jobs):
+def reduce_multi(jobs, sgd=None):
     """Several reduce_slabs in ONE launch. jobs: iterable of
     (src, n_src, stride, n, out, scale, accumulate) with reduce_slabs' meaning; the results are
-    bitwise identical to running reduce_slabs on each job."""
+    bitwise identical to running reduce_slabs on each job.
+
+    ``sgd`` (GPU): dict(grad=flat fp32 gradient the outputs live in, master=, mom=None,
+    shadow=None, lr=, momentum=0, weight_decay=0, lr_dev=None) -- the same launch also applies
+    the SGD step to every reduced element (bitwise equal to a following sgd_update over them)."""
     jobs = list(jobs)
     if not jobs:
         return
     if not jobs[0][0].is_cuda:
         for (src, n_src, stride, n, out, scale, acc) in jobs:
             ref.reduce_slabs(src, n_src, stride, n, out, scale, acc)
+        if sgd is not None:
+            sgd_update(sgd["master"], sgd["grad"], sgd.get("mom"), sgd.get("shadow"),
+                       lr=sgd["lr"], momentum=sgd.get("momentum", 0.0),
+                       weight_decay=sgd.get("weight_decay", 0.0), lr_dev=sgd.get("lr_dev"))
         return
     packed = []
     for (src, n_src, stride, n, out, scale, acc) in jobs:
@@ -507,7 +515,20 @@ def reduce_multi(jobs):
             raise ValueError("reduce_multi range out of bounds")
         packed.append((_p(src), int(stride), int(n_src), int(n), _p(out), float(scale),
                        int(acc)))
-    native().reduce_multi(packed, _stream(jobs[0][0]))
+    if sgd is None:
+        native().reduce_multi(packed, _stream(jobs[0][0]))
+        return
+    g, m = sgd["grad"], sgd["master"]
+    for t in (m, sgd.get("mom")):
+        if t is not None and (t.dtype != torch.float32 or t.numel() != g.numel()):
+            raise ValueError("fused SGD buffers must match the flat gradient")
+    sh = sgd.get("shadow")
+    if sh is not None and (sh.dtype != torch.bfloat16 or sh.numel() != g.numel()):
+        raise ValueError("fused SGD shadow must be bf16 like the flat gradient")
+    native().reduce_multi(packed, _stream(jobs[0][0]), grad_base=_p(g), master=_p(m),
+                          mom=_p(sgd.get("mom")), shadow=_p(sh), lr=float(sgd["lr"]),
+                          mu=float(sgd.get("momentum", 0.0)),
+                          wd=float(sgd.get("weight_decay", 0.0)), lr_dev=_p(sgd.get("lr_dev")))
 
 
 def sgd_update(p, g, mom=None, shadow=None, lr=0.01, momentum=0.0, weight_decay=0.0,

@@ -279,7 +279,17 @@ class PipelineExecutor:
                 if (st, "#finalized") not in plan:
                     plan.append((st, "FIN"))
                 plan.append((st, "O"))
-        self._plan = [(e[0], e[1], e[2] if len(e) > 2 else 0) for e in plan
+        # a stage's whole-step reduction followed by its SGD update: one fused launch (FINO)
+        # when recorded (Stage.fused_fin_sgd_ok); nothing of that stage runs in between
+        fused = []
+        for e in plan:
+            st, seg = e[0], e[1]
+            if seg == "O" and st is not None and "FINO" in st._prog.segments():
+                k = max(i for i, f in enumerate(fused) if f[0] is st and f[1] == "FIN")
+                fused[k] = (st, "FINO") + tuple(fused[k][2:])
+                continue
+            fused.append(e)
+        self._plan = [(e[0], e[1], e[2] if len(e) > 2 else 0) for e in fused
                       if not e[1].startswith("#")]
         return self._plan
 
