@@ -420,26 +420,34 @@ class Stage:
         """dgrad chain of micro-batch j; dZ of the last local layer must already be present."""
         if self._prog is not None and not self._recording:
             return self._replay(f"B{j}")
-        r = self.rows_of(j)
-        p = self.params
+        self._backward_pre(j)
+        for i in range(len(self.geoms) - 1, -1, -1):
+            self._backward_layer(j, i)
+
+    def _backward_pre(self, j: int) -> None:
         if not self.last and self._colsum_by is None:  # dZ of our last layer arrived from
             L = len(self.geoms) - 1                       # the next stage
-            ops.colsum_partial(self.dz[L][r], self._bpart(L, j), self.bp[L])
-        for i in range(len(self.geoms) - 1, -1, -1):
-            if i > 0:
-                prev = self.geoms[i - 1].spec.activation
-                m = self.relu_mask[i - 1]
-                ops.linear_dgrad(self.dz[i][r], p.wbf(i), self.dz[i - 1][r],
-                                 y_prev=self.acts[i - 1][r], act_prev=prev,
-                                 colsum=self._bpart(i - 1, j),
-                                 mask_prev=None if m is None else m[r])
-            elif not self.first:
-                # gradient for the previous stage, already multiplied by the derivative of its
-                # last layer's activation (its output is our input x_in)
-                up = self._colsum_for
-                ops.linear_dgrad(self.dz[0][r], p.wbf(0), self.dx_send[r], y_prev=self.x_in[r],
-                                 act_prev=self.prev_act,
-                                 colsum=None if up is None else up._bpart(len(up.geoms) - 1, j))
+            ops.colsum_partial(self.dz[L][self.rows_of(j)], self._bpart(L, j), self.bp[L])
+
+    def _backward_layer(self, j: int, i: int) -> None:
+        """dgrad of local layer i for micro-batch j: dZ of layer i -> dZ of layer i-1 (or the
+        gradient sent to the previous stage when i == 0)."""
+        r = self.rows_of(j)
+        p = self.params
+        if i > 0:
+            prev = self.geoms[i - 1].spec.activation
+            m = self.relu_mask[i - 1]
+            ops.linear_dgrad(self.dz[i][r], p.wbf(i), self.dz[i - 1][r],
+                             y_prev=self.acts[i - 1][r], act_prev=prev,
+                             colsum=self._bpart(i - 1, j),
+                             mask_prev=None if m is None else m[r])
+        elif not self.first:
+            # gradient for the previous stage, already multiplied by the derivative of its
+            # last layer's activation (its output is our input x_in)
+            up = self._colsum_for
+            ops.linear_dgrad(self.dz[0][r], p.wbf(0), self.dx_send[r], y_prev=self.x_in[r],
+                             act_prev=self.prev_act,
+                             colsum=None if up is None else up._bpart(len(up.geoms) - 1, j))
 
     def wgrad(self, j: int = -1) -> None:
         """Weight/bias gradients for micro-batch j (slab-accumulated) or all rows (j = -1)."""
@@ -618,6 +626,12 @@ class Stage:
             for j in range(self.nm):
                 prog.mark(f"B{j}")
                 self.backward(j)
+            for j in range(self.nm):  # per-layer dgrad segments (dgrad/wgrad overlap plans)
+                prog.mark(f"B{j}.pre")
+                self._backward_pre(j)
+                for i in range(len(self.geoms) - 1, -1, -1):
+                    prog.mark(f"B{j}.L{i}")
+                    self._backward_layer(j, i)
             self._has_w = self.wgrad_mode == "batched"
             if self._has_w:
                 for i in range(len(self.geoms)):

@@ -248,6 +248,11 @@ class PipelineExecutor:
             return None
         if any(st._prog is None or not st._has_w or not st._o_native for st in self.stages):
             return None
+        if os.environ.get("DNN_BW_OVERLAP", "0") == "1" and len(self.stages) == 1:
+            ov = self._overlap_plan(self.stages[0])
+            if ov is not None:
+                self._plan = ov
+                return ov
         order = []
         self._traverse(lambda s, op, j, nxt: order.append((s, op, j, nxt)))
         plan = []
@@ -293,6 +298,24 @@ class PipelineExecutor:
                       if not e[1].startswith("#")]
         return self._plan
 
+    def _overlap_plan(self, st):
+        """Single stage, one micro-batch: each layer's weight-gradient GEMM runs on the side
+        stream while the main stream computes the next dgrad (wgrad_i needs dZ_i, which is
+        ready before dgrad_i starts), so a memory-bound dgrad and a wgrad fill each other's
+        tails. Ends with a join, the first layer's wgrad and the gradient reduction/update."""
+        segs = st._prog.segments()
+        if st.nm != 1 or not st.first or not st.last or "W0" not in segs:
+            return None
+        L = len(st.geoms)
+        plan = [(st, "F0", 0), (None, "@fork", 0)]
+        for i in range(L - 1, 0, -1):
+            plan += [(st, f"W{i}", 1), (st, f"B0.L{i}", 0), (None, "@fork", 0)]
+        plan = plan[:-1] + [(st, "W0", 0), (None, "@join", 0)]
+        plan.append((st, "FINO", 0) if "FINO" in segs else (st, "FIN", 0))
+        if "FINO" not in segs:
+            plan.append((st, "O", 0))
+        return plan
+
     def run_step(self) -> None:
         self.pipe.begin_step()
         for st in self.stages:
@@ -302,7 +325,8 @@ class PipelineExecutor:
             dev = self.stages[0].device
             for st in self.stages:
                 st.params.set_lr(st.params.optim.lr)
-            if self._side is None and self.wgrad_streams > 1:
+            if self._side is None and (self.wgrad_streams > 1 or
+                                       any(e[1] == "@fork" for e in plan)):
                 self._side = torch.cuda.Stream(dev)
             native().run_plan([(st._prog if st is not None else None, seg, si)
                                for st, seg, si in plan],

@@ -1,0 +1,32 @@
+"""dgrad/wgrad overlap plan (DNN_BW_OVERLAP=1): wgrad_i on a side stream concurrent with the
+next dgrad; must be bitwise identical to the sequential native plan."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_overlap_plan_bitwise(dev, monkeypatch):
+    from docker_dist_nn_amd import NAMED_MODELS
+    from docker_dist_nn_amd.data import synthetic_mnist
+    from docker_dist_nn_amd.engine import OptimConfig, Trainer
+
+    x, y = synthetic_mnist(8192, seed=4)
+    xb = torch.zeros(8192, 832, dtype=torch.bfloat16)
+    xb[:, :784] = torch.from_numpy(x).to(torch.bfloat16)
+    xb, yb = xb.to(dev), torch.from_numpy(y).to(dev)
+    res = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("DNN_BW_OVERLAP", flag)
+        tr = Trainer(NAMED_MODELS["mnist-fcnn"], micro_batch=8192, num_micro=1,
+                     optim=OptimConfig(lr=0.1, momentum=0.9), device=dev)
+        losses = []
+        for _ in range(4):
+            tr.set_batch(xb, yb)
+            tr.step()
+            losses.append(tr.loss())
+        plan = tr.executor._native_plan()
+        assert any(seg == "@fork" for _, seg, _ in plan) == (flag == "1")
+        res.append((losses, tr.stages[0].params.master.clone()))
+    assert res[0][0] == res[1][0]
+    assert torch.equal(res[0][1], res[1][1])
