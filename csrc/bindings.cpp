@@ -17,6 +17,7 @@
 #include "kernels/elementwise.hpp"
 #include "kernels/gemm.hpp"
 #include "kernels/gemv.hpp"
+#include "kernels/mlp_tail.hpp"
 #include "runtime/graph.hpp"
 #include "runtime/json_weights.hpp"
 #include "runtime/matrix_codec.hpp"
@@ -50,6 +51,7 @@ static void check(int rc, const char* what) {
   if (rc != 0) {
     std::string msg = std::string(what) + " failed: ";
     if (std::string(what).rfind("gemm_bf16", 0) == 0) msg += dnn::gemm_error_string(rc);
+    else if (std::string(what) == "mlp_tail") msg += dnn::mlp_tail_error(rc);
     else msg += "precondition/launch error code " + std::to_string(rc);
     if (rc == -9) msg += std::string(" (") + hipGetErrorString(hipGetLastError()) + ")";
     throw std::invalid_argument(msg);
@@ -198,6 +200,63 @@ PYBIND11_MODULE(_native, m) {
         py::arg("loss_part"), py::arg("correct"), py::arg("stream"), py::arg("colsum") = 0,
         py::arg("ld_colsum") = 0);
   m.def("softmax_xent_blocks", &dnn::softmax_xent_blocks);
+  m.def(
+      "mlp_tail",
+      [](uintptr_t x, long ldx, uintptr_t w3, long ldw3, uintptr_t b3, uintptr_t w4, long ldw4,
+         uintptr_t b4, uintptr_t labels, uintptr_t h3, long ldh3, uintptr_t dz4, long lddz4,
+         uintptr_t dz3, long lddz3, uintptr_t dz2, long lddz2, uintptr_t loss_part,
+         uintptr_t correct, uintptr_t cs4, long ld_cs4, uintptr_t cs3, long ld_cs3, uintptr_t cs2,
+         long ld_cs2, int M, int K3, int N3, int N4, int n_cls, float scale, int act3, int act2,
+         uintptr_t stream) {
+        launch(
+            "mlp_tail",
+            [=](hipStream_t s, const dnn::Program& R) {
+              dnn::TailParams p{};
+              p.X = R.fix(P<const uint16_t>(x));
+              p.ldx = ldx;
+              p.W3 = R.fix(P<const uint16_t>(w3));
+              p.ldw3 = ldw3;
+              p.b3 = R.fix(P<const float>(b3));
+              p.W4 = R.fix(P<const uint16_t>(w4));
+              p.ldw4 = ldw4;
+              p.b4 = R.fix(P<const float>(b4));
+              p.labels = R.fix(P<const int>(labels));
+              p.H3 = R.fix(P<uint16_t>(h3));
+              p.ldh3 = ldh3;
+              p.DZ4 = R.fix(P<uint16_t>(dz4));
+              p.lddz4 = lddz4;
+              p.DZ3 = R.fix(P<uint16_t>(dz3));
+              p.lddz3 = lddz3;
+              p.DZ2 = R.fix(P<uint16_t>(dz2));
+              p.lddz2 = lddz2;
+              p.loss_part = R.fix(P<float>(loss_part));
+              p.correct = R.fix(P<int>(correct));
+              p.cs4 = R.fix(P<float>(cs4));
+              p.ld_cs4 = ld_cs4;
+              p.cs3 = R.fix(P<float>(cs3));
+              p.ld_cs3 = ld_cs3;
+              p.cs2 = R.fix(P<float>(cs2));
+              p.ld_cs2 = ld_cs2;
+              p.M = M;
+              p.K3 = K3;
+              p.N3 = N3;
+              p.N4 = N4;
+              p.n_cls = n_cls;
+              p.scale = scale;
+              p.act3 = act3;
+              p.act2 = act2;
+              return dnn::mlp_tail(p, s);
+            },
+            stream);
+      },
+      py::arg("x"), py::arg("ldx"), py::arg("w3"), py::arg("ldw3"), py::arg("b3"), py::arg("w4"),
+      py::arg("ldw4"), py::arg("b4"), py::arg("labels"), py::arg("h3"), py::arg("ldh3"),
+      py::arg("dz4"), py::arg("lddz4"), py::arg("dz3"), py::arg("lddz3"), py::arg("dz2"),
+      py::arg("lddz2"), py::arg("loss_part"), py::arg("correct"), py::arg("cs4"),
+      py::arg("ld_cs4"), py::arg("cs3"), py::arg("ld_cs3"), py::arg("cs2"), py::arg("ld_cs2"),
+      py::arg("M"), py::arg("K3"), py::arg("N3"), py::arg("N4"), py::arg("n_cls"),
+      py::arg("scale"), py::arg("act3"), py::arg("act2"), py::arg("stream"));
+  m.def("mlp_tail_blocks", &dnn::mlp_tail_blocks);
   m.def("softmax_rows", [](uintptr_t logits, long ld_in, uintptr_t out, long ld_out, int rows,
                            int n_cls, uintptr_t labels, uintptr_t pred, uintptr_t correct,
                            uintptr_t stream) {

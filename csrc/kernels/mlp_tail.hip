@@ -1,0 +1,369 @@
+// Fused classifier tail: forward of the last two layers, softmax cross-entropy, and the
+// dgrads of both layers in ONE launch (interface and math: mlp_tail.hpp).
+//
+// Why: on the headline 784-512-256-128-10 model the four kernels this replaces (fwd 256->128,
+// fwd 128->10 + CE, dgrad 10->128, dgrad 128->256) are all latency-bound -- short contractions,
+// one LDS stage in flight, an epilogue that re-reads the activation -- and cost ~63 us of a
+// ~370 us step while their data is ~110 MB (23 us of HBM time). Their weights are 64 + 16 KiB,
+// so they live in LDS for the whole launch and every intermediate stays on chip.
+//
+// Structure (one workgroup per CU, 8 waves, each wave walks 16-row blocks):
+//   * W3 [N3][K3] and W4 [64][N3] are staged once into LDS with LDS-DMA, in the MNMAJ image
+//     layout of gemm_tile.hpp: the forward reads them row-wise (16-B chunks), the dgrads read
+//     them transposed with ds_read_b64_tr_b16 (load_frag<MNMAJ>), so no transposed copy exists;
+//   * every product is computed with SWAPPED operands, mfma(W-fragment, X-fragment): a lane
+//     then holds 4 consecutive output features of ONE data row (row = lane & 15, features
+//     16 j + 4 (lane >> 4) + r), which is the layout of the bias/activation epilogue, of the
+//     8-byte stores, of the ReLU derivative of the next dgrad, and of the softmax (a row's 16
+//     class logits sit in 4 lanes);
+//   * an output that feeds the next product is written to a 16-row per-wave LDS scratch and
+//     read back as the next MFMA's B fragment (same-wave LDS order, no barrier);
+//   * the next block's input rows are loaded while the current block computes;
+//   * bias-gradient column sums: DPP row sums per block, accumulated in registers across the
+//     wave's blocks, reduced over the 8 waves in fixed order at the end (one partial per
+//     workgroup); softmax and loss follow xent_rows (gemm_tile.hpp) operation for operation.
+// Every MFMA chain accumulates its contraction in the same ascending k order as the unfused
+// GEMMs, so h3, dz4, dz3 and dz2 equal the unfused path's bit for bit (tests/test_mlp_tail_gpu.py).
+//
+// Reference parity: the forward is /root/reference/src/grpc_node.py:87 + :62-73 (z = x.W + b,
+// activation, softmax); the backward replaces the centralised autograd of
+// /root/reference/scripts/generate_mnist_pytorch.py:41-52.
+#include "gemm_tile.hpp"
+#include "mlp_tail.hpp"
+
+namespace dnn {
+namespace tail {
+
+// Waves per workgroup: 8 (two per SIMD, <= 256 registers each) for the branch-free ReLU form;
+// the generic-activation form needs more registers and runs 4 (one per SIMD, <= 512).
+template <bool RELU>
+constexpr int waves() { return RELU ? 8 : 4; }
+constexpr int BLOCK_ROWS = 128;  // rows per workgroup iteration that size the grid (8 x 16)
+constexpr int MAX_CLS = 16;  // classes held by one 16-wide MFMA block
+constexpr int W4_ROWS = 64;  // staged rows of W4 (the dgrad's contraction uses rows 0..31)
+
+template <int K3, int N3, int NW>
+struct Geo {
+  static constexpr int W3_BYTES = N3 * K3 * 2;
+  static constexpr int W4_BYTES = W4_ROWS * N3 * 2;
+  static constexpr int SP = (N3 + 8) * 2;  // scratch row pitch (bytes): h3, then dz3
+  static constexpr int S_BYTES = 16 * SP;
+  static constexpr int DP = 80;  // dz4 scratch row pitch: 32 bf16 + 16 B
+  static constexpr int WAVE_BYTES = S_BYTES + 16 * DP;
+  static constexpr int RC = K3 + N3 + MAX_CLS + 2;  // per-wave reduction row (floats)
+  static constexpr int SMEM = W3_BYTES + W4_BYTES + NW * WAVE_BYTES + NW * RC * 4;
+  static_assert(SMEM <= 160 * 1024, "LDS budget");
+  static_assert(K3 / 16 <= 16 && N3 / 16 <= 16, "column-sum lanes");
+};
+
+__device__ __forceinline__ float lo_bf(unsigned x) { return __uint_as_float(x << 16); }
+__device__ __forceinline__ float hi_bf(unsigned x) { return __uint_as_float(x & 0xffff0000u); }
+// 8-byte LDS store / load of a packed bf16 quad (HIP's uint2 has no address-space-3 operators)
+__device__ __forceinline__ void st8(char LDS_AS* p, uint2 v) {
+  *(unsigned long long LDS_AS*)p = ((unsigned long long)v.y << 32) | v.x;
+}
+
+// Activation / derivative: RELU = both activations are ReLU (the branch-free common case),
+// otherwise the runtime Act code (a uniform branch per element).
+template <bool RELU>
+__device__ __forceinline__ float act(float v, int code) {
+  if constexpr (RELU) return v > 0.f ? v : 0.f;
+  return act_fwd(v, code);
+}
+template <bool RELU>
+__device__ __forceinline__ float dact(float g, float y, int code) {
+  if constexpr (RELU) return y > 0.f ? g : 0.f;
+  return act_bwd(g, y, code);
+}
+
+// 16-B row chunk `c` of row `r` of an MNMAJ-swizzled [rows][T] image (the forward's A fragment:
+// lane holds W[r = 16 blk + (lane & 15)][8 c .. 8 c + 7] with c = 4 s + (lane >> 4)).
+template <int T>
+__device__ __forceinline__ bf16x8_t row_frag(const char LDS_AS* img, int blk, int s, int lane) {
+  const int r = blk * 16 + (lane & 15), c = 4 * s + (lane >> 4);
+  return *(const bf16x8_t LDS_AS*)(img + r * (T * 2) + ((c ^ mn_swz<T>(r)) << 4));
+}
+
+}  // namespace tail
+
+template <int K3, int N3, bool RELU>
+__global__ __launch_bounds__(64 * tail::waves<RELU>()) void mlp_tail_kernel(TailParams p) {
+  using tail::act;
+  using tail::dact;
+  constexpr int NW = tail::waves<RELU>();
+  using G = tail::Geo<K3, N3, NW>;
+  using tail::hi_bf;
+  using tail::lo_bf;
+  constexpr int NK = K3 / 32, NJ = N3 / 16, NS3 = N3 / 32, NKK = K3 / 16;
+  __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
+  char LDS_AS* lds = (char LDS_AS*)smem;
+  char LDS_AS* w3 = lds;
+  char LDS_AS* w4 = lds + G::W3_BYTES;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  char LDS_AS* S = w4 + G::W4_BYTES + wave * G::WAVE_BYTES;
+  char LDS_AS* D = S + G::S_BYTES;
+  float LDS_AS* red = (float LDS_AS*)(w4 + G::W4_BYTES + NW * G::WAVE_BYTES);
+
+  // ---- weights -> LDS (64-row pieces of the MNMAJ image, LDS-DMA) --------------------------
+#pragma unroll
+  for (int r0 = 0; r0 < N3; r0 += 64)
+    stage_tile<MNMAJ, K3, NW>(p.W3, p.ldw3, 0, r0, w3 + r0 * K3 * 2, wave, lane, K3);
+  stage_tile<MNMAJ, N3, NW>(p.W4, p.ldw4, 0, 0, w4, wave, lane, N3);
+
+  const int i16 = lane & 15, q = lane >> 4;
+  const int nrb = p.M >> 4;
+  const int nw = gridDim.x * NW;
+  int rb = blockIdx.x * NW + wave;
+
+  bf16x8_t xb[NK];
+  if (rb < nrb) {
+    const u16* src = p.X + (long)(rb * 16 + i16) * p.ldx + 8 * q;
+#pragma unroll
+    for (int s = 0; s < NK; ++s) xb[s] = *(const bf16x8_t*)(src + 32 * s);
+  }
+  __syncthreads();  // weights landed (the fence waits for the LDS-DMA loads too)
+
+  // biases in registers for the whole launch: a load inside the loop would queue behind the
+  // block's stores and the next block's prefetch (vmcnt counts in issue order) and stall on all
+  f32x4_t b3r[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) b3r[j] = *(const f32x4_t*)(p.b3 + 16 * j + 4 * q);
+  float b4r[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) b4r[e] = p.b4[4 * q + e];
+
+  float cs2a[4] = {0.f, 0.f, 0.f, 0.f}, cs3a[4] = {0.f, 0.f, 0.f, 0.f};
+  float cs4a[4] = {0.f, 0.f, 0.f, 0.f};
+  float loss_a = 0.f;
+  int corr_a = 0;
+  const int nc = p.n_cls;
+
+  for (; rb < nrb; rb += nw) {
+    const long row = (long)rb * 16 + i16;
+    // activation of layer L-3 at this lane's dz2 positions, and the label
+    uint2 hv[NKK];
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) hv[kk] = *(const uint2*)(p.X + row * p.ldx + 16 * kk + 4 * q);
+    const int label = p.labels[row];
+
+    // ---- h3 = act3(X . W3^T + b3) -------------------------------------------------------
+    f32x4_t a3[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      a3[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < NK; ++s)
+        a3[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tail::row_frag<K3>(w3, j, s, lane), xb[s],
+                                                        a3[j], 0, 0, 0);
+    }
+    if (rb + nw < nrb) {  // next block's rows (xb is dead once the MFMAs above have read it)
+      const u16* src = p.X + (long)((rb + nw) * 16 + i16) * p.ldx + 8 * q;
+#pragma unroll
+      for (int s = 0; s < NK; ++s) xb[s] = *(const bf16x8_t*)(src + 32 * s);
+    }
+    uint2 h3p[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int col = 16 * j + 4 * q;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = act<RELU>(a3[j][e] + b3r[j][e], p.act3);
+      h3p[j] = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+      *(uint2*)(p.H3 + row * p.ldh3 + col) = h3p[j];
+      tail::st8(S + i16 * G::SP + col * 2, h3p[j]);
+    }
+
+    // ---- logits (classes 0..15) = h3 . W4^T + b4; softmax cross-entropy ------------------
+    f32x4_t a4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NS3; ++s) {
+      const bf16x8_t hb = *(const bf16x8_t LDS_AS*)(S + i16 * G::SP + (32 * s + 8 * q) * 2);
+      a4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tail::row_frag<N3>(w4, 0, s, lane), hb, a4, 0,
+                                                   0, 0);
+    }
+    float lv[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) lv[e] = a4[e] + b4r[e];
+    float vals[tail::MAX_CLS];
+#pragma unroll
+    for (int c = 0; c < tail::MAX_CLS; ++c) vals[c] = __shfl(lv[c & 3], i16 + 16 * (c >> 2), 64);
+    float mx = -INFINITY;
+    int amax = 0;
+#pragma unroll
+    for (int c = 0; c < tail::MAX_CLS; ++c)
+      if (c < nc && vals[c] > mx) {
+        mx = vals[c];
+        amax = c;
+      }
+    float se = 0.f;
+#pragma unroll
+    for (int c = 0; c < tail::MAX_CLS; ++c)
+      if (c < nc) se += __expf(vals[c] - mx);
+    const float inv = 1.f / se;
+    float dz[4] = {0.f, 0.f, 0.f, 0.f};
+    if (label >= 0) {
+      float vl = 0.f;
+#pragma unroll
+      for (int c = 0; c < tail::MAX_CLS; ++c)
+        if (c == label) vl = vals[c];
+      if (q == 0) {
+        loss_a += -(vl - mx - __logf(se));
+        corr_a += amax == label;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = 4 * q + e;
+        if (c < nc) dz[e] = (__expf(lv[e] - mx) * inv - (c == label ? 1.f : 0.f)) * p.scale;
+      }
+    }
+    const uint2 d4 = make_uint2(pack_bf16x2(dz[0], dz[1]), pack_bf16x2(dz[2], dz[3]));
+    *(uint2*)(p.DZ4 + row * p.lddz4 + 4 * q) = d4;
+    for (int c = tail::MAX_CLS + 4 * q; c < p.N4; c += 16)
+      *(uint2*)(p.DZ4 + row * p.lddz4 + c) = make_uint2(0u, 0u);
+    cs4a[0] += row16_sum(lo_bf(d4.x));
+    cs4a[1] += row16_sum(hi_bf(d4.x));
+    cs4a[2] += row16_sum(lo_bf(d4.y));
+    cs4a[3] += row16_sum(hi_bf(d4.y));
+
+    // ---- dz3 = (dz4 . W4) * act3'(h3): contraction over classes 0..31 -------------------
+    tail::st8(D + i16 * G::DP + 8 * q, d4);
+    tail::st8(D + i16 * G::DP + 32 + 8 * q, make_uint2(0u, 0u));
+    const bf16x8_t df = *(const bf16x8_t LDS_AS*)(D + i16 * G::DP + 16 * q);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const f32x4_t a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+          load_frag<MNMAJ, N3>(w4, j, 0, lane), df, f32x4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      const float y[4] = {lo_bf(h3p[j].x), hi_bf(h3p[j].x), lo_bf(h3p[j].y), hi_bf(h3p[j].y)};
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = dact<RELU>(a[e], y[e], p.act3);
+      const uint2 o = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+      const int col = 16 * j + 4 * q;
+      *(uint2*)(p.DZ3 + row * p.lddz3 + col) = o;
+      tail::st8(S + i16 * G::SP + col * 2, o);
+      const float t[4] = {row16_sum(lo_bf(o.x)), row16_sum(hi_bf(o.x)), row16_sum(lo_bf(o.y)),
+                          row16_sum(hi_bf(o.y))};
+      if (i16 == j) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cs3a[e] += t[e];
+      }
+    }
+
+    // ---- dz2 = (dz3 . W3) * act2'(X) ------------------------------------------------------
+    bf16x8_t d3f[NS3];
+#pragma unroll
+    for (int s = 0; s < NS3; ++s)
+      d3f[s] = *(const bf16x8_t LDS_AS*)(S + i16 * G::SP + (32 * s + 8 * q) * 2);
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) {
+      f32x4_t a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < NS3; ++s)
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(load_frag<MNMAJ, K3>(w3, kk, s, lane), d3f[s],
+                                                    a, 0, 0, 0);
+      const float y[4] = {lo_bf(hv[kk].x), hi_bf(hv[kk].x), lo_bf(hv[kk].y), hi_bf(hv[kk].y)};
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = dact<RELU>(a[e], y[e], p.act2);
+      const uint2 o = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+      *(uint2*)(p.DZ2 + row * p.lddz2 + 16 * kk + 4 * q) = o;
+      const float t[4] = {row16_sum(lo_bf(o.x)), row16_sum(hi_bf(o.x)), row16_sum(lo_bf(o.y)),
+                          row16_sum(hi_bf(o.y))};
+      if (i16 == kk) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cs2a[e] += t[e];
+      }
+    }
+  }
+
+  // ---- per-workgroup partials: the 8 waves' column sums / loss / correct, fixed order -------
+  float LDS_AS* rw = red + wave * G::RC;
+  if (i16 < NKK) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) rw[16 * i16 + 4 * q + e] = cs2a[e];
+  }
+  if (i16 < NJ) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) rw[K3 + 16 * i16 + 4 * q + e] = cs3a[e];
+  }
+  if (i16 == 0) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) rw[K3 + N3 + 4 * q + e] = cs4a[e];
+  }
+  loss_a = wave_sum(loss_a);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) corr_a += __shfl_xor(corr_a, o, 64);
+  if (lane == 0) {
+    rw[K3 + N3 + tail::MAX_CLS] = loss_a;
+    rw[K3 + N3 + tail::MAX_CLS + 1] = (float)corr_a;
+  }
+  __syncthreads();
+  const long wg = blockIdx.x;
+  for (int c = threadIdx.x; c < K3 + N3 + tail::MAX_CLS + 2; c += NW * 64) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) t += red[w * G::RC + c];
+    if (c < K3) p.cs2[wg * p.ld_cs2 + c] = t;
+    else if (c < K3 + N3) p.cs3[wg * p.ld_cs3 + c - K3] = t;
+    else if (c < K3 + N3 + tail::MAX_CLS) p.cs4[wg * p.ld_cs4 + c - K3 - N3] = t;
+    else if (c == K3 + N3 + tail::MAX_CLS) {
+      if (p.loss_part) p.loss_part[wg] = t;
+    } else if (p.correct) {
+      p.correct[wg] = (int)t;
+    }
+  }
+  for (int c = tail::MAX_CLS + (int)threadIdx.x; c < p.N4; c += NW * 64)
+    p.cs4[wg * p.ld_cs4 + c] = 0.f;
+}
+
+int mlp_tail_blocks(int M) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+  }
+  const int blocks = (M + tail::BLOCK_ROWS - 1) / tail::BLOCK_ROWS;
+  return blocks < cus ? (blocks > 0 ? blocks : 1) : cus;
+}
+
+const char* mlp_tail_error(int code) {
+  switch (code) {
+    case -1: return "mlp_tail: rows must be a positive multiple of 16";
+    case -2: return "mlp_tail: unsupported widths (K3 in {64,128,256}, N3 in {64,128})";
+    case -3: return "mlp_tail: classes must be 1..16 with 64 or 128 padded columns";
+    case -4: return "mlp_tail: operand rows/columns must be 16-byte aligned";
+    case -9: return "mlp_tail: kernel launch failed";
+    default: return "mlp_tail: unknown error";
+  }
+}
+
+int mlp_tail(const TailParams& p, hipStream_t stream) {
+  if (p.M <= 0 || p.M % 16) return -1;
+  if (p.n_cls < 1 || p.n_cls > tail::MAX_CLS || (p.N4 != 64 && p.N4 != 128)) return -3;
+  const long lds[] = {p.ldx, p.ldw3, p.ldw4, p.ldh3, p.lddz4, p.lddz3, p.lddz2};
+  for (long l : lds)
+    if (l % 8) return -4;
+  typedef void (*fn_t)(TailParams);
+  fn_t fn = nullptr;
+  const bool relu = p.act3 == ACT_RELU && p.act2 == ACT_RELU;
+#define DNN_TAIL(K, N) \
+  if (p.K3 == K && p.N3 == N) fn = relu ? mlp_tail_kernel<K, N, true> : mlp_tail_kernel<K, N, false>;
+  DNN_TAIL(64, 64)
+  DNN_TAIL(128, 64)
+  DNN_TAIL(256, 64)
+  DNN_TAIL(64, 128)
+  DNN_TAIL(128, 128)
+  DNN_TAIL(256, 128)
+#undef DNN_TAIL
+  if (!fn) return -2;
+  hipLaunchKernelGGL(fn, dim3(mlp_tail_blocks(p.M)), dim3(64 * (relu ? tail::waves<true>()
+                                                                 : tail::waves<false>())),
+                     0, stream, p);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
+}  // namespace dnn

@@ -308,8 +308,15 @@ class Stage:
         self.dx_send = None if self.first else torch.zeros(R, g0.kp, dtype=bf, device=dev)
         self.labels = torch.full((R,), -1, dtype=torch.int32, device=dev) if self.last else None
         self.labels_buf = self.labels  # owned buffer; ``labels`` may alias a dataset slice
-        self.xent_per_micro = (self.mb // ops.xent_tiles(self.mb, gl.np_)[0] if self.fused_xent
-                               else ops.xent_blocks(self.mb))
+        # Narrow classifier tail (csrc/kernels/mlp_tail.hip): the forward of the last two
+        # layers, the softmax CE and both of their dgrads run as ONE kernel inside the last
+        # layer's forward; the second-to-last layer's forward and both dgrads are then no-ops.
+        self.tail = self._tail_ok()
+        if self.tail:
+            self.xent_per_micro = ops.tail_blocks(self.mb)
+        else:
+            self.xent_per_micro = (self.mb // ops.xent_tiles(self.mb, gl.np_)[0]
+                                   if self.fused_xent else ops.xent_blocks(self.mb))
         self.loss_part = torch.zeros(self.xent_per_micro * self.nm, dtype=f32, device=dev)
         # per-block correct counts, written (not accumulated) by the loss kernels
         self.correct = torch.zeros(self.xent_per_micro * self.nm, dtype=torch.int32, device=dev)
@@ -340,6 +347,9 @@ class Stage:
                 # one partial per 128 rows: enough workgroups to fill the chip (1024-row
                 # partitions left a 4096-row boundary colsum at 32 workgroups, 12 us)
                 self.bp.append(max(1, self.mb // 128))
+        if self.tail:  # dz of the last three local layers come from the tail kernel
+            for i in range(L - 3, L):
+                self.bp[i] = self.xent_per_micro
         self.bpart = [torch.zeros(self.bp[i] * self.nm, g.np_, dtype=f32, device=dev)
                       for i, g in enumerate(self.geoms)]
         self._w_done = 0
@@ -351,6 +361,16 @@ class Stage:
         self._has_w = False
         self._o_native = False  # "O" recorded (device-side lr / step)
         self._rx = self._rl = None
+
+    def _tail_ok(self) -> bool:
+        if not (self.fused_xent and self.device.type == "cuda" and len(self.geoms) >= 3 and
+                os.environ.get("DNN_TAIL", "1") == "1"):
+            return False
+        g2, g3, g4 = self.geoms[-3], self.geoms[-2], self.geoms[-1]
+        acts = ("relu", "sigmoid", "linear")
+        return (ops.tail_supported(g3.kp, g3.np_, g4.np_, self.n_cls) and
+                g3.spec.activation in acts and g2.spec.activation in acts and
+                self.mb % 16 == 0)
 
     def rows_of(self, j: int) -> slice:
         if not 0 <= j < self.nm:
@@ -396,7 +416,21 @@ class Stage:
         g = self.geoms[i]
         x = self.input_of(i)[r]
         y = self.acts[i][r]
-        if self.last and i == len(self.geoms) - 1 and self.fused_xent:
+        L = len(self.geoms)
+        if self.tail and i == L - 2:
+            return  # computed by the tail kernel at i == L - 1
+        if self.tail and i == L - 1:
+            k = j * self.xent_per_micro
+            ops.mlp_tail(self.acts[L - 3][r], p.wbf(L - 2), p.b32(L - 2), p.wbf(L - 1),
+                         p.b32(L - 1), self.labels[r], self.acts[L - 2][r], self.dz[L - 1][r],
+                         self.dz[L - 2][r], self.dz[L - 3][r], self.n_cls,
+                         1.0 / self.global_batch, act3=self.geoms[L - 2].spec.activation,
+                         act2=self.geoms[L - 3].spec.activation,
+                         loss_part=self.loss_part[k:k + self.xent_per_micro],
+                         correct=self.correct[k:k + self.xent_per_micro],
+                         cs4=self._bpart(L - 1, j), cs3=self._bpart(L - 2, j),
+                         cs2=self._bpart(L - 3, j))
+        elif self.last and i == len(self.geoms) - 1 and self.fused_xent:
             k = j * self.xent_per_micro
             ops.linear_fwd_xent(x, p.wbf(i), p.b32(i), self.dz[i][r], self.labels[r],
                                 self.n_cls, 1.0 / self.global_batch,
@@ -432,6 +466,8 @@ class Stage:
     def _backward_layer(self, j: int, i: int) -> None:
         """dgrad of local layer i for micro-batch j: dZ of layer i -> dZ of layer i-1 (or the
         gradient sent to the previous stage when i == 0)."""
+        if self.tail and i >= len(self.geoms) - 2:
+            return  # both dgrads ran inside the tail kernel (forward of micro-batch j)
         r = self.rows_of(j)
         p = self.params
         if i > 0:

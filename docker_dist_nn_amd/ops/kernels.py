@@ -448,6 +448,61 @@ def softmax_xent(logits, labels, dz, n_cls, scale, loss_part=None, correct=None,
                           colsum.stride(0) if colsum is not None else 0)
 
 
+TAIL_MAX_CLS = 16
+
+
+def tail_supported(k3: int, n3: int, n4: int, n_cls: int) -> bool:
+    """Geometries the fused classifier tail (csrc/kernels/mlp_tail.hip) handles."""
+    return k3 in (64, 128, 256) and n3 in (64, 128) and n4 in (64, 128) and \
+        1 <= n_cls <= TAIL_MAX_CLS
+
+
+def tail_blocks(rows: int) -> int:
+    """Partials (workgroups) of one mlp_tail launch over ``rows`` rows."""
+    if rows <= 0 or rows % 16:
+        raise ValueError("mlp_tail rows must be a positive multiple of 16")
+    if torch.cuda.is_available():
+        return int(native().mlp_tail_blocks(rows))
+    return max(1, min(NUM_CU, -(-rows // ref.TAIL_BLOCK_ROWS)))
+
+
+def mlp_tail(x, w3, b3, w4, b4, labels, h3, dz4, dz3, dz2, n_cls, scale, act3="relu",
+             act2="relu", loss_part=None, correct=None, cs4=None, cs3=None, cs2=None):
+    """The last two layers of a narrow classifier, forward AND backward, in one launch:
+    h3 = act3(x.w3^T + b3); dz4 = (softmax(h3.w4^T + b4) - onehot) * scale;
+    dz3 = (dz4.w4) * act3'(h3); dz2 = (dz3.w3) * act2'(x); bias-gradient partials
+    cs4/cs3/cs2 [tail_blocks(rows)][cols] and per-block loss / correct counts.
+    CPU: the unfused kernels' reference path (same contract, partials per 64-row block)."""
+    rows, k3 = x.shape
+    n3, n4 = w3.shape[0], w4.shape[0]
+    if not tail_supported(k3, n3, n4, n_cls) or w3.shape[1] != k3 or w4.shape[1] != n3:
+        raise ValueError(f"mlp_tail: unsupported geometry K3={k3} N3={n3} N4={n4} "
+                         f"classes={n_cls}")
+    nb = tail_blocks(rows)
+    for t, name, cols in ((cs4, "cs4", n4), (cs3, "cs3", n3), (cs2, "cs2", k3)):
+        if t is None or t.dtype != torch.float32 or t.dim() != 2 or t.shape[0] < nb or \
+                t.shape[1] < cols or t.stride(1) != 1:
+            raise ValueError(f"{name} must be fp32 [{nb}][>={cols}] row-major")
+    if loss_part is None or loss_part.numel() < nb or correct is None or \
+            correct.dtype != torch.int32 or correct.numel() < nb:
+        raise ValueError(f"loss_part / correct (int32) need {nb} entries")
+    if not x.is_cuda:
+        ref.mlp_tail(x, w3, b3, w4, b4, labels, h3, dz4, dz3, dz2, n_cls, scale, _act(act3),
+                     _act(act2), loss_part, correct, cs4, cs3, cs2, nb)
+        return
+    for t, name in ((x, "x"), (w3, "w3"), (w4, "w4"), (h3, "h3"), (dz4, "dz4"), (dz3, "dz3"),
+                    (dz2, "dz2")):
+        _rows(t, name, torch.bfloat16)
+    if labels.dtype != torch.int32 or labels.numel() < rows:
+        raise ValueError("labels must be int32 with one entry per row")
+    native().mlp_tail(_p(x), x.stride(0), _p(w3), w3.stride(0), _p(b3), _p(w4), w4.stride(0),
+                      _p(b4), _p(labels), _p(h3), h3.stride(0), _p(dz4), dz4.stride(0),
+                      _p(dz3), dz3.stride(0), _p(dz2), dz2.stride(0), _p(loss_part),
+                      _p(correct), _p(cs4), cs4.stride(0), _p(cs3), cs3.stride(0), _p(cs2),
+                      cs2.stride(0), rows, k3, n3, n4, n_cls, float(scale), _act(act3),
+                      _act(act2), _stream(x))
+
+
 def softmax_rows(logits, out, n_cls, labels=None, pred=None, correct=None):
     rows = logits.shape[0]
     if not logits.is_cuda:
