@@ -28,6 +28,10 @@
 // Reference parity: the forward is /root/reference/src/grpc_node.py:87 + :62-73 (z = x.W + b,
 // activation, softmax); the backward replaces the centralised autograd of
 // /root/reference/scripts/generate_mnist_pytorch.py:41-52.
+//
+// build-flags: -fno-slp-vectorize
+// (SLP pairs independent DPP row sums into v_mov_b32_dpp + v_pk_add_f32; without it each step
+// folds into one v_add_f32_dpp: -10 % instructions in the loop.)
 #include "gemm_tile.hpp"
 #include "mlp_tail.hpp"
 
@@ -50,7 +54,7 @@ struct Geo {
   static constexpr int S_BYTES = 16 * SP;
   static constexpr int DP = 80;  // dz4 scratch row pitch: 32 bf16 + 16 B
   static constexpr int WAVE_BYTES = S_BYTES + 16 * DP;
-  static constexpr int RC = K3 + N3 + MAX_CLS + 2;  // per-wave reduction row (floats)
+  static constexpr int RC = K3 + N3 + MAX_CLS + 4;  // per-wave reduction row (floats, 16-B rows)
   static constexpr int SMEM = W3_BYTES + W4_BYTES + NW * WAVE_BYTES + NW * RC * 4;
   static_assert(SMEM <= 160 * 1024, "LDS budget");
   static_assert(K3 / 16 <= 16 && N3 / 16 <= 16, "column-sum lanes");
@@ -61,6 +65,25 @@ __device__ __forceinline__ float hi_bf(unsigned x) { return __uint_as_float(x & 
 // 8-byte LDS store / load of a packed bf16 quad (HIP's uint2 has no address-space-3 operators)
 __device__ __forceinline__ void st8(char LDS_AS* p, uint2 v) {
   *(unsigned long long LDS_AS*)p = ((unsigned long long)v.y << 32) | v.x;
+}
+
+// rw[0..3] += column sums over the 16 rows (lanes of a DPP row) of the 4 bf16 values in v
+// (the four butterflies run step-major so consecutive DPP adds are independent: a DPP read of a
+// VGPR written by the previous VALU instruction costs wait states)
+__device__ __forceinline__ void acc4(float LDS_AS* rw, uint2 v) {
+  float x[4] = {lo_bf(v.x), hi_bf(v.x), lo_bf(v.y), hi_bf(v.y)};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) x[e] += dpp_f<0xB1>(x[e]);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) x[e] += dpp_f<0x4E>(x[e]);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) x[e] += dpp_f<0x141>(x[e]);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) x[e] += dpp_f<0x140>(x[e]);
+  f32x4_t t = *(f32x4_t LDS_AS*)rw;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) t[e] += x[e];
+  *(f32x4_t LDS_AS*)rw = t;
 }
 
 // Activation / derivative: RELU = both activations are ReLU (the branch-free common case),
@@ -133,8 +156,11 @@ __global__ __launch_bounds__(64 * tail::waves<RELU>()) void mlp_tail_kernel(Tail
 #pragma unroll
   for (int e = 0; e < 4; ++e) b4r[e] = p.b4[4 * q + e];
 
-  float cs2a[4] = {0.f, 0.f, 0.f, 0.f}, cs3a[4] = {0.f, 0.f, 0.f, 0.f};
-  float cs4a[4] = {0.f, 0.f, 0.f, 0.f};
+  // column sums accumulate in this wave's row of `red` (zeroed here; only this wave touches it
+  // until the final barrier). A DPP row sum leaves the same bits in all 16 lanes of the row, so
+  // all of them read-add-write the same 16-B slot: no lane masks, no registers per column.
+  float LDS_AS* rw = red + wave * G::RC;
+  for (int c = lane; c < G::RC; c += 64) rw[c] = 0.f;
   float loss_a = 0.f;
   int corr_a = 0;
   const int nc = p.n_cls;
@@ -221,10 +247,7 @@ __global__ __launch_bounds__(64 * tail::waves<RELU>()) void mlp_tail_kernel(Tail
     *(uint2*)(p.DZ4 + row * p.lddz4 + 4 * q) = d4;
     for (int c = tail::MAX_CLS + 4 * q; c < p.N4; c += 16)
       *(uint2*)(p.DZ4 + row * p.lddz4 + c) = make_uint2(0u, 0u);
-    cs4a[0] += row16_sum(lo_bf(d4.x));
-    cs4a[1] += row16_sum(hi_bf(d4.x));
-    cs4a[2] += row16_sum(lo_bf(d4.y));
-    cs4a[3] += row16_sum(hi_bf(d4.y));
+    tail::acc4(rw + K3 + N3 + 4 * q, d4);
 
     // ---- dz3 = (dz4 . W4) * act3'(h3): contraction over classes 0..31 -------------------
     tail::st8(D + i16 * G::DP + 8 * q, d4);
@@ -242,12 +265,7 @@ __global__ __launch_bounds__(64 * tail::waves<RELU>()) void mlp_tail_kernel(Tail
       const int col = 16 * j + 4 * q;
       *(uint2*)(p.DZ3 + row * p.lddz3 + col) = o;
       tail::st8(S + i16 * G::SP + col * 2, o);
-      const float t[4] = {row16_sum(lo_bf(o.x)), row16_sum(hi_bf(o.x)), row16_sum(lo_bf(o.y)),
-                          row16_sum(hi_bf(o.y))};
-      if (i16 == j) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) cs3a[e] += t[e];
-      }
+      tail::acc4(rw + K3 + col, o);
     }
 
     // ---- dz2 = (dz3 . W3) * act2'(X) ------------------------------------------------------
@@ -268,29 +286,11 @@ __global__ __launch_bounds__(64 * tail::waves<RELU>()) void mlp_tail_kernel(Tail
       for (int e = 0; e < 4; ++e) v[e] = dact<RELU>(a[e], y[e], p.act2);
       const uint2 o = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
       *(uint2*)(p.DZ2 + row * p.lddz2 + 16 * kk + 4 * q) = o;
-      const float t[4] = {row16_sum(lo_bf(o.x)), row16_sum(hi_bf(o.x)), row16_sum(lo_bf(o.y)),
-                          row16_sum(hi_bf(o.y))};
-      if (i16 == kk) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) cs2a[e] += t[e];
-      }
+      tail::acc4(rw + 16 * kk + 4 * q, o);
     }
   }
 
   // ---- per-workgroup partials: the 8 waves' column sums / loss / correct, fixed order -------
-  float LDS_AS* rw = red + wave * G::RC;
-  if (i16 < NKK) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) rw[16 * i16 + 4 * q + e] = cs2a[e];
-  }
-  if (i16 < NJ) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) rw[K3 + 16 * i16 + 4 * q + e] = cs3a[e];
-  }
-  if (i16 == 0) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) rw[K3 + N3 + 4 * q + e] = cs4a[e];
-  }
   loss_a = wave_sum(loss_a);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) corr_a += __shfl_xor(corr_a, o, 64);

@@ -74,6 +74,16 @@ def _flags(sanitize: bool) -> tuple[list[str], list[str]]:
     return dev, host
 
 
+def _file_flags(src: Path) -> list[str]:
+    """Per-file compiler flags from a ``// build-flags: ...`` line in the first 40 lines (e.g.
+    mlp_tail.hip turns off SLP vectorisation, which splits DPP row sums into mov + packed add)."""
+    with open(src, encoding="utf-8") as f:
+        for _, line in zip(range(40), f):
+            if line.startswith("// build-flags:"):
+                return line.split(":", 1)[1].split()
+    return []
+
+
 def _compile(cmd: list[str]) -> tuple[list[str], int, str]:
     r = subprocess.run(cmd, capture_output=True, text=True)
     return cmd, r.returncode, r.stdout + r.stderr
@@ -98,7 +108,7 @@ def build(force: bool = False, jobs: int | None = None, sanitize: bool = False,
         objs.append(obj)
         if force or not obj.exists() or obj.stat().st_mtime < src.stat().st_mtime:
             base = dev_cmd if src.suffix == ".hip" else host_cmd
-            jobs_to_run.append([*base, "-c", str(src), "-o", str(obj)])
+            jobs_to_run.append([*base, *_file_flags(src), "-c", str(src), "-o", str(obj)])
 
     if jobs_to_run:
         n = jobs or min(8, os.cpu_count() or 4)
