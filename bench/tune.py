@@ -87,7 +87,7 @@ def step_ms(spec, R, x, y, dev, steps, reps):
 
 
 def tune_config(R, model, dev, table, steps, reps, log, only=None, verbose=False,
-                persist_opts=(0,)):
+                persist_opts=(0,), blas="1"):
     spec = NAMED_MODELS.get(model) or MLPSpec.parse(model)
     kp0 = (spec.layers[0].in_dim + 63) // 64 * 64
     xs, ys = synthetic_mnist(min(R, 65536), seed=3)
@@ -105,31 +105,45 @@ def tune_config(R, model, dev, table, steps, reps, log, only=None, verbose=False
             continue
         prev = table.get(k)
         res = []
-        for (tile, s) in cands:
-            # 256x256 tiles also run the ping-pong form (stages 8, gemm_pp.hip)
-            forms = [(2, pers) for pers in persist_opts]
-            if tuple(tile) == (256, 256):
-                forms.append((8, 0))
-            for ns, pers in forms:
-                table[k] = {"tile": list(tile), "splits": s, "stages": ns, "persist": pers}
-                try:
-                    res.append((step_ms(spec, R, x, y, dev, steps, reps), tile, s, pers, ns))
-                    if verbose:
-                        log({"cand": k, "tile": list(tile), "splits": s, "persist": pers,
-                             "stages": ns, "step_ms": round(res[-1][0], 4)})
-                except (ValueError, RuntimeError) as e:
-                    log({"skip": k, "tile": tile, "splits": s, "persist": pers, "stages": ns,
-                         "err": str(e)[:80]})
-        ms, tile, s, pers, ns = min(res)
+        trials = []  # (tile, splits, stages, persist, blas)
+        if blas == "only" and prev is not None:
+            # incumbent vs the library GEMM only (csrc/runtime/blaslt.cpp)
+            trials.append((tuple(prev["tile"]), prev["splits"], prev.get("stages", 2),
+                           prev.get("persist", 0), 0))
+        else:
+            for (tile, s) in cands:
+                # 256x256 tiles also run the ping-pong form (stages 8, gemm_pp.hip)
+                forms = [(2, pers) for pers in persist_opts]
+                if tuple(tile) == (256, 256):
+                    forms.append((8, 0))
+                trials += [(tuple(tile), s, ns, pers, 0) for ns, pers in forms]
+        if blas in ("1", "only"):
+            tile0 = tuple(prev["tile"]) if prev else tuple(cands[0][0])
+            trials.append((tile0, 1, 2, 0, 1))
+        for tile, s, ns, pers, bl in trials:
+            table[k] = {"tile": list(tile), "splits": s, "stages": ns, "persist": pers,
+                        "blas": bl}
+            try:
+                res.append((step_ms(spec, R, x, y, dev, steps, reps), tile, s, pers, ns, bl))
+                if verbose:
+                    log({"cand": k, "tile": list(tile), "splits": s, "persist": pers,
+                         "stages": ns, "blas": bl, "step_ms": round(res[-1][0], 4)})
+            except (ValueError, RuntimeError) as e:
+                log({"skip": k, "tile": tile, "splits": s, "persist": pers, "stages": ns,
+                     "blas": bl, "err": str(e)[:80]})
+        ms, tile, s, pers, ns, bl = min(res)
         # keep the incumbent unless the challenger wins by more than noise (0.5 %)
         if prev is not None:
             inc = [r for r in res if list(r[1]) == prev["tile"] and r[2] == prev["splits"]
-                   and r[3] == prev.get("persist", 0) and r[4] == prev.get("stages", 2)]
+                   and r[3] == prev.get("persist", 0) and r[4] == prev.get("stages", 2)
+                   and r[5] == prev.get("blas", 0)]
             if inc and inc[0][0] <= ms * 1.005:
-                ms, tile, s, pers, ns = inc[0]
+                ms, tile, s, pers, ns, bl = inc[0]
         table[k] = {"tile": list(tile), "splits": s, "stages": ns, "persist": pers,
                     "step_ms": round(ms, 4), "model": model}
-        log({"sig": k, "best": [list(tile), s, pers, ns], "step_ms": round(ms, 4),
+        if bl:
+            table[k]["blas"] = 1
+        log({"sig": k, "best": [list(tile), s, pers, ns, bl], "step_ms": round(ms, 4),
              "worst_ms": round(max(r[0] for r in res), 4), "n": len(res)})
     final = step_ms(spec, R, x, y, dev, steps, reps)
     log({"rows": R, "model": model, "start_ms": round(base, 4), "final_ms": round(final, 4)})
@@ -147,7 +161,11 @@ def main():
     ap.add_argument("--persist", default="0,1",
                     help="GEMM forms to try: 0 = one tile per workgroup (gemm.hip), 1 = "
                     "persistent workgroups (gemm_persist.hip)")
+    ap.add_argument("--blas", default="1", choices=["0", "1", "only"],
+                    help="hipBLASLt library GEMM as a candidate: 0 no, 1 yes, only = incumbent "
+                    "vs library per GEMM (quick)")
     a = ap.parse_args()
+    os.environ.pop("DNN_BLAS", None)  # the table decides while tuning
     dev = torch.device("cuda")
     doc = {"device": torch.cuda.get_device_name(0), "generated_by": "bench/tune.py",
            "objective": "training step time (1 GPU, batched wgrad, SGD)",
@@ -167,7 +185,7 @@ def main():
         rows, model = cfg.split(":")
         tune_config(int(rows), model, dev, table, a.steps, a.reps, log,
                     only=set(a.only.split(",")) if a.only else None, verbose=a.verbose,
-                    persist_opts=tuple(int(v) for v in a.persist.split(",")))
+                    persist_opts=tuple(int(v) for v in a.persist.split(",")), blas=a.blas)
         doc["entries"] = dict(table)
         with open(a.out, "w") as f:
             json.dump(doc, f, indent=1, sort_keys=True)

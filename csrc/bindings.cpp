@@ -18,6 +18,7 @@
 #include "kernels/gemm.hpp"
 #include "kernels/gemv.hpp"
 #include "kernels/mlp_tail.hpp"
+#include "runtime/blaslt.hpp"
 #include "runtime/graph.hpp"
 #include "runtime/json_weights.hpp"
 #include "runtime/matrix_codec.hpp"
@@ -52,6 +53,7 @@ static void check(int rc, const char* what) {
     std::string msg = std::string(what) + " failed: ";
     if (std::string(what).rfind("gemm_bf16", 0) == 0) msg += dnn::gemm_error_string(rc);
     else if (std::string(what) == "mlp_tail") msg += dnn::mlp_tail_error(rc);
+    else if (std::string(what) == "blas_gemm") msg += dnn::blas_error(rc);
     else msg += "precondition/launch error code " + std::to_string(rc);
     if (rc == -9) msg += std::string(" (") + hipGetErrorString(hipGetLastError()) + ")";
     throw std::invalid_argument(msg);
@@ -257,6 +259,49 @@ PYBIND11_MODULE(_native, m) {
       py::arg("M"), py::arg("K3"), py::arg("N3"), py::arg("N4"), py::arg("n_cls"),
       py::arg("scale"), py::arg("act3"), py::arg("act2"), py::arg("stream"));
   m.def("mlp_tail_blocks", &dnn::mlp_tail_blocks);
+  m.def(
+      "blas_gemm",
+      [](int trans_a, int trans_b, int M, int N, int K, uintptr_t a, long lda, uintptr_t b,
+         long ldb, uintptr_t d, long ldd, int d_f32, uintptr_t bias, int relu, int accumulate,
+         uintptr_t stream) {
+        launch(
+            "blas_gemm",
+            [=](hipStream_t s, const dnn::Program& R) {
+              dnn::BlasGemm g{};
+              g.trans_a = trans_a;
+              g.trans_b = trans_b;
+              g.M = M;
+              g.N = N;
+              g.K = K;
+              g.A = R.fix(P<const uint16_t>(a));
+              g.lda = lda;
+              g.B = R.fix(P<const uint16_t>(b));
+              g.ldb = ldb;
+              g.D = R.fix(P<void>(d));
+              g.ldd = ldd;
+              g.d_f32 = d_f32;
+              g.bias = R.fix(P<const float>(bias));
+              g.relu = relu;
+              g.accumulate = accumulate;
+              return dnn::blas_gemm(g, s);
+            },
+            stream);
+      },
+      py::arg("trans_a"), py::arg("trans_b"), py::arg("M"), py::arg("N"), py::arg("K"),
+      py::arg("a"), py::arg("lda"), py::arg("b"), py::arg("ldb"), py::arg("d"), py::arg("ldd"),
+      py::arg("d_f32"), py::arg("bias"), py::arg("relu"), py::arg("accumulate"),
+      py::arg("stream"));
+  m.def("blas_available", &dnn::blas_available);
+  m.def("dact_colsum", [](uintptr_t x, long ld, uintptr_t aux, long ld_aux, int act, int rows,
+                          int cols, int n_part, uintptr_t part, uintptr_t stream) {
+    launch(
+        "dact_colsum",
+        [=](hipStream_t s, const dnn::Program& R) {
+          return dnn::dact_colsum(R.fix(P<uint16_t>(x)), ld, R.fix(P<const uint16_t>(aux)),
+                                  ld_aux, act, rows, cols, n_part, R.fix(P<float>(part)), s);
+        },
+        stream);
+  });
   m.def("softmax_rows", [](uintptr_t logits, long ld_in, uintptr_t out, long ld_out, int rows,
                            int n_cls, uintptr_t labels, uintptr_t pred, uintptr_t correct,
                            uintptr_t stream) {

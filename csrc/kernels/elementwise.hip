@@ -220,9 +220,14 @@ int softmax_rows(const float* logits, long ld_in, float* out, long ld_out, int r
 // Block = 64 columns x (32 row lanes); grid.y = number of partial row blocks. Writes
 // part[blockIdx.y][cols]; the optimizer-side reduce_slabs finishes the sum deterministically.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void colsum_partial_kernel(const u16* __restrict__ x, long ld,
+// With `aux` (dact_colsum): x = act'(aux) * x is applied in place first (the library-GEMM
+// dgrad's epilogue, csrc/runtime/blaslt.hpp) and the sums are of the stored bf16 values.
+template <bool DACT>
+__global__ __launch_bounds__(256) void colsum_partial_kernel(u16* __restrict__ x, long ld,
                                                              int rows, int cols, int rows_per,
-                                                             float* __restrict__ part) {
+                                                             float* __restrict__ part,
+                                                             const u16* __restrict__ aux,
+                                                             long ld_aux, int act) {
   __shared__ float red[32][65];
   const int cc = threadIdx.x & 7;   // 8-column chunk within the 64-column strip
   const int rl = threadIdx.x >> 3;  // row lane 0..31
@@ -231,14 +236,20 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const u16* __restri
   const int r_end = min(rows, r_begin + rows_per);
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (int r = r_begin + rl; r < r_end; r += 32) {
-    const bf16x8_t v = *(const bf16x8_t*)(x + (long)r * ld + col0);
+    bf16x8_t v = *(const bf16x8_t*)(x + (long)r * ld + col0);
+    if constexpr (DACT) {
+      const bf16x8_t y = *(const bf16x8_t*)(aux + (long)r * ld_aux + col0);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (short)f2bf(act_bwd(bf2f((u16)v[e]), bf2f((u16)y[e]), act));
+      *(bf16x8_t*)(x + (long)r * ld + col0) = v;
+    }
 #pragma unroll
     for (int e = 0; e < 8; ++e) s[e] += bf2f((u16)v[e]);
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) red[rl][cc * 8 + e] = s[e];
   __syncthreads();
-  if (threadIdx.x < 64) {
+  if (threadIdx.x < 64 && part) {
     float t = 0.f;
 #pragma unroll 8
     for (int i = 0; i < 32; ++i) t += red[i][threadIdx.x];
@@ -251,8 +262,20 @@ int colsum_partial(const uint16_t* x, long ld, int rows, int cols, int n_part, f
   if (rows <= 0 || cols <= 0 || cols % 64 || ld % 8 || ld < cols || n_part <= 0) return -1;
   if (((uintptr_t)x) & 15) return -5;
   const int rows_per = (rows + n_part - 1) / n_part;
-  hipLaunchKernelGGL(colsum_partial_kernel, dim3(cols / 64, n_part), dim3(256), 0, stream, x, ld,
-                     rows, cols, rows_per, part);
+  hipLaunchKernelGGL(colsum_partial_kernel<false>, dim3(cols / 64, n_part), dim3(256), 0, stream,
+                     const_cast<u16*>(x), ld, rows, cols, rows_per, part, nullptr, 0L, 0);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
+int dact_colsum(uint16_t* x, long ld, const uint16_t* aux, long ld_aux, int act, int rows,
+                int cols, int n_part, float* part, hipStream_t stream) {
+  if (rows <= 0 || cols <= 0 || cols % 64 || ld % 8 || ld < cols || ld_aux % 8 || n_part <= 0 ||
+      !aux)
+    return -1;
+  if ((((uintptr_t)x) | ((uintptr_t)aux)) & 15) return -5;
+  const int rows_per = (rows + n_part - 1) / n_part;
+  hipLaunchKernelGGL(colsum_partial_kernel<true>, dim3(cols / 64, n_part), dim3(256), 0, stream,
+                     x, ld, rows, cols, rows_per, part, aux, ld_aux, act);
   return hipGetLastError() == hipSuccess ? 0 : -9;
 }
 

@@ -14,6 +14,9 @@ int softmax_xent(const float* logits, long ld_logits, const int* labels, uint16_
 int softmax_xent_blocks(int rows);
 int softmax_rows(const float* logits, long ld_in, float* out, long ld_out, int rows, int n_cls,
                  const int* labels, int* pred, int* correct, hipStream_t stream);
+// x = act'(aux) * x in place, then colsum_partial of the result (library-GEMM dgrad epilogue).
+int dact_colsum(uint16_t* x, long ld, const uint16_t* aux, long ld_aux, int act, int rows,
+                int cols, int n_part, float* part, hipStream_t stream);
 int colsum_partial(const uint16_t* x, long ld, int rows, int cols, int n_part, float* part,
                    hipStream_t stream);
 int reduce_slabs(const float* src, long stride, int n_src, long n, float scale, float* out,

@@ -122,7 +122,7 @@ def build(force: bool = False, jobs: int | None = None, sanitize: bool = False,
     newest = max(o.stat().st_mtime for o in objs)
     if force or jobs_to_run or not out.exists() or out.stat().st_mtime < newest:
         link = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(out),
-                *map(str, objs), f"-L{ROCM / 'lib'}", "-lamdhip64"]
+                *map(str, objs), f"-L{ROCM / 'lib'}", "-lamdhip64", "-lhipblaslt"]
         if sanitize:
             link += ["-fsanitize=address,undefined"]
         cmd, rc, log = _compile(link)

@@ -77,6 +77,41 @@ def _persist(kind: str, entry) -> int:
     return -1 if v == 1 else int(v)
 
 
+def _blas(kind: str, entry) -> bool:
+    """Library (hipBLASLt) GEMM for this product? DNN_BLAS: "" / "table" = the tuned table's
+    ``blas`` flag, "0" = never, "1" = every product the library path supports, or per kind
+    ("fwd=1,dgrad=0,wgrad=1")."""
+    spec = os.environ.get("DNN_BLAS", "").strip()
+    if spec in ("", "table"):
+        return bool((entry or {}).get("blas", 0))
+    if "=" not in spec:
+        return spec == "1"
+    return dict(kv.split("=") for kv in spec.split(",")).get(kind, "0") == "1"
+
+
+def blas_gemm(a, b, d, *, trans_a: bool, trans_b: bool, M: int, N: int, K: int, bias=None,
+              relu: bool = False, accumulate: bool = False):
+    """hipBLASLt library GEMM (csrc/runtime/blaslt.hpp), row-major: d[M][N] (+)= op(a).op(b)
+    (+ bias, ReLU), a = [M][K] or (trans_a) [K][M], b = [K][N] or (trans_b) [N][K]."""
+    if not a.is_cuda:
+        raise ValueError("blas_gemm is a GPU path")
+    for t, name in ((a, "a"), (b, "b")):
+        _rows(t, name, torch.bfloat16)
+    if d.dtype not in (torch.bfloat16, torch.float32) or d.stride(-1) != 1:
+        raise ValueError("d must be a row-major bf16 or fp32 matrix")
+    native().blas_gemm(int(trans_a), int(trans_b), M, N, K, _p(a), a.stride(0), _p(b),
+                       b.stride(0), _p(d), d.stride(-2), int(d.dtype == torch.float32),
+                       _p(bias), int(relu), int(accumulate), _stream(a))
+
+
+def dact_colsum(x, aux, act, part=None, n_part: int = 1):
+    """x = act'(aux) * x in place (bf16), and (optional) part[n_part][cols] = column sums of the
+    result over n_part row blocks: the epilogue of a library-GEMM dgrad."""
+    rows, cols = x.shape
+    native().dact_colsum(_p(x), x.stride(0), _p(aux), aux.stride(0), _act(act), rows, cols,
+                         n_part, _p(part), _stream(x))
+
+
 def _stream(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 
@@ -147,6 +182,8 @@ def wgrad_config(M: int, N: int, K_total: int, max_splits: int = 48) -> tuple[in
     """Joint (bm, bn, splits) choice for the batch-contraction GEMM (see pick_splits): the
     tuned table's measured optimum when it has the shape, else the model below."""
     t = tuning.lookup("wgrad", M, N, K_total)
+    if _blas("wgrad", t):  # the library GEMM contracts all rows in one fp32 output
+        return (t["tile"][0], t["tile"][1], 1) if t else (*pick_tiles(M, N), 1)
     if t is not None:
         return t["tile"][0], t["tile"][1], t["splits"]
     ksteps = K_total // 64
@@ -277,6 +314,9 @@ def linear_fwd(x, w, bias, y, act="relu", mask=None):
     if M <= GEMV_MAX_ROWS:
         return gemv(x, w, bias, y, act)
     t = tuning.lookup("fwd", M, N, K)
+    if mask is None and act in ("relu", "linear", 0, 1) and _blas("fwd", t):
+        return blas_gemm(x, w, y, trans_a=False, trans_b=True, M=M, N=N, K=K, bias=bias,
+                         relu=_act(act) == 1)
     tiles = tuple(t["tile"]) if t else pick_tiles(M, N)
     return gemm(x, w, y, layout_a=KMAJ, layout_b=KMAJ, M=M, N=N, K=K, bias=bias, act=act,
                 tiles=tiles, stages=STAGES["fwd"] or (t or {}).get("stages", 0),
@@ -346,6 +386,14 @@ def linear_dgrad(dz, w, dx, y_prev=None, act_prev="linear", colsum=None, mask_pr
     elif y_prev is None:
         act_prev = "linear"
     t = tuning.lookup("dgrad", M, K, N)
+    if mask_prev is None and dz.is_cuda and _blas("dgrad", t):
+        blas_gemm(dz, w, dx, trans_a=False, trans_b=False, M=M, N=K, K=N)
+        n_part = -(-M // dgrad_tiles(M, K, N)[0])
+        if y_prev is not None and _act(act_prev) != 0:
+            dact_colsum(dx, y_prev, act_prev, colsum, n_part)
+        elif colsum is not None:
+            colsum_partial(dx, colsum, n_part)
+        return dx
     return gemm(dz, w, dx, layout_a=KMAJ, layout_b=MNMAJ, M=M, N=K, K=N, aux=y_prev,
                 act=act_prev, tiles=dgrad_tiles(M, K, N), colsum=colsum,
                 stages=STAGES["dgrad"] or (t or {}).get("stages", 0),
@@ -362,6 +410,9 @@ def linear_wgrad(dz, x, slabs, splits=1, accumulate=False):
     bm, bn, s = wgrad_config(N, K, R)
     tiles = (bm, bn) if s == splits else pick_tiles(N, K, splits)
     t = tuning.lookup("wgrad", N, K, R) if s == splits else None
+    if splits == 1 and dz.is_cuda and _blas("wgrad", tuning.lookup("wgrad", N, K, R)):
+        return blas_gemm(dz, x, slabs[0], trans_a=True, trans_b=False, M=N, N=K, K=R,
+                         accumulate=accumulate)
     return gemm(dz, x, slabs, layout_a=MNMAJ, layout_b=MNMAJ, M=N, N=K, K=R, k_total=R,
                 accumulate=accumulate, splits=splits, tiles=tiles,
                 stages=STAGES["wgrad"] or (t or {}).get("stages", 0),

@@ -9,7 +9,8 @@ Signatures (the GEMM as the kernel sees it: C[M][N] = sum over K):
   fwd   : M = rows, N = layer output width, K = layer input width (padded)
   dgrad : M = rows, N = layer input width,  K = layer output width
   wgrad : M = layer output width, N = layer input width, K = rows (split-K contraction)
-``DNN_TUNED=0`` disables the table (A/B against the rules).
+``DNN_TUNED=0`` disables the table (A/B against the rules); ``DNN_TUNED_TABLE`` reads another
+table file (A/B of two tunings).
 """
 from __future__ import annotations
 
@@ -17,7 +18,8 @@ import json
 import os
 from typing import Optional
 
-TABLE_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_gfx950.json")
+TABLE_PATH = (os.environ.get("DNN_TUNED_TABLE") or
+              os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_gfx950.json"))
 _table: Optional[dict] = None
 
 

@@ -77,7 +77,8 @@ def _unfused(dev, x, w3, b3, w4, b4, labels, n_cls, scale, act="relu"):
                                                      (8192, 128, 128, 64, 1, "relu"),
                                                      (4096, 256, 128, 64, 10, "sigmoid"),
                                                      (1024, 64, 64, 128, 7, "linear")])
-def test_tail_equals_unfused_kernels(dev, rows, k3, n3, n4, n_cls, act):
+def test_tail_equals_unfused_kernels(dev, monkeypatch, rows, k3, n3, n4, n_cls, act):
+    monkeypatch.setenv("DNN_BLAS", "0")  # the reference is the hand-written kernels
     case = _case(rows, k3, n3, n4, n_cls, seed=rows + k3 + n3 + n_cls)
     scale = 1.0 / rows
     got = _run_tail(dev, *case, n_cls, scale, act)
