@@ -106,3 +106,30 @@ def test_blas_is_deterministic(dev, M, K, N):
         outs.append((y, d, gw))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("replay", ["graph", "native"])
+def test_inference_with_library_gemms_in_graph_and_program(dev, monkeypatch, replay):
+    """Serving buckets capture the forward in a HIP graph (or a recorded Program); a library
+    GEMM inside must capture and replay like the kernels (65536-row bucket of the headline
+    model hits the tuned 512->256 library forward)."""
+    import numpy as np
+
+    from docker_dist_nn_amd.config import LayerWeights
+    from docker_dist_nn_amd.engine.inference import InferenceEngine
+
+    monkeypatch.setenv("DNN_SERVE_REPLAY", replay)
+    dims = [784, 512, 256, 128, 10]
+    rng = np.random.default_rng(0)
+    layers = [LayerWeights(rng.standard_normal((dims[i + 1], dims[i])) / np.sqrt(dims[i]),
+                           rng.standard_normal(dims[i + 1]) * 0.1,
+                           "softmax" if i == len(dims) - 2 else "relu")
+              for i in range(len(dims) - 1)]
+    x = rng.standard_normal((65536, 784))
+    outs = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("DNN_BLAS", flag)
+        eng = InferenceEngine([[l] for l in layers], dev, expected_input=784)
+        eng.predict(x)
+        outs.append(eng.predict(x))
+    np.testing.assert_allclose(outs[1], outs[0], rtol=3e-2, atol=3e-3)
