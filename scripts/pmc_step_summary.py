@@ -30,7 +30,7 @@ for pas in ("sq", "fetch", "write"):
 print(f"{'kernel':72s} {'grid':>8s} {'us':>7s} {'rd MB':>7s} {'wr MB':>7s} {'TB/s':>6s} "
       f"{'MFMA%':>6s} {'LDSc%':>6s}")
 for key, c in sorted(vals.items(), key=lambda kv: kv[0][0]):
-    if "gemm" not in key[0] and "reduce" not in key[0] and "sgd" not in key[0]:
+    if not any(t in key[0] for t in ("gemm", "reduce", "sgd", "mlp_tail", "Cijk", "colsum")):
         continue
     m = {k: sum(v) / len(v) for k, v in c.items()}
     us = dur.get(key) or dur.get((key[0], ""), [0.0])
