@@ -136,3 +136,33 @@ def test_engine_tail_matches_unfused_training(dev, monkeypatch, num_micro):
     for a, b in zip(res[0][0], res[1][0]):
         assert abs(a - b) <= 1e-4 * abs(a) + 1e-5
     torch.testing.assert_close(res[1][1], res[0][1], rtol=1e-3, atol=1e-5)
+
+
+@pytest.mark.parametrize("schedule", ["1f1b", "gpipe"])
+def test_loopback_pipeline_last_stage_uses_tail(dev, monkeypatch, schedule):
+    """Two stages on one GPU, distribution [1, 3]: the last stage holds three layers, so its
+    tail kernel produces the dZ that its own first layer's dgrad sends upstream."""
+    from docker_dist_nn_amd import NAMED_MODELS
+    from docker_dist_nn_amd.data import synthetic_mnist
+    from docker_dist_nn_amd.engine import OptimConfig, Trainer
+
+    x, y = synthetic_mnist(4096, seed=9)
+    xb = torch.zeros(4096, 832, dtype=torch.bfloat16)
+    xb[:, :784] = torch.from_numpy(x).to(torch.bfloat16)
+    xb, yb = xb.to(dev), torch.from_numpy(y).to(dev)
+    res = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("DNN_TAIL", flag)
+        tr = Trainer(NAMED_MODELS["mnist-fcnn"], micro_batch=1024, num_micro=4, pp=2,
+                     distribution=[1, 3], schedule=schedule, optim=OptimConfig(lr=0.1),
+                     device=dev)
+        assert tr.stages[-1].tail == (flag == "1") and not tr.stages[0].tail
+        losses = []
+        for _ in range(3):
+            tr.set_batch(xb, yb)
+            tr.step()
+            losses.append(tr.loss())
+        res.append((losses, torch.cat([s.params.master for s in tr.stages]).clone()))
+    for a, b in zip(res[0][0], res[1][0]):
+        assert abs(a - b) <= 1e-4 * abs(a) + 1e-5
+    torch.testing.assert_close(res[1][1], res[0][1], rtol=1e-3, atol=1e-5)
