@@ -67,6 +67,17 @@ __device__ __forceinline__ void st8(char LDS_AS* p, uint2 v) {
   *(unsigned long long LDS_AS*)p = ((unsigned long long)v.y << 32) | v.x;
 }
 
+// Global store of two 16-column blocks (j, j + 1) of one row as 16-byte chunks: the lanes of
+// group q hold columns 4 q .. 4 q + 3 of each block; v_permlane16_swap regroups them so group
+// 0 / 1 / 2 / 3 holds columns 0..7 of j / 0..7 of j+1 / 8..15 of j / 8..15 of j+1 (the
+// register-direct epilogue of gemm_tile.hpp). `row` points at column 0 of the output row.
+__device__ __forceinline__ void st16_pair(u16* row, int j, int q, uint2 a, uint2 b) {
+  const auto s0 = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
+  const auto s1 = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
+  *(uint4*)(row + 16 * j + 16 * (q & 1) + 8 * (q >> 1)) =
+      make_uint4(s0[0], s1[0], s0[1], s1[1]);
+}
+
 // rw[0..3] += column sums over the 16 rows (lanes of a DPP row) of the 4 bf16 values in v
 // (the four butterflies run step-major so consecutive DPP adds are independent: a DPP read of a
 // VGPR written by the previous VALU instruction costs wait states)
@@ -196,8 +207,8 @@ __global__ __launch_bounds__(64 * tail::waves<RELU>()) void mlp_tail_kernel(Tail
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = act<RELU>(a3[j][e] + b3r[j][e], p.act3);
       h3p[j] = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-      *(uint2*)(p.H3 + row * p.ldh3 + col) = h3p[j];
       tail::st8(S + i16 * G::SP + col * 2, h3p[j]);
+      if (j & 1) tail::st16_pair(p.H3 + row * p.ldh3, j - 1, q, h3p[j - 1], h3p[j]);
     }
 
     // ---- logits (classes 0..15) = h3 . W4^T + b4; softmax cross-entropy ------------------
@@ -244,15 +255,16 @@ __global__ __launch_bounds__(64 * tail::waves<RELU>()) void mlp_tail_kernel(Tail
       }
     }
     const uint2 d4 = make_uint2(pack_bf16x2(dz[0], dz[1]), pack_bf16x2(dz[2], dz[3]));
-    *(uint2*)(p.DZ4 + row * p.lddz4 + 4 * q) = d4;
-    for (int c = tail::MAX_CLS + 4 * q; c < p.N4; c += 16)
-      *(uint2*)(p.DZ4 + row * p.lddz4 + c) = make_uint2(0u, 0u);
+    tail::st16_pair(p.DZ4 + row * p.lddz4, 0, q, d4, make_uint2(0u, 0u));  // columns 0..31
+    for (int c = 2 * tail::MAX_CLS + 8 * q; c < p.N4; c += 32)
+      *(uint4*)(p.DZ4 + row * p.lddz4 + c) = make_uint4(0u, 0u, 0u, 0u);
     tail::acc4(rw + K3 + N3 + 4 * q, d4);
 
     // ---- dz3 = (dz4 . W4) * act3'(h3): contraction over classes 0..31 -------------------
     tail::st8(D + i16 * G::DP + 8 * q, d4);
     tail::st8(D + i16 * G::DP + 32 + 8 * q, make_uint2(0u, 0u));
     const bf16x8_t df = *(const bf16x8_t LDS_AS*)(D + i16 * G::DP + 16 * q);
+    uint2 prev = make_uint2(0u, 0u);
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const f32x4_t a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
@@ -263,7 +275,8 @@ __global__ __launch_bounds__(64 * tail::waves<RELU>()) void mlp_tail_kernel(Tail
       for (int e = 0; e < 4; ++e) v[e] = dact<RELU>(a[e], y[e], p.act3);
       const uint2 o = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
       const int col = 16 * j + 4 * q;
-      *(uint2*)(p.DZ3 + row * p.lddz3 + col) = o;
+      if (j & 1) tail::st16_pair(p.DZ3 + row * p.lddz3, j - 1, q, prev, o);
+      prev = o;
       tail::st8(S + i16 * G::SP + col * 2, o);
       tail::acc4(rw + K3 + col, o);
     }
@@ -285,7 +298,8 @@ __global__ __launch_bounds__(64 * tail::waves<RELU>()) void mlp_tail_kernel(Tail
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = dact<RELU>(a[e], y[e], p.act2);
       const uint2 o = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-      *(uint2*)(p.DZ2 + row * p.lddz2 + 16 * kk + 4 * q) = o;
+      if (kk & 1) tail::st16_pair(p.DZ2 + row * p.lddz2, kk - 1, q, prev, o);
+      prev = o;
       tail::acc4(rw + 16 * kk + 4 * q, o);
     }
   }
