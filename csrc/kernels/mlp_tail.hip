@@ -7,21 +7,22 @@
 // ~370 us step while their data is ~110 MB (23 us of HBM time). Their weights are 64 + 16 KiB,
 // so they live in LDS for the whole launch and every intermediate stays on chip.
 //
-// Structure (one workgroup per CU, 8 waves, each wave walks 16-row blocks):
+// Structure (one workgroup per CU; 8 waves for the ReLU form, 4 for other activations; each
+// wave walks 16-row blocks):
 //   * W3 [N3][K3] and W4 [64][N3] are staged once into LDS with LDS-DMA, in the MNMAJ image
 //     layout of gemm_tile.hpp: the forward reads them row-wise (16-B chunks), the dgrads read
 //     them transposed with ds_read_b64_tr_b16 (load_frag<MNMAJ>), so no transposed copy exists;
 //   * every product is computed with SWAPPED operands, mfma(W-fragment, X-fragment): a lane
 //     then holds 4 consecutive output features of ONE data row (row = lane & 15, features
 //     16 j + 4 (lane >> 4) + r), which is the layout of the bias/activation epilogue, of the
-//     8-byte stores, of the ReLU derivative of the next dgrad, and of the softmax (a row's 16
-//     class logits sit in 4 lanes);
+//     ReLU derivative of the next dgrad, and of the softmax (a row's 16 class logits sit in 4
+//     lanes); global stores pair two such blocks into 16-byte chunks (v_permlane16_swap);
 //   * an output that feeds the next product is written to a 16-row per-wave LDS scratch and
 //     read back as the next MFMA's B fragment (same-wave LDS order, no barrier);
 //   * the next block's input rows are loaded while the current block computes;
-//   * bias-gradient column sums: DPP row sums per block, accumulated in registers across the
-//     wave's blocks, reduced over the 8 waves in fixed order at the end (one partial per
-//     workgroup); softmax and loss follow xent_rows (gemm_tile.hpp) operation for operation.
+//   * bias-gradient column sums: DPP row sums per block, accumulated across the wave's blocks
+//     in the wave's own LDS row, reduced over the waves in fixed order at the end (one partial
+//     per workgroup); softmax and loss follow xent_rows (gemm_tile.hpp) operation for operation.
 // Every MFMA chain accumulates its contraction in the same ascending k order as the unfused
 // GEMMs, so h3, dz4, dz3 and dz2 equal the unfused path's bit for bit (tests/test_mlp_tail_gpu.py).
 //
