@@ -292,6 +292,24 @@ PYBIND11_MODULE(_native, m) {
       py::arg("d_f32"), py::arg("bias"), py::arg("relu"), py::arg("accumulate"),
       py::arg("stream"));
   m.def("blas_available", &dnn::blas_available);
+  m.def("blas_supported", [](int trans_a, int trans_b, int M, int N, int K, long lda, long ldb,
+                             long ldd, int d_f32, int has_bias, int relu, int accumulate) {
+    dnn::BlasGemm g{};
+    g.trans_a = trans_a;
+    g.trans_b = trans_b;
+    g.M = M;
+    g.N = N;
+    g.K = K;
+    g.lda = lda;
+    g.ldb = ldb;
+    g.ldd = ldd;
+    g.d_f32 = d_f32;
+    static const float one = 0.f;
+    g.bias = has_bias ? &one : nullptr;  // only its presence selects the epilogue
+    g.relu = relu;
+    g.accumulate = accumulate;
+    return dnn::blas_supported(g);
+  });
   m.def("dact_colsum", [](uintptr_t x, long ld, uintptr_t aux, long ld_aux, int act, int rows,
                           int cols, int n_part, uintptr_t part, uintptr_t stream) {
     launch(

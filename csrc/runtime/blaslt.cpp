@@ -130,6 +130,13 @@ const char* blas_error(int code) {
   }
 }
 
+int blas_supported(const BlasGemm& g) {
+  if (g.M <= 0 || g.N <= 0 || g.K <= 0 || (g.accumulate && !g.d_f32)) return 0;
+  std::lock_guard<std::mutex> lock(mu);
+  if (!init()) return 0;
+  return plan_for(g)->ok ? 1 : 0;
+}
+
 int blas_available() {
   std::lock_guard<std::mutex> lock(mu);
   return init() ? 1 : 0;

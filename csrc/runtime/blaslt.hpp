@@ -36,7 +36,9 @@ struct BlasGemm {
 // 0 on success; < 0: -1 bad arguments, -2 library error, -3 no algorithm for the problem.
 int blas_gemm(const BlasGemm& g, hipStream_t stream);
 const char* blas_error(int code);
-// Whether the library was initialised and found an algorithm for a problem (probe).
+// Whether the library initialises at all, and whether it has an algorithm for a problem
+// signature (pointers are ignored; the plan is cached for the later calls).
 int blas_available();
+int blas_supported(const BlasGemm& g);
 
 }  // namespace dnn

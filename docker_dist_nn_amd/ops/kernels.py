@@ -89,6 +89,22 @@ def _blas(kind: str, entry) -> bool:
     return dict(kv.split("=") for kv in spec.split(",")).get(kind, "0") == "1"
 
 
+_BLAS_OK: dict = {}
+
+
+def _blas_ok(a, b, d, trans_a, trans_b, M, N, K, bias, relu, accumulate) -> bool:
+    """Does hipBLASLt have an algorithm for this problem signature? (probed once per signature;
+    a table entry that asks for the library falls back to the MFMA kernels when it has none)"""
+    key = (trans_a, trans_b, M, N, K, a.stride(0), b.stride(0), d.stride(-2),
+           d.dtype == torch.float32, bias is not None, relu, accumulate)
+    ok = _BLAS_OK.get(key)
+    if ok is None:
+        ok = _BLAS_OK[key] = bool(native().blas_supported(
+            int(trans_a), int(trans_b), M, N, K, a.stride(0), b.stride(0), d.stride(-2),
+            int(d.dtype == torch.float32), int(bias is not None), int(relu), int(accumulate)))
+    return ok
+
+
 def blas_gemm(a, b, d, *, trans_a: bool, trans_b: bool, M: int, N: int, K: int, bias=None,
               relu: bool = False, accumulate: bool = False):
     """hipBLASLt library GEMM (csrc/runtime/blaslt.hpp), row-major: d[M][N] (+)= op(a).op(b)
@@ -314,7 +330,8 @@ def linear_fwd(x, w, bias, y, act="relu", mask=None):
     if M <= GEMV_MAX_ROWS:
         return gemv(x, w, bias, y, act)
     t = tuning.lookup("fwd", M, N, K)
-    if mask is None and act in ("relu", "linear", 0, 1) and _blas("fwd", t):
+    if mask is None and act in ("relu", "linear", 0, 1) and _blas("fwd", t) and \
+            _blas_ok(x, w, y, False, True, M, N, K, bias, _act(act) == 1, False):
         return blas_gemm(x, w, y, trans_a=False, trans_b=True, M=M, N=N, K=K, bias=bias,
                          relu=_act(act) == 1)
     tiles = tuple(t["tile"]) if t else pick_tiles(M, N)
@@ -386,7 +403,8 @@ def linear_dgrad(dz, w, dx, y_prev=None, act_prev="linear", colsum=None, mask_pr
     elif y_prev is None:
         act_prev = "linear"
     t = tuning.lookup("dgrad", M, K, N)
-    if mask_prev is None and dz.is_cuda and _blas("dgrad", t):
+    if mask_prev is None and dz.is_cuda and _blas("dgrad", t) and \
+            _blas_ok(dz, w, dx, False, False, M, K, N, None, False, False):
         blas_gemm(dz, w, dx, trans_a=False, trans_b=False, M=M, N=K, K=N)
         n_part = -(-M // dgrad_tiles(M, K, N)[0])
         if y_prev is not None and _act(act_prev) != 0:
@@ -410,7 +428,8 @@ def linear_wgrad(dz, x, slabs, splits=1, accumulate=False):
     bm, bn, s = wgrad_config(N, K, R)
     tiles = (bm, bn) if s == splits else pick_tiles(N, K, splits)
     t = tuning.lookup("wgrad", N, K, R) if s == splits else None
-    if splits == 1 and dz.is_cuda and _blas("wgrad", tuning.lookup("wgrad", N, K, R)):
+    if splits == 1 and dz.is_cuda and _blas("wgrad", tuning.lookup("wgrad", N, K, R)) and \
+            _blas_ok(dz, x, slabs[0], True, False, N, K, R, None, False, accumulate):
         return blas_gemm(dz, x, slabs[0], trans_a=True, trans_b=False, M=N, N=K, K=R,
                          accumulate=accumulate)
     return gemm(dz, x, slabs, layout_a=MNMAJ, layout_b=MNMAJ, M=N, N=K, K=R, k_total=R,

@@ -133,3 +133,21 @@ def test_inference_with_library_gemms_in_graph_and_program(dev, monkeypatch, rep
         eng.predict(x)
         outs.append(eng.predict(x))
     np.testing.assert_allclose(outs[1], outs[0], rtol=3e-2, atol=3e-3)
+
+
+def test_blas_probe_and_fallback(dev, monkeypatch):
+    """The per-signature probe finds algorithms for the products the tuned table routes to the
+    library; a forced-library product still runs (and matches) through linear_fwd."""
+    from docker_dist_nn_amd.ops import kernels as K
+
+    x = torch.randn(4096, 1024, device=dev).to(torch.bfloat16)
+    w = (torch.randn(1024, 1024, device=dev) * 0.03).to(torch.bfloat16)
+    b = torch.zeros(1024, device=dev)
+    y = torch.empty(4096, 1024, device=dev, dtype=torch.bfloat16)
+    assert K._blas_ok(x, w, y, False, True, 4096, 1024, 1024, b, True, False)
+    monkeypatch.setenv("DNN_BLAS", "1")
+    K.linear_fwd(x, w, b, y, act="relu")
+    monkeypatch.setenv("DNN_BLAS", "0")
+    y0 = torch.empty_like(y)
+    K.linear_fwd(x, w, b, y0, act="relu")
+    _close(y, y0)
