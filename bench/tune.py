@@ -41,8 +41,9 @@ def signatures(spec, R):
     for i, (kp, np_) in enumerate(geoms):
         last = i == len(geoms) - 1
         sigs = []
-        if not (last and np_ in (64, 128)):  # the fused linear+CE GEMM has a fixed tile
-            sigs.append(("fwd", R, np_, kp))
+        # the fused linear+CE GEMM has a fixed tile; its only alternative is the library
+        # logits GEMM + the softmax-CE kernel (candidate list "logits" below)
+        sigs.append(("fwd", R, np_, kp))
         if i > 0:
             sigs.append(("dgrad", R, kp, np_))
         sigs.append(("wgrad", np_, kp, R))
@@ -61,6 +62,8 @@ def signatures(spec, R):
                         s = max(1, min(K // 64, round(k * 256 / nt)))
                         if ((bm, bn), s) not in cands:
                             cands.append(((bm, bn), s))
+            elif op == "fwd" and last and np_ in (64, 128):
+                cands = "logits"
             else:
                 cands = [((bm, bn), 1) for (bm, bn) in TILES if M % bm == 0 and N % 64 == 0]
             out.append((op, M, N, K, cands))
@@ -106,6 +109,26 @@ def tune_config(R, model, dev, table, steps, reps, log, only=None, verbose=False
         prev = table.get(k)
         res = []
         trials = []  # (tile, splits, stages, persist, blas)
+        if cands == "logits":  # fused linear+CE (no table entry) vs library logits + CE kernel
+            if blas == "0":
+                continue
+            fused_ms = None
+            table.pop(k, None)
+            try:
+                fused_ms = step_ms(spec, R, x, y, dev, steps, reps)
+                table[k] = {"tile": [256, 64], "splits": 1, "stages": 2, "persist": 0, "blas": 1,
+                            "model": model}
+                lib_ms = step_ms(spec, R, x, y, dev, steps, reps)
+            except (ValueError, RuntimeError) as e:
+                log({"skip": k, "err": str(e)[:80]})
+                lib_ms = float("inf")
+            if fused_ms is None or lib_ms >= fused_ms * 0.995:
+                table.pop(k, None)
+            else:
+                table[k]["step_ms"] = round(lib_ms, 4)
+            log({"sig": k, "fused_ms": fused_ms and round(fused_ms, 4),
+                 "library_ms": round(lib_ms, 4), "library": k in table})
+            continue
         if blas == "only" and prev is not None:
             # incumbent vs the library GEMM only (csrc/runtime/blaslt.cpp)
             trials.append((tuple(prev["tile"]), prev["splits"], prev.get("stages", 2),

@@ -285,7 +285,8 @@ class Stage:
         # count is one 64/128-wide tile: logits then never exist in memory
         gl = self.geoms[-1]
         self.fused_xent = (self.last and gl.np_ in (64, 128) and
-                           os.environ.get("DNN_FUSED_XENT", "1") == "1")
+                           os.environ.get("DNN_FUSED_XENT", "1") == "1" and
+                           not self._logits_on_library(gl))
         self.acts: list[torch.Tensor] = []  # output of local layer i
         for i, g in enumerate(self.geoms):
             is_logits = self.last and i == len(self.geoms) - 1
@@ -361,6 +362,16 @@ class Stage:
         self._has_w = False
         self._o_native = False  # "O" recorded (device-side lr / step)
         self._rx = self._rl = None
+
+    def _logits_on_library(self, gl) -> bool:
+        """The tuned table routes the logits GEMM to hipBLASLt (long contractions, where the
+        one-row-tile fused cross-entropy GEMM cannot split K: the wide model's 8192-deep last
+        layer ran on 128 workgroups). Then logits are a library GEMM (fp32 out, bias epilogue)
+        followed by the softmax-CE kernel."""
+        if self.device.type != "cuda":
+            return False
+        t = ops.tuning.lookup("fwd", self.mb, gl.np_, gl.kp)
+        return ops.kernels._blas("fwd", t)
 
     def _tail_ok(self) -> bool:
         if not (self.fused_xent and self.device.type == "cuda" and len(self.geoms) >= 3 and
