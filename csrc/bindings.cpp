@@ -358,7 +358,9 @@ PYBIND11_MODULE(_native, m) {
                                                         float, int>>& jobs,
                            uintptr_t stream, uintptr_t grad_base, uintptr_t master,
                            uintptr_t mom, uintptr_t shadow, float lr, float mu, float wd,
-                           uintptr_t lr_dev) {
+                           uintptr_t lr_dev, int adam, uintptr_t v, float b1, float b2,
+                           float eps, int decoupled, uintptr_t step_dev, double db1, double db2,
+                           float bc1, float bc2) {
     std::vector<dnn::ReduceJob> J;
     J.reserve(jobs.size());
     for (const auto& t : jobs)
@@ -367,6 +369,18 @@ PYBIND11_MODULE(_native, m) {
     const bool fused = master != 0;
     dnn::FusedSgd sg{P<const float>(grad_base), P<float>(master), P<float>(mom),
                      P<uint16_t>(shadow), lr, mu, wd, P<const float>(lr_dev)};
+    sg.adam = adam;
+    sg.v = P<float>(v);
+    sg.b1 = b1;
+    sg.b2 = b2;
+    sg.eps = eps;
+    sg.decoupled = decoupled;
+    sg.step_dev = P<const int>(step_dev);
+    sg.db1 = db1;
+    sg.db2 = db2;
+    sg.bc1 = bc1;
+    sg.bc2 = bc2;
+    if (adam && (!mom || !v)) throw std::invalid_argument("fused Adam needs both moments");
     for (size_t k = 0; k < J.size(); k += dnn::REDUCE_MAX_JOBS) {
       const int n = (int)std::min<size_t>(dnn::REDUCE_MAX_JOBS, J.size() - k);
       std::vector<dnn::ReduceJob> part(J.begin() + k, J.begin() + k + n);
@@ -383,13 +397,17 @@ PYBIND11_MODULE(_native, m) {
             f.master = R.fix(f.master);
             f.mom = R.fix(f.mom);
             f.shadow = R.fix(f.shadow);
+            f.v = R.fix(f.v);
             return dnn::reduce_multi(q.data(), (int)q.size(), s, fused ? &f : nullptr);
           },
           stream);
     }
   }, py::arg("jobs"), py::arg("stream"), py::arg("grad_base") = 0, py::arg("master") = 0,
      py::arg("mom") = 0, py::arg("shadow") = 0, py::arg("lr") = 0.f, py::arg("mu") = 0.f,
-     py::arg("wd") = 0.f, py::arg("lr_dev") = 0);
+     py::arg("wd") = 0.f, py::arg("lr_dev") = 0, py::arg("adam") = 0, py::arg("v") = 0,
+     py::arg("b1") = 0.f, py::arg("b2") = 0.f, py::arg("eps") = 0.f, py::arg("decoupled") = 0,
+     py::arg("step_dev") = 0, py::arg("db1") = 0.0, py::arg("db2") = 0.0, py::arg("bc1") = 1.f,
+     py::arg("bc2") = 1.f);
   m.def(
       "sgd_update",
       [](uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t shadow, long n, float lr, float mu,

@@ -376,6 +376,32 @@ __device__ __forceinline__ void sgd4(float* __restrict__ p, f32x4_t gv, float* _
   }
 }
 
+// One Adam / AdamW step on 4 elements (torch.optim semantics): shared by adam_kernel and the
+// fused reduction, so both paths produce the same bits.
+__device__ __forceinline__ void adam4(float* __restrict__ p, f32x4_t gv, float* __restrict__ m,
+                                      float* __restrict__ v, u16* __restrict__ shadow, float lr,
+                                      float b1, float b2, float eps, float wd, int decoupled,
+                                      float bc1, float bc2) {
+  f32x4_t pv = *(const f32x4_t*)p;
+  if (decoupled) pv *= (1.f - lr * wd);
+  else gv += wd * pv;
+  f32x4_t mv = *(const f32x4_t*)m;
+  f32x4_t vv = *(const f32x4_t*)v;
+  mv = b1 * mv + (1.f - b1) * gv;
+  vv = b2 * vv + (1.f - b2) * gv * gv;
+  *(f32x4_t*)m = mv;
+  *(f32x4_t*)v = vv;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) pv[e] -= lr * (mv[e] * bc1) / (sqrtf(vv[e] * bc2) + eps);
+  *(f32x4_t*)p = pv;
+  if (shadow) {
+    bf16x4_t o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (short)f2bf(pv[e]);
+    *(bf16x4_t*)shadow = o;
+  }
+}
+
 template <int TY>
 __device__ __forceinline__ void reduce_block(const ReduceJob& jb, long blk, f32x4_t LDS_AS* red,
                                              const FusedSgd& sg) {
@@ -409,8 +435,20 @@ __device__ __forceinline__ void reduce_block(const ReduceJob& jb, long blk, f32x
     if (sg.master) {
       const long off = (jb.out + i * 4) - sg.grad_base;
       const float lr = sg.lr_dev ? *sg.lr_dev : sg.lr;
-      sgd4(sg.master + off, t, sg.mom ? sg.mom + off : nullptr,
-           sg.shadow ? sg.shadow + off : nullptr, lr, sg.mu, sg.wd);
+      if (sg.adam) {
+        float bc1 = sg.bc1, bc2 = sg.bc2;
+        if (sg.step_dev) {  // the double arithmetic of adam_kernel
+          const double tt = (double)(*sg.step_dev + 1);
+          bc1 = (float)(1.0 / (1.0 - pow(sg.db1, tt)));
+          bc2 = (float)(1.0 / (1.0 - pow(sg.db2, tt)));
+        }
+        adam4(sg.master + off, t, sg.mom + off, sg.v + off,
+              sg.shadow ? sg.shadow + off : nullptr, lr, sg.b1, sg.b2, sg.eps, sg.wd,
+              sg.decoupled, bc1, bc2);
+      } else {
+        sgd4(sg.master + off, t, sg.mom ? sg.mom + off : nullptr,
+             sg.shadow ? sg.shadow + off : nullptr, lr, sg.mu, sg.wd);
+      }
     }
   }
 }
@@ -500,27 +538,9 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
     bc1 = (float)(1.0 / (1.0 - pow(db1, t)));
     bc2 = (float)(1.0 / (1.0 - pow(db2, t)));
   }
-  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
-    f32x4_t pv = *(const f32x4_t*)(p + i * 4);
-    f32x4_t gv = *(const f32x4_t*)(g + i * 4);
-    if (decoupled) pv *= (1.f - lr * wd);
-    else gv += wd * pv;
-    f32x4_t mv = *(const f32x4_t*)(m + i * 4);
-    f32x4_t vv = *(const f32x4_t*)(v + i * 4);
-    mv = b1 * mv + (1.f - b1) * gv;
-    vv = b2 * vv + (1.f - b2) * gv * gv;
-    *(f32x4_t*)(m + i * 4) = mv;
-    *(f32x4_t*)(v + i * 4) = vv;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) pv[e] -= lr * (mv[e] * bc1) / (sqrtf(vv[e] * bc2) + eps);
-    *(f32x4_t*)(p + i * 4) = pv;
-    if (shadow) {
-      bf16x4_t o;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = (short)f2bf(pv[e]);
-      *(bf16x4_t*)(shadow + i * 4) = o;
-    }
-  }
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256)
+    adam4(p + i * 4, *(const f32x4_t*)(g + i * 4), m + i * 4, v + i * 4,
+          shadow ? shadow + i * 4 : nullptr, lr, b1, b2, eps, wd, decoupled, bc1, bc2);
 }
 
 int adam_update(float* p, const float* g, float* m, float* v, uint16_t* shadow, long n, float lr,

@@ -44,10 +44,19 @@ struct ReduceJobs {  // passed by value as the kernel argument
 struct FusedSgd {
   const float* grad_base;
   float* master;
-  float* mom;        // nullptr: no momentum
+  float* mom;        // nullptr: no momentum (Adam: the first moment)
   uint16_t* shadow;  // nullptr: no bf16 refresh
   float lr, mu, wd;
   const float* lr_dev;  // optional device-resident learning rate
+  // Adam / AdamW instead of SGD (adam != 0), the math of adam_update: v = second moment,
+  // bias corrections from step_dev (t = *step_dev + 1, double pow) or bc1 / bc2.
+  int adam;
+  float* v;
+  float b1, b2, eps;
+  int decoupled;
+  const int* step_dev;
+  double db1, db2;
+  float bc1, bc2;
 };
 // All jobs in one launch, each bitwise identical to reduce_slabs on the same inputs.
 int reduce_multi(const ReduceJob* job, int n_jobs, hipStream_t stream,

@@ -559,10 +559,11 @@ class Stage:
         return jobs
 
     def fused_fin_sgd_ok(self) -> bool:
-        """FIN + SGD as one launch: every gradient element must come out of a reduce job
-        (not stream-K wgrad, which writes weight gradients directly) and the optimizer is SGD."""
-        return (self.params.optim.name == "sgd" and self.wgrad_algo != "streamk" and
-                self.device.type == "cuda" and os.environ.get("DNN_FUSE_FIN_SGD", "1") == "1")
+        """FIN + optimizer step as one launch: every gradient element must come out of a reduce
+        job (not stream-K wgrad, which writes weight gradients directly); SGD, Adam or AdamW."""
+        return (self.params.optim.name in ("sgd", "adam", "adamw") and
+                self.wgrad_algo != "streamk" and self.device.type == "cuda" and
+                os.environ.get("DNN_FUSE_FIN_SGD", "1") == "1")
 
     def _record_fin_sgd(self) -> None:
         """Record the whole-stage gradient reduction with the SGD update fused in (segment
@@ -571,10 +572,19 @@ class Stage:
         p._device_scalars()
         o = p.optim
         jobs = self._jobs(tuple(range(len(self.geoms))))
-        ops.reduce_multi(jobs, sgd=dict(grad=p.grad, master=p.master,
-                                        mom=p.state[0] if p.state else None, shadow=p.shadow,
-                                        lr=o.lr, momentum=o.momentum,
-                                        weight_decay=o.weight_decay, lr_dev=p.lr_dev))
+        if o.name == "sgd":
+            ops.reduce_multi(jobs, sgd=dict(grad=p.grad, master=p.master,
+                                            mom=p.state[0] if p.state else None,
+                                            shadow=p.shadow, lr=o.lr, momentum=o.momentum,
+                                            weight_decay=o.weight_decay, lr_dev=p.lr_dev))
+            return
+        ops.reduce_multi(jobs, sgd=dict(grad=p.grad, master=p.master, mom=p.state[0],
+                                        v=p.state[1], shadow=p.shadow, lr=o.lr,
+                                        weight_decay=o.weight_decay, lr_dev=p.lr_dev,
+                                        adam=True, betas=o.betas, eps=o.eps,
+                                        decoupled=o.decoupled or o.name == "adamw",
+                                        step_dev=p.step_dev))
+        ops.step_advance(p.step_dev)  # as record_update: the segment replaces FIN + O
 
     def update_then_forward(self, j: int, s: int, lr: Optional[float] = None) -> None:
         """Deferred DP update of layers [s, L) (completing the step: advance) followed by the

@@ -618,14 +618,23 @@ def reduce_multi(jobs, sgd=None):
 
     ``sgd`` (GPU): dict(grad=flat fp32 gradient the outputs live in, master=, mom=None,
     shadow=None, lr=, momentum=0, weight_decay=0, lr_dev=None) -- the same launch also applies
-    the SGD step to every reduced element (bitwise equal to a following sgd_update over them)."""
+    the SGD step to every reduced element (bitwise equal to a following sgd_update over them).
+    With adam=True (and v=, betas=, eps=, decoupled=, step_dev= as for adam_update; mom = the
+    first moment) it applies the Adam / AdamW step instead, bitwise equal to adam_update; the
+    caller advances step_dev afterwards."""
     jobs = list(jobs)
     if not jobs:
         return
     if not jobs[0][0].is_cuda:
         for (src, n_src, stride, n, out, scale, acc) in jobs:
             ref.reduce_slabs(src, n_src, stride, n, out, scale, acc)
-        if sgd is not None:
+        if sgd is not None and sgd.get("adam"):
+            adam_update(sgd["master"], sgd["grad"], sgd["mom"], sgd["v"], sgd.get("shadow"),
+                        lr=sgd["lr"], betas=sgd["betas"], eps=sgd["eps"],
+                        weight_decay=sgd.get("weight_decay", 0.0),
+                        decoupled=sgd.get("decoupled", False), step=sgd.get("step", 1),
+                        lr_dev=sgd.get("lr_dev"), step_dev=sgd.get("step_dev"))
+        elif sgd is not None:
             sgd_update(sgd["master"], sgd["grad"], sgd.get("mom"), sgd.get("shadow"),
                        lr=sgd["lr"], momentum=sgd.get("momentum", 0.0),
                        weight_decay=sgd.get("weight_decay", 0.0), lr_dev=sgd.get("lr_dev"))
@@ -644,7 +653,10 @@ def reduce_multi(jobs, sgd=None):
         native().reduce_multi(packed, _stream(jobs[0][0]))
         return
     g, m = sgd["grad"], sgd["master"]
-    for t in (m, sgd.get("mom")):
+    adam = bool(sgd.get("adam"))
+    if adam and (sgd.get("mom") is None or sgd.get("v") is None):
+        raise ValueError("fused Adam needs both moment buffers")
+    for t in (m, sgd.get("mom"), sgd.get("v")):
         if t is not None and (t.dtype != torch.float32 or t.numel() != g.numel()):
             raise ValueError("fused SGD buffers must match the flat gradient")
     sh = sgd.get("shadow")
@@ -653,7 +665,20 @@ def reduce_multi(jobs, sgd=None):
     native().reduce_multi(packed, _stream(jobs[0][0]), grad_base=_p(g), master=_p(m),
                           mom=_p(sgd.get("mom")), shadow=_p(sh), lr=float(sgd["lr"]),
                           mu=float(sgd.get("momentum", 0.0)),
-                          wd=float(sgd.get("weight_decay", 0.0)), lr_dev=_p(sgd.get("lr_dev")))
+                          wd=float(sgd.get("weight_decay", 0.0)), lr_dev=_p(sgd.get("lr_dev")),
+                          **(_adam_args(sgd) if adam else {}))
+
+
+def _adam_args(sgd: dict) -> dict:
+    b1, b2 = sgd["betas"]
+    step = int(sgd.get("step", 1))
+    sd = sgd.get("step_dev")
+    if sd is not None and sd.dtype != torch.int32:
+        raise TypeError("step_dev must be int32")
+    return dict(adam=1, v=_p(sgd["v"]), b1=float(b1), b2=float(b2), eps=float(sgd["eps"]),
+                decoupled=int(bool(sgd.get("decoupled", False))), step_dev=_p(sd),
+                db1=float(b1), db2=float(b2), bc1=float(1.0 / (1.0 - b1 ** step)),
+                bc2=float(1.0 / (1.0 - b2 ** step)))
 
 
 def sgd_update(p, g, mom=None, shadow=None, lr=0.01, momentum=0.0, weight_decay=0.0,
