@@ -259,6 +259,50 @@ PYBIND11_MODULE(_native, m) {
       py::arg("M"), py::arg("K3"), py::arg("N3"), py::arg("N4"), py::arg("n_cls"),
       py::arg("scale"), py::arg("act3"), py::arg("act2"), py::arg("stream"));
   m.def("mlp_tail_blocks", &dnn::mlp_tail_blocks);
+  // Grouped GEMM launch (no epilogue extras: the split-K weight gradients of a step). problems:
+  // (a, lda, b, ldb, c, ldc, c_split_stride, M, N, K, k_total, accumulate, splits)
+  m.def(
+      "gemm_bf16_group",
+      [](const std::vector<std::tuple<uintptr_t, long, uintptr_t, long, uintptr_t, long, long,
+                                      int, int, int, int, int, int>>& probs,
+         int layout_a, int layout_b, int out_f32, int bm, int bn, int stages, uintptr_t stream) {
+        if (probs.empty() || probs.size() > (size_t)dnn::GEMM_GROUP_MAX)
+          throw std::invalid_argument("gemm_bf16_group: 1..8 problems");
+        std::vector<GemmParams> ps;
+        std::vector<int> splits;
+        for (const auto& t : probs) {
+          GemmParams p{};
+          p.A = P<const uint16_t>(std::get<0>(t));
+          p.lda = std::get<1>(t);
+          p.B = P<const uint16_t>(std::get<2>(t));
+          p.ldb = std::get<3>(t);
+          p.C = P<void>(std::get<4>(t));
+          p.ldc = std::get<5>(t);
+          p.c_split_stride = std::get<6>(t);
+          p.M = std::get<7>(t);
+          p.N = std::get<8>(t);
+          p.K = std::get<9>(t);
+          p.k_total = std::get<10>(t);
+          p.accumulate = std::get<11>(t);
+          ps.push_back(p);
+          splits.push_back(std::get<12>(t));
+        }
+        launch(
+            "gemm_bf16_group",
+            [=](hipStream_t s, const dnn::Program& R) {
+              std::vector<GemmParams> q = ps;
+              for (auto& p : q) {
+                p.A = R.fix(p.A);
+                p.B = R.fix(p.B);
+                p.C = R.fix(p.C);
+              }
+              return dnn::gemm_bf16_group(q.data(), splits.data(), (int)q.size(), layout_a,
+                                          layout_b, out_f32, bm, bn, stages, s);
+            },
+            stream);
+      },
+      py::arg("problems"), py::arg("layout_a"), py::arg("layout_b"), py::arg("out_f32"),
+      py::arg("bm"), py::arg("bn"), py::arg("stages"), py::arg("stream"));
   m.def(
       "blas_gemm",
       [](int trans_a, int trans_b, int M, int N, int K, uintptr_t a, long lda, uintptr_t b,

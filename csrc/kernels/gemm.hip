@@ -24,19 +24,18 @@
 
 namespace dnn {
 
+// One output tile (workgroup `bid` of a launch of nwg = tiles * splits workgroups).
 template <class C, int LA, int LB, bool OUT_F32>
-__global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(GemmParams p, int tiles_n, int tiles_m,
-                                                          int nwg) {
-  constexpr int BM = C::BM, BN = C::BN, NT = C::NT, CS_LD = C::CS_LD;
-  __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
-  char LDS_AS* lds = (char LDS_AS*)smem;
+__device__ __forceinline__ void gemm_tile_wg(const GemmParams& p, int tiles_n, int tiles_m,
+                                             int nwg, int bid, char LDS_AS* lds) {
+  constexpr int BM = C::BM, BN = C::BN;
 
   // XCD-aware bijective remap: hardware deals block b to XCD group b%8; give each group a
   // contiguous run of logical tiles. Within a split, tiles are walked in groups of
   // group_m row-tiles (column-major inside a group), so the ~32 workgroups an XCD holds at
   // once cover e.g. 4 row x 8 column tiles: 12 operand k-slices shared through its L2
   // instead of 33 for a 1 x 32 strip (guide §5.5 T1 + grouped raster order).
-  const int wgid = xcd_remap(blockIdx.x, nwg);
+  const int wgid = xcd_remap(bid, nwg);
   const int per_split = tiles_n * tiles_m;
   const int split = wgid / per_split;
   const int t = wgid - split * per_split;
@@ -66,6 +65,28 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(GemmParams p, int tile
   mma_tile<C, LA, LB>(p, m0, n0, kbase, nk, lds, acc, wave, lane);
 
   epilogue_staged<C, OUT_F32>(p, acc, lds, m0, n0, tm, split, wave, lane);
+}
+
+template <class C, int LA, int LB, bool OUT_F32>
+__global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(GemmParams p, int tiles_n, int tiles_m,
+                                                          int nwg) {
+  __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
+  gemm_tile_wg<C, LA, LB, OUT_F32>(p, tiles_n, tiles_m, nwg, blockIdx.x, (char LDS_AS*)smem);
+}
+
+// Grouped launch: up to GEMM_GROUP_MAX independent problems with one tile configuration (e.g.
+// every layer's weight gradient of a step) in ONE launch; problem j owns the workgroups
+// [start[j], start[j] + nwg[j]) (start rounded to multiples of 8 so each problem keeps its
+// XCD-aware raster). Small, latency-bound problems then fill each other's idle CUs.
+template <class C, int LA, int LB, bool OUT_F32>
+__global__ __launch_bounds__(C::NT) void gemm_group_kernel(GemmGroup g) {
+  __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
+  int j = 0;
+  while (j + 1 < g.n && (int)blockIdx.x >= g.start[j + 1]) ++j;
+  const int bid = blockIdx.x - g.start[j];
+  if (bid >= g.nwg[j]) return;  // padding to the next multiple of 8 (uniform per workgroup)
+  gemm_tile_wg<C, LA, LB, OUT_F32>(g.p[j], g.tiles_n[j], g.tiles_m[j], g.nwg[j], bid,
+                                   (char LDS_AS*)smem);
 }
 
 // ---- stream-K (balanced split-K) for batch-contraction GEMMs ---------------------------------
@@ -224,8 +245,7 @@ int default_stages(int bm, int bn) {
   return 2;
 }
 
-int gemm_bf16(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, int splits,
-              hipStream_t stream, int stages, int persist) {
+int gemm_check(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, int splits) {
   if (!gemm_tile_supported(bm, bn)) return -1;
   // partial edge tiles: M and N need only be multiples of 8 (16-byte rows / chunks)
   if (p.M <= 0 || p.N <= 0 || p.M % 8 || p.N % 8) return -2;
@@ -251,8 +271,16 @@ int gemm_bf16(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, 
   if (p.lda < a_row || p.ldb < b_row || p.ldc < p.N || (p.aux && p.ld_aux < p.N)) return -8;
   if ((p.mask_out || p.mask_in) &&
       (out_f32 || p.act != ACT_RELU || (p.mask_in && p.aux) || (p.mask_out && p.mask_in) ||
-       p.xent_labels || p.ld_mask < (p.N + 7) / 8 || persist))
+       p.xent_labels || p.ld_mask < (p.N + 7) / 8))
     return -13;
+  return 0;
+}
+
+int gemm_bf16(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, int splits,
+              hipStream_t stream, int stages, int persist) {
+  const int rc = gemm_check(p, la, lb, out_f32, bm, bn, splits);
+  if (rc) return rc;
+  if ((p.mask_out || p.mask_in) && persist) return -13;
 
   // (A 4-wave 256x256 form -- 128x128 per wave, one wave per SIMD, accumulators in AGPRs,
   // hipBLASLt's MT256x256 MIWT8_8 shape -- was built and measured: 7 % slower on 8192^3 fwd,
@@ -299,6 +327,48 @@ int gemm_bf16(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, 
   // XCD holds at a time; a caller-provided group_m wins
   if (q.group_m <= 0) q.group_m = tiles_n >= 8 ? 4 : 1;
   hipLaunchKernelGGL(fn, dim3(nwg), dim3(nt), 0, stream, q, tiles_n, tiles_m, nwg);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
+int gemm_bf16_group(const GemmParams* ps, const int* splits, int n, int la, int lb, int out_f32,
+                    int bm, int bn, int stages, hipStream_t stream) {
+  if (n <= 0 || n > GEMM_GROUP_MAX) return -1;
+  if (gemm_tile_threads(bm, bn) != 256 || (stages && stages != 2)) return -12;
+  GemmGroup g{};
+  g.n = n;
+  int blocks = 0;
+  for (int j = 0; j < n; ++j) {
+    // the one-problem validation (shapes, alignment, layouts, epilogue combinations)
+    const int rc = gemm_check(ps[j], la, lb, out_f32, bm, bn, splits[j]);
+    if (rc) return rc;
+    g.p[j] = ps[j];
+    g.tiles_n[j] = (ps[j].N + bn - 1) / bn;
+    g.tiles_m[j] = (ps[j].M + bm - 1) / bm;
+    g.nwg[j] = g.tiles_n[j] * g.tiles_m[j] * splits[j];
+    if (g.p[j].group_m <= 0) g.p[j].group_m = g.tiles_n[j] >= 8 ? 4 : 1;
+    g.start[j] = blocks;
+    blocks += (g.nwg[j] + 7) / 8 * 8;
+  }
+  g.start[n] = blocks;
+  typedef void (*fn_t)(GemmGroup);
+  fn_t fn = nullptr;
+#define DNN_GG(BM, BN)                                                                     \
+  if (bm == BM && bn == BN) {                                                              \
+    using C = Cfg<BM, BN, 2, 2, 2>;                                                        \
+    if (la == KMAJ && lb == KMAJ)                                                          \
+      fn = out_f32 ? gemm_group_kernel<C, KMAJ, KMAJ, true> : gemm_group_kernel<C, KMAJ, KMAJ, false>; \
+    else if (la == KMAJ && lb == MNMAJ)                                                    \
+      fn = out_f32 ? gemm_group_kernel<C, KMAJ, MNMAJ, true> : gemm_group_kernel<C, KMAJ, MNMAJ, false>; \
+    else if (la == MNMAJ && lb == MNMAJ && out_f32)                                        \
+      fn = gemm_group_kernel<C, MNMAJ, MNMAJ, true>;                                       \
+  }
+  DNN_GG(64, 64)
+  DNN_GG(64, 128)
+  DNN_GG(128, 64)
+  DNN_GG(128, 128)
+#undef DNN_GG
+  if (!fn) return -6;
+  hipLaunchKernelGGL(fn, dim3(blocks), dim3(256), 0, stream, g);
   return hipGetLastError() == hipSuccess ? 0 : -9;
 }
 

@@ -59,6 +59,20 @@ struct GemmParams {
 // persist: 0 = one tile per workgroup (gemm.hip); != 0 = persistent workgroups walking tile
 // runs with a register-direct epilogue (gemm_persist.hip): > 0 workgroup count, < 0 one round
 // of resident workgroups. The fused cross-entropy always runs the one-tile form.
+// Several problems with one 4-wave tile configuration (64|128 x 64|128, 2 stages) in ONE
+// launch (each validated like gemm_bf16; splits per problem).
+constexpr int GEMM_GROUP_MAX = 8;
+struct GemmGroup {
+  GemmParams p[GEMM_GROUP_MAX];
+  int tiles_n[GEMM_GROUP_MAX], tiles_m[GEMM_GROUP_MAX], nwg[GEMM_GROUP_MAX];
+  int start[GEMM_GROUP_MAX + 1];
+  int n;
+};
+int gemm_bf16_group(const GemmParams* ps, const int* splits, int n, int layout_a, int layout_b,
+                    int out_f32, int bm, int bn, int stages, hipStream_t stream);
+// The argument checks of gemm_bf16 (0 or its error code).
+int gemm_check(const GemmParams& p, int layout_a, int layout_b, int out_f32, int bm, int bn,
+               int splits);
 int gemm_bf16(const GemmParams& p, int layout_a, int layout_b, int out_f32, int bm, int bn,
               int splits, hipStream_t stream, int stages = 0, int persist = 0);
 // stages == 8 with 256x256 tiles: the ping-pong, half-tile-streamed main loop (gemm_pp.hip).

@@ -502,9 +502,26 @@ class Stage:
             self._replay("W")
             self._w_done += 1
             return
+        self._wgrad_all(j)
+        self._w_done += 1
+
+    def _wgrad_all(self, j: int = -1) -> None:
+        """Every local layer's weight gradient: one grouped launch per shared tile configuration
+        (ops.linear_wgrad_group; DNN_WGRAD_GROUP=0 disables), one launch per remaining layer."""
+        if (self.wgrad_algo == "splitk" and self.device.type == "cuda" and
+                os.environ.get("DNN_WGRAD_GROUP", "1") == "1" and len(self.geoms) > 1):
+            if j < 0:
+                r, acc = slice(0, self.rows), False
+            else:
+                r, acc = self.rows_of(j), self._w_done > 0
+            if j < 0 or self.wgrad_mode != "batched":
+                items = [(self.dz[i][r], self.input_of(i)[r], self.slabs[i], self.w_splits[i],
+                          acc) for i in range(len(self.geoms))]
+                for i in ops.linear_wgrad_group(items):
+                    self.wgrad_layer(i, j)
+                return
         for i in range(len(self.geoms)):
             self.wgrad_layer(i, j)
-        self._w_done += 1
 
     def _bpart(self, i: int, j: int) -> torch.Tensor:
         return self.bpart[i][j * self.bp[i]:(j + 1) * self.bp[i]]
@@ -695,8 +712,7 @@ class Stage:
                     prog.mark(f"W{i}")
                     self.wgrad_layer(i)
                 prog.mark("W")
-                for i in range(len(self.geoms)):
-                    self.wgrad_layer(i)
+                self._wgrad_all()
             L = len(self.geoms)
             for a in range(L):  # every contiguous layer range: one reduce launch per DP bucket
                 for b in range(a, L):

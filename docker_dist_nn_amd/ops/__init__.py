@@ -1,7 +1,7 @@
 from .kernels import (GEMV_MAX_ROWS, KMAJ, MNMAJ, STREAMK_WG, adam_update, blas_gemm,
                       colsum_partial, dact_colsum,
                       dgrad_tiles, gemm, gemv, linear_dgrad, linear_fwd, linear_fwd_xent,
-                      linear_wgrad, linear_wgrad_streamk, mlp_tail, pack_bf16, pick_splits, pick_tiles,
+                      linear_wgrad, linear_wgrad_group, linear_wgrad_streamk, mlp_tail, pack_bf16, pick_splits, pick_tiles,
                       reduce_multi, reduce_slabs, sgd_update, softmax_rows, softmax_xent,
                       step_advance, streamk_partial_elems, streamk_tiles, tail_blocks,
                       tail_supported, unpack_bf16, wgrad_config, xent_blocks, xent_tiles)
@@ -9,7 +9,7 @@ from .kernels import (GEMV_MAX_ROWS, KMAJ, MNMAJ, STREAMK_WG, adam_update, blas_
 __all__ = ["GEMV_MAX_ROWS", "KMAJ", "MNMAJ", "STREAMK_WG", "adam_update", "blas_gemm",
            "colsum_partial", "dact_colsum",
            "dgrad_tiles", "gemm", "gemv", "linear_dgrad", "linear_fwd", "linear_fwd_xent",
-           "linear_wgrad", "linear_wgrad_streamk", "mlp_tail", "pack_bf16", "pick_splits", "pick_tiles",
+           "linear_wgrad", "linear_wgrad_group", "linear_wgrad_streamk", "mlp_tail", "pack_bf16", "pick_splits", "pick_tiles",
            "reduce_multi", "reduce_slabs", "sgd_update", "softmax_rows", "softmax_xent",
            "step_advance", "streamk_partial_elems", "streamk_tiles", "tail_blocks", "tail_supported",
            "unpack_bf16", "wgrad_config", "xent_blocks", "xent_tiles"]

@@ -274,8 +274,8 @@ class PipelineExecutor:
                         plan += [(st, f"W{i}", 1) for i in range(L - 1, -1, -1) if i != big]
                         plan.append((st, f"W{big}"))
                         plan.append((None, "@join"))
-                    else:
-                        plan += [(st, f"W{i}") for i in range(L - 1, -1, -1)]
+                    else:  # one segment: a grouped launch when the layers share a tile
+                        plan.append((st, "W"))
                     plan.append((st, "FIN"))
                     plan.append((st, "#finalized"))
                 else:
