@@ -455,7 +455,8 @@ def linear_wgrad_group(items) -> list:
         bm, bn, s = wgrad_config(N, K, R)
         t = tuning.lookup("wgrad", N, K, R)
         stages = STAGES["wgrad"] or (t or {}).get("stages", 0) or 2
-        small = -(-N // bm) * -(-K // bn) * splits < NUM_CU  # under one round of the chip
+        small = -(-N // bm) * -(-K // bn) * splits < int(
+            os.environ.get("DNN_WGRAD_GROUP_MAX_WG", NUM_CU))  # under one round of the chip
         if (R % 64 or splits > R // 64 or s != splits or _persist("wgrad", t) or
                 _blas("wgrad", t) or stages != 2 or not small or
                 (bm, bn) not in ((64, 64), (64, 128), (128, 64), (128, 128))):
