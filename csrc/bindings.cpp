@@ -307,7 +307,7 @@ PYBIND11_MODULE(_native, m) {
       "blas_gemm",
       [](int trans_a, int trans_b, int M, int N, int K, uintptr_t a, long lda, uintptr_t b,
          long ldb, uintptr_t d, long ldd, int d_f32, uintptr_t bias, int relu, int accumulate,
-         uintptr_t stream) {
+         uintptr_t stream, int algo) {
         launch(
             "blas_gemm",
             [=](hipStream_t s, const dnn::Program& R) {
@@ -327,6 +327,7 @@ PYBIND11_MODULE(_native, m) {
               g.bias = R.fix(P<const float>(bias));
               g.relu = relu;
               g.accumulate = accumulate;
+              g.algo = algo;
               return dnn::blas_gemm(g, s);
             },
             stream);
@@ -334,7 +335,7 @@ PYBIND11_MODULE(_native, m) {
       py::arg("trans_a"), py::arg("trans_b"), py::arg("M"), py::arg("N"), py::arg("K"),
       py::arg("a"), py::arg("lda"), py::arg("b"), py::arg("ldb"), py::arg("d"), py::arg("ldd"),
       py::arg("d_f32"), py::arg("bias"), py::arg("relu"), py::arg("accumulate"),
-      py::arg("stream"));
+      py::arg("stream"), py::arg("algo") = 0);
   m.def("blas_available", &dnn::blas_available);
   m.def("blas_supported", [](int trans_a, int trans_b, int M, int N, int K, long lda, long ldb,
                              long ldd, int d_f32, int has_bias, int relu, int accumulate) {

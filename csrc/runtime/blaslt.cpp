@@ -10,12 +10,14 @@
 namespace dnn {
 namespace {
 
+constexpr int MAX_ALGOS = 8;
+
 struct Plan {
   hipblasLtMatmulDesc_t desc = nullptr;
   hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, ld = nullptr;
-  hipblasLtMatmulAlgo_t algo{};
-  size_t ws = 0;
   bool ok = false;
+  hipblasLtMatmulHeuristicResult_t cand[MAX_ALGOS];  // the heuristic's candidates
+  int n_cand = 0;
 };
 
 using Key = std::tuple<int, int, int, int, int, long, long, long, int, int, int, int>;
@@ -74,14 +76,12 @@ Plan* plan_for(const BlasGemm& g) {
   uint64_t ws = MAX_WS;
   hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &ws,
                                         sizeof(ws));
-  hipblasLtMatmulHeuristicResult_t res[1];
   int n = 0;
   const hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(handle, p.desc, p.la, p.lb, p.ld,
-                                                             p.ld, pref, 1, res, &n);
+                                                             p.ld, pref, MAX_ALGOS, p.cand, &n);
   hipblasLtMatmulPreferenceDestroy(pref);
   if (st != HIPBLAS_STATUS_SUCCESS || n < 1) return &p;
-  p.algo = res[0].algo;
-  p.ws = res[0].workspaceSize;
+  p.n_cand = n;
   p.ok = true;
   return &p;
 }
@@ -112,12 +112,16 @@ int blas_gemm(const BlasGemm& g, hipStream_t stream) {
                                         sizeof(bp)) != HIPBLAS_STATUS_SUCCESS)
       return -2;
   }
-  void* ws = p->ws ? workspace(stream, p->ws) : nullptr;
-  if (p->ws && !ws) return -2;
+  // candidate g.algo when the heuristic offers it (a table from another library version may
+  // name one it no longer lists: then its first choice)
+  const int k = g.algo > 0 && g.algo < p->n_cand ? g.algo : 0;
+  const size_t wsz = p->cand[k].workspaceSize;
+  void* ws = wsz ? workspace(stream, wsz) : nullptr;
+  if (wsz && !ws) return -2;
   const float alpha = 1.f, beta = g.accumulate ? 1.f : 0.f;
   const hipblasStatus_t st =
       hipblasLtMatmul(handle, p->desc, &alpha, g.B, p->la, g.A, p->lb, &beta, g.D, p->ld, g.D,
-                      p->ld, &p->algo, ws, p->ws, stream);
+                      p->ld, &p->cand[k].algo, ws, wsz, stream);
   return st == HIPBLAS_STATUS_SUCCESS ? 0 : -2;
 }
 

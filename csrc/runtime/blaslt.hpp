@@ -31,6 +31,8 @@ struct BlasGemm {
   const float* bias;   // [N] fp32 or null
   int relu;            // ReLU after the bias (fwd)
   int accumulate;      // D += result (fp32 D only)
+  int algo;            // index into the heuristic's candidate list (0 = its first choice;
+                       // the in-step tuner stores the measured best per GEMM)
 };
 
 // 0 on success; < 0: -1 bad arguments, -2 library error, -3 no algorithm for the problem.

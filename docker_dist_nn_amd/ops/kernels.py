@@ -106,7 +106,7 @@ def _blas_ok(a, b, d, trans_a, trans_b, M, N, K, bias, relu, accumulate) -> bool
 
 
 def blas_gemm(a, b, d, *, trans_a: bool, trans_b: bool, M: int, N: int, K: int, bias=None,
-              relu: bool = False, accumulate: bool = False):
+              relu: bool = False, accumulate: bool = False, algo: int = 0):
     """hipBLASLt library GEMM (csrc/runtime/blaslt.hpp), row-major: d[M][N] (+)= op(a).op(b)
     (+ bias, ReLU), a = [M][K] or (trans_a) [K][M], b = [K][N] or (trans_b) [N][K]."""
     if not a.is_cuda:
@@ -117,7 +117,7 @@ def blas_gemm(a, b, d, *, trans_a: bool, trans_b: bool, M: int, N: int, K: int, 
         raise ValueError("d must be a row-major bf16 or fp32 matrix")
     native().blas_gemm(int(trans_a), int(trans_b), M, N, K, _p(a), a.stride(0), _p(b),
                        b.stride(0), _p(d), d.stride(-2), int(d.dtype == torch.float32),
-                       _p(bias), int(relu), int(accumulate), _stream(a))
+                       _p(bias), int(relu), int(accumulate), _stream(a), int(algo))
 
 
 def dact_colsum(x, aux, act, part=None, n_part: int = 1):
@@ -333,7 +333,7 @@ def linear_fwd(x, w, bias, y, act="relu", mask=None):
     if mask is None and act in ("relu", "linear", 0, 1) and _blas("fwd", t) and \
             _blas_ok(x, w, y, False, True, M, N, K, bias, _act(act) == 1, False):
         return blas_gemm(x, w, y, trans_a=False, trans_b=True, M=M, N=N, K=K, bias=bias,
-                         relu=_act(act) == 1)
+                         relu=_act(act) == 1, algo=(t or {}).get("blas_algo", 0))
     tiles = tuple(t["tile"]) if t else pick_tiles(M, N)
     return gemm(x, w, y, layout_a=KMAJ, layout_b=KMAJ, M=M, N=N, K=K, bias=bias, act=act,
                 tiles=tiles, stages=STAGES["fwd"] or (t or {}).get("stages", 0),
@@ -405,7 +405,8 @@ def linear_dgrad(dz, w, dx, y_prev=None, act_prev="linear", colsum=None, mask_pr
     t = tuning.lookup("dgrad", M, K, N)
     if mask_prev is None and dz.is_cuda and _blas("dgrad", t) and \
             _blas_ok(dz, w, dx, False, False, M, K, N, None, False, False):
-        blas_gemm(dz, w, dx, trans_a=False, trans_b=False, M=M, N=K, K=N)
+        blas_gemm(dz, w, dx, trans_a=False, trans_b=False, M=M, N=K, K=N,
+                  algo=(t or {}).get("blas_algo", 0))
         n_part = -(-M // dgrad_tiles(M, K, N)[0])
         if y_prev is not None and _act(act_prev) != 0:
             dact_colsum(dx, y_prev, act_prev, colsum, n_part)
@@ -431,7 +432,8 @@ def linear_wgrad(dz, x, slabs, splits=1, accumulate=False):
     if splits == 1 and dz.is_cuda and _blas("wgrad", tuning.lookup("wgrad", N, K, R)) and \
             _blas_ok(dz, x, slabs[0], True, False, N, K, R, None, False, accumulate):
         return blas_gemm(dz, x, slabs[0], trans_a=True, trans_b=False, M=N, N=K, K=R,
-                         accumulate=accumulate)
+                         accumulate=accumulate,
+                         algo=(tuning.lookup("wgrad", N, K, R) or {}).get("blas_algo", 0))
     return gemm(dz, x, slabs, layout_a=MNMAJ, layout_b=MNMAJ, M=N, N=K, K=R, k_total=R,
                 accumulate=accumulate, splits=splits, tiles=tiles,
                 stages=STAGES["wgrad"] or (t or {}).get("stages", 0),
