@@ -73,3 +73,25 @@ def test_blas_switch(monkeypatch):
 def test_reference_tail_waves_match_kernel_forms():
     assert ref.tail_waves(1, 1) == 8  # branch-free ReLU form: 8 waves
     assert ref.tail_waves(2, 1) == 4 and ref.tail_waves(0, 0) == 4
+
+
+def test_tuner_signatures_include_logits_candidate():
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(__file__)), "bench"))
+    from tune import signatures
+
+    from docker_dist_nn_amd import NAMED_MODELS
+
+    sigs = signatures(NAMED_MODELS["mnist-fcnn"], 65536)
+    logits = [s for s in sigs if s[4] == "logits"]
+    assert [(op, M, N, K) for op, M, N, K, _ in logits] == [("fwd", 65536, 64, 128)]
+    wg = [s for s in sigs if s[0] == "wgrad"]
+    assert len(wg) == 4 and all(isinstance(s[4], list) and s[4] for s in wg)
+
+
+def test_wgrad_group_is_a_gpu_path():
+    x = torch.zeros(64, 64, dtype=torch.bfloat16)
+    items = [(x, x, torch.zeros(1, 64, 64), 1, False)] * 3
+    assert K.linear_wgrad_group(items) == [0, 1, 2]  # CPU: nothing launched, caller runs all
