@@ -182,15 +182,11 @@ def main(argv: Optional[list[str]] = None) -> int:
                                    weight_decay=a.weight_decay))
     start_step = 0
     if a.resume and a.checkpoint_dir and os.path.exists(os.path.join(a.checkpoint_dir, "meta.json")):
-        meta = ckpt.read_meta(a.checkpoint_dir)
-        if meta["layer_distribution"] == list(dist_):
-            for st in tr.stages:
-                start_step = ckpt.load_stage(a.checkpoint_dir, st)
-        else:  # re-partition onto the new layout
-            ws, bs, meta = ckpt.load_full_weights(a.checkpoint_dir)
-            tr.load_weights(ws, bs)
-            start_step = meta["step"]
-        log.info(f"resumed from {a.checkpoint_dir} at step {start_step}")
+        # any layout: weights AND optimizer state are stored per layer (re-partition is exact)
+        start_step = ckpt.restore_trainer(a.checkpoint_dir, tr)
+        log.info(f"resumed from {a.checkpoint_dir} at step {start_step} "
+                 f"(saved layout {ckpt.read_meta(a.checkpoint_dir)['layer_distribution']}, "
+                 f"now {list(dist_)})")
     elif mc is not None:
         tr.load_weights([L.weight for L in mc.layers], [L.bias for L in mc.layers])
 
@@ -208,8 +204,24 @@ def main(argv: Optional[list[str]] = None) -> int:
     sid = tr.stages[0].stage_index
     step, t0 = start_step, time.time()
     done = False
+    barrier = torch.distributed.barrier if world > 1 else None
+
+    def save(step_):
+        ckpt.save_trainer(a.checkpoint_dir, tr, step_, barrier=barrier, is_writer=replica == 0,
+                          extra={"seed": a.seed, "rows_per_step": rows, "dp": dp})
+
+    per_epoch = -(-x.shape[0] // rows)
+    if a.steps and start_step >= a.steps:
+        done = True
     for ep in range(max(1, a.epochs)):
-        for xb, yb, _ in _batches(x, y, rows, kp, dev, a.seed + ep):
+        if done:
+            break
+        if (ep + 1) * per_epoch <= start_step:
+            continue  # epoch fully consumed before the checkpoint
+        skip = max(0, start_step - ep * per_epoch)
+        for bi, (xb, yb, _) in enumerate(_batches(x, y, rows, kp, dev, a.seed + ep)):
+            if bi < skip:
+                continue  # resume: the batch order is seeded per epoch, skip what was trained
             faults.maybe_inject(sid, step, tr.stages[0])
             tr.set_batch(xb if tr.first else None, yb if tr.last else None)
             tr.step()
@@ -223,11 +235,8 @@ def main(argv: Optional[list[str]] = None) -> int:
                 check_finite(loss)
                 mw.write("train", step=step, loss=loss,
                          samples_per_s=(step - start_step) * rows * dp / (time.time() - t0))
-            if a.checkpoint_dir and a.checkpoint_every and step % a.checkpoint_every == 0 \
-                    and replica == 0:
-                tr.flush()  # deferred DP update of the last step
-                for st in tr.stages:
-                    ckpt.save_stage(a.checkpoint_dir, st, step, spec, dist_)
+            if a.checkpoint_dir and a.checkpoint_every and step % a.checkpoint_every == 0:
+                save(step)
             if a.steps and step >= a.steps:
                 done = True
                 break
@@ -244,9 +253,8 @@ def main(argv: Optional[list[str]] = None) -> int:
         prof.chrome_trace(a.trace.format(rank=rank))
         log.info(f"step profile: {StepProfiler.summarize(prof.steps[-1])}")
     tr.flush()
-    if a.checkpoint_dir and replica == 0:
-        for st in tr.stages:
-            ckpt.save_stage(a.checkpoint_dir, st, step, spec, dist_)
+    if a.checkpoint_dir:
+        save(step)
     rate = (step - start_step) * rows * dp / max(elapsed, 1e-9)
     mw.write("done", step=step, samples_per_s=rate, loss=tr.loss())
     mw.close()

@@ -130,12 +130,36 @@ class StageParams:
     def refresh_shadow(self) -> None:
         self.shadow.copy_(self.master.to(torch.bfloat16))
 
-    def export(self) -> tuple[list[np.ndarray], list[np.ndarray]]:
+    def _export_flat(self, buf: torch.Tensor) -> tuple[list[np.ndarray], list[np.ndarray]]:
         ws, bs = [], []
         for i, g in enumerate(self.geoms):
-            ws.append(self.w32(i)[:g.spec.out_dim, :g.spec.in_dim].detach().cpu().numpy().copy())
-            bs.append(self.b32(i)[:g.spec.out_dim].detach().cpu().numpy().copy())
+            w = buf[self.w_off[i]:self.w_off[i] + g.np_ * g.kp].view(g.np_, g.kp)
+            ws.append(w[:g.spec.out_dim, :g.spec.in_dim].detach().cpu().numpy().copy())
+            bs.append(buf[self.b_off[i]:self.b_off[i] + g.spec.out_dim]
+                      .detach().cpu().numpy().copy())
         return ws, bs
+
+    def export(self) -> tuple[list[np.ndarray], list[np.ndarray]]:
+        return self._export_flat(self.master)
+
+    def export_state(self, k: int) -> tuple[list[np.ndarray], list[np.ndarray]]:
+        """Unpadded per-layer view of optimizer state buffer k (momentum / Adam m, v)."""
+        return self._export_flat(self.state[k])
+
+    def load_state(self, k: int, weights: Sequence[np.ndarray],
+                   biases: Sequence[np.ndarray]) -> None:
+        """Set optimizer state buffer k from unpadded per-layer arrays (padding stays 0)."""
+        buf = self.state[k]
+        buf.zero_()
+        for i, g in enumerate(self.geoms):
+            w = torch.as_tensor(np.asarray(weights[i], dtype=np.float32))
+            b = torch.as_tensor(np.asarray(biases[i], dtype=np.float32))
+            if tuple(w.shape) != (g.spec.out_dim, g.spec.in_dim):
+                raise ValueError(f"layer {g.index}: state shape {tuple(w.shape)} != "
+                                 f"{(g.spec.out_dim, g.spec.in_dim)}")
+            view = buf[self.w_off[i]:self.w_off[i] + g.np_ * g.kp].view(g.np_, g.kp)
+            view[:g.spec.out_dim, :g.spec.in_dim] = w.to(self.device)
+            buf[self.b_off[i]:self.b_off[i] + g.spec.out_dim] = b.to(self.device)
 
     # optimizer ----------------------------------------------------------------------------
     def _device_scalars(self) -> None:

@@ -87,7 +87,11 @@ class MLPSpec:
         return sum(l.params for l in self.layers)
 
     def flops_per_sample_train(self) -> int:
-        return sum(l.flops_per_sample_train for l in self.layers)
+        """EXECUTED training FLOPs per sample: fwd + dgrad + wgrad of every layer, minus the
+        first layer's dgrad (the gradient w.r.t. the input data is never computed)."""
+        first = self.layers[0]
+        return sum(l.flops_per_sample_train for l in self.layers) - \
+            2 * first.in_dim * first.out_dim
 
     def describe(self) -> str:
         return "-".join(str(w) for w in self.widths)
