@@ -188,7 +188,7 @@ def main():
                     "persistent workgroups (gemm_persist.hip)")
     ap.add_argument("--margin", type=float, default=0.01,
                     help="relative win a challenger needs over the incumbent entry")
-    ap.add_argument("--blas", default="1", choices=["0", "1", "only"],
+    ap.add_argument("--blas", default="0", choices=["0", "1", "only"],
                     help="hipBLASLt library GEMM as a candidate: 0 no, 1 yes, only = incumbent "
                     "vs library per GEMM (quick)")
     a = ap.parse_args()

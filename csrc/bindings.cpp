@@ -25,6 +25,7 @@
 #include "runtime/p2p.hpp"
 #include "runtime/program.hpp"
 #include "runtime/schedule.hpp"
+#include "runtime/step_plan.hpp"
 
 namespace py = pybind11;
 using dnn::GemmParams;
@@ -505,6 +506,16 @@ PYBIND11_MODULE(_native, m) {
         },
         stream);
   });
+  m.def("transpose_bf16", [](uintptr_t src, long ld_src, int rows, int cols, uintptr_t dst,
+                             long ld_dst, uintptr_t stream) {
+    launch(
+        "transpose_bf16",
+        [=](hipStream_t s, const dnn::Program& R) {
+          return dnn::transpose_bf16(R.fix(P<const uint16_t>(src)), ld_src, rows, cols,
+                                     R.fix(P<uint16_t>(dst)), ld_dst, s);
+        },
+        stream);
+  });
   m.def("unpack_bf16", [](uintptr_t in, long ld_in, int rows, int cols, uintptr_t out,
                           long ld_out, uintptr_t stream) {
     launch(
@@ -723,6 +734,56 @@ PYBIND11_MODULE(_native, m) {
       py::arg("array"), "float64 [rows][cols] -> Matrix wire bytes");
 
   // ---- runtime: HIP graph executor ------------------------------------------------------
+  // ---- runtime: native multi-rank step (runtime/step_plan.hpp) ----------------------------
+  m.def("nccl_load", [](const std::string& path) { return dnn::nccl_load(path).path; },
+        py::arg("path"));
+  m.def("nccl_comm_info", [](uintptr_t comm) {
+    const dnn::NcclApi* a = dnn::nccl_api();
+    if (!a) throw std::runtime_error("nccl_load first");
+    int n = 0, r = 0;
+    if (a->comm_count(reinterpret_cast<void*>(comm), &n) != 0 ||
+        a->comm_user_rank(reinterpret_cast<void*>(comm), &r) != 0)
+      throw std::runtime_error("ncclCommCount / ncclCommUserRank failed");
+    return std::make_pair(n, r);
+  });
+  py::class_<dnn::StepPlan>(m, "StepPlan")
+      .def(py::init<int, int>(), py::arg("n_streams"), py::arg("n_events"))
+      .def(
+          "add",
+          [](dnn::StepPlan& sp, int kind, int stream, const dnn::Program* prog,
+             const std::string& seg, uintptr_t comm, uintptr_t a, uintptr_t b, uint64_t count,
+             int dtype, int peer, int64_t delta, int event) {
+            dnn::StepPlan::Op o;
+            o.kind = static_cast<dnn::StepPlan::Kind>(kind);
+            o.stream = stream;
+            o.prog = prog;
+            o.seg = seg;
+            o.comm = reinterpret_cast<void*>(comm);
+            o.a = a;
+            o.b = b;
+            o.count = count;
+            o.dtype = dtype;
+            o.peer = peer;
+            o.delta = delta;
+            o.event = event;
+            sp.add(o);
+          },
+          py::arg("kind"), py::arg("stream") = 0, py::arg("prog") = nullptr,
+          py::arg("seg") = std::string(), py::arg("comm") = 0, py::arg("a") = 0,
+          py::arg("b") = 0, py::arg("count") = 0, py::arg("dtype") = 0, py::arg("peer") = 0,
+          py::arg("delta") = 0, py::arg("event") = 0, py::keep_alive<1, 4>())
+      .def(
+          "run",
+          [](dnn::StepPlan& sp, uintptr_t stream) {
+            py::gil_scoped_release nogil;
+            sp.run(S(stream));
+          },
+          py::arg("stream"))
+      .def_property("seq", &dnn::StepPlan::seq, &dnn::StepPlan::set_seq)
+      .def_property_readonly("size", &dnn::StepPlan::size)
+      .def_property_readonly("n_streams", &dnn::StepPlan::n_streams)
+      .def("comm_error", &dnn::StepPlan::comm_error)
+      .def("clear_ops", &dnn::StepPlan::clear_ops);
   py::class_<dnn::GraphExec>(m, "GraphExec")
       .def(py::init<>())
       .def("begin_capture", [](dnn::GraphExec& g, uintptr_t s) { g.begin_capture(S(s)); })

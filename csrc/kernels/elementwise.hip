@@ -602,4 +602,46 @@ int unpack_bf16(const uint16_t* in, long ld_in, int rows, int cols, float* out, 
   return hipGetLastError() == hipSuccess ? 0 : -9;
 }
 
+// ------------------------------------------------------------------------------------------
+// bf16 transpose: dst[c][r] = src[r][c], 64x64 tiles through LDS (16-byte loads and stores).
+// Refreshes the transposed weight shadow W^T[Kp][Np] after an optimizer update, so the dgrad
+// GEMM reads both operands contraction-contiguous (ds_read_b128 fragments, the forward's main
+// loop) instead of transposing W with ds_read_b64_tr_b16 in every tile.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const u16* __restrict__ src,
+                                                             long ld_src, u16* __restrict__ dst,
+                                                             long ld_dst, int tiles_c) {
+  __shared__ u16 t[64][64 + 8];  // +16 B per row: the column reads below hit distinct banks
+  const int r0 = (blockIdx.x / tiles_c) * 64, c0 = (blockIdx.x % tiles_c) * 64;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int chunk = threadIdx.x + 256 * i, r = chunk >> 3, c = (chunk & 7) * 8;
+    const uint4 v = *(const uint4*)(src + (long)(r0 + r) * ld_src + c0 + c);
+    const u16* e = (const u16*)&v;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t[r][c + k] = e[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int chunk = threadIdx.x + 256 * i, c = chunk >> 3, r = (chunk & 7) * 8;
+    uint4 v;
+    u16* e = (u16*)&v;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) e[k] = t[r + k][c];
+    *(uint4*)(dst + (long)(c0 + c) * ld_dst + r0 + r) = v;
+  }
+}
+
+int transpose_bf16(const uint16_t* src, long ld_src, int rows, int cols, uint16_t* dst,
+                   long ld_dst, hipStream_t stream) {
+  if (rows <= 0 || cols <= 0 || rows % 64 || cols % 64) return -1;
+  if (ld_src < cols || ld_dst < rows || ld_src % 8 || ld_dst % 8) return -2;
+  if ((((uintptr_t)src) | ((uintptr_t)dst)) & 15) return -3;
+  const int tiles_c = cols / 64;
+  hipLaunchKernelGGL(transpose_bf16_kernel, dim3((rows / 64) * tiles_c), dim3(256), 0, stream,
+                     src, ld_src, dst, ld_dst, tiles_c);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
 }  // namespace dnn

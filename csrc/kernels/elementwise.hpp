@@ -75,4 +75,8 @@ int pack_bf16(const float* in, long ld_in, int rows, int cols, uint16_t* out, lo
 int unpack_bf16(const uint16_t* in, long ld_in, int rows, int cols, float* out, long ld_out,
                 hipStream_t stream);
 
+// dst[c][r] = src[r][c] for a bf16 [rows][cols] matrix (rows, cols multiples of 64).
+int transpose_bf16(const uint16_t* src, long ld_src, int rows, int cols, uint16_t* dst,
+                   long ld_dst, hipStream_t stream);
+
 }  // namespace dnn

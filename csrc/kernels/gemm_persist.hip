@@ -105,6 +105,10 @@ __global__ __launch_bounds__(C::NT) void gemm_persist_kernel(GemmParams p, int t
     if (lt < t_end) issue(lds + s * STAGE);
   int rd = 0, wr = NS - 1;
 
+  // the previous tile's epilogue was a full bf16 tile: exactly epilogue_direct_stores() stores
+  // per lane were issued after the next stage's DMA, so waiting for that stage need not drain
+  // them (the stores of tile t overlap the first k-steps of tile t + 1)
+  bool prev_full_bf16 = false;
   for (int t = t_begin; t < t_end; t += nwg) {
     const TileCoord cc = decode_tile(p, t, tiles_n, tiles_m, splits);
     f32x4_t acc[FM][FN];
@@ -115,8 +119,12 @@ __global__ __launch_bounds__(C::NT) void gemm_persist_kernel(GemmParams p, int t
 
     for (int kt = 0; kt < cc.nk; ++kt) {
       // the first step of a tile follows an epilogue whose stores also count in vmcnt
-      if (kt == 0) wait_vmcnt<0>();
-      else wait_stage<NS, C::PER_STAGE>(min(issued - consumed - 1, NS - 2));
+      if (kt == 0) {
+        if (prev_full_bf16 && NS == 2) wait_vmcnt<epilogue_direct_stores<FM, FN>()>();
+        else wait_vmcnt<0>();
+      } else {
+        wait_stage<NS, C::PER_STAGE>(min(issued - consumed - 1, NS - 2));
+      }
       lds_barrier();
       if (lt < t_end) issue(lds + wr * STAGE);
       const char LDS_AS* sa = lds + rd * STAGE;
@@ -141,6 +149,7 @@ __global__ __launch_bounds__(C::NT) void gemm_persist_kernel(GemmParams p, int t
 
     epilogue_direct<C::FM, C::FN, BN, C::SN, C::WM, NS, STAGE, OUT_F32>(
         p, acc, lds, rd, cc.tm, cc.tn, cc.split, wm, wn, lane, true);
+    prev_full_bf16 = !OUT_F32 && (cc.tm + 1) * BM <= p.M && (cc.tn + 1) * BN <= p.N;
   }
 }
 

@@ -2,6 +2,7 @@
 // workgroup, LDS-staged epilogue; gemm_persist.hip: persistent workgroups, direct epilogue).
 // See gemm.hip for the structure of the main loop.
 #pragma once
+#include <type_traits>
 #include "common.hpp"
 #include "gemm.hpp"
 
@@ -456,6 +457,12 @@ __device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
 // output stores each fragment's 16 bytes. with_colsum: the bias-gradient column sums are
 // reduced across the WM wave rows in the ring slot the last k-step consumed (`rd` is the ring
 // read cursor after the loop) -- callers whose waves are not in lock step pass false.
+// 16-byte stores every lane of a FULL tile issues in the bf16 form of epilogue_direct (before
+// an optional column-sum store): a persistent kernel that issued its next stage before the
+// epilogue may wait for it with vmcnt(this) instead of vmcnt(0) (stores retire in order).
+template <int FM, int FN>
+constexpr int epilogue_direct_stores() { return FM * FN / 2; }
+
 template <int FM, int FN, int BN, int SN, int WM, int NS, int STAGE, bool OUT_F32>
 __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&acc)[FM][FN],
                                                 char LDS_AS* lds, int rd, int tm, int tn,
@@ -500,25 +507,46 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&a
       // before the next k-step's barrier; wait until every wave has finished reading it
       float LDS_AS* red = (float LDS_AS*)(lds + (rd == 0 ? NS - 1 : rd - 1) * STAGE);
       if (want_sum) lds_barrier();
+      // Every global READ of the epilogue (bias, activation values for the derivative) is
+      // issued before its first store: loads and stores share vmcnt and retire in order, so a
+      // load issued after a store would make its wait drain that store too. With the reads up
+      // front the stores stream out unwaited, and a persistent caller only waits for its next
+      // stage (issued before them) with vmcnt(#stores) -- see epilogue_direct_stores.
+      // Two instantiations of the store loop (activation derivative from `aux`, or bias +
+      // activation), so only one kind of hoisted operand is live at a time.
+      auto body = [&](auto has_aux) {
+      constexpr bool AUX = decltype(has_aux)::value;
+      [[maybe_unused]] f32x4_t bv[AUX ? 1 : FN];
+      [[maybe_unused]] uint2 yv[AUX ? FN : 1][FM];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int c = col0 + 16 * j;
+        if constexpr (AUX) {
+          const u16* ya = p.aux + min(c, p.N - 4);
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+            yv[j][i] = *(const uint2*)(ya + min(row0 + 16 * i, p.M - 1) * p.ld_aux);
+        } else {
+          bv[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+          if (p.bias && c < p.N) bv[j] = *(const f32x4_t*)(p.bias + c);
+        }
+      }
 #pragma unroll
       for (int j = 0; j < FN; j += 2) {
-        const int c0 = col0 + 16 * j, c1 = c0 + 16;
         f32x4_t b0 = {0.f, 0.f, 0.f, 0.f}, b1 = {0.f, 0.f, 0.f, 0.f};
-        if (p.bias) {
-          if (c0 < p.N) b0 = *(const f32x4_t*)(p.bias + c0);
-          if (c1 < p.N) b1 = *(const f32x4_t*)(p.bias + c1);
-        }
-        // activation values for the derivative, all issued before the first use
-        uint2 y0[FM], y1[FM];
-        if (p.aux) {
-          const u16* ya = p.aux + min(c0, p.N - 4);
-          const u16* yb = p.aux + min(c1, p.N - 4);
-#pragma unroll
-          for (int i = 0; i < FM; ++i) {
-            const long r = min(row0 + 16 * i, p.M - 1) * p.ld_aux;
-            y0[i] = *(const uint2*)(ya + r);
-            y1[i] = *(const uint2*)(yb + r);
+        [[maybe_unused]] const uint2* y0 = nullptr;
+        [[maybe_unused]] const uint2* y1 = nullptr;
+        if constexpr (AUX) {
+          y0 = yv[j];
+          y1 = yv[j + 1];
+          if (p.bias) {  // (no caller combines bias and aux; kept correct, not hoisted)
+            const int c0 = col0 + 16 * j;
+            if (c0 < p.N) b0 = *(const f32x4_t*)(p.bias + c0);
+            if (c0 + 16 < p.N) b1 = *(const f32x4_t*)(p.bias + c0 + 16);
           }
+        } else {
+          b0 = bv[j];
+          b1 = bv[j + 1];
         }
         float cs0[4] = {0.f, 0.f, 0.f, 0.f}, cs1[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -530,7 +558,7 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&a
             v0[e] = acc[i][j][e] + b0[e];
             v1[e] = acc[i][j + 1][e] + b1[e];
           }
-          if (p.aux) {
+          if constexpr (AUX) {
             const unsigned ya[2] = {y0[i].x, y0[i].y}, yb[2] = {y1[i].x, y1[i].y};
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -580,6 +608,9 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&a
           }
         }
       }
+      };
+      if (p.aux) body(std::true_type{});
+      else body(std::false_type{});
       if (want_sum) {
         lds_barrier();
         if ((int)threadIdx.x < BN) {

@@ -1,0 +1,187 @@
+#include "runtime/step_plan.hpp"
+
+#include <dlfcn.h>
+
+#include <mutex>
+#include <set>
+#include <stdexcept>
+
+namespace dnn {
+namespace {
+
+void ck(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+NcclApi g_api;
+bool g_loaded = false;
+std::mutex g_mu;
+
+template <class F>
+void sym(void* h, const char* name, F& f) {
+  f = reinterpret_cast<F>(dlsym(h, name));
+  if (!f) throw std::runtime_error(std::string("librccl: missing symbol ") + name);
+}
+
+}  // namespace
+
+const NcclApi& nccl_load(const std::string& path) {
+  std::lock_guard<std::mutex> g(g_mu);
+  if (g_loaded) {
+    if (path != g_api.path) throw std::runtime_error("nccl_load: a different librccl is bound");
+    return g_api;
+  }
+  // NOLOAD: bind to the RCCL instance that created the communicators (torch's), never a
+  // second copy whose internal state would not know them
+  void* h = dlopen(path.c_str(), RTLD_LAZY | RTLD_NOLOAD);
+  if (!h) throw std::runtime_error("nccl_load: " + path + " is not loaded in this process");
+  NcclApi a;
+  sym(h, "ncclSend", a.send);
+  sym(h, "ncclRecv", a.recv);
+  sym(h, "ncclAllReduce", a.all_reduce);
+  sym(h, "ncclReduceScatter", a.reduce_scatter);
+  sym(h, "ncclAllGather", a.all_gather);
+  sym(h, "ncclGroupStart", a.group_start);
+  sym(h, "ncclGroupEnd", a.group_end);
+  sym(h, "ncclCommCount", a.comm_count);
+  sym(h, "ncclCommUserRank", a.comm_user_rank);
+  sym(h, "ncclCommGetAsyncError", a.async_error);
+  sym(h, "ncclGetErrorString", a.error_string);
+  a.path = path;
+  g_api = a;
+  g_loaded = true;
+  return g_api;
+}
+
+const NcclApi* nccl_api() { return g_loaded ? &g_api : nullptr; }
+
+StepPlan::StepPlan(int n_streams, int n_events) {
+  if (n_streams < 1 || n_events < 0) throw std::invalid_argument("StepPlan: bad sizes");
+  for (int i = 1; i < n_streams; ++i) {
+    hipStream_t s;
+    ck(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+    streams_.push_back(s);
+    hipEvent_t e;
+    ck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    join_.push_back(e);
+  }
+  for (int i = 0; i < n_events; ++i) {
+    hipEvent_t e;
+    ck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    events_.push_back(e);
+  }
+  ck(hipEventCreateWithFlags(&fork_, hipEventDisableTiming), "hipEventCreate");
+}
+
+StepPlan::~StepPlan() {
+  for (auto e : events_) (void)hipEventDestroy(e);
+  for (auto e : join_) (void)hipEventDestroy(e);
+  if (fork_) (void)hipEventDestroy(fork_);
+  for (auto s : streams_) (void)hipStreamDestroy(s);
+}
+
+void StepPlan::add(const Op& op) {
+  if (op.stream < 0 || op.stream > (int)streams_.size())
+    throw std::out_of_range("StepPlan op: stream index");
+  if ((op.kind == REC || op.kind == WAIT) && (op.event < 0 || op.event >= (int)events_.size()))
+    throw std::out_of_range("StepPlan op: event id");
+  if (op.kind == SEG && (!op.prog || op.seg.empty()))
+    throw std::invalid_argument("StepPlan op: SEG needs a program and a segment");
+  const bool rccl = op.kind == SEND || op.kind == RECV || op.kind == ALLREDUCE ||
+                    op.kind == REDUCE_SCATTER || op.kind == ALL_GATHER;
+  if (rccl && (!op.comm || !nccl_api()))
+    throw std::invalid_argument("StepPlan op: RCCL op without a communicator / nccl_load");
+  if ((op.kind == SIGNAL || op.kind == WAITV) && !op.a)
+    throw std::invalid_argument("StepPlan op: flag address");
+  ops_.push_back(op);
+}
+
+static void nck(int rc, const char* what) {
+  if (rc != 0) {
+    const NcclApi* a = nccl_api();
+    throw std::runtime_error(std::string(what) + " failed: " +
+                             (a ? a->error_string(rc) : "rccl") + " (" + std::to_string(rc) + ")");
+  }
+}
+
+void StepPlan::run(hipStream_t main) {
+  ++seq_;
+  ck(hipEventRecord(fork_, main), "hipEventRecord");
+  for (auto s : streams_) ck(hipStreamWaitEvent(s, fork_, 0), "hipStreamWaitEvent");
+  std::vector<std::string> one(1);
+  const NcclApi* nc = nccl_api();
+  for (const Op& o : ops_) {
+    hipStream_t s = stream(o.stream, main);
+    switch (o.kind) {
+      case SEG:
+        one[0] = o.seg;
+        o.prog->run(one, s);
+        break;
+      case SEND:
+        nck(nc->send(reinterpret_cast<const void*>(o.a), o.count, o.dtype, o.peer, o.comm, s),
+            "ncclSend");
+        break;
+      case RECV:
+        nck(nc->recv(reinterpret_cast<void*>(o.a), o.count, o.dtype, o.peer, o.comm, s),
+            "ncclRecv");
+        break;
+      case ALLREDUCE:  // in place, sum
+        nck(nc->all_reduce(reinterpret_cast<const void*>(o.a), reinterpret_cast<void*>(o.a),
+                           o.count, o.dtype, 0, o.comm, s),
+            "ncclAllReduce");
+        break;
+      case REDUCE_SCATTER:  // a = full input, b = this rank's chunk (count elements)
+        nck(nc->reduce_scatter(reinterpret_cast<const void*>(o.a), reinterpret_cast<void*>(o.b),
+                               o.count, o.dtype, 0, o.comm, s),
+            "ncclReduceScatter");
+        break;
+      case ALL_GATHER:  // a = this rank's chunk (count elements), b = full output
+        nck(nc->all_gather(reinterpret_cast<const void*>(o.a), reinterpret_cast<void*>(o.b),
+                           o.count, o.dtype, o.comm, s),
+            "ncclAllGather");
+        break;
+      case COPY:
+        ck(hipMemcpyAsync(reinterpret_cast<void*>(o.b), reinterpret_cast<const void*>(o.a),
+                          o.count, hipMemcpyDeviceToDevice, s),
+           "hipMemcpyAsync");
+        break;
+      case SIGNAL:
+        ck(hipStreamWriteValue32(s, reinterpret_cast<void*>(o.a),
+                                 (uint32_t)((int64_t)seq_ + o.delta), 0),
+           "hipStreamWriteValue32");
+        break;
+      case WAITV:
+        ck(hipStreamWaitValue32(s, reinterpret_cast<void*>(o.a),
+                                (uint32_t)((int64_t)seq_ + o.delta), hipStreamWaitValueGte,
+                                0xFFFFFFFFu),
+           "hipStreamWaitValue32");
+        break;
+      case REC:
+        ck(hipEventRecord(events_[o.event], s), "hipEventRecord");
+        break;
+      case WAIT:
+        ck(hipStreamWaitEvent(s, events_[o.event], 0), "hipStreamWaitEvent");
+        break;
+    }
+  }
+  for (size_t i = 0; i < streams_.size(); ++i) {
+    ck(hipEventRecord(join_[i], streams_[i]), "hipEventRecord");
+    ck(hipStreamWaitEvent(main, join_[i], 0), "hipStreamWaitEvent");
+  }
+}
+
+int StepPlan::comm_error() const {
+  const NcclApi* nc = nccl_api();
+  if (!nc) return 0;
+  std::set<void*> seen;
+  for (const Op& o : ops_) {
+    if (!o.comm || !seen.insert(o.comm).second) continue;
+    int err = 0;
+    const int rc = nc->async_error(o.comm, &err);
+    if (rc != 0) return rc;
+    if (err != 0) return err;
+  }
+  return 0;
+}
+
+}  // namespace dnn

@@ -67,6 +67,9 @@ class StageParams:
         self.grad = torch.zeros(off, dtype=torch.float32, device=device)
         self.state: list[torch.Tensor] = []
         self.step_count = 0
+        # transposed bf16 weight shadows W^T[Kp][Np] of the layers whose dgrad reads them
+        # (enable_wt); refreshed after every update of their layer (refresh_t)
+        self.wt: dict[int, torch.Tensor] = {}
         self._init_state()
 
     def _init_state(self):
@@ -129,6 +132,26 @@ class StageParams:
 
     def refresh_shadow(self) -> None:
         self.shadow.copy_(self.master.to(torch.bfloat16))
+        self.refresh_t()
+
+    def enable_wt(self, i: int) -> None:
+        g = self.geoms[i]
+        if i not in self.wt:
+            self.wt[i] = torch.zeros(g.kp, g.np_, dtype=torch.bfloat16, device=self.device)
+            ops.transpose_bf16(self.wbf(i), self.wt[i])
+
+    def refresh_t(self, a: int = 0, b: Optional[int] = None) -> None:
+        """Re-derive W^T of the local layers [a, b) that keep one (after their update)."""
+        b = len(self.geoms) if b is None else b
+        for i in range(a, b):
+            if i in self.wt:
+                ops.transpose_bf16(self.wbf(i), self.wt[i])
+
+    def _layers_of(self, e0: int, e1: int) -> tuple[int, int]:
+        """Local layers whose parameters lie in the flat element range [e0, e1)."""
+        ls = [i for i in range(len(self.geoms)) if self.w_off[i] < e1 and
+              self.b_off[i] + self.geoms[i].np_ > e0]
+        return (ls[0], ls[-1] + 1) if ls else (0, 0)
 
     def _export_flat(self, buf: torch.Tensor) -> tuple[list[np.ndarray], list[np.ndarray]]:
         ws, bs = [], []
@@ -198,6 +221,7 @@ class StageParams:
                             decoupled=o.decoupled or o.name == "adamw", lr_dev=self.lr_dev,
                             step_dev=self.step_dev)
             ops.step_advance(self.step_dev)
+        self.refresh_t()
 
     def record_update_range(self, a: int, b: int, advance: bool) -> None:
         """record_update over the flat element range [a, b) only (a DP bucket of whole layers);
@@ -218,6 +242,7 @@ class StageParams:
                             step_dev=self.step_dev)
         if advance and o.name != "sgd":
             ops.step_advance(self.step_dev)
+        self.refresh_t(*self._layers_of(a, b))
 
     def update_range(self, a: int, b: int, lr: Optional[float], advance: bool) -> None:
         """Optimizer update of the flat range [a, b) (see record_update_range); the host step
@@ -239,6 +264,7 @@ class StageParams:
                                 self.state[1][sl], self.shadow[sl], lr=lr, betas=o.betas,
                                 eps=o.eps, weight_decay=o.weight_decay,
                                 decoupled=o.decoupled or o.name == "adamw", step=step)
+            self.refresh_t(*self._layers_of(a, b))
         if advance:
             self.step_count += 1
 
@@ -265,6 +291,7 @@ class StageParams:
             ops.adam_update(self.master, self.grad, self.state[0], self.state[1], self.shadow,
                             lr=lr, betas=o.betas, eps=o.eps, weight_decay=o.weight_decay,
                             decoupled=o.decoupled or o.name == "adamw", step=self.step_count)
+        self.refresh_t()
 
 
 class Stage:
@@ -337,6 +364,13 @@ class Stage:
         # layers, the softmax CE and both of their dgrads run as ONE kernel inside the last
         # layer's forward; the second-to-last layer's forward and both dgrads are then no-ops.
         self.tail = self._tail_ok()
+        # dgrad GEMMs read W^T (contraction-contiguous B operand, see ops.linear_dgrad)
+        if dev.type == "cuda" and os.environ.get("DNN_DGRAD_WT", "1") == "1":
+            L = len(self.geoms)
+            for i in range(L):
+                if (i > 0 or not self.first) and not (self.tail and i >= L - 2) and \
+                        not (i > 0 and self.relu_mask[i - 1] is not None):
+                    self.params.enable_wt(i)
         if self.tail:
             self.xent_per_micro = ops.tail_blocks(self.mb)
         else:
@@ -511,14 +545,15 @@ class Stage:
             ops.linear_dgrad(self.dz[i][r], p.wbf(i), self.dz[i - 1][r],
                              y_prev=self.acts[i - 1][r], act_prev=prev,
                              colsum=self._bpart(i - 1, j),
-                             mask_prev=None if m is None else m[r])
+                             mask_prev=None if m is None else m[r], wt=p.wt.get(i))
         elif not self.first:
             # gradient for the previous stage, already multiplied by the derivative of its
             # last layer's activation (its output is our input x_in)
             up = self._colsum_for
             ops.linear_dgrad(self.dz[0][r], p.wbf(0), self.dx_send[r], y_prev=self.x_in[r],
                              act_prev=self.prev_act,
-                             colsum=None if up is None else up._bpart(len(up.geoms) - 1, j))
+                             colsum=None if up is None else up._bpart(len(up.geoms) - 1, j),
+                             wt=p.wt.get(0))
 
     def wgrad(self, j: int = -1) -> None:
         """Weight/bias gradients for micro-batch j (slab-accumulated) or all rows (j = -1)."""
@@ -618,6 +653,7 @@ class Stage:
                                             mom=p.state[0] if p.state else None,
                                             shadow=p.shadow, lr=o.lr, momentum=o.momentum,
                                             weight_decay=o.weight_decay, lr_dev=p.lr_dev))
+            p.refresh_t()
             return
         ops.reduce_multi(jobs, sgd=dict(grad=p.grad, master=p.master, mom=p.state[0],
                                         v=p.state[1], shadow=p.shadow, lr=o.lr,
@@ -626,6 +662,7 @@ class Stage:
                                         decoupled=o.decoupled or o.name == "adamw",
                                         step_dev=p.step_dev))
         ops.step_advance(p.step_dev)  # as record_update: the segment replaces FIN + O
+        p.refresh_t()
 
     def update_then_forward(self, j: int, s: int, lr: Optional[float] = None) -> None:
         """Deferred DP update of layers [s, L) (completing the step: advance) followed by the

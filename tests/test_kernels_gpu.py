@@ -487,3 +487,38 @@ def test_gemv_matches_fp32(dev, M, N, K):
     yb = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
     ops.linear_fwd(x, w, b, yb, act="relu")  # dispatches to gemv for <= 8 rows
     torch.testing.assert_close(yb.float(), torch.relu(ref), rtol=1.6e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("rows,cols", [(64, 64), (512, 832), (1024, 192)])
+def test_transpose_bf16(dev, rows, cols):
+    gen = torch.Generator().manual_seed(rows + cols)
+    src = torch.randn(rows, cols, generator=gen).to(torch.bfloat16).to(dev)
+    dst = torch.full((cols, rows), 7.0, dtype=torch.bfloat16, device=dev)
+    ops.transpose_bf16(src, dst)
+    assert torch.equal(dst, src.t())
+
+
+@pytest.mark.parametrize("M,N,K,tiles", [(512, 128, 832, None), (1024, 1024, 1024, None),
+                                         (4096, 1024, 1024, (256, 256))])
+def test_dgrad_transposed_weight_bitwise(dev, M, N, K, tiles):
+    """dgrad through the transposed weight shadow (both operands contraction-contiguous) equals
+    the transposing-read dgrad bit for bit: same fragments, same MFMA k order; epilogue with the
+    ReLU derivative and the bias-gradient partials included."""
+    gen = torch.Generator().manual_seed(M + N + K)
+    dz = torch.randn(M, N, generator=gen).to(torch.bfloat16).to(dev)
+    w = torch.randn(N, K, generator=gen).to(torch.bfloat16).to(dev)
+    wt = torch.empty(K, N, dtype=torch.bfloat16, device=dev)
+    ops.transpose_bf16(w, wt)
+    y_prev = torch.randn(M, K, generator=gen).clamp_min(0).to(torch.bfloat16).to(dev)
+    bm = ops.dgrad_tiles(M, K, N)[0]
+    outs = []
+    for use_t in (False, True):
+        dx = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
+        part = torch.zeros(M // bm, K, device=dev)
+        ops.linear_dgrad(dz, w, dx, y_prev=y_prev, act_prev="relu", colsum=part,
+                         wt=wt if use_t else None)
+        outs.append((dx, part))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    ref = (dz.float() @ w.float()) * (y_prev.float() > 0)
+    torch.testing.assert_close(outs[1][0].float(), ref, rtol=2e-2, atol=2e-2 * K ** 0.5)
