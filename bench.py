@@ -9,19 +9,37 @@ JSON line.
 Model: BASELINE.json config "784-512-256-128-10 MNIST FCNN bf16" (random init, synthetic
 MNIST-shaped data resident in HBM). One step = forward + backward + SGD update of the global
 batch (bf16 operands, fp32 accumulation/master weights), on our own gfx950 kernels.
-Parallel layout: ``--parallelism auto`` lets the planner pick pp x dp for N GPUs (see
-docker_dist_nn_amd/parallel/planner.py); ``ppS`` forces an S-stage pipeline, ``dpN`` pure data
-parallelism, ``ppSdpD`` both.
+
+Parallel layout (the metric is "... at 1/2/4/8-stage pipeline"):
+  * ``--parallelism pipeline`` (default): N = 1 is the single-GPU step; for N > 1 the deepest
+    pipeline that divides N and fits the layers, data parallel over the rest
+    (planner.pipeline_layout: pp2, pp4, pp4dp2 at 2/4/8 GPUs for this model), one stage per
+    GPU, the layer split chosen by the planner's hop/compute model, 1F1B micro-batching, and
+    the native multi-rank step (parallel/native_step.py: one C++ call per step, RCCL P2P on
+    per-direction communicators, DP buckets on their own stream);
+  * after the pipeline number, the same N GPUs also run pure data parallelism (``dp_only`` in
+    the JSON; ``--no-dp-compare`` skips it);
+  * ``ppS`` / ``dpN`` / ``ppSdpD`` force a layout; ``best`` lets the planner pick.
+Weak scaling: every GPU contributes ``--batch`` rows per step.
 """
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
 import time
 
-import torch
+# Multi-rank steps run up to four busy streams per rank (compute, forward hops, backward hops,
+# DP buckets; parallel/native_step.py) next to torch's RCCL streams. HIP multiplexes streams
+# onto GPU_MAX_HW_QUEUES hardware queues (default 4) in order, so two streams sharing a queue
+# would serialise a spinning RCCL receive in one direction with a send in the other. Give
+# every stream its own queue (set before the HIP runtime initialises; <= 32 by pool policy).
+if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+
+import torch  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -38,6 +56,10 @@ BASELINE_SAMPLES_PER_S = 10_800.0
 MODEL_LABEL = {"mnist-fcnn": "784-512-256-128-10 MNIST FCNN",
                "mlp8": "784-1024x7-10 MLP (8 Linear)", "mlp7": "784-1024x6-10 MLP",
                "wide": "784-8192-8192-10 MLP"}
+# behaviour switches echoed into the JSON (the values in effect for this run)
+SWITCHES = ("DNN_BLAS", "DNN_TUNED", "DNN_TUNED_TABLE", "DNN_PIPE", "DNN_NATIVE_DIST",
+            "DNN_NATIVE_EXEC", "DNN_DGRAD_WT", "DNN_TAIL", "DNN_FUSED_XENT", "DNN_DP_DEFER",
+            "DNN_GEMM_STAGES", "DNN_GEMM_PERSIST", "DNN_WGRAD_GROUP", "DNN_DIST_BACKEND")
 
 
 def parse_args(argv=None):
@@ -48,7 +70,7 @@ def parse_args(argv=None):
     ap.add_argument("--model", default="mnist-fcnn")
     ap.add_argument("--batch", type=int, default=65536,
                     help="rows per GPU per step (global batch = batch x N)")
-    ap.add_argument("--parallelism", default="auto")
+    ap.add_argument("--parallelism", default="pipeline")
     ap.add_argument("--schedule", default="1f1b")
     ap.add_argument("--micro", type=int, default=0, help="micro-batch rows (0 = planner)")
     ap.add_argument("--lr", type=float, default=0.05)
@@ -57,52 +79,45 @@ def parse_args(argv=None):
                     help="replay the step as a HIP graph (1 GPU); eager is faster at large batch")
     ap.add_argument("--graph-copies", type=int, default=2,
                     help="alternate between this many instantiations of the step graph")
+    ap.add_argument("--no-dp-compare", action="store_true",
+                    help="N > 1: skip the data-parallel-only comparison run")
     ap.add_argument("--seed", type=int, default=0)
     return ap.parse_args(argv)
 
 
-def main(argv=None):
-    a = parse_args(argv)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if a.gpus != world and world > 1:
-        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
-    n = max(a.gpus, world)
-    spec = NAMED_MODELS.get(a.model) or MLPSpec.parse(a.model)
-
-    # DNN_FORCE_DEVICE / DNN_DIST_BACKEND exist only to rehearse the multi-rank path on a
-    # one-GPU box (several gloo ranks sharing cuda:0); real runs use one GPU per rank + RCCL.
-    local = int(os.environ.get("DNN_FORCE_DEVICE", os.environ.get("LOCAL_RANK", "0")))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-
-    mesh = None
-    if world > 1:
-        from docker_dist_nn_amd.parallel.groups import build_mesh, init_distributed
-
-        init_distributed(os.environ.get("DNN_DIST_BACKEND", "nccl"))
-    pp, dp = parse_parallelism(a.parallelism, n, loopback=world == 1)
+def _plan(a, spec, n, world, text):
     planner = Planner()
-    gpus_per_replica = 1 if world == 1 else None  # loopback: every stage on the one GPU
+    loopback = world == 1
+    pp, dp = parse_parallelism(text, n, loopback=loopback)
     if pp is None:
-        plan = planner.best(spec, n, a.batch)
-    else:
-        plan = planner.evaluate(spec, pp, dp, a.batch * (gpus_per_replica or pp))
+        if text == "best":
+            return planner.best(spec, n, a.batch)
+        if n == 1:
+            return planner.evaluate(spec, 1, 1, a.batch)
+        return planner.pipeline_layout(spec, n, a.batch)
+    rows = a.batch * (1 if loopback else pp)  # loopback: every stage on the one GPU
+    return planner.evaluate(spec, pp, dp, rows)
+
+
+def measure(a, spec, n, world, dev, text):
+    """Build the trainer for one layout, W warm-up + K timed steps; returns the JSON fields."""
+    plan = _plan(a, spec, n, world, text)
     mb = a.micro or plan.micro_batch
-    # rows per replica per step (weak scaling: `batch` rows per GPU)
-    rows = a.batch * (gpus_per_replica or plan.pp)
+    rows = a.batch * (1 if world == 1 else plan.pp)  # rows per replica per step
     nm = max(1, rows // mb)
     if mb * nm != rows or mb % 64:
         raise SystemExit(f"batch {rows} must split into micro-batches of a multiple of 64")
+    mesh = None
     if world > 1:
-        mesh = build_mesh(plan.pp, plan.dp)
-        # communicator set-up (RCCL rings/channels) happens at a group's first collective:
-        # do it here, outside the W warm-up steps and the timed region
-        t = torch.ones(1024, device=dev)
-        if mesh.dp_group is not None:
-            torch.distributed.all_reduce(t, group=mesh.dp_group)
-        torch.distributed.all_reduce(t)
-        torch.cuda.synchronize(dev)
+        from docker_dist_nn_amd.parallel.groups import build_mesh
 
+        mesh = build_mesh(plan.pp, plan.dp)
+        # communicator set-up happens at a group's first collective: do it here, outside the
+        # W warm-up steps and the timed region
+        t = torch.ones(1024, device=dev)
+        for g in (mesh.fwd_group, mesh.bwd_group, mesh.dp_group, None):
+            torch.distributed.all_reduce(t, group=g)
+        torch.cuda.synchronize(dev)
     tr = Trainer(spec, micro_batch=mb, num_micro=nm, distribution=plan.distribution,
                  pp=plan.pp, dp=plan.dp, schedule=a.schedule,
                  optim=OptimConfig(name=a.optimizer, lr=a.lr),
@@ -143,40 +158,81 @@ def main(argv=None):
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
-
     loss = tr.loss()
+    if world > 1:  # the last stage of replica 0 owns the loss; rank 0 prints
+        lt = torch.tensor([loss if loss is not None else -1.0], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(lt, op=torch.distributed.ReduceOp.MAX)
+        loss = float(lt.item())
     global_batch = rows * plan.dp
-    samples = global_batch * a.steps
-    value = samples / elapsed
+    value = global_batch * a.steps / elapsed
+    out = {
+        "value": round(value, 1), "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+        "global_batch": global_batch,
+        "parallelism": plan.parallelism + ("-loopback" if world == 1 and plan.pp > 1 else ""),
+        "layer_distribution": plan.distribution, "micro_batch": mb, "num_micro": nm,
+        "schedule": a.schedule if plan.pp > 1 else "none",
+        "transport": tr.transport, "native_step": tr.native_step is not None or world == 1,
+        "hip_graph": use_graph, "graph_copies": a.graph_copies if use_graph else 0,
+        "loss": loss, "planner_predicted": round(plan.samples_per_s, 1),
+    }
+    del tr, data
+    gc.collect()
+    torch.cuda.empty_cache()
+    return out
+
+
+def main(argv=None):
+    a = parse_args(argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.gpus != world and world > 1:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    n = max(a.gpus, world)
+    spec = NAMED_MODELS.get(a.model) or MLPSpec.parse(a.model)
+
+    # DNN_FORCE_DEVICE / DNN_DIST_BACKEND exist only to rehearse the multi-rank path on a
+    # one-GPU box (several gloo ranks sharing cuda:0); real runs use one GPU per rank + RCCL.
+    local = int(os.environ.get("DNN_FORCE_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        from docker_dist_nn_amd.parallel.groups import init_distributed
+
+        init_distributed(os.environ.get("DNN_DIST_BACKEND", "nccl"))
+
+    m = measure(a, spec, n, world, dev, a.parallelism)
+    dp_only = None
+    if world > 1 and not a.no_dp_compare and not m["parallelism"].startswith("dp"):
+        d = measure(a, spec, n, world, dev, f"dp{n}")
+        dp_only = {k: d[k] for k in ("value", "ms_per_step", "parallelism", "global_batch",
+                                     "transport", "native_step")}
     out = {
         "metric": METRIC,
-        "value": round(value, 1),
+        "value": m["value"],
         "unit": "samples/s",
         "n_gpus": n,
         "steps": a.steps,
         "warmup": a.warmup,
-        "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+        "ms_per_step": m["ms_per_step"],
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": round(value / BASELINE_SAMPLES_PER_S, 1),
+        "vs_baseline": round(m["value"] / BASELINE_SAMPLES_PER_S, 1),
         "dtype": "bf16",
         "data": "synthetic (MNIST-shaped 784-feature inputs, teacher labels; random-init weights)",
         "config": {
             "model": MODEL_LABEL.get(a.model, spec.describe()),
-            "global_batch": global_batch,
+            "global_batch": m["global_batch"],
             "seq_len": None,
-            "parallelism": plan.parallelism + ("-loopback" if world == 1 and plan.pp > 1
-                                               else ""),
-            "layer_distribution": plan.distribution,
-            "micro_batch": mb,
-            "num_micro": nm,
-            "schedule": a.schedule if plan.pp > 1 else "none",
+            **{k: m[k] for k in ("parallelism", "layer_distribution", "micro_batch", "num_micro",
+                                 "schedule", "transport", "native_step", "hip_graph",
+                                 "graph_copies")},
             "optimizer": a.optimizer,
-            "hip_graph": use_graph,
-            "graph_copies": a.graph_copies if use_graph else 0,
         },
-        "model_tflops": round(spec.flops_per_sample_train() * value / 1e12, 1),
-        "last_loss": None if loss is None else round(loss, 5),
+        # EXECUTED FLOPs (no dgrad of the first layer: models/mlp.py)
+        "model_tflops": round(spec.flops_per_sample_train() * m["value"] / 1e12, 1),
+        "last_loss": None if m["loss"] is None else round(m["loss"], 5),
+        "planner_predicted": m["planner_predicted"],
+        "dp_only": dp_only,
+        "switches": {k: os.environ[k] for k in SWITCHES if k in os.environ},
     }
     rank = int(os.environ.get("RANK", "0"))
     if rank == 0:

@@ -19,7 +19,11 @@ import time
 from typing import Optional
 
 import numpy as np
-import torch
+
+if int(os.environ.get("WORLD_SIZE", "1")) > 1:  # one hardware queue per stream: see bench.py
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+
+import torch  # noqa: E402
 
 log = logging.getLogger("train")
 

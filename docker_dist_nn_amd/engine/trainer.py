@@ -38,6 +38,18 @@ def default_distribution(spec: MLPSpec, pp: int) -> list[int]:
     return balanced_distribution([l.flops_per_sample_train for l in spec.layers], pp)
 
 
+def _warm_groups(mesh: Mesh, device) -> None:
+    """Make sure the RCCL communicators of this rank's groups exist (one tiny collective each,
+    in the same group order on every rank) before their handles are taken."""
+    import torch.distributed as dist
+
+    t = torch.zeros(1, device=device)
+    for g in (mesh.fwd_group, mesh.bwd_group, mesh.dp_group):
+        if g is not None:
+            dist.all_reduce(t, group=g)
+    torch.cuda.synchronize(device)
+
+
 class Trainer:
     def __init__(self, spec: MLPSpec, *, micro_batch: int, num_micro: int = 1, pp: int = 1,
                  dp: int = 1, distribution: Optional[Sequence[int]] = None,
@@ -96,6 +108,23 @@ class Trainer:
         if self.native_exec:
             for st in self.stages:
                 st.compile_native()
+        # native multi-rank step (parallel/native_step.py): the rank's whole step -- segment
+        # replays, RCCL hops / xGMI peer copies, DP buckets -- as ONE C++ call per step
+        self.native_step = None
+        self.transport = ("loopback" if mesh is None else
+                          "ipc" if isinstance(self.pipe, IpcPipe) else
+                          "rccl" if mesh.backend == "nccl" else mesh.backend)
+        if mesh is not None and self.native_exec and \
+                os.environ.get("DNN_NATIVE_DIST", "1") != "0":
+            from ..parallel.native_step import NativeStep, native_step_supported
+
+            why = native_step_supported(self.executor, mesh)
+            if why is None and self.transport in ("rccl", "ipc"):
+                if mesh.backend == "nccl":
+                    _warm_groups(mesh, self.device)
+                self.native_step = NativeStep(self.executor, mesh, self.transport,
+                                              ipc=self.pipe if self.transport == "ipc" else None)
+                self.executor.native_step = self.native_step
         self._graph = None
         self._stream = None
         self.graph_nodes = 0

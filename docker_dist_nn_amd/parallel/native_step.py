@@ -1,0 +1,250 @@
+"""Native multi-rank training step: the whole step of a rank as ONE C++ call.
+
+The Python executor (pipeline.PipelineExecutor._run_op) walks the schedule op by op and issues
+every pipeline hop and DP bucket through torch.distributed. For a rank that owns one stage this
+module instead compiles the SAME schedule once into a ``StepPlan`` (csrc/runtime/step_plan.hpp)
+of recorded-segment replays, RCCL calls on the communicators torch already created (or xGMI
+peer copies + stream flags), and event edges between four streams:
+
+  stream 0  compute (the caller's stream): F{j}, B{j}, W{i}, FIN*, O / FINO segments
+  stream 1  forward hops:   recv F(j) from the previous stage, send F(j) to the next
+  stream 2  backward hops:  recv B(j) from the next stage,     send B(j) to the previous
+  stream 3  data-parallel gradient all-reduce buckets
+
+Each direction keeps its own FIFO in micro-batch order on its own communicator (the fwd / bwd
+process groups of parallel/groups.py), so a blocked transfer in one direction never stalls the
+other and no send/recv grouping is needed; compute waits only for the receive it consumes.
+DP buckets (pipeline.dp_buckets: largest layer first) are all-reduced on stream 3 while the
+remaining weight-gradient GEMMs run, then the update waits for all of them.
+
+Per step the host does: lr scalar refresh, one ``StepPlan.run``. No Python per hop, no host
+synchronisation, and the plan forks/joins its streams from the caller's stream, so the whole
+step can be captured into a HIP graph.
+
+Reference: the stage chain /root/reference/src/grpc_node.py:120-135 (one synchronous RPC per
+hop) and its spawn/topology /root/reference/src/run_grpc_fcnn.py:199-248.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+
+from ..utils.native import native
+from .pipeline import dp_buckets
+
+SEG, SEND, RECV, ALLREDUCE, REDUCE_SCATTER, ALL_GATHER, COPY, SIGNAL, WAITV, REC, WAIT = range(11)
+NCCL_BF16, NCCL_F32 = 9, 7
+MAIN, FWD, BWD, DPS = 0, 1, 2, 3
+
+
+def torch_rccl_path() -> str:
+    """The librccl torch loaded (its communicators live in that instance)."""
+    return os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+
+
+def comm_ptr(group, device) -> int:
+    """ncclComm_t of a torch process group (created eagerly by a collective if needed)."""
+    be = group._get_backend(device)
+    p = int(be._comm_ptr())
+    if not p:
+        raise RuntimeError("process group has no RCCL communicator yet")
+    return p
+
+
+class NativeStep:
+    """Builds and runs the StepPlan of one rank. ``transport``: "rccl" (RCCL P2P on the fwd /
+    bwd groups) or "ipc" (an IpcPipe's mapped peer buffers and flags)."""
+
+    def __init__(self, executor, mesh, transport: str, ipc=None):
+        if len(executor.stages) != 1:
+            raise ValueError("native multi-rank step: one stage per rank")
+        st = executor.stages[0]
+        if st._prog is None or not st._has_w or not st._o_native:
+            raise ValueError("native multi-rank step needs a recorded stage (compile_native)")
+        self.ex, self.mesh, self.st = executor, mesh, st
+        self.transport = transport
+        self.ipc = ipc
+        self.n = native()
+        dev = st.device
+        self.dp = mesh.dp if mesh is not None else 1
+        if transport == "rccl" or self.dp > 1:
+            self.n.nccl_load(torch_rccl_path())
+        self.comm_f = self.comm_b = self.comm_dp = 0
+        if transport == "rccl" and mesh.pp > 1:
+            self.comm_f = comm_ptr(mesh.fwd_group, dev)
+            self.comm_b = comm_ptr(mesh.bwd_group, dev)
+        if self.dp > 1:
+            self.comm_dp = comm_ptr(mesh.dp_group, dev)
+        self._ev = 0
+        self.ops: list[tuple] = []
+        self._build()
+        self.plan = self.n.StepPlan(4, max(1, self._ev))
+        for o in self.ops:
+            self.plan.add(**o)
+
+    # ---- plan construction -------------------------------------------------------------
+    def _event(self) -> int:
+        self._ev += 1
+        return self._ev - 1
+
+    def _edge(self, src: int, dst: int) -> None:
+        """Stream ``dst`` waits for everything enqueued on ``src`` so far."""
+        e = self._event()
+        self.ops.append(dict(kind=REC, stream=src, event=e))
+        self.ops.append(dict(kind=WAIT, stream=dst, event=e))
+
+    def _seg(self, name: str, stream: int = MAIN) -> None:
+        self.ops.append(dict(kind=SEG, stream=stream, prog=self.st._prog, seg=name))
+
+    def _rows(self, t: torch.Tensor, j: int) -> tuple[int, int]:
+        r = self.st.rows_of(j)
+        v = t[r]
+        return v.data_ptr(), v.numel()
+
+    def _recv(self, direction: str, j: int) -> None:
+        st, m = self.st, self.mesh
+        t = st.x_in if direction == "f" else st.grad_out
+        if self.transport == "ipc":  # the producer's copy + flag: wait on the compute stream
+            base = self.ipc.flags.data_ptr()
+            idx = j if direction == "f" else st.nm + j
+            self.ops.append(dict(kind=WAITV, stream=MAIN, a=base + 4 * idx, delta=0))
+            return
+        ptr, cnt = self._rows(t, j)
+        s = FWD if direction == "f" else BWD
+        peer = m.stage - 1 if direction == "f" else m.stage + 1
+        self.ops.append(dict(kind=RECV, stream=s, comm=self.comm_f if s == FWD else self.comm_b,
+                             a=ptr, count=cnt, dtype=NCCL_BF16, peer=peer))
+        self._edge(s, MAIN)
+
+    def _send(self, direction: str, j: int) -> None:
+        st, m = self.st, self.mesh
+        t = st.output if direction == "f" else st.dx_send
+        s = FWD if direction == "f" else BWD
+        self._edge(MAIN, s)
+        ptr, cnt = self._rows(t, j)
+        if self.transport == "ipc":
+            p = self.ipc
+            peer = p.next if direction == "f" else p.prev
+            nm = st.nm
+            if j == 0:  # the peer finished reading that buffer in the previous step (ack)
+                self.ops.append(dict(kind=WAITV, stream=s,
+                                     a=p.flags.data_ptr() + 4 * (2 * nm + (0 if direction == "f"
+                                                                          else 1)),
+                                     delta=-1))
+            dst_base = peer["x_in"] if direction == "f" else peer["grad_out"]
+            row_bytes = p.row_bytes_f if direction == "f" else p.row_bytes_b
+            off = st.rows_of(j).start * row_bytes
+            self.ops.append(dict(kind=COPY, stream=s, a=ptr, b=dst_base + off,
+                                 count=cnt * t.element_size()))
+            idx = j if direction == "f" else nm + j
+            self.ops.append(dict(kind=SIGNAL, stream=s, a=peer["flags"] + 4 * idx, delta=0))
+            return
+        peer = m.stage + 1 if direction == "f" else m.stage - 1
+        self.ops.append(dict(kind=SEND, stream=s, comm=self.comm_f if s == FWD else self.comm_b,
+                             a=ptr, count=cnt, dtype=NCCL_BF16, peer=peer))
+
+    def _wgrad_update(self) -> None:
+        st = self.st
+        segs = st._prog.segments()
+        if self.dp <= 1:
+            self._seg("W")
+            if "FINO" in segs:
+                self._seg("FINO")
+            else:
+                self._seg("FIN")
+                self._seg("O")
+            return
+        p = st.params
+        for bucket in dp_buckets(st):
+            for i in bucket:
+                self._seg(f"W{i}")
+            a, b = bucket[0], bucket[-1]
+            self._seg(f"FIN{a}" if a == b else f"FIN{a}-{b}")
+            e0, _ = p.layer_grad_range(a)
+            _, e1 = p.layer_grad_range(b)
+            self._edge(MAIN, DPS)
+            self.ops.append(dict(kind=ALLREDUCE, stream=DPS, comm=self.comm_dp,
+                                 a=p.grad.data_ptr() + 4 * e0, count=e1 - e0, dtype=NCCL_F32))
+        self._edge(DPS, MAIN)
+        self._seg("O")
+
+    def _build(self) -> None:
+        m, st = self.mesh, self.st
+        ops = self.ex.ops[0]
+        has_prev = m is not None and m.prev_rank is not None
+        has_next = m is not None and m.next_rank is not None
+        for k, (op, j) in enumerate(ops):
+            nxt = ops[k + 1][0] if k + 1 < len(ops) else None
+            if op == "F":
+                if has_prev:
+                    self._recv("f", j)
+                self._seg(f"F{j}")
+                if has_next:
+                    self._send("f", j)
+            elif op == "B":
+                if has_next:
+                    self._recv("b", j)
+                self._seg(f"B{j}")
+                if has_prev:
+                    self._send("b", j)
+            elif op == "W":
+                if j >= 0 or nxt != "O":
+                    raise ValueError("native multi-rank step: batched W followed by O only")
+                self._wgrad_update()
+            elif op == "O":
+                pass  # emitted with the batched W
+        if self.transport == "ipc":  # release the buffers I receive into for the next step
+            p, nm = self.ipc, st.nm
+            if p.prev is not None:
+                self.ops.append(dict(kind=SIGNAL, stream=MAIN, a=p.prev["flags"] + 4 * (2 * nm),
+                                     delta=0))
+            if p.next is not None:
+                self.ops.append(dict(kind=SIGNAL, stream=MAIN,
+                                     a=p.next["flags"] + 4 * (2 * nm + 1), delta=0))
+
+    # ---- execution -----------------------------------------------------------------------
+    def run(self, stream: int) -> None:
+        p = self.st.params
+        p.set_lr(p.optim.lr)
+        if self.transport == "ipc":
+            self.plan.seq = self.ipc.seq  # one sequence space with the Python IpcPipe
+        self.plan.run(stream)
+        if self.transport == "ipc":
+            self.ipc.seq = self.plan.seq
+        p.step_count += 1
+
+    def comm_error(self) -> int:
+        return self.plan.comm_error()
+
+    def describe(self) -> dict:
+        kinds = {}
+        for o in self.ops:
+            kinds[o["kind"]] = kinds.get(o["kind"], 0) + 1
+        names = ["SEG", "SEND", "RECV", "ALLREDUCE", "REDUCE_SCATTER", "ALL_GATHER", "COPY",
+                 "SIGNAL", "WAITV", "REC", "WAIT"]
+        return {"transport": self.transport, "ops": len(self.ops),
+                "by_kind": {names[k]: v for k, v in sorted(kinds.items())}}
+
+
+def native_step_supported(executor, mesh) -> Optional[str]:
+    """None if the executor's step can run as a NativeStep, else the reason it cannot."""
+    if mesh is None:
+        return "single process (the loopback plan covers it)"
+    if len(executor.stages) != 1:
+        return "several stages in one process"
+    st = executor.stages[0]
+    if st.device.type != "cuda":
+        return "CPU stage"
+    if st._prog is None or not st._has_w or not st._o_native:
+        return "stage not recorded"
+    if executor.hooks["before_op"] or executor.hooks["after_op"] or executor.lr_fn is not None:
+        return "per-op hooks / lr schedule"
+    ops = executor.ops[0]
+    for k, (op, j) in enumerate(ops):
+        if op == "W" and (j >= 0 or k + 1 >= len(ops) or ops[k + 1][0] != "O"):
+            return "per-micro-batch weight gradients"
+    if mesh.dp > 1 and mesh.backend != "nccl":
+        return "data-parallel group is not RCCL"
+    return None

@@ -317,6 +317,12 @@ class PipelineExecutor:
         return plan
 
     def run_step(self) -> None:
+        ns = getattr(self, "native_step", None)
+        if ns is not None:  # one C++ call: parallel/native_step.py
+            for st in self.stages:
+                st.begin_step()
+            ns.run(torch.cuda.current_stream(self.stages[0].device).cuda_stream)
+            return
         self.pipe.begin_step()
         for st in self.stages:
             st.begin_step()

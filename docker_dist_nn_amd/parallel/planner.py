@@ -1,28 +1,32 @@
 """Parallel-layout planner: choose (pp, dp, layer_distribution, micro-batching) for N GPUs.
 
-MI355X-first reasoning, encoded as a cost model:
+MI355X-first reasoning, encoded as a cost model (all constants overridable):
 
-* a pipeline hop moves ``rows x width x 2`` bytes of bf16 activations forward and the same
-  amount of gradients backward over ONE xGMI link (point-to-point, ~50-64 GB/s per direction
-  achieved); per sample that is ``4 * width`` bytes per hop against ``6 * in * out`` FLOPs of
-  stage compute, so thin (MNIST-width) layers make a pipeline link-bound long before it is
-  compute-bound;
-* a data-parallel replica instead moves only its gradients, once per step, with a ring
-  all-reduce that RCCL spreads over the fully connected xGMI mesh, overlapped with the
-  remaining weight-gradient GEMMs.
+* compute: a stage's time is its EXECUTED training FLOPs (fwd + dgrad + wgrad, no dgrad for the
+  network's first layer) at the step rate measured on one MI355X (``tflops``);
+* a pipeline hop moves ``width x 2`` bytes per sample (bf16) forward over the direct xGMI link
+  between two GPUs and the same backward on the opposite direction of that link; the native
+  step (parallel/native_step.py) runs each direction on its own stream, overlapped with
+  compute, so in steady state a micro-batch costs ``max(stage compute, hop in, hop out)``
+  (``link_gbps`` = achieved per-direction point-to-point rate; xGMI is 7 links x ~153 GB/s per
+  GPU, not all of it reachable by one P2P stream);
+* a data-parallel replica all-reduces its stage gradient (fp32) once per step with RCCL's
+  rings over the fully connected mesh (``allreduce_gbps`` bus bandwidth), bucketed and about
+  half hidden behind the remaining weight-gradient GEMMs.
 
-The planner evaluates every (pp, dp) with pp * dp = N (pp <= number of layers), the balanced
-layer split for each pp, and the 1F1B step time including the bubble, and returns the fastest.
-Constants can be overridden from measurements (``Planner(link_gbps=..., tflops=...)``).
+``pipeline_layout`` is the layout the benchmark runs for N GPUs (the metric is "... at
+1/2/4/8-stage pipeline"): the deepest pipeline that divides N and fits the layers, data
+parallel over the rest, with the layer split this model scores best -- which weighs boundary
+WIDTH (hop bytes) against compute balance, not FLOPs alone. ``best`` searches every
+(pp, dp) instead (the data-parallel-only number the benchmark also reports).
 """
 from __future__ import annotations
 
-import math
-from dataclasses import dataclass
+import itertools
+from dataclasses import dataclass, field
 from typing import Optional
 
 from ..models.mlp import MLPSpec
-from ..partition import balanced_distribution
 
 
 @dataclass
@@ -34,6 +38,7 @@ class Plan:
     micro_batch: int
     step_time_s: float
     samples_per_s: float
+    detail: dict = field(default_factory=dict)
 
     @property
     def parallelism(self) -> str:
@@ -44,48 +49,79 @@ class Plan:
         return f"pp{self.pp}dp{self.dp}"
 
 
+def layer_train_flops(spec: MLPSpec) -> list[float]:
+    """Executed training FLOPs per sample of each layer (no dgrad for layer 0)."""
+    out = []
+    for i, l in enumerate(spec.layers):
+        out.append((4.0 if i == 0 else 6.0) * l.in_dim * l.out_dim)
+    return out
+
+
+def compositions(n: int, k: int):
+    """Every split of n consecutive layers into k non-empty contiguous stages."""
+    for cuts in itertools.combinations(range(1, n), k - 1):
+        b = (0,) + cuts + (n,)
+        yield [b[i + 1] - b[i] for i in range(k)]
+
+
 class Planner:
-    # Defaults calibrated on MI355X: measured training steps run at 565 (784-512-256-128-10),
-    # 730 (784-1024x7-10) and 935 (784-8192-8192-10) model TFLOP/s with no launch gaps
-    # (profiles/r1_tiles/configs_vs_torch.jsonl); xGMI P2P and all-reduce rates are
-    # conservative estimates (not measurable on the 1-GPU test pool).
-    def __init__(self, tflops: float = 700.0, link_gbps: float = 55.0, hop_latency_us: float = 25.0,
-                 allreduce_gbps: float = 120.0, step_overhead_us: float = 20.0):
+    # Calibrated on MI355X (one GPU, own kernels, profiles/r2_own_kernels): headline step 0.36 ms
+    # at 65536 rows = ~470 executed TFLOP/s; 784-1024x7-10 ~600; 784-8192-8192-10 ~880. The
+    # xGMI rates are estimates (the 1-GPU pool cannot time a cross-GPU hop).
+    def __init__(self, tflops: float = 550.0, link_gbps: float = 64.0,
+                 hop_latency_us: float = 15.0, allreduce_gbps: float = 150.0,
+                 step_overhead_us: float = 20.0, boundary_bytes: float = 2.0):
         self.rate = tflops * 1e12
         self.link = link_gbps * 1e9
         self.lat = hop_latency_us * 1e-6
         self.ar = allreduce_gbps * 1e9
         self.ovh = step_overhead_us * 1e-6
+        self.bb = boundary_bytes  # bytes per boundary element on the wire (bf16 = 2)
+
+    def _stage_costs(self, spec: MLPSpec, dist: list[int], mb: int):
+        fl = layer_train_flops(spec)
+        comp, hops, g = [], [], 0
+        for k in dist:
+            comp.append(sum(fl[g:g + k]) * mb / self.rate)
+            g += k
+            if g < len(spec.layers):
+                hops.append(self.lat + mb * spec.layers[g - 1].out_dim * self.bb / self.link)
+        return comp, hops
+
+    def best_distribution(self, spec: MLPSpec, pp: int, mb: int) -> list[int]:
+        best, best_t = None, float("inf")
+        for dist in compositions(len(spec.layers), pp):
+            comp, hops = self._stage_costs(spec, dist, mb)
+            t = max(comp + hops)
+            if t < best_t - 1e-15:
+                best, best_t = dist, t
+        return best
 
     def evaluate(self, spec: MLPSpec, pp: int, dp: int, rows_per_replica: int,
-                 micro_batch: Optional[int] = None) -> Plan:
+                 micro_batch: Optional[int] = None,
+                 distribution: Optional[list[int]] = None) -> Plan:
         L = spec.layers
-        flops = [l.flops_per_sample_train for l in L]
-        dist = balanced_distribution(flops, pp)
         mb = micro_batch or (rows_per_replica if pp == 1 else
                              max(64, rows_per_replica // (4 * pp) // 64 * 64))
         M = max(1, rows_per_replica // mb)
-        # per micro-batch stage time and boundary transfer time
-        stage_t, bounds, g = [], [], 0
-        for k in dist:
-            stage_t.append(sum(flops[g:g + k]) * mb / self.rate)
-            g += k
-            if g < len(L):
-                bounds.append(self.lat + mb * L[g - 1].out_dim * 2 / self.link)
-        per_micro = max(stage_t + bounds) if bounds else max(stage_t)
-        pipe = (M + pp - 1) * per_micro
-        # largest stage gradient all-reduce (bucketed, ~half hidden behind wgrad)
-        g, ar = 0, 0.0
+        dist = distribution or (self.best_distribution(spec, pp, mb) if pp > 1 else [len(L)])
+        comp, hops = self._stage_costs(spec, dist, mb)
+        per_micro = max(comp + hops)
+        pipe = (M + pp - 1) * per_micro if pp > 1 else comp[0]
+        ar, g = 0.0, 0
         for k in dist:
             params = sum(l.params for l in L[g:g + k])
             g += k
             if dp > 1:
                 ar = max(ar, 2 * (dp - 1) / dp * params * 4 / self.ar)
         t = pipe + 0.5 * ar + self.ovh
-        return Plan(pp, dp, dist, M, mb, t, rows_per_replica * dp / t)
+        detail = {"stage_ms_per_micro": [round(c * 1e3, 4) for c in comp],
+                  "hop_ms_per_micro": [round(h * 1e3, 4) for h in hops],
+                  "bubble": round((pp - 1) / (M + pp - 1), 3) if pp > 1 else 0.0,
+                  "allreduce_ms": round(ar * 1e3, 4)}
+        return Plan(pp, dp, dist, M, mb, t, rows_per_replica * dp / t, detail)
 
-    def best(self, spec: MLPSpec, n_gpus: int, rows_per_gpu: int,
-             min_pp: int = 1) -> Plan:
+    def best(self, spec: MLPSpec, n_gpus: int, rows_per_gpu: int, min_pp: int = 1) -> Plan:
         cands = []
         for pp in range(1, n_gpus + 1):
             if n_gpus % pp or pp > len(spec.layers) or pp < min_pp:
@@ -97,13 +133,22 @@ class Planner:
             raise ValueError(f"no valid layout for {n_gpus} GPUs and {len(spec.layers)} layers")
         return max(cands, key=lambda p: p.samples_per_s)
 
+    def pipeline_layout(self, spec: MLPSpec, n_gpus: int, rows_per_gpu: int) -> Plan:
+        """The deepest pipeline for N GPUs: pp = largest divisor of N that is <= #layers,
+        dp = N / pp (e.g. 784-512-256-128-10: pp2, pp4, pp4dp2 at 2/4/8; 784-8192-8192-10 at
+        8: pp2dp4 -- BASELINE.json's configurations)."""
+        pp = max(p for p in range(1, n_gpus + 1)
+                 if n_gpus % p == 0 and p <= len(spec.layers))
+        return self.evaluate(spec, pp, n_gpus // pp, rows_per_gpu * pp)
+
 
 def parse_parallelism(text: str, n_gpus: int,
                       loopback: bool = False) -> tuple[Optional[int], Optional[int]]:
-    """'auto' -> (None, None); 'pp4' / 'dp8' / 'pp2dp4' -> explicit degrees. With
-    ``loopback`` (one process), 'ppS' may exceed the GPU count: all S stages then run in the
-    one process (loopback channels) -- the pipeline engine without the interconnect."""
-    if text == "auto":
+    """'auto' / 'pipeline' / 'dp' -> (None, None) (the caller picks); 'pp4' / 'dp8' / 'pp2dp4'
+    -> explicit degrees. With ``loopback`` (one process), 'ppS' may exceed the GPU count: all S
+    stages then run in the one process (loopback channels) -- the pipeline engine without the
+    interconnect."""
+    if text in ("auto", "pipeline", "best"):
         return None, None
     import re
 

@@ -120,3 +120,96 @@ def test_pp2_ipc_pipe_bitwise_equals_rccl_path(dev):
             a = np.load(os.path.join(d, f"rccl_w{k}.npy"))
             b = np.load(os.path.join(d, f"ipc_w{k}.npy"))
             assert np.array_equal(a, b), k
+
+
+def _native_worker(rank, world, port, native_dist, steps, nm, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DNN_PIPE="ipc",
+                      DNN_NATIVE_DIST=native_dist)
+    import time
+
+    import torch.distributed as dist
+
+    from docker_dist_nn_amd import MLPSpec
+    from docker_dist_nn_amd.engine import OptimConfig, Trainer
+    from docker_dist_nn_amd.parallel.groups import build_mesh
+
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mesh = build_mesh(world, 1)
+    tr = Trainer(MLPSpec.parse(SPEC), micro_batch=256, num_micro=nm, mesh=mesh, device=dev,
+                 schedule="1f1b", optim=OptimConfig(name="sgd", lr=0.05, momentum=0.9))
+    assert (tr.native_step is not None) == (native_dist == "1")
+    xt, yt = _batch(256 * nm)
+    xd, yd = xt.to(dev), yt.to(dev)
+    host = []
+    for _ in range(steps):
+        tr.set_batch(xd if tr.first else None, yd if tr.last else None, zero_copy=True)
+        t0 = time.perf_counter()
+        tr.step()
+        host.append(time.perf_counter() - t0)
+    torch.cuda.synchronize()
+    for k, (w, _b) in tr.local_weights().items():
+        np.save(os.path.join(out_dir, f"n{native_dist}_w{k}.npy"), w)
+    np.save(os.path.join(out_dir, f"n{native_dist}_host_r{rank}.npy"), np.array(host))
+    if tr.last is not None:
+        np.save(os.path.join(out_dir, f"n{native_dist}_loss.npy"), np.array([tr.loss()]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,nm", [(2, 4), (4, 6)])
+def test_native_multirank_step_bitwise_equals_python(dev, world, nm):
+    """The native multi-rank step (parallel/native_step.py: ONE StepPlan call per step, xGMI
+    peer-copy transport) gives bit-identical weights and loss to the op-by-op Python executor
+    over the same transport; ranks = processes sharing cuda:0. Also bounds the host time of a
+    native step (the plan enqueues everything; no per-op Python)."""
+    steps = 4
+    with tempfile.TemporaryDirectory() as d:
+        for native_dist in ("0", "1"):
+            mp.start_processes(_native_worker,
+                               args=(world, _free_port(), native_dist, steps, nm, d),
+                               nprocs=world, join=True, start_method="spawn")
+        for k in range(4):
+            a = np.load(os.path.join(d, f"n0_w{k}.npy"))
+            b = np.load(os.path.join(d, f"n1_w{k}.npy"))
+            assert np.array_equal(a, b), k
+        assert np.array_equal(np.load(os.path.join(d, "n0_loss.npy")),
+                              np.load(os.path.join(d, "n1_loss.npy")))
+        host = [np.median(np.load(os.path.join(d, f"n1_host_r{r}.npy"))[1:])
+                for r in range(world)]
+        print("native host s/step per rank:", host)
+        assert max(host) < 2e-3, host
+
+
+def test_step_plan_rccl_allreduce_one_rank(dev):
+    """The StepPlan's RCCL entry points bind to torch's librccl and drive the communicator
+    torch created (world of one rank: all-reduce is a copy), on a plan-owned stream."""
+    import torch.distributed as dist
+
+    from docker_dist_nn_amd.parallel.native_step import (ALLREDUCE, NCCL_F32, REC, WAIT,
+                                                         comm_ptr, torch_rccl_path)
+    from docker_dist_nn_amd.utils.native import native
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        t = torch.ones(1, device=dev)
+        dist.all_reduce(t)
+        n = native()
+        n.nccl_load(torch_rccl_path())
+        comm = comm_ptr(dist.group.WORLD, dev)
+        assert n.nccl_comm_info(comm) == (1, 0)
+        x = torch.arange(4096, dtype=torch.float32, device=dev)
+        ref = x.clone()
+        plan = n.StepPlan(2, 2)
+        plan.add(kind=REC, stream=0, event=0)
+        plan.add(kind=WAIT, stream=1, event=0)
+        plan.add(kind=ALLREDUCE, stream=1, comm=comm, a=x.data_ptr(), count=x.numel(),
+                 dtype=NCCL_F32)
+        plan.run(torch.cuda.current_stream(dev).cuda_stream)
+        plan.run(torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize(dev)
+        assert torch.equal(x, ref) and plan.seq == 2 and plan.comm_error() == 0
+    finally:
+        dist.destroy_process_group()
