@@ -48,6 +48,8 @@ def build_parser(script_dir: str) -> argparse.ArgumentParser:
     ap.add_argument("--layer-distribution", type=str, default=None,
                     help="override, e.g. '[1,1,1]'")
     ap.add_argument("--cache-dir", type=str, default=os.path.join(script_dir, "cache/neuron_configs"))
+    ap.add_argument("--hop-timeout", type=float, default=10.0,
+                    help="per-hop deadline of the stage chain (reference: 10 s, grpc_node.py:133)")
     ap.add_argument("--run-for", type=float, default=0.0,
                     help="serve this many seconds then shut down (0 = until Ctrl+C)")
     ap.add_argument("--no-serve", action="store_true", help="exit after setup/training")
@@ -210,7 +212,7 @@ def main(argv: Optional[list[str]] = None, script_dir: str = SCRIPT_DIR_DEFAULT)
             from ..launch import spawn_ranks, wait_for_port
 
             plan_path = os.path.join(a.cache_dir, "chain_plan.json")
-            json.dump({"stages": stage_entries, "port": a.port,
+            json.dump({"stages": stage_entries, "port": a.port, "hop_timeout": a.hop_timeout,
                        "device": "cpu" if a.device == "cpu" else "auto"}, open(plan_path, "w"))
             job = spawn_ranks("docker_dist_nn_amd.serve.chain", ["--plan", plan_path], n_st,
                               devices=list(range(n_st)) if a.device != "cpu" else None,

@@ -1,28 +1,47 @@
 """Distributed inference chain: one rank (process / GPU) per non-empty stage.
 
 Reference behaviour (/root/reference/src/grpc_node.py:99-158): stage i computes its layers and
-forwards to stage i+1 over a fresh gRPC channel; the last stage's result unwinds back through
-every hop. Here:
+forwards to stage i+1 over a fresh gRPC channel with a 10 s deadline per hop (:130-133); the
+last stage's result unwinds back through every hop; a downstream failure keeps its gRPC code
+and is reported as "Failed to forward request to <next>" (:136-140). Here:
 
-* rank 0 hosts the gRPC ingress (port 5101) and stage 0; a request becomes a small header
-  tensor (request id, rows, cols, status) plus the padded bf16 activations, sent rank to rank
-  with torch.distributed (RCCL over xGMI on GPUs, gloo on CPU);
-* the LAST rank sends the fp32 result straight back to rank 0 -- one hop, not S;
-* a stage that fails turns the header status into an error code carrying its stage index; the
-  error travels on to rank 0, which raises ``StageFailure`` -> gRPC status + "Failed to forward
-  request to <stage>: ..." like grpc_node.py:136-140;
+* rank 0 hosts the gRPC ingress (port 5101, a 10-worker pool like grpc_node.py:169) and
+  stage 0; a request becomes a small header tensor (request id, rows, width, status, extra)
+  plus the padded bf16 activations, sent rank to rank with torch.distributed (RCCL over xGMI
+  on GPUs, gloo on CPU) on a FORWARD group;
+* several requests are in flight at once: rank 0 only serialises its own stage's compute
+  (shared per-bucket buffers); a sender thread feeds the chain, a receiver thread collects
+  results that the LAST rank sends straight back to rank 0 on a separate RETURN group (one
+  hop, not S; its own communicator, so a pending receive never blocks a send), and hands each
+  to the waiting request by id. Stages 1..S-1 process requests in arrival order, so stage k
+  works on request n while stage k-1 already computes request n+1;
+* every request waits with a deadline (``--hop-timeout`` x hops, capped by the client's own
+  gRPC deadline): a hung or dead downstream stage maps to DEADLINE_EXCEEDED "Failed to
+  forward request to layer_container_1: ..." within the deadline, the ingress keeps
+  answering, and a late result is dropped by request id instead of being delivered to the
+  wrong caller;
+* a stage that fails turns the header status into an error code carrying its stage index;
+  rank 0 raises ``StageFailure`` -> the reference's gRPC code + details;
 * ``STOP`` headers shut the chain down in order.
 
 Run by the launcher: ``python -m docker_dist_nn_amd.serve.chain --plan plan.json``.
+Fault injection (tests): ``DNN_FAULT_STAGE=<rank>`` with ``DNN_FAULT_KIND=raise`` (default:
+the stage reports INTERNAL) or ``hang`` (the stage stops responding after
+``DNN_FAULT_AFTER`` requests, default 0).
 """
 from __future__ import annotations
 
 import argparse
+import itertools
 import json
 import logging
 import os
+import queue
 import signal
 import threading
+import time
+from concurrent.futures import Future
+from concurrent.futures import TimeoutError as FutureTimeout
 from typing import Optional
 
 import grpc
@@ -40,6 +59,7 @@ log = logging.getLogger(__name__)
 
 ST_OK, ST_STOP, ST_VALUE, ST_INTERNAL = 0, 1, 2, 3
 _CODES = {ST_VALUE: grpc.StatusCode.INVALID_ARGUMENT, ST_INTERNAL: grpc.StatusCode.INTERNAL}
+HOP_TIMEOUT_S = 10.0  # grpc_node.py:133
 
 
 def bucket(rows: int) -> int:
@@ -55,27 +75,43 @@ def bucket(rows: int) -> int:
 
 class ChainRank:
     def __init__(self, stage: InferenceStage, rank: int, world: int, names: list[str],
-                 device: torch.device):
+                 device: torch.device, hop_timeout: float = HOP_TIMEOUT_S):
         self.stage, self.rank, self.world, self.names = stage, rank, world, names
         self.device = device
         self.comm_dev = device if dist.get_backend() == "nccl" else torch.device("cpu")
-        self.lock = threading.Lock()
-        self.req = 0
+        self.hop_timeout = float(hop_timeout)
         self.out_pad = round_up(stage.out_dim, 64)
+        # groups: every rank calls new_group in the same order
+        self.fwd_group = dist.new_group(list(range(world))) if world > 1 else None
+        self.ret_group = dist.new_group(sorted({0, world - 1})) if world > 1 else None
+        self.compute_lock = threading.Lock()
+        self._ids = itertools.count(1)
+        self._pending: dict[int, Future] = {}
+        self._pending_lock = threading.Lock()
+        self._sendq: "queue.Queue" = queue.Queue()
+        self._threads: list[threading.Thread] = []
+        self.fault_stage = os.environ.get("DNN_FAULT_STAGE")
+        self.fault_kind = os.environ.get("DNN_FAULT_KIND", "raise")
+        self.fault_after = int(os.environ.get("DNN_FAULT_AFTER", "0"))
+        if rank == 0 and world > 1:
+            for fn, nm in ((self._sender, "chain-send"), (self._receiver, "chain-recv")):
+                t = threading.Thread(target=fn, name=nm, daemon=True)
+                t.start()
+                self._threads.append(t)
 
     # -- transport ----------------------------------------------------------------------------
     def _hdr(self, *vals) -> torch.Tensor:
         return torch.tensor(list(vals), dtype=torch.int64, device=self.comm_dev)
 
-    def _send(self, t: torch.Tensor, dst: int) -> None:
-        dist.send(t if t.device == self.comm_dev else t.to(self.comm_dev), dst)
+    def _send(self, t: torch.Tensor, dst: int, group) -> None:
+        dist.send(t if t.device == self.comm_dev else t.to(self.comm_dev), dst, group=group)
 
-    def _recv_into(self, t: torch.Tensor, src: int) -> torch.Tensor:
+    def _recv_into(self, t: torch.Tensor, src: int, group) -> torch.Tensor:
         if t.device == self.comm_dev:
-            dist.recv(t, src)
+            dist.recv(t, src, group=group)
             return t
         tmp = torch.empty(t.shape, dtype=t.dtype, device=self.comm_dev)
-        dist.recv(tmp, src)
+        dist.recv(tmp, src, group=group)
         t.copy_(tmp)
         return t
 
@@ -84,15 +120,14 @@ class ChainRank:
             torch.cuda.current_stream(self.device).synchronize()
 
     # -- rank 0 -------------------------------------------------------------------------------
-    def predict(self, x: np.ndarray) -> np.ndarray:
+    def predict(self, x: np.ndarray, timeout: Optional[float] = None) -> np.ndarray:
         x = np.asarray(x)
         if x.ndim != 2:
             x = x.reshape(x.shape[0], -1)
         rows, cols = x.shape
         self.stage.check_input_dim(cols)  # ValueError -> INVALID_ARGUMENT
         R = bucket(rows)
-        with self.lock:
-            self.req += 1
+        with self.compute_lock:  # this rank's per-bucket buffers are shared
             buf = self.stage.buffers(R)
             xb = buf["x"]
             xb.zero_()
@@ -100,62 +135,123 @@ class ChainRank:
                           xb[:rows])
             out = self.stage.forward(R)
             if self.world == 1:
-                res = out[:rows, :self.stage.out_dim].double().cpu().numpy()
-                return res
+                return out[:rows, :self.stage.out_dim].double().cpu().numpy()
+            payload = out.clone()  # the next request may overwrite `out` while this one flies
             self._sync()
-            self._send(self._hdr(self.req, R, out.shape[1], ST_OK, rows), 1)
-            self._send(out, 1)
-            hdr = self._recv_into(self._hdr(0, 0, 0, 0, 0), self.world - 1).tolist()
-            status = hdr[3]
-            if status != ST_OK:
-                bad = self.names[hdr[4]] if 0 <= hdr[4] < len(self.names) else "stage"
-                raise StageFailure(bad, _CODES.get(status, grpc.StatusCode.INTERNAL),
-                                   f"stage {bad} failed (status {status})")
-            n_out = hdr[2]
-            res = torch.empty(R, n_out, dtype=torch.float32, device=self.device)
-            self._recv_into(res, self.world - 1)
-            return res[:rows].double().cpu().numpy()
+        rid = next(self._ids)
+        fut: Future = Future()
+        with self._pending_lock:
+            self._pending[rid] = fut
+        self._sendq.put((rid, R, rows, payload))
+        limit = self.hop_timeout * (self.world - 1)
+        if timeout is not None:
+            limit = min(limit, max(0.0, timeout))
+        try:
+            hdr, res = fut.result(timeout=limit)
+        except FutureTimeout:
+            with self._pending_lock:
+                self._pending.pop(rid, None)
+            raise StageFailure(self.names[1], grpc.StatusCode.DEADLINE_EXCEEDED,
+                               f"Deadline Exceeded (no answer from the chain within "
+                               f"{limit:.1f} s)") from None
+        status = hdr[3]
+        if status != ST_OK:
+            bad = self.names[hdr[4]] if 0 <= hdr[4] < len(self.names) else "stage"
+            raise StageFailure(bad, _CODES.get(status, grpc.StatusCode.INTERNAL),
+                               f"stage {bad} failed (status {status})")
+        return res[:rows].double().numpy()
 
-    def stop_chain(self) -> None:
+    def _sender(self) -> None:
+        """Feeds the chain in request order (the only thread sending on the forward group)."""
+        while True:
+            item = self._sendq.get()
+            if item is None:
+                self._send(self._hdr(0, 0, 0, ST_STOP, 0), 1, self.fwd_group)
+                return
+            rid, R, rows, payload = item
+            self._send(self._hdr(rid, R, payload.shape[1], ST_OK, rows), 1, self.fwd_group)
+            self._send(payload, 1, self.fwd_group)
+
+    def _receiver(self) -> None:
+        """Collects results from the last rank and completes the waiting requests."""
+        last = self.world - 1
+        while True:
+            hdr = self._recv_into(self._hdr(0, 0, 0, 0, 0), last, self.ret_group).tolist()
+            rid, R, n_out, status, extra = hdr
+            if status == ST_STOP:
+                return
+            res = None
+            if status == ST_OK:
+                res = torch.empty(R, n_out, dtype=torch.float32, device=self.comm_dev)
+                self._recv_into(res, last, self.ret_group)
+                res = res.cpu()
+            with self._pending_lock:
+                fut = self._pending.pop(rid, None)
+            if fut is not None:
+                fut.set_result((hdr, res))
+            else:
+                log.warning(f"dropping the late answer of request {rid} (its caller timed out)")
+
+    def stop_chain(self, timeout: float = 10.0) -> None:
         if self.world > 1:
-            with self.lock:
-                self._send(self._hdr(0, 0, 0, ST_STOP, 0), 1)
+            self._sendq.put(None)
+            for t in self._threads:
+                t.join(timeout)
 
     # -- ranks > 0 ------------------------------------------------------------------------------
+    def _maybe_fault(self, served: int) -> None:
+        if self.fault_stage != str(self.rank) or served < self.fault_after:
+            return
+        if self.fault_kind == "hang":
+            log.error(f"({self.names[self.rank]}) injected hang")
+            while True:
+                time.sleep(3600)
+        raise RuntimeError("injected fault")
+
     def loop(self) -> None:
         prev = self.rank - 1
         last = self.rank == self.world - 1
-        nxt = 0 if last else self.rank + 1
+        served = 0
         while True:
-            hdr = self._recv_into(self._hdr(0, 0, 0, 0, 0), prev).tolist()
+            hdr = self._recv_into(self._hdr(0, 0, 0, 0, 0), prev, self.fwd_group).tolist()
             req, R, width, status, extra = hdr
             if status == ST_STOP:
-                if not last:
-                    self._send(self._hdr(0, 0, 0, ST_STOP, 0), nxt)
+                if last:
+                    self._send(self._hdr(0, 0, 0, ST_STOP, 0), 0, self.ret_group)
+                else:
+                    self._send(self._hdr(0, 0, 0, ST_STOP, 0), self.rank + 1, self.fwd_group)
                 return
             if status != ST_OK:  # propagate an upstream failure
-                self._send(self._hdr(req, R, 0, status, extra), nxt)
+                self._forward_hdr(last, req, R, 0, status, extra)
                 continue
             buf = self.stage.buffers(R)
-            self._recv_into(buf["x"], prev)
+            self._recv_into(buf["x"], prev, self.fwd_group)
             try:
-                if os.environ.get("DNN_FAULT_STAGE") == str(self.rank):
-                    raise RuntimeError("injected fault")
+                self._maybe_fault(served)
                 out = self.stage.forward(R)
                 self._sync()
             except ValueError:
-                self._send(self._hdr(req, R, 0, ST_VALUE, self.rank), nxt)
+                self._forward_hdr(last, req, R, 0, ST_VALUE, self.rank)
                 continue
             except Exception:  # noqa: BLE001
                 log.exception(f"({self.names[self.rank]}) stage failure")
-                self._send(self._hdr(req, R, 0, ST_INTERNAL, self.rank), nxt)
+                self._forward_hdr(last, req, R, 0, ST_INTERNAL, self.rank)
                 continue
+            finally:
+                served += 1
             if last:
-                self._send(self._hdr(req, R, self.stage.out_dim, ST_OK, 0), nxt)
-                self._send(out[:, :self.stage.out_dim].contiguous(), nxt)
+                self._send(self._hdr(req, R, self.stage.out_dim, ST_OK, 0), 0, self.ret_group)
+                self._send(out[:, :self.stage.out_dim].contiguous(), 0, self.ret_group)
             else:
-                self._send(self._hdr(req, R, out.shape[1], ST_OK, 0), nxt)
-                self._send(out, nxt)
+                self._send(self._hdr(req, R, out.shape[1], ST_OK, 0), self.rank + 1,
+                           self.fwd_group)
+                self._send(out, self.rank + 1, self.fwd_group)
+
+    def _forward_hdr(self, last: bool, req, R, width, status, extra) -> None:
+        if last:
+            self._send(self._hdr(req, R, width, status, extra), 0, self.ret_group)
+        else:
+            self._send(self._hdr(req, R, width, status, extra), self.rank + 1, self.fwd_group)
 
 
 def main(argv: Optional[list[str]] = None) -> int:
@@ -179,7 +275,8 @@ def main(argv: Optional[list[str]] = None) -> int:
     names = [s["name"] for s in plan["stages"]]
     stage = InferenceStage(layers, device, expected_input=st["expected_input"], name=st["name"],
                            is_last=rank == world - 1)
-    cr = ChainRank(stage, rank, world, names, device)
+    cr = ChainRank(stage, rank, world, names, device,
+                   hop_timeout=plan.get("hop_timeout", HOP_TIMEOUT_S))
     log.info(f"({st['name']}) stage ready on {device}: {len(layers)} layer(s), "
              f"expected input dim {st['expected_input']}")
     if rank == 0:
@@ -194,6 +291,10 @@ def main(argv: Optional[list[str]] = None) -> int:
         done.wait()
         server.stop(grace=1.0)
         cr.stop_chain()
+        if any(t.is_alive() for t in cr._threads):  # a stage never answered the STOP
+            log.warning(f"({st['name']}) chain did not drain; exiting without teardown")
+            logging.shutdown()
+            os._exit(0)
     else:
         signal.signal(signal.SIGINT, signal.SIG_IGN)
         cr.loop()

@@ -45,11 +45,20 @@ class StageFailure(Exception):
 
 
 def make_handler(predict: Callable[[np.ndarray], np.ndarray], name: str = "layer_container_0"):
+    import inspect
+
+    try:  # a chain's predict honours the caller's deadline (serve/chain.py)
+        takes_timeout = "timeout" in inspect.signature(predict).parameters
+    except (TypeError, ValueError):
+        takes_timeout = False
+
     def process(x: np.ndarray, context) -> np.ndarray:
         try:
             if x.size == 0:
                 log.info(f"({name}) Received empty input matrix.")
                 return np.zeros((0, 0))
+            if takes_timeout:
+                return predict(x, timeout=context.time_remaining())
             return predict(x)
         except StageFailure as e:
             context.set_code(e.code)

@@ -46,12 +46,12 @@ def model_files(tmp_path_factory):
     return cfg, inp, x, y
 
 
-def _start(cfg, inp, port, mode, tmp, extra_env=None):
+def _start(cfg, inp, port, mode, tmp, extra_env=None, args=()):
     env = dict(os.environ, PYTHONPATH=ROOT, **(extra_env or {}))
     p = subprocess.Popen([sys.executable, os.path.join(ROOT, "src", "run_grpc_fcnn.py"),
                           "--config", str(cfg), "--inputs", str(inp), "--port", str(port),
                           "--mode", mode, "--device", "cpu", "--run-for", "120",
-                          "--cache-dir", str(tmp / f"cache_{mode}")],
+                          "--cache-dir", str(tmp / f"cache_{mode}"), *args],
                          env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     t0 = time.time()
     while time.time() - t0 < 90:
@@ -152,3 +152,85 @@ def test_reference_mapping_errors_are_logged(model_files, tmp_path):
     doc = json.load(open(f))
     assert list(doc) == ["layer_1"] and len(doc["layer_1"]) == 32
     assert len(doc["layer_1"][0]["weights"]) == 64
+
+
+def test_hung_middle_stage_maps_to_deadline_and_ingress_keeps_answering(model_files, tmp_path):
+    """A stage that stops responding (after serving one request) must not wedge the chain:
+    the caller gets DEADLINE_EXCEEDED "Failed to forward request to layer_container_1" within
+    the per-hop deadline (reference: 10 s per hop, grpc_node.py:133-140), later requests are
+    answered within their deadline too, stage-0 validation errors still come back at once,
+    and teardown completes."""
+    cfg, inp, x, y = model_files
+    port = _port()
+    p = _start(cfg, inp, port, "ranks", tmp_path,
+               {"DNN_FAULT_STAGE": "1", "DNN_FAULT_KIND": "hang", "DNN_FAULT_AFTER": "1"},
+               args=("--hop-timeout", "1.5"))
+    try:
+        c = LayerClient(f"127.0.0.1:{port}", timeout=30)
+        ref = model_forward(load_model_config(str(cfg)).layers, x[:4])
+        np.testing.assert_allclose(c.process(x[:4]), ref, atol=2e-2)  # served before the hang
+        for _ in range(2):
+            t0 = time.monotonic()
+            with pytest.raises(grpc.RpcError) as ei:
+                c.process(x[:4])
+            dt = time.monotonic() - t0
+            assert ei.value.code() == grpc.StatusCode.DEADLINE_EXCEEDED, ei.value
+            assert "Failed to forward request to layer_container_1" in ei.value.details()
+            assert dt < 2 * 1.5 + 2.0, dt  # 2 hops x 1.5 s, plus slack
+        with pytest.raises(grpc.RpcError) as ei:  # the ingress itself is not blocked
+            c.process(np.ones((2, 5)))
+        assert ei.value.code() == grpc.StatusCode.INVALID_ARGUMENT
+        c.close()
+    finally:
+        t0 = time.monotonic()
+        out = _stop(p)
+        assert time.monotonic() - t0 < 40
+    assert "Shutdown complete." in out
+
+
+def test_concurrent_requests_through_rank_chain(model_files, tmp_path):
+    """Several requests in flight through a 3-rank chain at once (10 ingress workers, the
+    reference's pool size): every caller gets its own rows back."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    cfg, inp, x, y = model_files
+    port = _port()
+    p = _start(cfg, inp, port, "ranks", tmp_path)
+    try:
+        layers = load_model_config(str(cfg)).layers
+        c = LayerClient(f"127.0.0.1:{port}", timeout=60)
+        chunks = [x[i * 7:(i + 1) * 7 + i] for i in range(24)]  # distinct sizes and rows
+        with ThreadPoolExecutor(8) as pool:
+            outs = list(pool.map(c.process, chunks))
+        for ch, out in zip(chunks, outs):
+            np.testing.assert_allclose(out, model_forward(layers, ch), atol=2e-2)
+        c.close()
+    finally:
+        _stop(p)
+
+
+REF_CLIENT = "/root/reference/src/run_grpc_inference.py"
+
+
+@pytest.mark.skipif(not os.path.exists(REF_CLIENT), reason="reference checkout not present")
+@pytest.mark.parametrize("mode", ["local", "ranks"])
+def test_unmodified_reference_client_interop(model_files, tmp_path, mode):
+    """The ORIGINAL client (/root/reference/src/run_grpc_inference.py with its own generated
+    dist_nn_pb2 / dist_nn_pb2_grpc stubs: Matrix{Row{values}} on
+    /grpc_dist_nn.LayerService/Process) runs unmodified against our ingress. It is executed
+    read-only (-B, no bytecode written into the reference tree)."""
+    cfg, inp, x, y = model_files
+    port = _port()
+    p = _start(cfg, inp, port, mode, tmp_path)
+    try:
+        r = subprocess.run([sys.executable, "-B", REF_CLIENT, "--inputs", str(inp),
+                            "--port", str(port), "--batch-size", "100", "--timeout", "30"],
+                           capture_output=True, text=True, timeout=180, cwd=str(tmp_path),
+                           env=dict(os.environ, PYTHONDONTWRITEBYTECODE="1"))
+        log = r.stdout + r.stderr
+        assert "Batch 3/3 completed" in log, log
+        n = int(log.split("Correct predictions: ")[1].split(" ")[0])
+        assert n >= 290 and "out of 300" in log, log
+        assert "Inference process completed." in log
+    finally:
+        _stop(p)
