@@ -41,8 +41,10 @@ def build_parser(script_dir: str) -> argparse.ArgumentParser:
                     default=os.path.join(script_dir, "../config/example_inputs/mnist_examples_5.json"),
                     help="Path to the example inputs JSON file")
     # additive flags
-    ap.add_argument("--mode", choices=["auto", "local", "ranks"], default="auto",
-                    help="ranks: one process per stage/GPU (RCCL); local: all stages in-process")
+    ap.add_argument("--mode", choices=["auto", "local", "ranks", "workers"], default="auto",
+                    help="ranks: one process per stage/GPU (RCCL); local: all stages in-process; "
+                         "workers: one gRPC stage process per stage on the reference's env "
+                         "contract (grpc_node.py), chained over gRPC")
     ap.add_argument("--device", default="auto", help="auto | cpu | cuda")
     ap.add_argument("--port", type=int, default=5101)
     ap.add_argument("--layer-distribution", type=str, default=None,
@@ -208,6 +210,35 @@ def main(argv: Optional[list[str]] = None, script_dir: str = SCRIPT_DIR_DEFAULT)
             eng = InferenceEngine([mc.layers[p.layer_start:p.layer_end] for p in plans], dev,
                                   expected_input=input_dim, names=[s["name"] for s in stage_entries])
             server = serve(eng.predict, port=a.port, name=stage_entries[0]["name"])
+        elif mode == "workers":
+            from ..launch import spawn_workers, wait_for_port
+            from ..weights_io import stage_files_from_model
+
+            envs = stage_files_from_model(mc, a.cache_dir, input_dim, distribution)
+            order = sorted(envs)
+            port_of = {}
+            for k, ci in enumerate(order):  # base port --port, +100 per stage (5101, 5201, ...)
+                port_of[str(envs[ci]["LISTEN_PORT"])] = str(a.port + 100 * k)
+            stage_envs = []
+            for k, ci in enumerate(order):
+                e = dict(envs[ci])
+                e["LISTEN_PORT"] = port_of[e["LISTEN_PORT"]]
+                # containers resolved each other by name on the Docker network; local stage
+                # processes are on 127.0.0.1
+                e["NEXT_NODES"] = json.dumps([{"host": "127.0.0.1",
+                                               "port": port_of.get(str(n["port"]), str(n["port"]))}
+                                              for n in json.loads(e["NEXT_NODES"])])
+                e["DNN_HOP_TIMEOUT"] = str(a.hop_timeout)
+                e["DNN_WORKER_DEVICE"] = "cpu" if a.device == "cpu" else "auto"
+                e["LOCAL_RANK"] = str(k)
+                stage_envs.append(e)
+            job = spawn_workers("docker_dist_nn_amd.serve.worker", stage_envs,
+                                names=[s["name"] for s in stage_entries], pid_dir=a.cache_dir)
+            for e in stage_envs:  # every stage must listen (the reference probed stage 0 only)
+                if not wait_for_port(int(e["LISTEN_PORT"]), timeout=120.0, alive=job.alive):
+                    job.poll()
+                    raise RuntimeError(f"stage {e['CONTAINER_NAME']} did not start listening "
+                                       f"on port {e['LISTEN_PORT']}")
         else:
             from ..launch import spawn_ranks, wait_for_port
 
@@ -223,16 +254,27 @@ def main(argv: Optional[list[str]] = None, script_dir: str = SCRIPT_DIR_DEFAULT)
         log.info(f"Distributed FCNN setup completed in {time.time() - start_time:.3f} seconds.")
         log.info(f"{n_st} stage(s) running ({mode} mode). Press Ctrl+C to shut down.")
         t0 = time.time()
+        reported = set()
         while not a.run_for or time.time() - t0 < a.run_for:
             time.sleep(0.2)
-            if job is not None:
-                job.poll()
+            if job is not None and mode == "workers":
+                # independent stage servers, like the reference's containers: a dead stage is
+                # reported (its upstream answers UNAVAILABLE "Failed to forward request to
+                # ..."), the others keep serving
+                for r, pr in enumerate(job.procs):
+                    if pr.poll() is not None and r not in reported:
+                        reported.add(r)
+                        log.error(f"stage {job.names[r]} exited with code {pr.returncode}")
+            elif job is not None:
+                job.poll()  # RCCL ranks: one dead rank breaks the communicators -> fail fast
     except KeyboardInterrupt:
         log.info("Shutdown signal received (Ctrl+C).")
     except Exception as e:  # noqa: BLE001
         log.error(f"An unexpected error occurred during setup/runtime: {e}")
         rc = 1
     finally:
+        signal.signal(signal.SIGTERM, signal.SIG_IGN)  # a second signal must not cut teardown
+        signal.signal(signal.SIGINT, signal.SIG_IGN)
         log.info("Shutting down and cleaning up stages...")
         if server is not None:
             server.stop(grace=1.0)

@@ -137,6 +137,36 @@ def spawn_ranks(module: str, args: Sequence[str], nprocs: int,
     return job
 
 
+def spawn_workers(module: str, envs: Sequence[dict], names: Optional[Sequence[str]] = None,
+                  log_dir: Optional[str] = None, pid_dir: Optional[str] = None) -> Job:
+    """Start ``python -m module`` once per stage with that stage's own env contract (the
+    reference's per-container environment, run_grpc_fcnn.py:101-126); no rendezvous.
+    ``pid_dir``: write ``<name>.pid`` per stage (the container-id analogue)."""
+    job = Job(names=list(names or [e.get("CONTAINER_NAME", f"stage{i}")
+                                   for i, e in enumerate(envs)]))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    try:
+        for i, extra in enumerate(envs):
+            e = dict(os.environ)
+            e.update(extra)
+            e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+            e["PYTHONPATH"] = root + (os.pathsep + e["PYTHONPATH"] if e.get("PYTHONPATH") else "")
+            out = None
+            if log_dir:
+                os.makedirs(log_dir, exist_ok=True)
+                out = open(os.path.join(log_dir, f"{job.names[i]}.log"), "w")
+            job.procs.append(subprocess.Popen([sys.executable, "-m", module], env=e,
+                                              start_new_session=True, stdout=out,
+                                              stderr=subprocess.STDOUT if out else None))
+            if pid_dir:
+                with open(os.path.join(pid_dir, f"{job.names[i]}.pid"), "w") as f:
+                    f.write(str(job.procs[-1].pid))
+    except Exception:
+        job.terminate()
+        raise
+    return job
+
+
 def install_signal_teardown(job: Job) -> None:
     def handler(signum, frame):
         log.info("Shutdown signal received; tearing down ranks...")

@@ -84,7 +84,7 @@ def _client(inp, port, *args):
     return r.stdout + r.stderr
 
 
-@pytest.mark.parametrize("mode", ["local", "ranks"])
+@pytest.mark.parametrize("mode", ["local", "ranks", "workers"])
 def test_fcnn_chain_serves_reference_protocol(model_files, tmp_path, mode):
     cfg, inp, x, y = model_files
     port = _port()
@@ -213,7 +213,7 @@ REF_CLIENT = "/root/reference/src/run_grpc_inference.py"
 
 
 @pytest.mark.skipif(not os.path.exists(REF_CLIENT), reason="reference checkout not present")
-@pytest.mark.parametrize("mode", ["local", "ranks"])
+@pytest.mark.parametrize("mode", ["local", "ranks", "workers"])
 def test_unmodified_reference_client_interop(model_files, tmp_path, mode):
     """The ORIGINAL client (/root/reference/src/run_grpc_inference.py with its own generated
     dist_nn_pb2 / dist_nn_pb2_grpc stubs: Matrix{Row{values}} on
@@ -232,5 +232,56 @@ def test_unmodified_reference_client_interop(model_files, tmp_path, mode):
         n = int(log.split("Correct predictions: ")[1].split(" ")[0])
         assert n >= 290 and "out of 300" in log, log
         assert "Inference process completed." in log
+    finally:
+        _stop(p)
+
+
+def test_worker_env_contract_and_forward_failure(model_files, tmp_path):
+    """--mode workers: each stage process is configured ONLY by the reference's env contract
+    (NEURONS_CONFIG inline for small stages, NEURONS_FILE_CONFIG for > 1000 characters); a dead
+    downstream stage surfaces as the reference's "Failed to forward request to <host:port>"
+    with the downstream gRPC code (UNAVAILABLE), and the first stage keeps serving errors."""
+    from docker_dist_nn_amd.serve.worker import StageWorker
+    from docker_dist_nn_amd.weights_io import stage_files_from_model
+
+    cfg, inp, x, y = model_files
+    mc = load_model_config(str(cfg))
+    envs = stage_files_from_model(mc, str(tmp_path / "c"), 784, [2, 1])
+    assert "NEURONS_FILE_CONFIG" in envs[0] and "NEURONS_CONFIG" not in envs[0]
+    w0 = StageWorker(dict(envs[0], DNN_WORKER_DEVICE="cpu"))
+    assert w0.container_name == "layer_container_0" and len(w0.layers) == 2
+    assert w0.next_nodes == [{"host": "layer_container_1", "port": "5201"}]
+    tiny = tmp_path / "tiny.json"
+    export_model_json(str(tiny), [np.ones((3, 4)), np.ones((2, 3))], [np.zeros(3), np.zeros(2)],
+                      ["relu", "softmax"], layer_distribution=[1, 1])
+    small = stage_files_from_model(load_model_config(str(tiny)), str(tmp_path / "c2"), 4)
+    for env in small.values():  # < 1000 characters: inline, like run_grpc_fcnn.py:126
+        assert "NEURONS_CONFIG" in env and json.loads(env["NEURONS_CONFIG"])["layer_1"]
+    w1 = StageWorker(dict(small[1], DNN_WORKER_DEVICE="cpu"))
+    assert w1.expected_input_dim == 3 and w1.next_nodes == []
+    np.testing.assert_allclose(w1.predict(np.ones((1, 3))), [[0.5, 0.5]], atol=1e-6)
+    port = _port()
+    p = _start(cfg, inp, port, "workers", tmp_path)
+    try:
+        c = LayerClient(f"127.0.0.1:{port}", timeout=30)
+        ref = model_forward(mc.layers, x[:3])
+        np.testing.assert_allclose(c.process(x[:3]), ref, atol=2e-2)
+        # kill the last stage: the previous hop reports UNAVAILABLE for it
+        last_port = port + 200
+        pid = int(open(tmp_path / "cache_workers" / "layer_container_2.pid").read())
+        os.kill(pid, 9)
+        time.sleep(0.5)
+        errs = []
+        for _ in range(3):  # the first call may see the dying connection rather than a refusal
+            with pytest.raises(grpc.RpcError) as ei:
+                c.process(x[:3])
+            errs.append((ei.value.code(), ei.value.details()))
+            if ei.value.code() == grpc.StatusCode.UNAVAILABLE and \
+                    f"Failed to forward request to 127.0.0.1:{last_port}" in ei.value.details():
+                break
+            time.sleep(0.5)
+        else:
+            raise AssertionError(errs)
+        c.close()
     finally:
         _stop(p)
