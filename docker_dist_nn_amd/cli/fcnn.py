@@ -253,6 +253,11 @@ def main(argv: Optional[list[str]] = None, script_dir: str = SCRIPT_DIR_DEFAULT)
                 raise RuntimeError(f"first stage did not start listening on port {a.port}")
         log.info(f"Distributed FCNN setup completed in {time.time() - start_time:.3f} seconds.")
         log.info(f"{n_st} stage(s) running ({mode} mode). Press Ctrl+C to shut down.")
+        # readiness marker for orchestration: every stage is up (the reference only probed
+        # stage 0 and ignored the result, run_grpc_fcnn.py:319)
+        with open(os.path.join(a.cache_dir, "chain_ready.json"), "w") as f:
+            json.dump({"mode": mode, "port": a.port, "stages": [s["name"] for s in stage_entries],
+                       "pid": os.getpid()}, f)
         t0 = time.time()
         reported = set()
         while not a.run_for or time.time() - t0 < a.run_for:

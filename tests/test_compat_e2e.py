@@ -265,7 +265,19 @@ def test_worker_env_contract_and_forward_failure(model_files, tmp_path):
     try:
         c = LayerClient(f"127.0.0.1:{port}", timeout=30)
         ref = model_forward(mc.layers, x[:3])
-        np.testing.assert_allclose(c.process(x[:3]), ref, atol=2e-2)
+        t0 = time.monotonic()
+        while True:  # stage 0 listens first; wait until the whole chain answers
+            try:
+                got = c.process(x[:3])
+                break
+            except grpc.RpcError:
+                if time.monotonic() - t0 > 60:
+                    raise
+                time.sleep(0.3)
+        np.testing.assert_allclose(got, ref, atol=2e-2)
+        ready = tmp_path / "cache_workers" / "chain_ready.json"
+        while not ready.exists() and time.monotonic() - t0 < 60:  # setup fully finished
+            time.sleep(0.1)
         # kill the last stage: the previous hop reports UNAVAILABLE for it
         last_port = port + 200
         pid = int(open(tmp_path / "cache_workers" / "layer_container_2.pid").read())
