@@ -140,7 +140,11 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--resume", action="store_true")
     ap.add_argument("--metrics", default=None, help="JSONL metrics path ({rank} expands)")
     ap.add_argument("--trace", default=None, help="chrome trace of the last step ({rank})")
-    ap.add_argument("--watchdog", type=float, default=0.0, help="seconds without progress")
+    ap.add_argument("--watchdog", type=float, default=None,
+                    help="seconds without step progress before the rank dumps its stacks and "
+                         "exits (default: 300 for multi-rank jobs, off for one process; 0 = off)")
+    ap.add_argument("--check-every", type=int, default=20,
+                    help="steps between loss finiteness / RCCL async-error checks")
     return ap
 
 
@@ -200,9 +204,11 @@ def main(argv: Optional[list[str]] = None) -> int:
     rows = a.micro_batch * a.num_micro_batches
     shard = slice(replica, None, dp)  # each replica sees a disjoint strided shard
     x, y = x[shard], y[shard]
-    kp = tr.stages[0].x_in.shape[1]
+    kp = (spec.in_dim + 63) // 64 * 64  # the FIRST stage's padded input width (on every rank)
     mw = MetricsWriter(a.metrics.format(rank=rank) if a.metrics else None, rank)
     prof = StepProfiler(tr.executor, rank, enabled=bool(a.trace))
+    if a.watchdog is None:  # on by default wherever a peer can hang us
+        a.watchdog = 300.0 if world > 1 else 0.0
     wd = Watchdog(a.watchdog, name=f"rank{rank}").start() if a.watchdog else None
     faults = FaultInjector()
     sid = tr.stages[0].stage_index
@@ -234,7 +240,11 @@ def main(argv: Optional[list[str]] = None) -> int:
                 wd.beat(f"step {step}")
             if a.trace:
                 prof.collect()
-            if step % 20 == 0:
+            if a.check_every and step % a.check_every == 0:
+                if tr.native_step is not None:  # RCCL async errors of this rank's comms
+                    err = tr.native_step.comm_error()
+                    if err:
+                        raise RuntimeError(f"rank {rank}: RCCL async error {err} at step {step}")
                 loss = tr.loss()
                 check_finite(loss)
                 mw.write("train", step=step, loss=loss,
