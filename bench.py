@@ -45,6 +45,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from docker_dist_nn_amd import NAMED_MODELS, MLPSpec  # noqa: E402
+from docker_dist_nn_amd import switches  # noqa: E402
 from docker_dist_nn_amd.data import DeviceDataset, synthetic_mnist  # noqa: E402
 from docker_dist_nn_amd.engine import OptimConfig, Trainer  # noqa: E402
 from docker_dist_nn_amd.parallel.planner import Planner, parse_parallelism  # noqa: E402
@@ -56,10 +57,6 @@ BASELINE_SAMPLES_PER_S = 10_800.0
 MODEL_LABEL = {"mnist-fcnn": "784-512-256-128-10 MNIST FCNN",
                "mlp8": "784-1024x7-10 MLP (8 Linear)", "mlp7": "784-1024x6-10 MLP",
                "wide": "784-8192-8192-10 MLP"}
-# behaviour switches echoed into the JSON (the values in effect for this run)
-SWITCHES = ("DNN_BLAS", "DNN_TUNED", "DNN_TUNED_TABLE", "DNN_PIPE", "DNN_NATIVE_DIST",
-            "DNN_NATIVE_EXEC", "DNN_DGRAD_WT", "DNN_TAIL", "DNN_FUSED_XENT", "DNN_DP_DEFER",
-            "DNN_GEMM_STAGES", "DNN_GEMM_PERSIST", "DNN_WGRAD_GROUP", "DNN_DIST_BACKEND")
 
 
 def parse_args(argv=None):
@@ -191,13 +188,13 @@ def main(argv=None):
 
     # DNN_FORCE_DEVICE / DNN_DIST_BACKEND exist only to rehearse the multi-rank path on a
     # one-GPU box (several gloo ranks sharing cuda:0); real runs use one GPU per rank + RCCL.
-    local = int(os.environ.get("DNN_FORCE_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+    local = int(switches.get("DNN_FORCE_DEVICE") or os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         from docker_dist_nn_amd.parallel.groups import init_distributed
 
-        init_distributed(os.environ.get("DNN_DIST_BACKEND", "nccl"))
+        init_distributed(switches.get("DNN_DIST_BACKEND"))
 
     m = measure(a, spec, n, world, dev, a.parallelism)
     dp_only = None
@@ -232,7 +229,7 @@ def main(argv=None):
         "last_loss": None if m["loss"] is None else round(m["loss"], 5),
         "planner_predicted": m["planner_predicted"],
         "dp_only": dp_only,
-        "switches": {k: os.environ[k] for k in SWITCHES if k in os.environ},
+        "switches": switches.active(),  # non-default DNN_* switches of this run
     }
     rank = int(os.environ.get("RANK", "0"))
     if rank == 0:

@@ -160,56 +160,3 @@ def load_model_config(path: str, native_parser: Optional[bool] = None) -> ModelC
     with open(path, "r") as f:
         cfg = json.load(f)
     return model_config_from_dict(cfg, source=path)
-
-
-@dataclass
-class RunConfig:
-    """Everything a training / inference run needs; CLI flags and DNN_* env vars map here."""
-
-    model: str = "mnist-fcnn"
-    config_path: Optional[str] = None
-    layer_distribution: Optional[list[int]] = None
-    dp: int = 1
-    micro_batch: int = 8192
-    num_micro: int = 1
-    schedule: str = "1f1b"
-    optimizer: str = "sgd"
-    lr: float = 0.05
-    momentum: float = 0.0
-    weight_decay: float = 0.0
-    epochs: int = 1
-    steps: int = 0
-    seed: int = 0
-    dtype: str = "bf16"
-    synthetic: int = 60000
-    device: str = "auto"
-    backend: str = "auto"
-    graph: bool = True
-    metrics_path: Optional[str] = None
-    checkpoint_dir: Optional[str] = None
-    extra: dict[str, Any] = field(default_factory=dict)
-
-    @property
-    def global_batch_per_replica(self) -> int:
-        return self.micro_batch * self.num_micro
-
-    def apply_env(self, env: Optional[dict] = None) -> "RunConfig":
-        env = os.environ if env is None else env
-        for k, v in env.items():
-            if not k.startswith("DNN_"):
-                continue
-            name = k[4:].lower()
-            if not hasattr(self, name) or name == "extra":
-                continue
-            cur = getattr(self, name)
-            if isinstance(cur, bool):
-                setattr(self, name, v.lower() in ("1", "true", "yes"))
-            elif isinstance(cur, int):
-                setattr(self, name, int(v))
-            elif isinstance(cur, float):
-                setattr(self, name, float(v))
-            elif name == "layer_distribution":
-                setattr(self, name, json.loads(v))
-            else:
-                setattr(self, name, v)
-        return self

@@ -26,6 +26,7 @@ from .. import ops
 from ..config import LayerWeights
 from ..models.mlp import normalize_activation, round_up
 from ..utils.native import native
+from .. import switches
 
 
 class InferenceStage:
@@ -133,7 +134,7 @@ class InferenceEngine:
         self.n_out = self.stages[-1].out_dim
         self._stage_bufs: dict = {}
         # per-bucket replay: "graph" (HIP graph) or "native" (recorded launch Program)
-        self.replay = os.environ.get("DNN_SERVE_REPLAY", "graph")
+        self.replay = switches.get("DNN_SERVE_REPLAY")
         self._programs: dict[int, tuple] = {}
 
     @property

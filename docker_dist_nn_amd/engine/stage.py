@@ -31,6 +31,7 @@ import torch
 from .. import ops
 from ..models.mlp import LayerGeom, MLPSpec, round_up
 from ..utils.native import native
+from .. import switches
 
 _ALIGN = 64  # elements; keeps every layer's region 256-B aligned
 
@@ -316,7 +317,7 @@ class Stage:
         self.device = device
         self.global_batch = global_batch or self.rows
         self.wgrad_mode = wgrad
-        self.wgrad_algo = wgrad_algo or os.environ.get("DNN_WGRAD_ALGO", "splitk")
+        self.wgrad_algo = wgrad_algo or switches.get("DNN_WGRAD_ALGO")
         if self.wgrad_algo not in ("streamk", "splitk"):
             raise ValueError(f"wgrad_algo must be streamk | splitk, got {self.wgrad_algo!r}")
         self.geoms = [LayerGeom(i, spec.layers[i]) for i in range(layer_start, layer_end)]
@@ -336,7 +337,7 @@ class Stage:
         # count is one 64/128-wide tile: logits then never exist in memory
         gl = self.geoms[-1]
         self.fused_xent = (self.last and gl.np_ in (64, 128) and
-                           os.environ.get("DNN_FUSED_XENT", "1") == "1" and
+                           switches.get("DNN_FUSED_XENT") == "1" and
                            not self._logits_on_library(gl))
         self.acts: list[torch.Tensor] = []  # output of local layer i
         for i, g in enumerate(self.geoms):
@@ -351,7 +352,7 @@ class Stage:
         # the byte-granular mask stores/loads cost more than the activation bytes saved):
         # the dgrad epilogue then reads N/8 bytes per row instead of the bf16 activation (the
         # activation itself is still kept: it is the next layer's wgrad operand)
-        use_mask = dev.type == "cuda" and os.environ.get("DNN_RELU_MASK", "0") == "1"
+        use_mask = dev.type == "cuda" and switches.get("DNN_RELU_MASK") == "1"
         self.relu_mask = [torch.zeros(R, g.np_ // 8, dtype=torch.uint8, device=dev)
                           if use_mask and i < len(self.geoms) - 1 and
                           g.spec.activation == "relu" else None
@@ -365,7 +366,7 @@ class Stage:
         # layer's forward; the second-to-last layer's forward and both dgrads are then no-ops.
         self.tail = self._tail_ok()
         # dgrad GEMMs read W^T (contraction-contiguous B operand, see ops.linear_dgrad)
-        if dev.type == "cuda" and os.environ.get("DNN_DGRAD_WT", "1") == "1":
+        if dev.type == "cuda" and switches.get("DNN_DGRAD_WT") == "1":
             L = len(self.geoms)
             for i in range(L):
                 if (i > 0 or not self.first) and not (self.tail and i >= L - 2) and \
@@ -433,7 +434,7 @@ class Stage:
 
     def _tail_ok(self) -> bool:
         if not (self.fused_xent and self.device.type == "cuda" and len(self.geoms) >= 3 and
-                os.environ.get("DNN_TAIL", "1") == "1"):
+                switches.get("DNN_TAIL") == "1"):
             return False
         g2, g3, g4 = self.geoms[-3], self.geoms[-2], self.geoms[-1]
         acts = ("relu", "sigmoid", "linear")
@@ -568,7 +569,7 @@ class Stage:
         """Every local layer's weight gradient: one grouped launch per shared tile configuration
         (ops.linear_wgrad_group; DNN_WGRAD_GROUP=0 disables), one launch per remaining layer."""
         if (self.wgrad_algo == "splitk" and self.device.type == "cuda" and
-                os.environ.get("DNN_WGRAD_GROUP", "1") == "1" and len(self.geoms) > 1):
+                switches.get("DNN_WGRAD_GROUP") == "1" and len(self.geoms) > 1):
             if j < 0:
                 r, acc = slice(0, self.rows), False
             else:
@@ -639,7 +640,7 @@ class Stage:
         job (not stream-K wgrad, which writes weight gradients directly); SGD, Adam or AdamW."""
         return (self.params.optim.name in ("sgd", "adam", "adamw") and
                 self.wgrad_algo != "streamk" and self.device.type == "cuda" and
-                os.environ.get("DNN_FUSE_FIN_SGD", "1") == "1")
+                switches.get("DNN_FUSE_FIN_SGD") == "1")
 
     def _record_fin_sgd(self) -> None:
         """Record the whole-stage gradient reduction with the SGD update fused in (segment

@@ -31,6 +31,7 @@ from ..parallel.pipeline import GradSync, PipelineExecutor
 from ..partition import balanced_distribution, plan_stages
 from ..utils.native import native
 from .stage import OptimConfig, Stage
+from .. import switches
 
 
 def default_distribution(spec: MLPSpec, pp: int) -> list[int]:
@@ -93,7 +94,7 @@ class Trainer:
             st.params.init_default(seed)
             self.stages = [st]
             # DNN_PIPE=ipc: xGMI peer writes into IPC-mapped buffers instead of RCCL P2P
-            use_ipc = (os.environ.get("DNN_PIPE", "rccl") == "ipc" and
+            use_ipc = (switches.get("DNN_PIPE") == "ipc" and
                        self.device.type == "cuda" and mesh.pp > 1)
             self.pipe = IpcPipe(mesh, st) if use_ipc else DistPipe(mesh, st)
             ids = [mesh.stage]
@@ -103,7 +104,7 @@ class Trainer:
         # pipe has aliased loopback buffers, so the recorded pointers are the final ones)
         if native_exec is None:
             native_exec = (self.device.type == "cuda" and
-                           os.environ.get("DNN_NATIVE_EXEC", "1") != "0")
+                           switches.get("DNN_NATIVE_EXEC") != "0")
         self.native_exec = bool(native_exec)
         if self.native_exec:
             for st in self.stages:
@@ -115,7 +116,7 @@ class Trainer:
                           "ipc" if isinstance(self.pipe, IpcPipe) else
                           "rccl" if mesh.backend == "nccl" else mesh.backend)
         if mesh is not None and self.native_exec and \
-                os.environ.get("DNN_NATIVE_DIST", "1") != "0":
+                switches.get("DNN_NATIVE_DIST") != "0":
             from ..parallel.native_step import NativeStep, native_step_supported
 
             why = native_step_supported(self.executor, mesh)

@@ -23,6 +23,7 @@ import threading
 import time
 from dataclasses import dataclass
 from typing import Optional
+from . import switches
 
 log = logging.getLogger(__name__)
 
@@ -93,7 +94,7 @@ def parse_fault(text: Optional[str]) -> Optional[FaultSpec]:
 
 class FaultInjector:
     def __init__(self, spec: Optional[FaultSpec] = None):
-        self.spec = spec if spec is not None else parse_fault(os.environ.get("DNN_FAULT"))
+        self.spec = spec if spec is not None else parse_fault(switches.get("DNN_FAULT"))
 
     def maybe_inject(self, stage_index: int, step: int, stage=None) -> None:
         s = self.spec

@@ -21,6 +21,7 @@ from ..models.mlp import ACT_CODE
 from ..utils.native import native
 from . import reference as ref
 from . import tuning
+from .. import switches
 
 KMAJ, MNMAJ = 0, 1
 
@@ -44,7 +45,7 @@ def _parse_stages(spec: str) -> dict:
 
 # LDS pipeline depth (2..4) per GEMM kind; see mma_tile in csrc/kernels/gemm.hip. 8 selects the
 # ping-pong half-tile-streamed form of the 256x256 tile (csrc/kernels/gemm_pp.hip).
-STAGES = _parse_stages(os.environ.get("DNN_GEMM_STAGES", ""))
+STAGES = _parse_stages(switches.get("DNN_GEMM_STAGES"))
 
 
 def _parse_persist(spec: str) -> dict:
@@ -65,7 +66,7 @@ def _parse_persist(spec: str) -> dict:
 
 
 # Persistent-workgroup GEMM form (csrc/kernels/gemm_persist.hip) per GEMM kind.
-PERSIST = _parse_persist(os.environ.get("DNN_GEMM_PERSIST", ""))
+PERSIST = _parse_persist(switches.get("DNN_GEMM_PERSIST"))
 
 
 def _persist(kind: str, entry) -> int:
@@ -81,7 +82,7 @@ def _blas(kind: str, entry) -> bool:
     """Library (hipBLASLt) GEMM for this product? DNN_BLAS: "" / "table" = the tuned table's
     ``blas`` flag, "0" = never, "1" = every product the library path supports, or per kind
     ("fwd=1,dgrad=0,wgrad=1")."""
-    spec = os.environ.get("DNN_BLAS", "").strip()
+    spec = switches.get("DNN_BLAS").strip()
     if spec in ("", "table"):
         return bool((entry or {}).get("blas", 0))
     if "=" not in spec:
@@ -482,7 +483,7 @@ def linear_wgrad_group(items) -> list:
         t = tuning.lookup("wgrad", N, K, R)
         stages = STAGES["wgrad"] or (t or {}).get("stages", 0) or 2
         small = -(-N // bm) * -(-K // bn) * splits < int(
-            os.environ.get("DNN_WGRAD_GROUP_MAX_WG", NUM_CU))  # under one round of the chip
+            switches.get("DNN_WGRAD_GROUP_MAX_WG"))  # under one round of the chip
         if (R % 64 or splits > R // 64 or s != splits or _persist("wgrad", t) or
                 _blas("wgrad", t) or stages != 2 or not small or
                 (bm, bn) not in ((64, 64), (64, 128), (128, 64), (128, 128))):

@@ -17,8 +17,9 @@ from __future__ import annotations
 import json
 import os
 from typing import Optional
+from .. import switches
 
-TABLE_PATH = (os.environ.get("DNN_TUNED_TABLE") or
+TABLE_PATH = (switches.get("DNN_TUNED_TABLE") or
               os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_gfx950.json"))
 _table: Optional[dict] = None
 
@@ -40,7 +41,7 @@ def key(op: str, M: int, N: int, K: int) -> str:
 
 def lookup(op: str, M: int, N: int, K: int) -> Optional[dict]:
     """{"tile": [bm, bn], "splits": s, "stages": ns} or None."""
-    if os.environ.get("DNN_TUNED", "1") == "0":
+    if switches.get("DNN_TUNED") == "0":
         return None
     return _load().get(key(op, M, N, K))
 

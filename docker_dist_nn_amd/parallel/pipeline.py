@@ -24,6 +24,7 @@ import torch
 import torch.distributed as dist
 
 from ..utils.native import native
+from .. import switches
 
 
 def schedule_ops(kind: str, num_stages: int, num_micro: int, stage: int):
@@ -125,11 +126,11 @@ class PipelineExecutor:
                     for st, sid in zip(self.stages, self.stage_ids)]
         self.hooks: dict[str, list[Callable]] = {"before_op": [], "after_op": []}
         # concurrent wgrad streams in native single-process plans (DNN_WGRAD_STREAMS)
-        self.wgrad_streams = int(os.environ.get("DNN_WGRAD_STREAMS", "1"))
+        self.wgrad_streams = int(switches.get("DNN_WGRAD_STREAMS"))
         self._side = None
         # deferred data-parallel update (DNN_DP_DEFER=0 disables): see dp_split
         self.defer = (grad_sync is not None and grad_sync.world > 1 and
-                      os.environ.get("DNN_DP_DEFER", "1") != "0")
+                      switches.get("DNN_DP_DEFER") != "0")
         self._split = {id(st): (dp_split(st) if self.defer else 0) for st in self.stages}
         self._pending = {}  # id(stage) -> (work of layers [s, L), s)
         self._works = {}    # id(stage) -> [work of [0, s), work of [s, L)] this step
@@ -241,14 +242,14 @@ class PipelineExecutor:
         from .comm import LoopbackPipe
 
         self._plan = None
-        if os.environ.get("DNN_NATIVE_PLAN", "1") == "0":  # per-op replay (A/B, host cost)
+        if switches.get("DNN_NATIVE_PLAN") == "0":  # per-op replay (A/B, host cost)
             return None
         if not isinstance(self.pipe, LoopbackPipe) or self.grad_sync is not None or \
                 self.hooks["before_op"] or self.hooks["after_op"] or self.lr_fn is not None:
             return None
         if any(st._prog is None or not st._has_w or not st._o_native for st in self.stages):
             return None
-        if os.environ.get("DNN_BW_OVERLAP", "0") == "1" and len(self.stages) == 1:
+        if switches.get("DNN_BW_OVERLAP") == "1" and len(self.stages) == 1:
             ov = self._overlap_plan(self.stages[0])
             if ov is not None:
                 self._plan = ov

@@ -54,6 +54,7 @@ from ..config import load_model_config
 from ..engine.inference import InferenceStage
 from ..models.mlp import round_up
 from .ingress import StageFailure, serve
+from .. import switches
 
 log = logging.getLogger(__name__)
 
@@ -90,9 +91,9 @@ class ChainRank:
         self._pending_lock = threading.Lock()
         self._sendq: "queue.Queue" = queue.Queue()
         self._threads: list[threading.Thread] = []
-        self.fault_stage = os.environ.get("DNN_FAULT_STAGE")
-        self.fault_kind = os.environ.get("DNN_FAULT_KIND", "raise")
-        self.fault_after = int(os.environ.get("DNN_FAULT_AFTER", "0"))
+        self.fault_stage = switches.get("DNN_FAULT_STAGE")
+        self.fault_kind = switches.get("DNN_FAULT_KIND")
+        self.fault_after = int(switches.get("DNN_FAULT_AFTER"))
         if rank == 0 and world > 1:
             for fn, nm in ((self._sender, "chain-send"), (self._receiver, "chain-recv")):
                 t = threading.Thread(target=fn, name=nm, daemon=True)

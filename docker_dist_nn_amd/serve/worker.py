@@ -34,9 +34,10 @@ from typing import Optional
 
 import grpc
 import numpy as np
+from .. import switches
 
 log = logging.getLogger("worker")
-HOP_TIMEOUT_S = float(os.environ.get("DNN_HOP_TIMEOUT", "10"))
+HOP_TIMEOUT_S = float(switches.get("DNN_HOP_TIMEOUT"))
 
 
 class StageWorker:

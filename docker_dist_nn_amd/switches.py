@@ -1,0 +1,72 @@
+"""Every behaviour switch of the framework, in one registry.
+
+The reference steers itself with module constants, argparse flags and a per-stage env contract
+(/root/reference/src/run_grpc_fcnn.py:17-27, /root/reference/src/grpc_node.py:18-57). Ours adds
+engine / kernel switches for A/B measurements and fault injection; they are all declared here
+with their default and meaning, read through :func:`get` (the environment is consulted on every
+call, so tests can monkeypatch), and reported by :func:`active` -- the benchmark JSON echoes the
+switches in effect for its run. Nothing else in the package reads ``DNN_*`` variables.
+"""
+from __future__ import annotations
+
+import os
+
+SWITCHES: dict[str, tuple[str, str]] = {
+    # kernels / tuning
+    "DNN_TUNED": ("1", "0 = ignore the tuned GEMM table (ops/tuned_gfx950.json)"),
+    "DNN_TUNED_TABLE": ("", "path of another tuned table (A/B of two tunings)"),
+    "DNN_BLAS": ("", "hipBLASLt comparison path: '' never (own kernels), 1 = every product "
+                     "it supports, or per kind 'fwd=1,dgrad=0,wgrad=1' (bench only)"),
+    "DNN_GEMM_STAGES": ("", "LDS pipeline depth per GEMM kind ('3' or 'fwd=3,dgrad=2'); 8 = "
+                            "ping-pong 256x256 form"),
+    "DNN_GEMM_PERSIST": ("", "persistent-workgroup GEMM form per kind ('1', 'fwd=1,wgrad=0')"),
+    "DNN_WGRAD_GROUP_MAX_WG": ("256", "grouped wgrad launch: size bound in workgroups"),
+    # engine
+    "DNN_DGRAD_WT": ("1", "dgrad reads the transposed weight shadow W^T (0 = transpose per tile)"),
+    "DNN_TAIL": ("1", "fused classifier tail kernel (mlp_tail.hip)"),
+    "DNN_FUSED_XENT": ("1", "softmax cross-entropy fused into the logits GEMM epilogue"),
+    "DNN_RELU_MASK": ("0", "1-bit ReLU masks instead of the activation in dgrad epilogues"),
+    "DNN_WGRAD_ALGO": ("splitk", "weight-gradient algorithm: splitk | streamk"),
+    "DNN_WGRAD_GROUP": ("1", "one grouped launch for small split-K weight gradients"),
+    "DNN_FUSE_FIN_SGD": ("1", "gradient reduction and optimizer step in one launch (FINO)"),
+    "DNN_NATIVE_EXEC": ("1", "record each stage's launches once and replay them from C++"),
+    "DNN_NATIVE_PLAN": ("1", "single-process pipeline step as one native call"),
+    "DNN_NATIVE_DIST": ("1", "multi-rank step as one StepPlan call (parallel/native_step.py)"),
+    "DNN_WGRAD_STREAMS": ("1", "concurrent wgrad streams in native single-process plans"),
+    "DNN_BW_OVERLAP": ("0", "wgrad_i on a side stream concurrent with dgrad_i (1 stage)"),
+    "DNN_DP_DEFER": ("1", "deferred data-parallel update (Python executor path)"),
+    "DNN_PIPE": ("rccl", "pipeline transport: rccl | ipc (xGMI peer copies + stream flags)"),
+    "DNN_SERVE_REPLAY": ("graph", "serving engine replay: graph | native | eager"),
+    "DNN_SYNC_DEBUG": ("0", "synchronise + check after every kernel (race / fault hunting)"),
+    "DNN_AUTOBUILD": ("1", "build the native extension on import if it is missing"),
+    # multi-rank rehearsal on one GPU
+    "DNN_FORCE_DEVICE": ("", "run every rank on this device (one-GPU rehearsals)"),
+    "DNN_DIST_BACKEND": ("nccl", "process-group backend of bench.py (gloo for rehearsals)"),
+    # serving / failure handling
+    "DNN_HOP_TIMEOUT": ("10", "per-hop deadline of the stage worker (grpc_node.py:133)"),
+    "DNN_FAULT": ("", "training fault injection 'stage:S,step:N,kind:crash|hang|nan|raise'"),
+    "DNN_FAULT_STAGE": ("", "serving chain: rank that fails"),
+    "DNN_FAULT_KIND": ("raise", "serving chain fault kind: raise | hang"),
+    "DNN_FAULT_AFTER": ("0", "serving chain: requests served before the fault"),
+    "DNN_WORKER_DEVICE": ("auto", "stage worker device: auto | cpu"),
+}
+
+
+def get(name: str) -> str:
+    if name not in SWITCHES:
+        raise KeyError(f"undeclared switch {name}")
+    return os.environ.get(name, SWITCHES[name][0])
+
+
+def flag(name: str) -> bool:
+    return get(name) == "1"
+
+
+def active() -> dict[str, str]:
+    """The switches set to a non-default value in this process."""
+    return {k: os.environ[k] for k in SWITCHES
+            if k in os.environ and os.environ[k] != SWITCHES[k][0]}
+
+
+def describe() -> str:
+    return "\n".join(f"{k:24s} default {v[0]!r:10s} {v[1]}" for k, v in SWITCHES.items())

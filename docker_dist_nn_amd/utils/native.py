@@ -14,6 +14,7 @@ import os
 import threading
 
 import torch  # noqa: F401  (must precede the extension import, see module doc)
+from .. import switches
 
 _lock = threading.Lock()
 _mod = None
@@ -28,7 +29,7 @@ def _try_import():
         try:
             _mod = importlib.import_module("docker_dist_nn_amd._native")
         except ImportError as e:  # not built yet
-            if os.environ.get("DNN_AUTOBUILD", "1") == "1":
+            if switches.get("DNN_AUTOBUILD") == "1":
                 try:
                     from .._build import build
 
@@ -81,7 +82,7 @@ def native():
         raise RuntimeError(
             "docker_dist_nn_amd native extension is not available "
             f"({_err}); build it with `python -m docker_dist_nn_amd._build`")
-    if os.environ.get("DNN_SYNC_DEBUG", "0") == "1":
+    if switches.get("DNN_SYNC_DEBUG") == "1":
         if _debug is None:
             _debug = _SyncDebug(_mod)
         return _debug
