@@ -74,8 +74,11 @@ PYBIND11_MODULE(_native, m) {
          int layout_a, int layout_b, int out_f32, int bm, int bn, int splits, uintptr_t stream,
          uintptr_t colsum, long ld_colsum, uintptr_t xent_labels, int n_cls, float xent_scale,
          uintptr_t loss_part, uintptr_t correct, int k_total, int stages, int group_m,
-         int persist, uintptr_t mask_out, uintptr_t mask_in, long ld_mask) {
+         int persist, uintptr_t mask_out, uintptr_t mask_in, long ld_mask, uintptr_t ct,
+         long ld_ct) {
         GemmParams p{};
+        p.ct = P<uint16_t>(ct);
+        p.ld_ct = ld_ct;
         p.group_m = group_m;
         p.mask_out = P<unsigned char>(mask_out);
         p.mask_in = P<const unsigned char>(mask_in);
@@ -118,6 +121,7 @@ PYBIND11_MODULE(_native, m) {
               q.correct = R.fix(q.correct);
               q.mask_out = R.fix(q.mask_out);
               q.mask_in = R.fix(q.mask_in);
+              q.ct = R.fix(q.ct);
               return dnn::gemm_bf16(q, layout_a, layout_b, out_f32, bm, bn, splits, s, stages,
                                     persist);
             },
@@ -131,7 +135,8 @@ PYBIND11_MODULE(_native, m) {
       py::arg("xent_labels") = 0, py::arg("n_cls") = 0, py::arg("xent_scale") = 0.f,
       py::arg("loss_part") = 0, py::arg("correct") = 0, py::arg("k_total") = 0,
       py::arg("stages") = 0, py::arg("group_m") = 0, py::arg("persist") = 0,
-      py::arg("mask_out") = 0, py::arg("mask_in") = 0, py::arg("ld_mask") = 0);
+      py::arg("mask_out") = 0, py::arg("mask_in") = 0, py::arg("ld_mask") = 0,
+      py::arg("ct") = 0, py::arg("ld_ct") = 0);
   m.def("gemm_default_stages", &dnn::default_stages);
 
   m.def("gemv_max_rows", []() { return dnn::GEMV_MAX_ROWS; });

@@ -51,6 +51,11 @@ struct GemmParams {
   unsigned char* mask_out;
   const unsigned char* mask_in;
   long ld_mask;
+  // optional second bf16 output, TRANSPOSED: ct[n][m] = the stored C[m][n] (bf16 output, the
+  // one-tile form). A forward writes the next weight gradient's X^T, a dgrad its dZ^T, so that
+  // wgrad reads both operands contraction-contiguous (ds_read_b128, no per-tile transpose).
+  uint16_t* ct;
+  long ld_ct;
 };
 
 // Returns 0 on success, a negative code when a shape/alignment precondition fails

@@ -337,6 +337,7 @@ __device__ __forceinline__ void epilogue_staged(const GemmParams& p,
       }
     }
     const long gm0 = m0 + chunk * C::EPI_ROWS + crow;
+    [[maybe_unused]] bf16x8_t ov[ITER];  // the stored values, for the transposed copy
     [[maybe_unused]] bf16x8_t yv[ITER];
     [[maybe_unused]] unsigned mk[ITER];
     [[maybe_unused]] f32x4_t cp0[ITER], cp1[ITER];
@@ -410,7 +411,33 @@ __device__ __forceinline__ void epilogue_staged(const GemmParams& p,
           bits |= (bf2f(h) > 0.f ? 1u : 0u) << e;
         }
         *(bf16x8_t*)((u16*)p.C + gm * p.ldc + gn) = o;
+        ov[it] = o;
         if (p.mask_out) p.mask_out[gm * p.ld_mask + (gn >> 3)] = (unsigned char)bits;
+      }
+    }
+    if constexpr (!OUT_F32) {
+      if (p.ct) {  // uniform: transposed copy of this chunk through LDS (bf16 [BN][rows])
+        constexpr int TLD = C::EPI_ROWS + 8;  // +16 B per row: spread the 2-byte writes
+        static_assert(BN * TLD * 2 <= C::SMEM, "transposed chunk fits the staging LDS");
+        u16 LDS_AS* tt = (u16 LDS_AS*)lds;
+        __syncthreads();  // every thread is done reading the fp32 staging tile
+#pragma unroll
+        for (int it = 0; it < ITER; ++it) {
+          const int row = crow + it * RSTEP;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) tt[(ccol + e) * TLD + row] = (u16)ov[it][e];
+        }
+        __syncthreads();
+        constexpr int RC = C::EPI_ROWS / 8;  // 16-byte chunks per transposed row
+        const long m_base = m0 + chunk * C::EPI_ROWS;
+#pragma unroll 2
+        for (int idx = threadIdx.x; idx < BN * RC; idx += NT) {
+          const int col = idx / RC, r8 = (idx % RC) * 8;
+          const long gcol = n0 + col, grow = m_base + r8;
+          if (gcol >= p.N || grow >= p.M) continue;  // partial edge tile
+          const bf16x8_t v = *(const bf16x8_t LDS_AS*)(tt + col * TLD + r8);
+          *(bf16x8_t*)(p.ct + gcol * p.ld_ct + grow) = v;
+        }
       }
     }
   }

@@ -365,6 +365,23 @@ class Stage:
         # layers, the softmax CE and both of their dgrads run as ONE kernel inside the last
         # layer's forward; the second-to-last layer's forward and both dgrads are then no-ops.
         self.tail = self._tail_ok()
+        # K-major weight gradients (ops.linear_wgrad dzt / xt): for big hidden layers whose dZ
+        # and input activation come from this stage's own one-tile GEMMs, those GEMMs also write
+        # the transposed copies in their epilogues (+1 write of each, -20 % wgrad time)
+        self.dzT: dict[int, torch.Tensor] = {}
+        self.actT: dict[int, torch.Tensor] = {}
+        kk = switches.get("DNN_WGRAD_KK")
+        if dev.type == "cuda" and self.wgrad_mode == "batched" and kk != "0":
+            L = len(self.geoms)
+            for i in range(1, L):
+                g = self.geoms[i]
+                big = kk == "1" or g.np_ * g.kp >= (1 << 24)
+                dz_by_dgrad = i + 1 < L and not (self.tail and i + 1 >= L - 2) and \
+                    self.relu_mask[i] is None
+                x_by_fwd = not (self.tail and i - 1 >= L - 2) and self.relu_mask[i - 1] is None
+                if big and dz_by_dgrad and x_by_fwd:
+                    self.dzT[i] = torch.zeros(g.np_, R, dtype=bf, device=dev)
+                    self.actT[i - 1] = torch.zeros(g.kp, R, dtype=bf, device=dev)
         # dgrad GEMMs read W^T (contraction-contiguous B operand, see ops.linear_dgrad)
         if dev.type == "cuda" and switches.get("DNN_DGRAD_WT") == "1":
             L = len(self.geoms)
@@ -518,7 +535,8 @@ class Stage:
         else:
             m = self.relu_mask[i]
             ops.linear_fwd(x, p.wbf(i), p.b32(i), y, act=g.spec.activation,
-                           mask=None if m is None else m[r])
+                           mask=None if m is None else m[r],
+                           yt=self.actT[i][:, r] if i in self.actT else None)
 
     def backward(self, j: int) -> None:
         """dgrad chain of micro-batch j; dZ of the last local layer must already be present."""
@@ -546,7 +564,8 @@ class Stage:
             ops.linear_dgrad(self.dz[i][r], p.wbf(i), self.dz[i - 1][r],
                              y_prev=self.acts[i - 1][r], act_prev=prev,
                              colsum=self._bpart(i - 1, j),
-                             mask_prev=None if m is None else m[r], wt=p.wt.get(i))
+                             mask_prev=None if m is None else m[r], wt=p.wt.get(i),
+                             dxt=self.dzT[i - 1][:, r] if (i - 1) in self.dzT else None)
         elif not self.first:
             # gradient for the previous stage, already multiplied by the derivative of its
             # last layer's activation (its output is our input x_in)
@@ -602,8 +621,11 @@ class Stage:
                                      self.params.gw(i).view(g.np_, g.kp), self.sk_part,
                                      accumulate=accumulate)
         else:
+            kk = j < 0 and i in self.dzT
             ops.linear_wgrad(self.dz[i][r], self.input_of(i)[r], self.slabs[i],
-                             splits=self.w_splits[i], accumulate=accumulate)
+                             splits=self.w_splits[i], accumulate=accumulate,
+                             dzt=self.dzT[i] if kk else None,
+                             xt=self.actT[i - 1] if kk else None)
 
     def finalize_grads(self, layers: Optional[Sequence[int]] = None) -> None:
         """Reduce bias partials (and, for split-K, weight slabs) into the flat gradient."""

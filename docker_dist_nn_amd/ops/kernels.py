@@ -223,7 +223,7 @@ def wgrad_config(M: int, N: int, K_total: int, max_splits: int = 48) -> tuple[in
 def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=None, aux=None,
          act=0, accumulate: bool = False, splits: int = 1, tiles: tuple[int, int] | None = None,
          colsum=None, k_total: int = 0, stages: int = 0, group_m: int = 0, persist: int = 0,
-         mask_out=None, mask_in=None):
+         mask_out=None, mask_in=None, ct=None):
     """C (+)= epilogue(A.B). See csrc/kernels/gemm.hpp for the layout/epilogue contract.
 
     ``persist`` != 0 runs the persistent-workgroup form with the register-direct epilogue
@@ -250,10 +250,16 @@ def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=
         if m is not None and (m.dtype != torch.uint8 or m.dim() != 2 or m.stride(1) != 1 or
                               m.shape[0] < M or m.shape[1] < -(-N // 8)):
             raise ValueError(f"relu mask must be uint8 [{M}][>={-(-N // 8)}] row-major")
+    if ct is not None and (ct.dtype != torch.bfloat16 or ct.dim() != 2 or ct.stride(1) != 1 or
+                           ct.shape[0] < N or ct.shape[1] < M or out_f32):
+        raise ValueError(f"ct must be a bf16 [>={N}][>={M}] row-major transposed output")
     if not a.is_cuda:
-        return ref.gemm(a, b, c, layout_a=layout_a, layout_b=layout_b, M=M, N=N, K=K, bias=bias,
-                        aux=aux, act=act, accumulate=accumulate, splits=splits, colsum=colsum,
-                        colsum_rows=tiles[0] if tiles else 0, k_total=k_total)
+        ref.gemm(a, b, c, layout_a=layout_a, layout_b=layout_b, M=M, N=N, K=K, bias=bias,
+                 aux=aux, act=act, accumulate=accumulate, splits=splits, colsum=colsum,
+                 colsum_rows=tiles[0] if tiles else 0, k_total=k_total)
+        if ct is not None:
+            ct[:N, :M] = c[:M, :N].t()
+        return c
     _rows(a, "A", torch.bfloat16)
     _rows(b, "B", torch.bfloat16)
     if splits > 1:
@@ -290,7 +296,8 @@ def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=
                        stages=int(stages), group_m=int(group_m), persist=int(persist),
                        mask_out=_p(mask_out), mask_in=_p(mask_in),
                        ld_mask=(mask_out if mask_out is not None else mask_in).stride(0)
-                       if (mask_out is not None or mask_in is not None) else 0)
+                       if (mask_out is not None or mask_in is not None) else 0,
+                       ct=_p(ct), ld_ct=ct.stride(0) if ct is not None else 0)
     return c
 
 
@@ -320,14 +327,16 @@ def gemv(x, w, bias, y, act="relu"):
     return y
 
 
-def linear_fwd(x, w, bias, y, act="relu", mask=None):
+def linear_fwd(x, w, bias, y, act="relu", mask=None, yt=None):
     """y[M][Np] = act(x[M][Kp] . w[Np][Kp]^T + bias). y bf16 (activation) or fp32 (logits).
     M <= 8 rows (serving) runs the GEMV kernel; otherwise the MFMA GEMM. ``mask`` (GPU, relu):
-    also write the 1-bit mask of y for the next dgrad."""
+    also write the 1-bit mask of y for the next dgrad. ``yt`` (bf16 [Np][>=M], may be a column
+    slice): also write y transposed (the next layer's weight gradient reads it K-major)."""
     M, K = x.shape
     N = w.shape[0]
     if not x.is_cuda:  # CPU reference: any row count
-        return gemm(x, w, y, layout_a=KMAJ, layout_b=KMAJ, M=M, N=N, K=K, bias=bias, act=act)
+        return gemm(x, w, y, layout_a=KMAJ, layout_b=KMAJ, M=M, N=N, K=K, bias=bias, act=act,
+                    ct=yt)
     if M <= GEMV_MAX_ROWS:
         return gemv(x, w, bias, y, act)
     t = tuning.lookup("fwd", M, N, K)
@@ -338,7 +347,8 @@ def linear_fwd(x, w, bias, y, act="relu", mask=None):
     tiles = tuple(t["tile"]) if t else pick_tiles(M, N)
     return gemm(x, w, y, layout_a=KMAJ, layout_b=KMAJ, M=M, N=N, K=K, bias=bias, act=act,
                 tiles=tiles, stages=STAGES["fwd"] or (t or {}).get("stages", 0),
-                persist=0 if mask is not None else _persist("fwd", t), mask_out=mask)
+                persist=0 if (mask is not None or yt is not None) else _persist("fwd", t),
+                mask_out=mask, ct=yt)
 
 
 def xent_tiles(M: int, N: int) -> tuple[int, int]:
@@ -409,7 +419,7 @@ def transpose_bf16(src, dst):
 
 
 def linear_dgrad(dz, w, dx, y_prev=None, act_prev="linear", colsum=None, mask_prev=None,
-                 wt=None):
+                 wt=None, dxt=None):
     """dx[M][Kp] = (dz[M][Np] . w[Np][Kp]) * act_prev'(y_prev) (mask fused in the epilogue).
     ``colsum`` [M/bm][Kp] receives the bias-gradient partials of the PREVIOUS layer (column
     sums of dx), fused in the same epilogue. ``wt`` = w^T [Kp][Np] (the transposed weight
@@ -437,18 +447,29 @@ def linear_dgrad(dz, w, dx, y_prev=None, act_prev="linear", colsum=None, mask_pr
         return gemm(dz, wt, dx, layout_a=KMAJ, layout_b=KMAJ, M=M, N=K, K=N, aux=y_prev,
                     act=act_prev, tiles=dgrad_tiles(M, K, N), colsum=colsum,
                     stages=STAGES["dgrad"] or (t or {}).get("stages", 0),
-                    persist=_persist("dgrad", t))
+                    persist=0 if dxt is not None else _persist("dgrad", t), ct=dxt)
     return gemm(dz, w, dx, layout_a=KMAJ, layout_b=MNMAJ, M=M, N=K, K=N, aux=y_prev,
                 act=act_prev, tiles=dgrad_tiles(M, K, N), colsum=colsum,
                 stages=STAGES["dgrad"] or (t or {}).get("stages", 0),
-                persist=0 if mask_prev is not None else _persist("dgrad", t),
-                mask_in=mask_prev)
+                persist=0 if (mask_prev is not None or dxt is not None)
+                else _persist("dgrad", t), mask_in=mask_prev, ct=dxt)
 
 
-def linear_wgrad(dz, x, slabs, splits=1, accumulate=False):
-    """slabs[s][Np][Kp] (+)= dz[rows_s]^T . x[rows_s] over the batch rows of split s (fp32)."""
+def linear_wgrad(dz, x, slabs, splits=1, accumulate=False, dzt=None, xt=None):
+    """slabs[s][Np][Kp] (+)= dz[rows_s]^T . x[rows_s] over the batch rows of split s (fp32).
+    ``dzt`` / ``xt`` (bf16 [Np][R] / [Kp][R], written transposed by the producing GEMMs'
+    epilogues): the contraction runs K-major on both operands (the forward's main loop,
+    bench/layout_ab.py: 1.2x on 8192x8192 weights); same k order, same result bits."""
     R, N = dz.shape
     K = x.shape[1]
+    if dzt is not None and xt is not None and dz.is_cuda:
+        bm, bn, s = wgrad_config(N, K, R)
+        tiles = (bm, bn) if s == splits else pick_tiles(N, K, splits)
+        t = tuning.lookup("wgrad", N, K, R) if s == splits else None
+        return gemm(dzt, xt, slabs, layout_a=KMAJ, layout_b=KMAJ, M=N, N=K, K=R, k_total=R,
+                    accumulate=accumulate, splits=splits, tiles=tiles,
+                    stages=STAGES["wgrad"] or (t or {}).get("stages", 0),
+                    persist=_persist("wgrad", t))
     if R % 64 or splits > R // 64:
         raise ValueError("rows must be a multiple of 64 with at least 64 rows per split")
     bm, bn, s = wgrad_config(N, K, R)

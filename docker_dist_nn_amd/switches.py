@@ -23,6 +23,8 @@ SWITCHES: dict[str, tuple[str, str]] = {
     "DNN_WGRAD_GROUP_MAX_WG": ("256", "grouped wgrad launch: size bound in workgroups"),
     # engine
     "DNN_DGRAD_WT": ("1", "dgrad reads the transposed weight shadow W^T (0 = transpose per tile)"),
+    "DNN_WGRAD_KK": ("auto", "K-major weight gradients from transposed dZ / X copies written by "
+                             "the producing GEMMs: auto (layers >= 16M weights) | 1 | 0"),
     "DNN_TAIL": ("1", "fused classifier tail kernel (mlp_tail.hip)"),
     "DNN_FUSED_XENT": ("1", "softmax cross-entropy fused into the logits GEMM epilogue"),
     "DNN_RELU_MASK": ("0", "1-bit ReLU masks instead of the activation in dgrad epilogues"),

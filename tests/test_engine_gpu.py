@@ -171,3 +171,24 @@ def test_native_and_graph_optimizers_with_lr_schedule(dev, optim):
         assert l1 == l0
         for k in w0:
             assert np.array_equal(w0[k][0], w1[k][0])
+
+
+@pytest.mark.parametrize("model", ["784-256-256-256-10", "784-512-512-512-256-10"])
+def test_kmajor_wgrad_training_bitwise(dev, monkeypatch, model):
+    """Training with K-major weight gradients (forward / dgrad epilogues also write X^T and
+    dZ^T, wgrad reads both K-major; DNN_WGRAD_KK=1 forces it on these small layers) gives the
+    same weights, bit for bit, as the transposing-read path (DNN_WGRAD_KK=0)."""
+    spec = MLPSpec.parse(model)
+    x, y = _batch(1024, dev)
+    out = []
+    for kk in ("0", "1"):
+        monkeypatch.setenv("DNN_WGRAD_KK", kk)
+        tr = Trainer(spec, device=dev, micro_batch=512, num_micro=2, pp=1,
+                     optim=OptimConfig(lr=0.1, momentum=0.9))
+        assert bool(tr.stages[0].dzT) == (kk == "1")
+        for _ in range(3):
+            tr.set_batch(x, y)
+            tr.step()
+        out.append(tr.local_weights())
+    for k in out[0]:
+        assert np.array_equal(out[0][k][0], out[1][k][0]), k

@@ -522,3 +522,36 @@ def test_dgrad_transposed_weight_bitwise(dev, M, N, K, tiles):
     assert torch.equal(outs[0][1], outs[1][1])
     ref = (dz.float() @ w.float()) * (y_prev.float() > 0)
     torch.testing.assert_close(outs[1][0].float(), ref, rtol=2e-2, atol=2e-2 * K ** 0.5)
+
+
+@pytest.mark.parametrize("M,N,K,tiles", [(512, 256, 832, (256, 256)), (384, 192, 128, (128, 64)),
+                                         (296, 136, 64, (64, 64))])
+def test_gemm_transposed_second_output(dev, M, N, K, tiles):
+    """ct (the transposed bf16 copy written by the staged epilogue) equals C^T bit for bit,
+    including partial edge tiles and a column-slice destination (a micro-batch of a
+    [N][rows] buffer)."""
+    gen = torch.Generator().manual_seed(M + N)
+    x = torch.randn(M, K, generator=gen).to(torch.bfloat16).to(dev)
+    w = torch.randn(N, K, generator=gen).to(torch.bfloat16).to(dev)
+    b = torch.randn(N, generator=gen).to(dev)
+    y = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    big = torch.full((N, 2 * M + 8), 3.0, dtype=torch.bfloat16, device=dev)
+    ct = big[:, M:2 * M]  # column slice: ld_ct = 2M + 8
+    ops.gemm(x, w, y, layout_a=KMAJ, layout_b=KMAJ, M=M, N=N, K=K, bias=b, act="relu",
+             tiles=tiles, ct=ct)
+    assert torch.equal(ct, y.t())
+    assert torch.all(big[:, :M] == 3.0) and torch.all(big[:, 2 * M:] == 3.0)
+
+
+def test_wgrad_kmajor_bitwise_equals_transposing(dev):
+    """K-major wgrad on transposed copies == the transposing-read wgrad, bit for bit."""
+    gen = torch.Generator().manual_seed(5)
+    R, N, K = 2048, 512, 768
+    dz = torch.randn(R, N, generator=gen).to(torch.bfloat16).to(dev)
+    x = torch.randn(R, K, generator=gen).to(torch.bfloat16).to(dev)
+    for splits in (1, 3):
+        a = torch.empty(splits, N, K, device=dev)
+        b = torch.empty(splits, N, K, device=dev)
+        ops.linear_wgrad(dz, x, a, splits=splits)
+        ops.linear_wgrad(dz, x, b, splits=splits, dzt=dz.t().contiguous(), xt=x.t().contiguous())
+        assert torch.equal(a, b)
