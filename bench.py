@@ -93,7 +93,7 @@ def _plan(a, spec, n, world, text):
             return planner.evaluate(spec, 1, 1, a.batch)
         return planner.pipeline_layout(spec, n, a.batch)
     rows = a.batch * (1 if loopback else pp)  # loopback: every stage on the one GPU
-    return planner.evaluate(spec, pp, dp, rows)
+    return planner.evaluate(spec, pp, dp, rows, loopback=loopback)
 
 
 def measure(a, spec, n, world, dev, text):

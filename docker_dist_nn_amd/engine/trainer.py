@@ -200,6 +200,7 @@ class Trainer:
         if self.first is not None and self.first.x_in.data_ptr() != self.first.x_buf.data_ptr():
             self.first.x_in = self.first.x_buf  # a graph needs the fixed input buffer
         graphs = []
+        self.executor.capturing = True  # single-stream plan: the graph serialises anyway
         with torch.cuda.stream(self._stream):
             for _ in range(warmup):
                 self.executor.run_step()

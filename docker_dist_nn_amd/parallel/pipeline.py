@@ -317,6 +317,43 @@ class PipelineExecutor:
             plan.append((st, "O", 0))
         return plan
 
+    def _loopback_step_plan(self, plan):
+        """Several stages in one process (loopback): run each stage on ITS OWN stream, with an
+        event edge per micro-batch hop (F(s, j) after F(s-1, j); B(s, j) after B(s+1, j)).
+        Stages then execute concurrently on the one GPU like a real pipeline, instead of the
+        whole schedule serialised on one stream: micro-batch GEMMs are small (a 4-stage,
+        16-micro-batch step at 65536 rows runs 4096-row GEMMs) and fill the chip only together.
+        Built once into a StepPlan (csrc/runtime/step_plan.hpp): one C++ call per step."""
+        from .native_step import REC, SEG, WAIT
+
+        S = len(self.stages)
+        idx = {id(st): k for k, st in enumerate(self.stages)}
+        ev = {}
+        ops = []
+
+        def event(key):
+            ev[key] = len(ev)
+            return ev[key]
+
+        for st, seg, si in plan:
+            if st is None or si:
+                return None  # fork/join side streams: keep the single-stream plan
+            s = idx[id(st)]
+            kind, j = seg[0], seg[1:]
+            if kind in "FB" and j.isdigit():
+                j = int(j)
+                dep = ("F", s - 1, j) if kind == "F" else ("B", s + 1, j)
+                if dep in ev:
+                    ops.append(dict(kind=WAIT, stream=s, event=ev[dep]))
+                ops.append(dict(kind=SEG, stream=s, prog=st._prog, seg=seg))
+                ops.append(dict(kind=REC, stream=s, event=event((kind, s, j))))
+            else:
+                ops.append(dict(kind=SEG, stream=s, prog=st._prog, seg=seg))
+        sp = native().StepPlan(S, max(1, len(ev)))
+        for o in ops:
+            sp.add(**o)
+        return sp
+
     def run_step(self) -> None:
         ns = getattr(self, "native_step", None)
         if ns is not None:  # one C++ call: parallel/native_step.py
@@ -328,6 +365,18 @@ class PipelineExecutor:
         for st in self.stages:
             st.begin_step()
         plan = self._native_plan()
+        if plan is not None and len(self.stages) > 1 and not getattr(self, "capturing", False) \
+                and switches.get("DNN_LOOPBACK_STREAMS") == "1":
+            if getattr(self, "_lb_plan", False) is False:
+                self._lb_plan = self._loopback_step_plan(plan)
+            if self._lb_plan is not None:
+                for st in self.stages:
+                    st.params.set_lr(st.params.optim.lr)
+                self._lb_plan.run(torch.cuda.current_stream(self.stages[0].device).cuda_stream)
+                for st in self.stages:
+                    st.params.step_count += 1
+                self.pipe.end_step()
+                return
         if plan is not None:
             dev = self.stages[0].device
             for st in self.stages:

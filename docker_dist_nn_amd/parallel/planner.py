@@ -99,8 +99,13 @@ class Planner:
 
     def evaluate(self, spec: MLPSpec, pp: int, dp: int, rows_per_replica: int,
                  micro_batch: Optional[int] = None,
-                 distribution: Optional[list[int]] = None) -> Plan:
+                 distribution: Optional[list[int]] = None, loopback: bool = False) -> Plan:
         L = spec.layers
+        if loopback and pp > 1 and not micro_batch:
+            # every stage on ONE GPU: the stages overlap only through their streams, so the
+            # micro-batch GEMMs must stay big enough to fill the chip (>= 8192 rows), 2 per stage
+            micro_batch = max(8192, rows_per_replica // (2 * pp)) // 64 * 64
+            micro_batch = min(micro_batch, rows_per_replica)
         mb = micro_batch or (rows_per_replica if pp == 1 else
                              max(64, rows_per_replica // (4 * pp) // 64 * 64))
         M = max(1, rows_per_replica // mb)

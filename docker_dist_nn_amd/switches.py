@@ -33,6 +33,8 @@ SWITCHES: dict[str, tuple[str, str]] = {
     "DNN_FUSE_FIN_SGD": ("1", "gradient reduction and optimizer step in one launch (FINO)"),
     "DNN_NATIVE_EXEC": ("1", "record each stage's launches once and replay them from C++"),
     "DNN_NATIVE_PLAN": ("1", "single-process pipeline step as one native call"),
+    "DNN_LOOPBACK_STREAMS": ("1", "single-process pipeline: one stream per stage, event edges "
+                                  "per micro-batch hop (0 = the schedule on one stream)"),
     "DNN_NATIVE_DIST": ("1", "multi-rank step as one StepPlan call (parallel/native_step.py)"),
     "DNN_WGRAD_STREAMS": ("1", "concurrent wgrad streams in native single-process plans"),
     "DNN_BW_OVERLAP": ("0", "wgrad_i on a side stream concurrent with dgrad_i (1 stage)"),
