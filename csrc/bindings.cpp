@@ -521,6 +521,36 @@ PYBIND11_MODULE(_native, m) {
         },
         stream);
   });
+  m.def("transpose_multi",
+        [](const std::vector<std::tuple<uintptr_t, long, int, int, uintptr_t, long>>& jobs,
+           uintptr_t stream) {
+          if (jobs.empty() || jobs.size() > (size_t)dnn::TRANSPOSE_MAX_JOBS)
+            throw std::invalid_argument("transpose_multi: 1..16 jobs");
+          for (const auto& [src, lds, rows, cols, dst, ldd] : jobs)
+            if (rows <= 0 || cols <= 0 || rows % 64 || cols % 64 || lds < cols || ldd < rows ||
+                lds % 8 || ldd % 8 || ((src | dst) & 15))
+              throw std::invalid_argument("transpose_multi: bad job shape / alignment");
+          launch(
+              "transpose_multi",
+              [=](hipStream_t s, const dnn::Program& R) {
+                dnn::TransposeJobs J{};
+                J.n = (int)jobs.size();
+                int t = 0;
+                for (int k = 0; k < J.n; ++k) {
+                  const auto& [src, lds, rows, cols, dst, ldd] = jobs[k];
+                  J.src[k] = R.fix(P<const uint16_t>(src));
+                  J.dst[k] = R.fix(P<uint16_t>(dst));
+                  J.ld_src[k] = lds;
+                  J.ld_dst[k] = ldd;
+                  J.tiles_c[k] = cols / 64;
+                  J.start[k] = t;
+                  t += (rows / 64) * (cols / 64);
+                }
+                J.start[J.n] = t;
+                return dnn::transpose_multi(J, s);
+              },
+              stream);
+        });
   m.def("unpack_bf16", [](uintptr_t in, long ld_in, int rows, int cols, uintptr_t out,
                           long ld_out, uintptr_t stream) {
     launch(

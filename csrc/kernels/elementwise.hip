@@ -608,11 +608,11 @@ int unpack_bf16(const uint16_t* in, long ld_in, int rows, int cols, float* out, 
 // GEMM reads both operands contraction-contiguous (ds_read_b128 fragments, the forward's main
 // loop) instead of transposing W with ds_read_b64_tr_b16 in every tile.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void transpose_bf16_kernel(const u16* __restrict__ src,
-                                                             long ld_src, u16* __restrict__ dst,
-                                                             long ld_dst, int tiles_c) {
+__device__ __forceinline__ void transpose_tile(const u16* __restrict__ src, long ld_src,
+                                               u16* __restrict__ dst, long ld_dst, int tiles_c,
+                                               int tile) {
   __shared__ u16 t[64][64 + 8];  // +16 B per row: the column reads below hit distinct banks
-  const int r0 = (blockIdx.x / tiles_c) * 64, c0 = (blockIdx.x % tiles_c) * 64;
+  const int r0 = (tile / tiles_c) * 64, c0 = (tile % tiles_c) * 64;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int chunk = threadIdx.x + 256 * i, r = chunk >> 3, c = (chunk & 7) * 8;
@@ -631,6 +631,28 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const u16* __restri
     for (int k = 0; k < 8; ++k) e[k] = t[r + k][c];
     *(uint4*)(dst + (long)(c0 + c) * ld_dst + r0 + r) = v;
   }
+}
+
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const u16* __restrict__ src,
+                                                             long ld_src, u16* __restrict__ dst,
+                                                             long ld_dst, int tiles_c) {
+  transpose_tile(src, ld_src, dst, ld_dst, tiles_c, blockIdx.x);
+}
+
+// Several transposes in ONE launch (every W^T refresh of a stage after its update: small
+// weights are launch-latency bound one by one).
+__global__ __launch_bounds__(256) void transpose_multi_kernel(TransposeJobs J) {
+  int j = 0;
+  while (j + 1 < J.n && (int)blockIdx.x >= J.start[j + 1]) ++j;
+  transpose_tile(J.src[j], J.ld_src[j], J.dst[j], J.ld_dst[j], J.tiles_c[j],
+                 blockIdx.x - J.start[j]);
+}
+
+int transpose_multi(const TransposeJobs& jobs, hipStream_t stream) {
+  if (jobs.n <= 0 || jobs.n > TRANSPOSE_MAX_JOBS) return -1;
+  hipLaunchKernelGGL(transpose_multi_kernel, dim3(jobs.start[jobs.n]), dim3(256), 0, stream,
+                     jobs);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
 }
 
 int transpose_bf16(const uint16_t* src, long ld_src, int rows, int cols, uint16_t* dst,

@@ -75,6 +75,17 @@ int pack_bf16(const float* in, long ld_in, int rows, int cols, uint16_t* out, lo
 int unpack_bf16(const uint16_t* in, long ld_in, int rows, int cols, float* out, long ld_out,
                 hipStream_t stream);
 
+constexpr int TRANSPOSE_MAX_JOBS = 16;
+struct TransposeJobs {
+  const uint16_t* src[TRANSPOSE_MAX_JOBS];
+  uint16_t* dst[TRANSPOSE_MAX_JOBS];
+  long ld_src[TRANSPOSE_MAX_JOBS], ld_dst[TRANSPOSE_MAX_JOBS];
+  int tiles_c[TRANSPOSE_MAX_JOBS];
+  int start[TRANSPOSE_MAX_JOBS + 1];  // first 64x64 tile (= workgroup) of each job
+  int n;
+};
+// Every job of transpose_bf16 in one launch (jobs validated by the caller: see bindings).
+int transpose_multi(const TransposeJobs& jobs, hipStream_t stream);
 // dst[c][r] = src[r][c] for a bf16 [rows][cols] matrix (rows, cols multiples of 64).
 int transpose_bf16(const uint16_t* src, long ld_src, int rows, int cols, uint16_t* dst,
                    long ld_dst, hipStream_t stream);

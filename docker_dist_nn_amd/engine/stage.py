@@ -144,9 +144,7 @@ class StageParams:
     def refresh_t(self, a: int = 0, b: Optional[int] = None) -> None:
         """Re-derive W^T of the local layers [a, b) that keep one (after their update)."""
         b = len(self.geoms) if b is None else b
-        for i in range(a, b):
-            if i in self.wt:
-                ops.transpose_bf16(self.wbf(i), self.wt[i])
+        ops.transpose_multi([(self.wbf(i), self.wt[i]) for i in range(a, b) if i in self.wt])
 
     def _layers_of(self, e0: int, e1: int) -> tuple[int, int]:
         """Local layers whose parameters lie in the flat element range [e0, e1)."""

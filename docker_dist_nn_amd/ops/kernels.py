@@ -418,6 +418,27 @@ def transpose_bf16(src, dst):
     return dst
 
 
+def transpose_multi(pairs):
+    """transpose_bf16 for every (src, dst) pair, one launch on the GPU (<= 16 pairs)."""
+    pairs = list(pairs)
+    if not pairs:
+        return
+    if not pairs[0][0].is_cuda:
+        for src, dst in pairs:
+            transpose_bf16(src, dst)
+        return
+    jobs = []
+    for src, dst in pairs:
+        rows, cols = src.shape
+        _rows(src, "src", torch.bfloat16)
+        _rows(dst, "dst", torch.bfloat16)
+        if dst.shape[0] < cols or dst.shape[1] < rows:
+            raise ValueError("transpose_multi: dst too small")
+        jobs.append((_p(src), src.stride(0), rows, cols, _p(dst), dst.stride(0)))
+    for k in range(0, len(jobs), 16):
+        native().transpose_multi(jobs[k:k + 16], _stream(pairs[0][0]))
+
+
 def linear_dgrad(dz, w, dx, y_prev=None, act_prev="linear", colsum=None, mask_prev=None,
                  wt=None, dxt=None):
     """dx[M][Kp] = (dz[M][Np] . w[Np][Kp]) * act_prev'(y_prev) (mask fused in the epilogue).

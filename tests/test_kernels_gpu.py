@@ -555,3 +555,13 @@ def test_wgrad_kmajor_bitwise_equals_transposing(dev):
         ops.linear_wgrad(dz, x, a, splits=splits)
         ops.linear_wgrad(dz, x, b, splits=splits, dzt=dz.t().contiguous(), xt=x.t().contiguous())
         assert torch.equal(a, b)
+
+
+def test_transpose_multi(dev):
+    gen = torch.Generator().manual_seed(3)
+    shapes = [(64, 64), (512, 832), (1024, 192), (128, 1024)] * 5  # > 16 jobs: two launches
+    srcs = [torch.randn(r, c, generator=gen).to(torch.bfloat16).to(dev) for r, c in shapes]
+    dsts = [torch.zeros(c, r, dtype=torch.bfloat16, device=dev) for r, c in shapes]
+    ops.transpose_multi(list(zip(srcs, dsts)))
+    for s_, d_ in zip(srcs, dsts):
+        assert torch.equal(d_, s_.t())
