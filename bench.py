@@ -76,6 +76,9 @@ def parse_args(argv=None):
                     help="replay the step as a HIP graph (1 GPU); eager is faster at large batch")
     ap.add_argument("--graph-copies", type=int, default=2,
                     help="alternate between this many instantiations of the step graph")
+    ap.add_argument("--boundary", default="bf16", choices=["bf16", "fp8"],
+                    help="pipeline hop format: bf16 (default) or e4m3 rows + fp32 row scales "
+                         "(half the xGMI bytes; opt-in, reduced-precision hops)")
     ap.add_argument("--no-dp-compare", action="store_true",
                     help="N > 1: skip the data-parallel-only comparison run")
     ap.add_argument("--seed", type=int, default=0)
@@ -118,7 +121,7 @@ def measure(a, spec, n, world, dev, text):
     tr = Trainer(spec, micro_batch=mb, num_micro=nm, distribution=plan.distribution,
                  pp=plan.pp, dp=plan.dp, schedule=a.schedule,
                  optim=OptimConfig(name=a.optimizer, lr=a.lr),
-                 device=dev, seed=a.seed, mesh=mesh)
+                 device=dev, seed=a.seed, mesh=mesh, boundary=a.boundary)
     replica = mesh.replica if mesh else 0
     x, y = synthetic_mnist(max(60000, 2 * rows), seed=a.seed + 1000 * replica)
     data = DeviceDataset(x, y, rows, dev, kp=tr.stages[0].x_in.shape[1] if tr.first else None)
@@ -169,6 +172,7 @@ def measure(a, spec, n, world, dev, text):
         "layer_distribution": plan.distribution, "micro_batch": mb, "num_micro": nm,
         "schedule": a.schedule if plan.pp > 1 else "none",
         "transport": tr.transport, "native_step": tr.native_step is not None or world == 1,
+        "boundary": tr.boundary,
         "hip_graph": use_graph, "graph_copies": a.graph_copies if use_graph else 0,
         "loss": loss, "planner_predicted": round(plan.samples_per_s, 1),
     }
@@ -220,7 +224,7 @@ def main(argv=None):
             "global_batch": m["global_batch"],
             "seq_len": None,
             **{k: m[k] for k in ("parallelism", "layer_distribution", "micro_batch", "num_micro",
-                                 "schedule", "transport", "native_step", "hip_graph",
+                                 "schedule", "transport", "native_step", "boundary", "hip_graph",
                                  "graph_copies")},
             "optimizer": a.optimizer,
         },

@@ -551,6 +551,27 @@ PYBIND11_MODULE(_native, m) {
               },
               stream);
         });
+  m.def("quant_rows_fp8", [](uintptr_t x, long ldx, int rows, int cols, uintptr_t q, long ldq,
+                             uintptr_t scale, uintptr_t stream) {
+    launch(
+        "quant_rows_fp8",
+        [=](hipStream_t s, const dnn::Program& R) {
+          return dnn::quant_rows_fp8(R.fix(P<const uint16_t>(x)), ldx, rows, cols,
+                                     R.fix(P<unsigned char>(q)), ldq, R.fix(P<float>(scale)), s);
+        },
+        stream);
+  });
+  m.def("dequant_rows_fp8", [](uintptr_t q, long ldq, uintptr_t scale, int rows, int cols,
+                               uintptr_t x, long ldx, uintptr_t stream) {
+    launch(
+        "dequant_rows_fp8",
+        [=](hipStream_t s, const dnn::Program& R) {
+          return dnn::dequant_rows_fp8(R.fix(P<const unsigned char>(q)), ldq,
+                                       R.fix(P<const float>(scale)), rows, cols,
+                                       R.fix(P<uint16_t>(x)), ldx, s);
+        },
+        stream);
+  });
   m.def("unpack_bf16", [](uintptr_t in, long ld_in, int rows, int cols, uintptr_t out,
                           long ld_out, uintptr_t stream) {
     launch(

@@ -666,4 +666,93 @@ int transpose_bf16(const uint16_t* src, long ld_src, int rows, int cols, uint16_
   return hipGetLastError() == hipSuccess ? 0 : -9;
 }
 
+// ------------------------------------------------------------------------------------------
+// fp8 pipeline boundary (opt-in): a row of a bf16 activation / gradient is sent as OCP e4m3
+// bytes plus one fp32 scale (row amax / 448), halving the bytes on the xGMI hop. One wave per
+// row; 8 elements (one 16-byte bf16 load, one 8-byte fp8 store) per lane per iteration.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ float wave_amax(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__global__ __launch_bounds__(256) void quant_rows_fp8_kernel(const u16* __restrict__ x, long ldx,
+                                                             int rows, int cols,
+                                                             unsigned char* __restrict__ q,
+                                                             long ldq, float* __restrict__ scale) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;  // wave-uniform
+  const u16* xr = x + (long)row * ldx;
+  float amax = 0.f;
+  for (int c = lane * 8; c < cols; c += 512) {
+    const uint4 v = *(const uint4*)(xr + c);
+    const u16* e = (const u16*)&v;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) amax = fmaxf(amax, fabsf(bf2f(e[k])));
+  }
+  amax = wave_amax(amax);
+  const float s = amax / 448.f, inv = amax > 0.f ? 448.f / amax : 0.f;
+  if (lane == 0) scale[row] = s;
+  unsigned char* qr = q + (long)row * ldq;
+  for (int c = lane * 8; c < cols; c += 512) {
+    const uint4 v = *(const uint4*)(xr + c);
+    const u16* e = (const u16*)&v;
+    unsigned lo = 0, hi = 0;
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f(e[0]) * inv, bf2f(e[1]) * inv, lo, false);
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f(e[2]) * inv, bf2f(e[3]) * inv, lo, true);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f(e[4]) * inv, bf2f(e[5]) * inv, hi, false);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(bf2f(e[6]) * inv, bf2f(e[7]) * inv, hi, true);
+    *(uint2*)(qr + c) = make_uint2(lo, hi);
+  }
+}
+
+__global__ __launch_bounds__(256) void dequant_rows_fp8_kernel(const unsigned char* __restrict__ q,
+                                                               long ldq,
+                                                               const float* __restrict__ scale,
+                                                               int rows, int cols,
+                                                               u16* __restrict__ x, long ldx) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float s = scale[row];
+  const unsigned char* qr = q + (long)row * ldq;
+  u16* xr = x + (long)row * ldx;
+  for (int c = lane * 8; c < cols; c += 512) {
+    const uint2 b = *(const uint2*)(qr + c);
+    uint4 out;
+    u16* o = (u16*)&out;
+    o[0] = f2bf(__builtin_amdgcn_cvt_f32_fp8(b.x, 0) * s);
+    o[1] = f2bf(__builtin_amdgcn_cvt_f32_fp8(b.x, 1) * s);
+    o[2] = f2bf(__builtin_amdgcn_cvt_f32_fp8(b.x, 2) * s);
+    o[3] = f2bf(__builtin_amdgcn_cvt_f32_fp8(b.x, 3) * s);
+    o[4] = f2bf(__builtin_amdgcn_cvt_f32_fp8(b.y, 0) * s);
+    o[5] = f2bf(__builtin_amdgcn_cvt_f32_fp8(b.y, 1) * s);
+    o[6] = f2bf(__builtin_amdgcn_cvt_f32_fp8(b.y, 2) * s);
+    o[7] = f2bf(__builtin_amdgcn_cvt_f32_fp8(b.y, 3) * s);
+    *(uint4*)(xr + c) = out;
+  }
+}
+
+int quant_rows_fp8(const uint16_t* x, long ldx, int rows, int cols, unsigned char* q, long ldq,
+                   float* scale, hipStream_t stream) {
+  if (rows <= 0 || cols <= 0 || cols % 8 || ldx < cols || ldq < cols || ldx % 8 || ldq % 8)
+    return -1;
+  if (((uintptr_t)x & 15) || ((uintptr_t)q & 7)) return -2;
+  hipLaunchKernelGGL(quant_rows_fp8_kernel, dim3((rows + 3) / 4), dim3(256), 0, stream, x, ldx,
+                     rows, cols, q, ldq, scale);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
+int dequant_rows_fp8(const unsigned char* q, long ldq, const float* scale, int rows, int cols,
+                     uint16_t* x, long ldx, hipStream_t stream) {
+  if (rows <= 0 || cols <= 0 || cols % 8 || ldx < cols || ldq < cols || ldx % 8 || ldq % 8)
+    return -1;
+  if (((uintptr_t)x & 15) || ((uintptr_t)q & 7)) return -2;
+  hipLaunchKernelGGL(dequant_rows_fp8_kernel, dim3((rows + 3) / 4), dim3(256), 0, stream, q, ldq,
+                     scale, rows, cols, x, ldx);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
 }  // namespace dnn

@@ -90,4 +90,10 @@ int transpose_multi(const TransposeJobs& jobs, hipStream_t stream);
 int transpose_bf16(const uint16_t* src, long ld_src, int rows, int cols, uint16_t* dst,
                    long ld_dst, hipStream_t stream);
 
+// fp8 (OCP e4m3) pipeline boundary: row-wise amax scaling; q [rows][ldq] bytes, scale [rows].
+int quant_rows_fp8(const uint16_t* x, long ldx, int rows, int cols, unsigned char* q, long ldq,
+                   float* scale, hipStream_t stream);
+int dequant_rows_fp8(const unsigned char* q, long ldq, const float* scale, int rows, int cols,
+                     uint16_t* x, long ldx, hipStream_t stream);
+
 }  // namespace dnn

@@ -436,6 +436,8 @@ class Stage:
         self._has_w = False
         self._o_native = False  # "O" recorded (device-side lr / step)
         self._rx = self._rl = None
+        self.boundary = "bf16"
+        self._fp8_next = self._fp8_prev = False
 
     def _logits_on_library(self, gl) -> bool:
         """The tuned table routes the logits GEMM to hipBLASLt (long contractions, where the
@@ -456,6 +458,51 @@ class Stage:
         return (ops.tail_supported(g3.kp, g3.np_, g4.np_, self.n_cls) and
                 g3.spec.activation in acts and g2.spec.activation in acts and
                 self.mb % 16 == 0)
+
+    # ---- fp8 pipeline boundary (opt-in: Trainer(boundary="fp8")) -------------------------
+    def enable_fp8_boundary(self, has_prev: bool, has_next: bool) -> None:
+        """Hops to/from neighbouring stages carry OCP e4m3 rows + one fp32 scale per row
+        (ops.quant_rows_fp8): half the bytes of bf16 on the xGMI link, for activations forward
+        and gradients backward. Buffers are step-sized like the bf16 ones."""
+        R, dev, u8 = self.rows, self.device, torch.uint8
+        self.boundary = "fp8"
+        if has_next:
+            w = self.output.shape[1]
+            self.q_out, self.s_out = torch.zeros(R, w, dtype=u8, device=dev), \
+                torch.zeros(R, device=dev)
+            self.q_gin, self.s_gin = torch.zeros(R, w, dtype=u8, device=dev), \
+                torch.zeros(R, device=dev)
+        if has_prev:
+            w = self.x_buf.shape[1]
+            self.q_in, self.s_in = torch.zeros(R, w, dtype=u8, device=dev), \
+                torch.zeros(R, device=dev)
+            self.q_dx, self.s_dx = torch.zeros(R, w, dtype=u8, device=dev), \
+                torch.zeros(R, device=dev)
+        self._fp8_next, self._fp8_prev = has_next, has_prev
+
+    def pack_fwd(self, j: int) -> None:
+        if self._prog is not None and not self._recording:
+            return self._replay(f"QF{j}")
+        r = self.rows_of(j)
+        ops.quant_rows_fp8(self.output[r], self.q_out[r], self.s_out[r])
+
+    def unpack_fwd(self, j: int) -> None:
+        if self._prog is not None and not self._recording:
+            return self._replay(f"DQF{j}")
+        r = self.rows_of(j)
+        ops.dequant_rows_fp8(self.q_in[r], self.s_in[r], self.x_in[r])
+
+    def pack_bwd(self, j: int) -> None:
+        if self._prog is not None and not self._recording:
+            return self._replay(f"QB{j}")
+        r = self.rows_of(j)
+        ops.quant_rows_fp8(self.dx_send[r], self.q_dx[r], self.s_dx[r])
+
+    def unpack_bwd(self, j: int) -> None:
+        if self._prog is not None and not self._recording:
+            return self._replay(f"DQB{j}")
+        r = self.rows_of(j)
+        ops.dequant_rows_fp8(self.q_gin[r], self.s_gin[r], self.grad_out[r])
 
     def rows_of(self, j: int) -> slice:
         if not 0 <= j < self.nm:
@@ -815,6 +862,17 @@ class Stage:
             prog.mark("OADV")
             if self.params.optim.name != "sgd":
                 ops.step_advance(self.params.step_dev)
+            for j in range(self.nm):  # fp8 boundary packs / unpacks per micro-batch
+                if self._fp8_next:
+                    prog.mark(f"QF{j}")
+                    self.pack_fwd(j)
+                    prog.mark(f"DQB{j}")
+                    self.unpack_bwd(j)
+                if self._fp8_prev:
+                    prog.mark(f"DQF{j}")
+                    self.unpack_fwd(j)
+                    prog.mark(f"QB{j}")
+                    self.pack_bwd(j)
             self._o_native = True
         finally:
             nat.record_end()

@@ -57,7 +57,7 @@ class Trainer:
                  schedule: str = "1f1b", optim: Optional[OptimConfig] = None,
                  device: Optional[torch.device] = None, seed: int = 0,
                  mesh: Optional[Mesh] = None, wgrad: Optional[str] = None,
-                 native_exec: Optional[bool] = None):
+                 native_exec: Optional[bool] = None, boundary: str = "bf16"):
         self.spec = spec
         self.mesh = mesh
         self.device = device or (torch.device("cuda", torch.cuda.current_device())
@@ -80,7 +80,13 @@ class Trainer:
                              num_micro=num_micro, device=self.device,
                              global_batch=self.global_batch, optim=self.optim, wgrad=wmode,
                              stage_index=p.stage, num_stages=pp)
+        if boundary not in ("bf16", "fp8"):
+            raise ValueError(f"boundary must be bf16 | fp8, got {boundary!r}")
+        self.boundary = boundary if (mesh is not None and pp > 1) else "bf16"
         if mesh is None:
+            if boundary == "fp8" and pp > 1:
+                raise ValueError("the fp8 boundary is a multi-rank hop format (loopback stages "
+                                 "share their buffers; there is no hop to compress)")
             if dp != 1:
                 raise ValueError("data parallelism needs a distributed mesh (one rank per GPU)")
             self.stages = [mk(p) for p in self.plans]
@@ -93,6 +99,10 @@ class Trainer:
             st = mk(self.plans[mesh.stage])
             st.params.init_default(seed)
             self.stages = [st]
+            if boundary == "fp8" and mesh.pp > 1:  # e4m3 rows + fp32 row scales on the hops
+                if switches.get("DNN_PIPE") == "ipc":
+                    raise ValueError("the fp8 boundary runs on the message transport (rccl/gloo)")
+                st.enable_fp8_boundary(mesh.prev_rank is not None, mesh.next_rank is not None)
             # DNN_PIPE=ipc: xGMI peer writes into IPC-mapped buffers instead of RCCL P2P
             use_ipc = (switches.get("DNN_PIPE") == "ipc" and
                        self.device.type == "cuda" and mesh.pp > 1)

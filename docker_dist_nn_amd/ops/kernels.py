@@ -439,6 +439,39 @@ def transpose_multi(pairs):
         native().transpose_multi(jobs[k:k + 16], _stream(pairs[0][0]))
 
 
+FP8_MAX = 448.0  # OCP e4m3 (gfx950's fp8; not the fnuz variant of MI300)
+
+
+def quant_rows_fp8(x, q, scale):
+    """Pipeline-boundary compression: q[r] = e4m3(x[r] / scale[r]), scale[r] = amax(x[r])/448.
+    x bf16 [rows][cols], q uint8 [rows][>=cols], scale fp32 [rows]."""
+    rows, cols = x.shape
+    if q.dtype != torch.uint8 or q.shape[0] < rows or q.shape[1] < cols or scale.numel() < rows:
+        raise ValueError("quant_rows_fp8: q must be uint8 [rows][>=cols], scale fp32 [>=rows]")
+    if not x.is_cuda:
+        xf = x.float()
+        amax = xf.abs().amax(1)
+        inv = torch.where(amax > 0, FP8_MAX / amax, torch.zeros_like(amax))
+        q[:rows, :cols] = (xf * inv[:, None]).to(torch.float8_e4m3fn).view(torch.uint8)
+        scale[:rows] = amax / FP8_MAX
+        return
+    _rows(x, "x", torch.bfloat16)
+    native().quant_rows_fp8(_p(x), x.stride(0), rows, cols, _p(q), q.stride(0), _p(scale),
+                            _stream(x))
+
+
+def dequant_rows_fp8(q, scale, x):
+    """Inverse of quant_rows_fp8 into bf16 x [rows][cols]."""
+    rows, cols = x.shape
+    if not x.is_cuda:
+        v = q[:rows, :cols].view(torch.float8_e4m3fn).float() * scale[:rows, None]
+        x.copy_(v.to(torch.bfloat16))
+        return
+    _rows(x, "x", torch.bfloat16)
+    native().dequant_rows_fp8(_p(q), q.stride(0), _p(scale), rows, cols, _p(x), x.stride(0),
+                              _stream(x))
+
+
 def linear_dgrad(dz, w, dx, y_prev=None, act_prev="linear", colsum=None, mask_prev=None,
                  wt=None, dxt=None):
     """dx[M][Kp] = (dz[M][Np] . w[Np][Kp]) * act_prev'(y_prev) (mask fused in the epilogue).

@@ -107,33 +107,57 @@ class DistPipe:
 
     def begin_step(self):
         m, s = self.mesh, self.stage
+        fp8 = s.boundary == "fp8"
         # post every receive of the step now, in micro-batch order, per direction channel
+        # (fp8 boundary: the e4m3 rows, then their scales -- the same order on both sides)
         if m.prev_rank is not None:
             for j in range(s.nm):
-                self._recv_f[j] = self._irecv(s.x_in[s.rows_of(j)], m.prev_rank, m.fwd_group,
-                                              ("rf", j))
+                r = s.rows_of(j)
+                bufs = (s.q_in[r], s.s_in[r]) if fp8 else (s.x_in[r],)
+                self._recv_f[j] = [self._irecv(b, m.prev_rank, m.fwd_group, ("rf", j, k))
+                                   for k, b in enumerate(bufs)]
         if m.next_rank is not None:
             for j in range(s.nm):
-                self._recv_b[j] = self._irecv(s.grad_out[s.rows_of(j)], m.next_rank,
-                                              m.bwd_group, ("rb", j))
+                r = s.rows_of(j)
+                bufs = (s.q_gin[r], s.s_gin[r]) if fp8 else (s.grad_out[r],)
+                self._recv_b[j] = [self._irecv(b, m.next_rank, m.bwd_group, ("rb", j, k))
+                                   for k, b in enumerate(bufs)]
 
     def recv_fwd(self, stage, j):
         if self.mesh.prev_rank is not None:
-            self._finish_recv(self._recv_f.pop(j))
+            for rec in self._recv_f.pop(j):
+                self._finish_recv(rec)
+            if stage.boundary == "fp8":
+                stage.unpack_fwd(j)
 
     def send_fwd(self, stage, j):
         if self.mesh.next_rank is not None:
-            self._isend(stage.output[stage.rows_of(j)], self.mesh.next_rank, self.mesh.fwd_group,
-                        ("sf", j))
+            r = stage.rows_of(j)
+            if stage.boundary == "fp8":
+                stage.pack_fwd(j)
+                bufs = (stage.q_out[r], stage.s_out[r])
+            else:
+                bufs = (stage.output[r],)
+            for k, b in enumerate(bufs):
+                self._isend(b, self.mesh.next_rank, self.mesh.fwd_group, ("sf", j, k))
 
     def recv_bwd(self, stage, j):
         if self.mesh.next_rank is not None:
-            self._finish_recv(self._recv_b.pop(j))
+            for rec in self._recv_b.pop(j):
+                self._finish_recv(rec)
+            if stage.boundary == "fp8":
+                stage.unpack_bwd(j)
 
     def send_bwd(self, stage, j):
         if self.mesh.prev_rank is not None:
-            self._isend(stage.dx_send[stage.rows_of(j)], self.mesh.prev_rank,
-                        self.mesh.bwd_group, ("sb", j))
+            r = stage.rows_of(j)
+            if stage.boundary == "fp8":
+                stage.pack_bwd(j)
+                bufs = (stage.q_dx[r], stage.s_dx[r])
+            else:
+                bufs = (stage.dx_send[r],)
+            for k, b in enumerate(bufs):
+                self._isend(b, self.mesh.prev_rank, self.mesh.bwd_group, ("sb", j, k))
 
     def end_step(self):
         for w in self._sends:

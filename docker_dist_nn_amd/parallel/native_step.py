@@ -35,7 +35,7 @@ from ..utils.native import native
 from .pipeline import dp_buckets
 
 SEG, SEND, RECV, ALLREDUCE, REDUCE_SCATTER, ALL_GATHER, COPY, SIGNAL, WAITV, REC, WAIT = range(11)
-NCCL_BF16, NCCL_F32 = 9, 7
+NCCL_BF16, NCCL_F32, NCCL_U8 = 9, 7, 1
 MAIN, FWD, BWD, DPS = 0, 1, 2, 3
 
 
@@ -105,6 +105,18 @@ class NativeStep:
 
     def _recv(self, direction: str, j: int) -> None:
         st, m = self.st, self.mesh
+        if st.boundary == "fp8":  # e4m3 rows then fp32 row scales, then unpack on compute
+            s = FWD if direction == "f" else BWD
+            peer = m.stage - 1 if direction == "f" else m.stage + 1
+            q, sc = (st.q_in, st.s_in) if direction == "f" else (st.q_gin, st.s_gin)
+            for t, dt in ((q, NCCL_U8), (sc, NCCL_F32)):
+                ptr, cnt = self._rows(t, j)
+                self.ops.append(dict(kind=RECV, stream=s,
+                                     comm=self.comm_f if s == FWD else self.comm_b,
+                                     a=ptr, count=cnt, dtype=dt, peer=peer))
+            self._edge(s, MAIN)
+            self._seg(f"DQF{j}" if direction == "f" else f"DQB{j}")
+            return
         t = st.x_in if direction == "f" else st.grad_out
         if self.transport == "ipc":  # the producer's copy + flag: wait on the compute stream
             base = self.ipc.flags.data_ptr()
@@ -120,6 +132,18 @@ class NativeStep:
 
     def _send(self, direction: str, j: int) -> None:
         st, m = self.st, self.mesh
+        if st.boundary == "fp8":
+            s = FWD if direction == "f" else BWD
+            self._seg(f"QF{j}" if direction == "f" else f"QB{j}")
+            self._edge(MAIN, s)
+            peer = m.stage + 1 if direction == "f" else m.stage - 1
+            q, sc = (st.q_out, st.s_out) if direction == "f" else (st.q_dx, st.s_dx)
+            for t, dt in ((q, NCCL_U8), (sc, NCCL_F32)):
+                ptr, cnt = self._rows(t, j)
+                self.ops.append(dict(kind=SEND, stream=s,
+                                     comm=self.comm_f if s == FWD else self.comm_b,
+                                     a=ptr, count=cnt, dtype=dt, peer=peer))
+            return
         t = st.output if direction == "f" else st.dx_send
         s = FWD if direction == "f" else BWD
         self._edge(MAIN, s)

@@ -565,3 +565,33 @@ def test_transpose_multi(dev):
     ops.transpose_multi(list(zip(srcs, dsts)))
     for s_, d_ in zip(srcs, dsts):
         assert torch.equal(d_, s_.t())
+
+
+@pytest.mark.parametrize("rows,cols", [(1, 64), (300, 512), (64, 1024), (33, 136)])
+def test_fp8_boundary_kernels_match_reference(dev, rows, cols):
+    """gfx950 e4m3 row quantisation (v_cvt_pk_fp8_f32, OCP encoding) vs torch float8_e4m3fn:
+    identical scales; codes identical except rare one-step rounding ties (the hardware and
+    torch's software conversion may break exact ties / subnormal rounding differently), so
+    the dequantised values agree within one e4m3 step."""
+    gen = torch.Generator().manual_seed(rows * cols)
+    x = (torch.randn(rows, cols, generator=gen) * 3).to(torch.bfloat16)
+    if rows > 2:
+        x[1] = 0
+    q_c, s_c = torch.empty(rows, cols, dtype=torch.uint8), torch.empty(rows)
+    ops.quant_rows_fp8(x, q_c, s_c)
+    xd = x.to(dev)
+    q_g = torch.empty(rows, cols, dtype=torch.uint8, device=dev)
+    s_g = torch.empty(rows, device=dev)
+    ops.quant_rows_fp8(xd, q_g, s_g)
+    assert torch.equal(s_g.cpu(), s_c)
+    assert (q_g.cpu() != q_c).float().mean() < 2e-3
+    y_c, y_g = torch.empty_like(x), torch.empty_like(xd)
+    ops.dequant_rows_fp8(q_c, s_c, y_c)
+    ops.dequant_rows_fp8(q_g, s_g, y_g)
+    yc, yg = y_c.float(), y_g.cpu().float()
+    amax = x.float().abs().amax(1, keepdim=True)
+    assert torch.all((yg - yc).abs() <= 0.125 * yc.abs() + amax * 2.0 ** -9 / 448 * 2 + 1e-6)
+    # and the GPU dequantiser itself is exact on the same codes
+    y_g2 = torch.empty_like(xd)
+    ops.dequant_rows_fp8(q_c.to(dev), s_c.to(dev), y_g2)
+    assert torch.equal(y_g2.cpu(), y_c)
