@@ -86,7 +86,7 @@ def parse_args(argv=None):
 
 
 def _plan(a, spec, n, world, text):
-    planner = Planner()
+    planner = Planner.calibrated(spec)
     loopback = world == 1
     pp, dp = parse_parallelism(text, n, loopback=loopback)
     if pp is None:

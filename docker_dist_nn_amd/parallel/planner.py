@@ -64,6 +64,15 @@ def compositions(n: int, k: int):
         yield [b[i + 1] - b[i] for i in range(k)]
 
 
+# Measured one-GPU training steps on MI355X with the round-2 own-kernel table
+# (profiles/r2_check, profiles/r2_own_kernels): widths -> (rows, ms per step).
+MEASURED_STEP_MS = {
+    (784, 512, 256, 128, 10): (65536, 0.373),
+    (784, 1024, 1024, 1024, 1024, 1024, 1024, 1024, 10): (65536, 3.418),
+    (784, 8192, 8192, 10): (16384, 6.716),
+}
+
+
 class Planner:
     # Calibrated on MI355X (one GPU, own kernels, profiles/r2_own_kernels): headline step 0.36 ms
     # at 65536 rows = ~470 executed TFLOP/s; 784-1024x7-10 ~600; 784-8192-8192-10 ~880. The
@@ -77,6 +86,16 @@ class Planner:
         self.ar = allreduce_gbps * 1e9
         self.ovh = step_overhead_us * 1e-6
         self.bb = boundary_bytes  # bytes per boundary element on the wire (bf16 = 2)
+
+    @classmethod
+    def calibrated(cls, spec: MLPSpec, **kw) -> "Planner":
+        """A planner whose compute rate is this model's MEASURED one-GPU step rate (executed
+        FLOPs / step time), when one is on record; else the default rate."""
+        m = MEASURED_STEP_MS.get(tuple(spec.widths))
+        if m is not None and "tflops" not in kw:
+            rows, ms = m
+            kw["tflops"] = sum(layer_train_flops(spec)) * rows / (ms * 1e-3) / 1e12
+        return cls(**kw)
 
     def _stage_costs(self, spec: MLPSpec, dist: list[int], mb: int):
         fl = layer_train_flops(spec)
