@@ -327,13 +327,15 @@ __device__ __forceinline__ void epilogue_staged(const GemmParams& p,
   float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
   for (int chunk = 0; chunk < C::CHUNKS; ++chunk) {
-    if (chunk) __syncthreads();  // previous chunk's stores have read the staging tile
+    // Epilogue barriers are LDS-only (lds_barrier): __syncthreads' release fence would wait
+    // for every global store of the previous chunk (vmcnt(0)), serialising the chunks.
+    if (chunk) lds_barrier();  // every thread has read the previous chunk's staging tile
     acc_to_lds<C>(acc, cs, chunk, wave, lane);
-    __syncthreads();
+    lds_barrier();
     if constexpr (!OUT_F32 && C::NW == 4 && C::CHUNKS == 1) {
       if (xent) {  // fused softmax-CE, one thread per row of the tile
         xent_rows<C>(p, cs, m0);
-        __syncthreads();
+        lds_barrier();
       }
     }
     const long gm0 = m0 + chunk * C::EPI_ROWS + crow;
@@ -417,25 +419,32 @@ __device__ __forceinline__ void epilogue_staged(const GemmParams& p,
     }
     if constexpr (!OUT_F32) {
       if (p.ct) {  // uniform: transposed copy of this chunk through LDS (bf16 [BN][rows])
-        constexpr int TLD = C::EPI_ROWS + 8;  // +16 B per row: spread the 2-byte writes
+        // bf16 [BN][TLD] transposed tile. The 8-row block of a row index is XOR-swizzled by
+        // the column's 8-column group (sw): together with the +8 pad, the 2-byte writes of a
+        // half-wave (32 column groups, one row) spread over 16 banks instead of 2, and every
+        // 8-row block stays a contiguous, aligned 16-byte read.
+        constexpr int TLD = C::EPI_ROWS + 8;
+        constexpr int RC = C::EPI_ROWS / 8;  // 16-byte chunks per transposed row
         static_assert(BN * TLD * 2 <= C::SMEM, "transposed chunk fits the staging LDS");
+        static_assert((RC & (RC - 1)) == 0, "row blocks: power of two");
         u16 LDS_AS* tt = (u16 LDS_AS*)lds;
-        __syncthreads();  // every thread is done reading the fp32 staging tile
+        lds_barrier();  // every thread is done reading the fp32 staging tile
+        const int sw = ((ccol >> 3) & (RC - 1)) << 3;
 #pragma unroll
         for (int it = 0; it < ITER; ++it) {
-          const int row = crow + it * RSTEP;
+          const int row = (crow + it * RSTEP) ^ sw;
 #pragma unroll
           for (int e = 0; e < 8; ++e) tt[(ccol + e) * TLD + row] = (u16)ov[it][e];
         }
-        __syncthreads();
-        constexpr int RC = C::EPI_ROWS / 8;  // 16-byte chunks per transposed row
+        lds_barrier();
         const long m_base = m0 + chunk * C::EPI_ROWS;
 #pragma unroll 2
         for (int idx = threadIdx.x; idx < BN * RC; idx += NT) {
           const int col = idx / RC, r8 = (idx % RC) * 8;
           const long gcol = n0 + col, grow = m_base + r8;
           if (gcol >= p.N || grow >= p.M) continue;  // partial edge tile
-          const bf16x8_t v = *(const bf16x8_t LDS_AS*)(tt + col * TLD + r8);
+          const int rs = r8 ^ (((col >> 3) & (RC - 1)) << 3);
+          const bf16x8_t v = *(const bf16x8_t LDS_AS*)(tt + col * TLD + rs);
           *(bf16x8_t*)(p.ct + gcol * p.ld_ct + grow) = v;
         }
       }
@@ -443,11 +452,11 @@ __device__ __forceinline__ void epilogue_staged(const GemmParams& p,
   }
   if constexpr (!OUT_F32) {
     if (p.colsum) {  // uniform across the block
-      __syncthreads();  // all reads of the staging tile are done
+      lds_barrier();  // all reads of the staging tile are done
       f32x4_t LDS_AS* red = (f32x4_t LDS_AS*)lds;
       red[2 * threadIdx.x] = f32x4_t{csum[0], csum[1], csum[2], csum[3]};
       red[2 * threadIdx.x + 1] = f32x4_t{csum[4], csum[5], csum[6], csum[7]};
-      __syncthreads();
+      lds_barrier();
       if ((int)threadIdx.x < BN) {
         const int col = threadIdx.x, cc = col >> 3, e = col & 7;
         const float LDS_AS* rf = (const float LDS_AS*)lds;
