@@ -325,6 +325,18 @@ __device__ __forceinline__ void epilogue_staged(const GemmParams& p,
     }
   }
   float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  // Activation rows of the dgrad's act' (aux) are read one chunk AHEAD: chunk c+1's loads are
+  // in flight while chunk c is stored, so only chunk 0's round trip is exposed.
+  [[maybe_unused]] bf16x8_t yv[ITER], yn[ITER];
+  const bool aux_rows = !OUT_F32 && p.aux && !xent;  // uniform
+  auto load_aux = [&](int ch, bf16x8_t (&dst)[ITER]) {
+    const long r0 = m0 + ch * C::EPI_ROWS + crow;
+#pragma unroll
+    for (int it = 0; it < ITER; ++it)
+      if (col_ok && r0 + it * RSTEP < p.M)
+        dst[it] = *(const bf16x8_t*)(p.aux + (r0 + it * RSTEP) * p.ld_aux + gn);
+  };
+  if (aux_rows) load_aux(0, yv);
 #pragma unroll 1
   for (int chunk = 0; chunk < C::CHUNKS; ++chunk) {
     // Epilogue barriers are LDS-only (lds_barrier): __syncthreads' release fence would wait
@@ -340,7 +352,6 @@ __device__ __forceinline__ void epilogue_staged(const GemmParams& p,
     }
     const long gm0 = m0 + chunk * C::EPI_ROWS + crow;
     [[maybe_unused]] bf16x8_t ov[ITER];  // the stored values, for the transposed copy
-    [[maybe_unused]] bf16x8_t yv[ITER];
     [[maybe_unused]] unsigned mk[ITER];
     [[maybe_unused]] f32x4_t cp0[ITER], cp1[ITER];
     if constexpr (OUT_F32) {
@@ -355,11 +366,8 @@ __device__ __forceinline__ void epilogue_staged(const GemmParams& p,
         }
       }
     } else {
-      if (p.aux && !xent) {
-#pragma unroll
-        for (int it = 0; it < ITER; ++it)
-          if (col_ok && gm0 + it * RSTEP < p.M)
-            yv[it] = *(const bf16x8_t*)(p.aux + (gm0 + it * RSTEP) * p.ld_aux + gn);
+      if (aux_rows) {
+        if (chunk + 1 < C::CHUNKS) load_aux(chunk + 1, yn);
       } else if (p.mask_in) {
 #pragma unroll
         for (int it = 0; it < ITER; ++it)
@@ -448,6 +456,10 @@ __device__ __forceinline__ void epilogue_staged(const GemmParams& p,
           *(bf16x8_t*)(p.ct + gcol * p.ld_ct + grow) = v;
         }
       }
+    }
+    if (aux_rows) {
+#pragma unroll
+      for (int it = 0; it < ITER; ++it) yv[it] = yn[it];
     }
   }
   if constexpr (!OUT_F32) {
