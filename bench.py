@@ -79,6 +79,9 @@ def parse_args(argv=None):
     ap.add_argument("--boundary", default="bf16", choices=["bf16", "fp8"],
                     help="pipeline hop format: bf16 (default) or e4m3 rows + fp32 row scales "
                          "(half the xGMI bytes; opt-in, reduced-precision hops)")
+    ap.add_argument("--dp-reduce", default="shard", choices=["allreduce", "shard"],
+                    help="data-parallel gradient exchange: bf16 reduce-scatter + sharded "
+                         "optimizer + bf16 all-gather (default) or fp32 all-reduce")
     ap.add_argument("--no-dp-compare", action="store_true",
                     help="N > 1: skip the data-parallel-only comparison run")
     ap.add_argument("--seed", type=int, default=0)
@@ -121,7 +124,8 @@ def measure(a, spec, n, world, dev, text):
     tr = Trainer(spec, micro_batch=mb, num_micro=nm, distribution=plan.distribution,
                  pp=plan.pp, dp=plan.dp, schedule=a.schedule,
                  optim=OptimConfig(name=a.optimizer, lr=a.lr),
-                 device=dev, seed=a.seed, mesh=mesh, boundary=a.boundary)
+                 device=dev, seed=a.seed, mesh=mesh, boundary=a.boundary,
+                 dp_reduce=a.dp_reduce)
     replica = mesh.replica if mesh else 0
     x, y = synthetic_mnist(max(60000, 2 * rows), seed=a.seed + 1000 * replica)
     data = DeviceDataset(x, y, rows, dev, kp=tr.stages[0].x_in.shape[1] if tr.first else None)
@@ -172,7 +176,7 @@ def measure(a, spec, n, world, dev, text):
         "layer_distribution": plan.distribution, "micro_batch": mb, "num_micro": nm,
         "schedule": a.schedule if plan.pp > 1 else "none",
         "transport": tr.transport, "native_step": tr.native_step is not None or world == 1,
-        "boundary": tr.boundary,
+        "boundary": tr.boundary, "dp_reduce": tr.dp_reduce if plan.dp > 1 else None,
         "hip_graph": use_graph, "graph_copies": a.graph_copies if use_graph else 0,
         "loss": loss, "planner_predicted": round(plan.samples_per_s, 1),
     }
@@ -205,7 +209,7 @@ def main(argv=None):
     if world > 1 and not a.no_dp_compare and not m["parallelism"].startswith("dp"):
         d = measure(a, spec, n, world, dev, f"dp{n}")
         dp_only = {k: d[k] for k in ("value", "ms_per_step", "parallelism", "global_batch",
-                                     "transport", "native_step")}
+                                     "transport", "native_step", "dp_reduce")}
     out = {
         "metric": METRIC,
         "value": m["value"],
@@ -224,8 +228,8 @@ def main(argv=None):
             "global_batch": m["global_batch"],
             "seq_len": None,
             **{k: m[k] for k in ("parallelism", "layer_distribution", "micro_batch", "num_micro",
-                                 "schedule", "transport", "native_step", "boundary", "hip_graph",
-                                 "graph_copies")},
+                                 "schedule", "transport", "native_step", "boundary",
+                                 "dp_reduce", "hip_graph", "graph_copies")},
             "optimizer": a.optimizer,
         },
         # EXECUTED FLOPs (no dgrad of the first layer: models/mlp.py)

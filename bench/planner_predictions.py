@@ -1,0 +1,38 @@
+"""Planner predictions for every BASELINE config at N = 1, 2, 4, 8 GPUs (weak scaling):
+the pipeline layout bench.py runs (bf16 and fp8 hops) and the data-parallel-only layout.
+
+    python bench/planner_predictions.py > profiles/r2_planner/predictions.jsonl
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from docker_dist_nn_amd.models.mlp import NAMED_MODELS  # noqa: E402
+from docker_dist_nn_amd.parallel.planner import Planner  # noqa: E402
+
+FP8_BYTES = 1.0 + 4.0 / 64  # e4m3 element + one fp32 scale per row (>= 64 elements)
+
+
+def main():
+    for model, rows in (("mnist-fcnn", 65536), ("mlp8", 65536), ("wide", 16384)):
+        spec = NAMED_MODELS[model]
+        pl = Planner.calibrated(spec)
+        p8 = Planner.calibrated(spec, boundary_bytes=FP8_BYTES)
+        for n in (1, 2, 4, 8):
+            a = pl.pipeline_layout(spec, n, rows)
+            b = p8.evaluate(spec, a.pp, a.dp, rows * a.pp, distribution=a.distribution)
+            d = pl.evaluate(spec, 1, n, rows)
+            print(json.dumps({"model": model, "n": n, "layout": a.parallelism,
+                              "dist": a.distribution, "nm": a.num_micro,
+                              "pipe_bf16_Msps": round(a.samples_per_s / 1e6, 1),
+                              "pipe_fp8_Msps": round(b.samples_per_s / 1e6, 1),
+                              "dp_only_Msps": round(d.samples_per_s / 1e6, 1),
+                              "dp_allreduce_ms": d.detail["allreduce_ms"]}))
+
+
+if __name__ == "__main__":
+    main()

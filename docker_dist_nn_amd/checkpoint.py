@@ -117,6 +117,9 @@ def save_trainer(d: str, trainer, step: int, *, barrier: Optional[Callable[[], N
     ``barrier`` (all ranks must call this; ``is_writer`` False on DP replicas > 0, which only
     take part in the barrier)."""
     trainer.flush()  # deferred DP update of the last step
+    gather = getattr(trainer, "gather_sharded", None)
+    if gather is not None:  # sharded DP: every rank (collective) makes master / state whole
+        gather()
     if is_writer:
         for st in trainer.stages:
             save_stage(d, st, step, trainer.spec, trainer.distribution)

@@ -143,6 +143,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--watchdog", type=float, default=None,
                     help="seconds without step progress before the rank dumps its stacks and "
                          "exits (default: 300 for multi-rank jobs, off for one process; 0 = off)")
+    ap.add_argument("--dp-reduce", default="allreduce", choices=["allreduce", "shard"],
+                    help="data-parallel gradients: fp32 all-reduce + replicated optimizer, or "
+                         "bf16 reduce-scatter + sharded optimizer + bf16 weight all-gather")
     ap.add_argument("--check-every", type=int, default=20,
                     help="steps between loss finiteness / RCCL async-error checks")
     return ap
@@ -187,7 +190,7 @@ def main(argv: Optional[list[str]] = None) -> int:
     tr = Trainer(spec, micro_batch=a.micro_batch, num_micro=a.num_micro_batches, pp=pp, dp=dp,
                  distribution=dist_, schedule=a.schedule, mesh=mesh, device=dev, seed=a.seed,
                  optim=OptimConfig(name=a.optimizer, lr=a.lr, momentum=a.momentum,
-                                   weight_decay=a.weight_decay))
+                                   weight_decay=a.weight_decay), dp_reduce=a.dp_reduce)
     start_step = 0
     if a.resume and a.checkpoint_dir and os.path.exists(os.path.join(a.checkpoint_dir, "meta.json")):
         # any layout: weights AND optimizer state are stored per layer (re-partition is exact)

@@ -51,21 +51,42 @@ class StageParams:
     """Flat parameter / gradient / optimizer buffers of a stage's layers."""
 
     def __init__(self, geoms: Sequence[LayerGeom], device: torch.device,
-                 optim: Optional[OptimConfig] = None):
+                 optim: Optional[OptimConfig] = None, shard: Optional[tuple[int, int]] = None):
         self.geoms = list(geoms)
         self.device = device
         self.optim = optim or OptimConfig()
+        # sharded data parallelism (shard = (dp, dp_rank), see shard_piece): every layer's
+        # region ends on a multiple of dp * _ALIGN, so any bucket of whole layers splits into
+        # dp equal, aligned pieces
+        self.sharded = shard is not None
+        self.dp, self.dp_rank = shard or (1, 0)
         off = 0
         self.w_off, self.b_off = [], []
-        for g in self.geoms:
-            self.w_off.append(off)
-            off = round_up(off + g.np_ * g.kp, _ALIGN)
-            self.b_off.append(off)
-            off = round_up(off + g.np_, _ALIGN)
+        if self.sharded:
+            # weights first, each padded to dp pieces; then every bias (replicated update)
+            for g in self.geoms:
+                self.w_off.append(off)
+                off = round_up(off + g.np_ * g.kp, _ALIGN * self.dp)
+            self.bias_lo = off
+            for g in self.geoms:
+                self.b_off.append(off)
+                off = round_up(off + g.np_, _ALIGN)
+        else:
+            for g in self.geoms:
+                self.w_off.append(off)
+                off = round_up(off + g.np_ * g.kp, _ALIGN)
+                self.b_off.append(off)
+                off = round_up(off + g.np_, _ALIGN)
         self.numel = off
         self.master = torch.zeros(off, dtype=torch.float32, device=device)
         self.shadow = torch.zeros(off, dtype=torch.bfloat16, device=device)
         self.grad = torch.zeros(off, dtype=torch.float32, device=device)
+        if self.sharded:
+            # bf16 gradient (reduce-scatter input) and the reduced pieces this rank owns: the
+            # piece of bucket [e0, e1) lives at [e0 / dp, e1 / dp) of grad_piece
+            self.grad16 = torch.zeros(off, dtype=torch.bfloat16, device=device)
+            self.grad_piece = torch.zeros(off // self.dp, dtype=torch.bfloat16, device=device)
+            self.shard_buckets: list[tuple[int, int]] = []
         self.state: list[torch.Tensor] = []
         self.step_count = 0
         # transposed bf16 weight shadows W^T[Kp][Np] of the layers whose dgrad reads them
@@ -102,7 +123,11 @@ class StageParams:
         return self.grad[self.b_off[i]:self.b_off[i] + self.geoms[i].np_]
 
     def layer_grad_range(self, i) -> tuple[int, int]:
-        """Flat [start, end) of layer i's W and b gradients (a DP all-reduce bucket)."""
+        """Flat [start, end) of layer i's W and b gradients (a DP all-reduce bucket). Sharded
+        layout: layer i's WEIGHTS only (the biases live together at [bias_lo, numel))."""
+        if self.sharded:
+            return self.w_off[i], (self.w_off[i + 1] if i + 1 < len(self.geoms)
+                                   else self.bias_lo)
         end = self.w_off[i + 1] if i + 1 < len(self.geoms) else self.numel
         return self.w_off[i], end
 
@@ -222,10 +247,11 @@ class StageParams:
             ops.step_advance(self.step_dev)
         self.refresh_t()
 
-    def record_update_range(self, a: int, b: int, advance: bool) -> None:
+    def record_update_range(self, a: int, b: int, advance: bool, refresh: bool = True) -> None:
         """record_update over the flat element range [a, b) only (a DP bucket of whole layers);
         the device step counter advances only when ``advance`` (once per step: the last range
-        of a split update)."""
+        of a split update). ``refresh=False``: leave W^T alone (a shard piece, whose layers are
+        complete only after the all-gather)."""
         self._device_scalars()
         o = self.optim
         sl = slice(a, b)
@@ -241,16 +267,53 @@ class StageParams:
                             step_dev=self.step_dev)
         if advance and o.name != "sgd":
             ops.step_advance(self.step_dev)
-        self.refresh_t(*self._layers_of(a, b))
+        if refresh:
+            self.refresh_t(*self._layers_of(a, b))
 
-    def update_range(self, a: int, b: int, lr: Optional[float], advance: bool) -> None:
+    # sharded data parallelism --------------------------------------------------------------
+    # Per bucket [e0, e1) of whole layers' WEIGHTS: the fp32 gradient is cast to bf16
+    # (shard_pack), reduce-scattered over the DP group (rank r receives the sum of piece r),
+    # cast back into grad[piece] (shard_unpack) and only that piece is updated (fp32 master +
+    # optimizer state of the piece are authoritative on this rank); the bf16 shadow is then
+    # all-gathered and W^T refreshed. The biases (fp32 in the GEMM epilogues, a few KB) are
+    # all-reduced in fp32 and updated on every rank. Bytes on the wire: 2 x (dp-1)/dp x 2 B per
+    # weight, half of an fp32 all-reduce, and the optimizer touches 1/dp of the weights.
+    def shard_piece(self, e0: int, e1: int) -> tuple[int, int]:
+        c = (e1 - e0) // self.dp
+        if c * self.dp != e1 - e0:
+            raise ValueError("bucket length is not a multiple of the DP degree")
+        return e0 + self.dp_rank * c, e0 + (self.dp_rank + 1) * c
+
+    def shard_pack(self, e0: int, e1: int) -> None:
+        ops.pack_bf16(self.grad[e0:e1].view(1, -1), self.grad16[e0:e1].view(1, -1))
+
+    def shard_unpack(self, e0: int, e1: int) -> None:
+        p0, p1 = self.shard_piece(e0, e1)
+        d = self.dp
+        ops.unpack_bf16(self.grad_piece[e0 // d:e1 // d].view(1, -1),
+                        self.grad[p0:p1].view(1, -1))
+
+    def gather_full(self, group) -> None:
+        """All-gather the fp32 master and optimizer state over the DP group: afterwards every
+        rank holds the whole (checkpoint / export); a no-op without sharding."""
+        if not self.sharded or not self.shard_buckets:
+            return
+        import torch.distributed as dist
+
+        for buf in [self.master] + list(self.state):
+            for e0, e1 in self.shard_buckets:
+                p0, p1 = self.shard_piece(e0, e1)
+                dist.all_gather_into_tensor(buf[e0:e1], buf[p0:p1].clone(), group=group)
+
+    def update_range(self, a: int, b: int, lr: Optional[float], advance: bool,
+                     refresh: bool = True) -> None:
         """Optimizer update of the flat range [a, b) (see record_update_range); the host step
         counter counts whole steps (advance=True)."""
         o = self.optim
         lr = o.lr if lr is None else lr
         if self.device.type == "cuda":
             self.set_lr(lr)
-            self.record_update_range(a, b, advance)
+            self.record_update_range(a, b, advance, refresh)
         else:
             sl = slice(a, b)
             step = self.step_count + 1
@@ -263,12 +326,15 @@ class StageParams:
                                 self.state[1][sl], self.shadow[sl], lr=lr, betas=o.betas,
                                 eps=o.eps, weight_decay=o.weight_decay,
                                 decoupled=o.decoupled or o.name == "adamw", step=step)
-            self.refresh_t(*self._layers_of(a, b))
+            if refresh:
+                self.refresh_t(*self._layers_of(a, b))
         if advance:
             self.step_count += 1
 
     def layers_range(self, a: int, b: int) -> tuple[int, int]:
         """Flat [start, end) of layers a..b-1 (weights, biases and alignment padding)."""
+        if self.sharded:
+            raise ValueError("sharded layout: layer ranges are not contiguous")
         return self.w_off[a], (self.w_off[b] if b < len(self.geoms) else self.numel)
 
     def optimizer_step(self, lr: Optional[float] = None) -> None:
@@ -299,7 +365,8 @@ class Stage:
     def __init__(self, spec: MLPSpec, layer_start: int, layer_end: int, *, micro_batch: int,
                  num_micro: int, device: torch.device, global_batch: Optional[int] = None,
                  optim: Optional[OptimConfig] = None, wgrad: str = "batched",
-                 stage_index: int = 0, num_stages: int = 1, wgrad_algo: Optional[str] = None):
+                 stage_index: int = 0, num_stages: int = 1, wgrad_algo: Optional[str] = None,
+                 dp_shard: Optional[tuple[int, int]] = None):
         if not 0 <= layer_start < layer_end <= len(spec.layers):
             raise ValueError("bad layer range")
         if micro_batch <= 0 or micro_batch % 64:
@@ -319,7 +386,7 @@ class Stage:
         if self.wgrad_algo not in ("streamk", "splitk"):
             raise ValueError(f"wgrad_algo must be streamk | splitk, got {self.wgrad_algo!r}")
         self.geoms = [LayerGeom(i, spec.layers[i]) for i in range(layer_start, layer_end)]
-        self.params = StageParams(self.geoms, device, optim)
+        self.params = StageParams(self.geoms, device, optim, shard=dp_shard)
         self.prev_act = spec.layers[layer_start - 1].activation if not self.first else "linear"
         self.n_cls = spec.out_dim
         self._alloc()
@@ -761,6 +828,19 @@ class Stage:
             self.wgrad_layer(i)
         self.finalize_grads(sorted(ls))
 
+    def shard_update(self, e0: int, e1: int, lr: Optional[float] = None) -> None:
+        """Sharded DP: unpack this rank's reduced piece of bucket [e0, e1) and update it (no
+        step advance, no W^T refresh: both follow once per step)."""
+        p = self.params
+        p.shard_unpack(e0, e1)
+        p0, p1 = p.shard_piece(e0, e1)
+        p.update_range(p0, p1, lr, advance=False, refresh=False)
+
+    def bias_update(self, lr: Optional[float] = None) -> None:
+        """Sharded DP: every rank updates all biases (their fp32 gradients are all-reduced)."""
+        p = self.params
+        p.update_range(p.bias_lo, p.numel, lr, advance=False, refresh=False)
+
     def update_layers(self, a: int, b: int, lr: Optional[float] = None,
                       advance: bool = True) -> None:
         """Optimizer update of local layers [a, b) only (``advance``: this completes the
@@ -854,7 +934,8 @@ class Stage:
                 self._record_fin_sgd()
             prog.mark("O")
             self.params.record_update()
-            for a in range(L):  # split updates: every contiguous layer range, no step advance
+            for a in range(L if not self.params.sharded else 0):
+                # split updates: every contiguous layer range, no step advance
                 for b in range(a + 1, L + 1):
                     prog.mark(f"O{a}-{b}")
                     e0, e1 = self.params.layers_range(a, b)
@@ -862,6 +943,20 @@ class Stage:
             prog.mark("OADV")
             if self.params.optim.name != "sgd":
                 ops.step_advance(self.params.step_dev)
+            if self.params.sharded:  # sharded DP: per bucket pack / unpack + piece update
+                p = self.params
+                for a in range(L):
+                    for b in range(a, L):
+                        e0, _ = p.layer_grad_range(a)
+                        _, e1 = p.layer_grad_range(b)
+                        prog.mark(f"SP{a}-{b}")
+                        p.shard_pack(e0, e1)
+                        prog.mark(f"SU{a}-{b}")
+                        self.shard_update(e0, e1)
+                prog.mark("SB")
+                self.bias_update()
+                prog.mark("T")
+                p.refresh_t()
             for j in range(self.nm):  # fp8 boundary packs / unpacks per micro-batch
                 if self._fp8_next:
                     prog.mark(f"QF{j}")

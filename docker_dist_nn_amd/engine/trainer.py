@@ -57,7 +57,8 @@ class Trainer:
                  schedule: str = "1f1b", optim: Optional[OptimConfig] = None,
                  device: Optional[torch.device] = None, seed: int = 0,
                  mesh: Optional[Mesh] = None, wgrad: Optional[str] = None,
-                 native_exec: Optional[bool] = None, boundary: str = "bf16"):
+                 native_exec: Optional[bool] = None, boundary: str = "bf16",
+                 dp_reduce: str = "allreduce"):
         self.spec = spec
         self.mesh = mesh
         self.device = device or (torch.device("cuda", torch.cuda.current_device())
@@ -76,10 +77,20 @@ class Trainer:
         self.global_batch = micro_batch * num_micro * dp
         self.optim = optim or OptimConfig()
         wmode = wgrad or ("per_micro" if schedule in ("1f1b_w", "zb") else "batched")
+        # data-parallel gradient exchange: "allreduce" (fp32 all-reduce, replicated optimizer)
+        # or "shard" (bf16 reduce-scatter -> optimizer on this rank's 1/dp piece -> bf16
+        # all-gather of the weights; pipeline.GradSync)
+        if dp_reduce not in ("allreduce", "shard"):
+            raise ValueError(f"dp_reduce must be allreduce | shard, got {dp_reduce!r}")
+        # (a DP group of one rank -- mesh.dp_group set with dp == 1 -- runs the sharded path
+        # with one piece per bucket: the single-GPU check of its native plan)
+        self.dp_reduce = dp_reduce if (mesh is not None and mesh.dp_group is not None) \
+            else "allreduce"
+        shard = (mesh.dp, mesh.replica) if self.dp_reduce == "shard" else None
         mk = lambda p: Stage(spec, p.layer_start, p.layer_end, micro_batch=micro_batch,
                              num_micro=num_micro, device=self.device,
                              global_batch=self.global_batch, optim=self.optim, wgrad=wmode,
-                             stage_index=p.stage, num_stages=pp)
+                             stage_index=p.stage, num_stages=pp, dp_shard=shard)
         if boundary not in ("bf16", "fp8"):
             raise ValueError(f"boundary must be bf16 | fp8, got {boundary!r}")
         self.boundary = boundary if (mesh is not None and pp > 1) else "bf16"
@@ -108,7 +119,8 @@ class Trainer:
                        self.device.type == "cuda" and mesh.pp > 1)
             self.pipe = IpcPipe(mesh, st) if use_ipc else DistPipe(mesh, st)
             ids = [mesh.stage]
-            sync = GradSync(mesh.dp_group, mesh.dp) if mesh.dp > 1 else None
+            sync = (GradSync(mesh.dp_group, mesh.dp, shard=self.dp_reduce == "shard")
+                    if mesh.dp > 1 or self.dp_reduce == "shard" else None)
         self.executor = PipelineExecutor(self.stages, self.pipe, schedule, pp, ids, sync)
         # native step executor: record each stage's launches once, replay from C++ (after the
         # pipe has aliased loopback buffers, so the recorded pointers are the final ones)
@@ -256,8 +268,16 @@ class Trainer:
         before reading weights or ending a timed region; training steps need not."""
         self.executor.flush()
 
+    def gather_sharded(self) -> None:
+        """Sharded DP: make the fp32 master weights and optimizer state whole on every rank
+        (each rank updates only its pieces); before export / checkpoint."""
+        if self.dp_reduce == "shard":
+            for st in self.stages:
+                st.params.gather_full(self.mesh.dp_group)
+
     def local_weights(self) -> dict[int, tuple[np.ndarray, np.ndarray]]:
         self.flush()
+        self.gather_sharded()
         out = {}
         for st in self.stages:
             ws, bs = st.params.export()

@@ -69,13 +69,14 @@ class NativeStep:
         self.n = native()
         dev = st.device
         self.dp = mesh.dp if mesh is not None else 1
-        if transport == "rccl" or self.dp > 1:
+        self.sharded = st.params.sharded
+        if transport == "rccl" or self.dp > 1 or self.sharded:
             self.n.nccl_load(torch_rccl_path())
         self.comm_f = self.comm_b = self.comm_dp = 0
         if transport == "rccl" and mesh.pp > 1:
             self.comm_f = comm_ptr(mesh.fwd_group, dev)
             self.comm_b = comm_ptr(mesh.bwd_group, dev)
-        if self.dp > 1:
+        if self.dp > 1 or self.sharded:
             self.comm_dp = comm_ptr(mesh.dp_group, dev)
         self._ev = 0
         self.ops: list[tuple] = []
@@ -172,7 +173,7 @@ class NativeStep:
     def _wgrad_update(self) -> None:
         st = self.st
         segs = st._prog.segments()
-        if self.dp <= 1:
+        if self.dp <= 1 and not self.sharded:
             self._seg("W")
             if "FINO" in segs:
                 self._seg("FINO")
@@ -181,6 +182,9 @@ class NativeStep:
                 self._seg("O")
             return
         p = st.params
+        if self.sharded:
+            self._sharded_update()
+            return
         for bucket in dp_buckets(st):
             for i in bucket:
                 self._seg(f"W{i}")
@@ -193,6 +197,49 @@ class NativeStep:
                                  a=p.grad.data_ptr() + 4 * e0, count=e1 - e0, dtype=NCCL_F32))
         self._edge(DPS, MAIN)
         self._seg("O")
+
+    def _sharded_update(self) -> None:
+        """Sharded DP (pipeline.GradSync shard): per bucket, W segments -> FIN -> bf16 pack on
+        the compute stream, then the bucket's bf16 reduce-scatter on the DP stream (overlapping
+        the next bucket's wgrads). Per bucket again: unpack + update of this rank's piece, then
+        the bf16 all-gather of the piece's shadow weights; the W^T refresh waits for all."""
+        st = self.st
+        p = st.params
+        buckets = []
+        for bucket in dp_buckets(st):
+            a, b = bucket[0], bucket[-1]
+            e0, _ = p.layer_grad_range(a)
+            _, e1 = p.layer_grad_range(b)
+            buckets.append((a, b, e0, e1))
+        p.shard_buckets = [(e0, e1) for _, _, e0, e1 in buckets]
+        d = p.dp
+        for (a, b, e0, e1), bucket in zip(buckets, dp_buckets(st)):
+            for i in bucket:
+                self._seg(f"W{i}")
+            self._seg(f"FIN{a}" if a == b else f"FIN{a}-{b}")
+            self._seg(f"SP{a}-{b}")
+            self._edge(MAIN, DPS)
+            self.ops.append(dict(kind=REDUCE_SCATTER, stream=DPS, comm=self.comm_dp,
+                                 a=p.grad16.data_ptr() + 2 * e0,
+                                 b=p.grad_piece.data_ptr() + 2 * (e0 // d),
+                                 count=(e1 - e0) // d, dtype=NCCL_BF16))
+        # every bias gradient (fp32, a few KB): all-reduced, then updated on every rank
+        self.ops.append(dict(kind=ALLREDUCE, stream=DPS, comm=self.comm_dp,
+                             a=p.grad.data_ptr() + 4 * p.bias_lo, count=p.numel - p.bias_lo,
+                             dtype=NCCL_F32))
+        self._edge(DPS, MAIN)
+        self._seg("SB")
+        for a, b, e0, e1 in buckets:
+            self._seg(f"SU{a}-{b}")
+            self._edge(MAIN, DPS)
+            p0, _ = p.shard_piece(e0, e1)
+            self.ops.append(dict(kind=ALL_GATHER, stream=DPS, comm=self.comm_dp,
+                                 a=p.shadow.data_ptr() + 2 * p0, b=p.shadow.data_ptr() + 2 * e0,
+                                 count=(e1 - e0) // d, dtype=NCCL_BF16))
+        if p.optim.name != "sgd":
+            self._seg("OADV")
+        self._edge(DPS, MAIN)
+        self._seg("T")
 
     def _build(self) -> None:
         m, st = self.mesh, self.st
@@ -269,6 +316,6 @@ def native_step_supported(executor, mesh) -> Optional[str]:
     for k, (op, j) in enumerate(ops):
         if op == "W" and (j >= 0 or k + 1 >= len(ops) or ops[k + 1][0] != "O"):
             return "per-micro-batch weight gradients"
-    if mesh.dp > 1 and mesh.backend != "nccl":
+    if (mesh.dp > 1 or st.params.sharded) and mesh.backend != "nccl":
         return "data-parallel group is not RCCL"
     return None

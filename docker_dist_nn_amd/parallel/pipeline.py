@@ -37,17 +37,37 @@ def schedule_ops(kind: str, num_stages: int, num_micro: int, stage: int):
 
 
 class GradSync:
-    """Bucketed, asynchronous gradient all-reduce over the data-parallel group."""
+    """Bucketed, asynchronous gradient all-reduce over the data-parallel group.
 
-    def __init__(self, group, world: int):
+    ``shard=True``: sharded data parallelism instead (StageParams.shard_piece): per bucket a
+    bf16 reduce-scatter of the gradient, the optimizer on this rank's piece only, and a bf16
+    all-gather of the updated shadow weights -- half the bytes of the fp32 all-reduce."""
+
+    def __init__(self, group, world: int, shard: bool = False):
         self.group = group
         self.world = world
+        self.shard = shard
         self._works = []
+
+    def reduce_scatter(self, p, e0: int, e1: int):
+        """Async bf16 reduce-scatter of bucket [e0, e1) of p.grad16 into p.grad_piece."""
+        d = self.world
+        w = dist.reduce_scatter_tensor(p.grad_piece[e0 // d:e1 // d], p.grad16[e0:e1],
+                                       group=self.group, async_op=True)
+        self._works.append(w)
+        return w
+
+    def all_gather_shadow(self, p, e0: int, e1: int):
+        p0, p1 = p.shard_piece(e0, e1)
+        w = dist.all_gather_into_tensor(p.shadow[e0:e1], p.shadow[p0:p1], group=self.group,
+                                        async_op=True)
+        self._works.append(w)
+        return w
 
     def launch(self, flat_grad, start: int, end: int):
         """Async all-reduce of flat_grad[start:end]; returns the work handle (also kept for
         wait())."""
-        if self.world <= 1:
+        if self.world <= 1 and not self.shard:
             return None
         w = dist.all_reduce(flat_grad[start:end], group=self.group, async_op=True)
         self._works.append(w)
@@ -130,7 +150,7 @@ class PipelineExecutor:
         self._side = None
         # deferred data-parallel update (DNN_DP_DEFER=0 disables): see dp_split
         self.defer = (grad_sync is not None and grad_sync.world > 1 and
-                      switches.get("DNN_DP_DEFER") != "0")
+                      not grad_sync.shard and switches.get("DNN_DP_DEFER") != "0")
         self._split = {id(st): (dp_split(st) if self.defer else 0) for st in self.stages}
         self._pending = {}  # id(stage) -> (work of layers [s, L), s)
         self._works = {}    # id(stage) -> [work of [0, s), work of [s, L)] this step
@@ -164,6 +184,9 @@ class PipelineExecutor:
             if sp:
                 self._optimizer_deferred(st, sp)
                 return self._after(st, op, j)
+            if self.grad_sync is not None and self.grad_sync.shard:
+                self._sharded_update(st)
+                return self._after(st, op, j)
             if not getattr(st, "_finalized", False):
                 st.finalize_grads()
                 if self.grad_sync is not None:
@@ -177,6 +200,45 @@ class PipelineExecutor:
     def _after(self, st, op, j):
         for h in self.hooks["after_op"]:
             h(st, op, j)
+
+    def _shard_buckets(self, st) -> list[tuple[list[int], int, int]]:
+        """(layers, e0, e1) of every DP bucket of a sharded stage, in launch order."""
+        out = []
+        for bucket in dp_buckets(st):
+            e0, _ = st.params.layer_grad_range(bucket[0])
+            _, e1 = st.params.layer_grad_range(bucket[-1])
+            out.append((bucket, e0, e1))
+        st.params.shard_buckets = [(e0, e1) for _, e0, e1 in out]
+        return out
+
+    def _sharded_update(self, st) -> None:
+        """O of a sharded stage: (buckets reduce-scattered in _wgrad_finalize_overlapped, or
+        now for per-micro-batch W schedules) -> unpack + update this rank's piece of every
+        bucket -> all-gather the bf16 shadow -> refresh W^T."""
+        gs, p = self.grad_sync, st.params
+        buckets = self._shard_buckets(st)
+        if not getattr(st, "_finalized", False):
+            st.finalize_grads()
+            for _, e0, e1 in buckets:
+                p.shard_pack(e0, e1)
+                gs.reduce_scatter(p, e0, e1)
+            gs.launch(p.grad, p.bias_lo, p.numel)
+        gs.wait()
+        st._finalized = False
+        lr = self.lr_fn() if self.lr_fn else None
+        for _, e0, e1 in buckets:
+            st.shard_update(e0, e1, lr)
+        st.bias_update(lr)
+        if p.optim.name != "sgd":  # the step's one device-counter advance (Adam)
+            if p.device.type == "cuda":
+                from .. import ops
+
+                ops.step_advance(p.step_dev)
+        p.step_count += 1
+        for _, e0, e1 in buckets:
+            gs.all_gather_shadow(p, e0, e1)
+        gs.wait()
+        p.refresh_t()
 
     def _optimizer_deferred(self, st, sp: int) -> None:
         """O with a deferred split: all-reduce [0, sp) must be done -> update it now; the
@@ -207,7 +269,7 @@ class PipelineExecutor:
     def _wgrad_finalize_overlapped(self, st):
         """Batched W: per layer (last first) wgrad -> reduce -> async bucket all-reduce. Without
         a DP group there is nothing to overlap: all wgrads, then ONE reduce launch."""
-        if self.grad_sync is None or self.grad_sync.world <= 1:
+        if self.grad_sync is None or (self.grad_sync.world <= 1 and not self.grad_sync.shard):
             for i in range(len(st.geoms) - 1, -1, -1):
                 st.wgrad_layer(i)
             st.finalize_grads()
@@ -222,6 +284,17 @@ class PipelineExecutor:
                 e0, e1 = st.params.layers_range(a, b)
                 works.append(self.grad_sync.launch(st.params.grad, e0, e1))
             self._works[id(st)] = works
+            st._finalized = True
+            return
+        if self.grad_sync.shard:  # bf16 reduce-scatter per bucket, overlapping later wgrads
+            for bucket, e0, e1 in self._shard_buckets(st):
+                for i in bucket:
+                    st.wgrad_layer(i)
+                st.finalize_grads(bucket)
+                st.params.shard_pack(e0, e1)
+                self.grad_sync.reduce_scatter(st.params, e0, e1)
+            p = st.params  # every bias gradient: one small fp32 all-reduce
+            self.grad_sync.launch(p.grad, p.bias_lo, p.numel)
             st._finalized = True
             return
         for bucket in dp_buckets(st):

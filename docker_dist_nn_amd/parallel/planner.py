@@ -10,9 +10,11 @@ MI355X-first reasoning, encoded as a cost model (all constants overridable):
   compute, so in steady state a micro-batch costs ``max(stage compute, hop in, hop out)``
   (``link_gbps`` = achieved per-direction point-to-point rate; xGMI is 7 links x ~153 GB/s per
   GPU, not all of it reachable by one P2P stream);
-* a data-parallel replica all-reduces its stage gradient (fp32) once per step with RCCL's
-  rings over the fully connected mesh (``allreduce_gbps`` bus bandwidth), bucketed and about
-  half hidden behind the remaining weight-gradient GEMMs.
+* a data-parallel replica exchanges its stage gradient once per step with RCCL's rings over
+  the fully connected mesh (``allreduce_gbps`` bus bandwidth), bucketed and about half hidden
+  behind the remaining weight-gradient GEMMs: by default as a bf16 reduce-scatter + bf16
+  all-gather of the updated weights (sharded optimizer, ``dp_grad_bytes`` = 2), or as an fp32
+  all-reduce (``dp_grad_bytes`` = 4).
 
 ``pipeline_layout`` is the layout the benchmark runs for N GPUs (the metric is "... at
 1/2/4/8-stage pipeline"): the deepest pipeline that divides N and fits the layers, data
@@ -79,13 +81,15 @@ class Planner:
     # xGMI rates are estimates (the 1-GPU pool cannot time a cross-GPU hop).
     def __init__(self, tflops: float = 550.0, link_gbps: float = 64.0,
                  hop_latency_us: float = 15.0, allreduce_gbps: float = 150.0,
-                 step_overhead_us: float = 20.0, boundary_bytes: float = 2.0):
+                 step_overhead_us: float = 20.0, boundary_bytes: float = 2.0,
+                 dp_grad_bytes: float = 2.0):
         self.rate = tflops * 1e12
         self.link = link_gbps * 1e9
         self.lat = hop_latency_us * 1e-6
         self.ar = allreduce_gbps * 1e9
         self.ovh = step_overhead_us * 1e-6
         self.bb = boundary_bytes  # bytes per boundary element on the wire (bf16 = 2)
+        self.gb = dp_grad_bytes   # bytes per parameter per DP collective (shard bf16 = 2)
 
     @classmethod
     def calibrated(cls, spec: MLPSpec, **kw) -> "Planner":
@@ -108,12 +112,14 @@ class Planner:
         return comp, hops
 
     def best_distribution(self, spec: MLPSpec, pp: int, mb: int) -> list[int]:
-        best, best_t = None, float("inf")
+        """The split minimising the slowest stage / hop per micro-batch; among hop-bound ties
+        (equal-width boundaries), the one with the most balanced compute."""
+        best, best_k = None, (float("inf"), float("inf"))
         for dist in compositions(len(spec.layers), pp):
             comp, hops = self._stage_costs(spec, dist, mb)
-            t = max(comp + hops)
-            if t < best_t - 1e-15:
-                best, best_t = dist, t
+            k = (round(max(comp + hops), 12), max(comp))
+            if k < best_k:
+                best, best_k = dist, k
         return best
 
     def evaluate(self, spec: MLPSpec, pp: int, dp: int, rows_per_replica: int,
@@ -137,7 +143,7 @@ class Planner:
             params = sum(l.params for l in L[g:g + k])
             g += k
             if dp > 1:
-                ar = max(ar, 2 * (dp - 1) / dp * params * 4 / self.ar)
+                ar = max(ar, 2 * (dp - 1) / dp * params * self.gb / self.ar)
         t = pipe + 0.5 * ar + self.ovh
         detail = {"stage_ms_per_micro": [round(c * 1e3, 4) for c in comp],
                   "hop_ms_per_micro": [round(h * 1e3, 4) for h in hops],
