@@ -89,7 +89,9 @@ def parse_args(argv=None):
 
 
 def _plan(a, spec, n, world, text):
-    planner = Planner.calibrated(spec)
+    relays = int(switches.get("DNN_IPC_RELAYS")) if switches.get("DNN_PIPE") == "ipc" else 0
+    planner = Planner.calibrated(spec, relays=relays,
+                                 dp_grad_bytes=2.0 if a.dp_reduce == "shard" else 4.0)
     loopback = world == 1
     pp, dp = parse_parallelism(text, n, loopback=loopback)
     if pp is None:

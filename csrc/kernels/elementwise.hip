@@ -12,6 +12,7 @@
 //   sgd / adam     : fused multi-tensor optimizer over the flat fp32 master buffer, refreshing
 //                    the bf16 shadow weights in the same pass
 //   pack_bf16      : fp32 host data -> padded bf16 device layout (and back)
+#include <algorithm>
 #include "common.hpp"
 #include "elementwise.hpp"
 
@@ -752,6 +753,49 @@ int dequant_rows_fp8(const unsigned char* q, long ldq, const float* scale, int r
   if (((uintptr_t)x & 15) || ((uintptr_t)q & 7)) return -2;
   hipLaunchKernelGGL(dequant_rows_fp8_kernel, dim3((rows + 3) / 4), dim3(256), 0, stream, q, ldq,
                      scale, rows, cols, x, ldx);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
+// ------------------------------------------------------------------------------------------
+// Stream-ordered peer copy and flag write as KERNELS. hipMemcpyAsync / hipStreamWriteValue32
+// into IPC-imported memory were measured to block the issuing host thread until the stream's
+// earlier work completed (bench/relay_diag.py, DNN_PLAN_TRACE): a rank then cannot enqueue the
+// rest of its step (e.g. the relay copies another rank is waiting for) -- a cross-rank
+// deadlock, and a host-serialised step even without one. A kernel launch never blocks.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void p2p_copy_kernel(const uint4* __restrict__ src,
+                                                       uint4* __restrict__ dst, long n16,
+                                                       const unsigned char* __restrict__ src_t,
+                                                       unsigned char* __restrict__ dst_t,
+                                                       int tail) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n16; i += (long)gridDim.x * 256)
+    dst[i] = src[i];
+  if (blockIdx.x == 0 && (int)threadIdx.x < tail) dst_t[threadIdx.x] = src_t[threadIdx.x];
+}
+
+// One lane stores the flag word with system-scope release semantics (a vector store; the
+// kernel boundary before it has made the preceding copy's writes visible).
+__global__ void p2p_signal_kernel(unsigned* flag, unsigned value) {
+  const unsigned l = threadIdx.x;
+  if (l == 0) __hip_atomic_store(flag + l, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+int p2p_copy(void* dst, const void* src, size_t bytes, hipStream_t stream) {
+  if (bytes == 0) return 0;
+  if ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) return -1;
+  const long n16 = (long)(bytes / 16);
+  const int tail = (int)(bytes % 16);
+  const int grid = (int)std::min<long>(std::max<long>(1, (n16 + 255) / 256), 2048);
+  hipLaunchKernelGGL(p2p_copy_kernel, dim3(grid), dim3(256), 0, stream,
+                     reinterpret_cast<const uint4*>(src), reinterpret_cast<uint4*>(dst), n16,
+                     reinterpret_cast<const unsigned char*>(src) + n16 * 16,
+                     reinterpret_cast<unsigned char*>(dst) + n16 * 16, tail);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
+int p2p_signal(uint32_t* flag, uint32_t value, hipStream_t stream) {
+  if (reinterpret_cast<uintptr_t>(flag) & 3) return -1;
+  hipLaunchKernelGGL(p2p_signal_kernel, dim3(1), dim3(64), 0, stream, flag, value);
   return hipGetLastError() == hipSuccess ? 0 : -9;
 }
 

@@ -96,4 +96,8 @@ int quant_rows_fp8(const uint16_t* x, long ldx, int rows, int cols, unsigned cha
 int dequant_rows_fp8(const unsigned char* q, long ldq, const float* scale, int rows, int cols,
                      uint16_t* x, long ldx, hipStream_t stream);
 
+// Peer copy (16-byte aligned) and flag write as kernels: never block the issuing host thread.
+int p2p_copy(void* dst, const void* src, size_t bytes, hipStream_t stream);
+int p2p_signal(uint32_t* flag, uint32_t value, hipStream_t stream);
+
 }  // namespace dnn

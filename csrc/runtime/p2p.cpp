@@ -1,5 +1,7 @@
 #include "p2p.hpp"
 
+#include "kernels/elementwise.hpp"
+
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -51,12 +53,15 @@ void ipc_close_all() {
   opened.clear();
 }
 
+// Copies and flag writes are kernels (kernels/elementwise.hip p2p_copy / p2p_signal): the
+// runtime's hipMemcpyAsync / hipStreamWriteValue32 into IPC-imported memory block the host.
 void copy_async(void* dst, const void* src, size_t n, hipStream_t s) {
-  ck(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, s), "hipMemcpyAsync");
+  if (p2p_copy(dst, src, n, s) != 0) throw std::runtime_error("p2p_copy failed");
 }
 
 void signal_u32(hipStream_t s, void* flag, uint32_t v) {
-  ck(hipStreamWriteValue32(s, flag, v, 0), "hipStreamWriteValue32");
+  if (p2p_signal(reinterpret_cast<uint32_t*>(flag), v, s) != 0)
+    throw std::runtime_error("p2p_signal failed");
 }
 
 void wait_geq_u32(hipStream_t s, void* flag, uint32_t v) {

@@ -1,6 +1,11 @@
 #include "runtime/step_plan.hpp"
+#include "runtime/p2p.hpp"
 
 #include <dlfcn.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 
 #include <mutex>
 #include <set>
@@ -104,14 +109,33 @@ static void nck(int rc, const char* what) {
   }
 }
 
+// DNN_PLAN_TRACE=1: host timestamp of every op before it is issued (stderr) -- finds an
+// issue call that blocks the host thread (a plan must never wait on the GPU while enqueuing).
+static bool plan_trace() {
+  static const bool on = [] {
+    const char* e = std::getenv("DNN_PLAN_TRACE");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 void StepPlan::run(hipStream_t main) {
   ++seq_;
   ck(hipEventRecord(fork_, main), "hipEventRecord");
   for (auto s : streams_) ck(hipStreamWaitEvent(s, fork_, 0), "hipStreamWaitEvent");
   std::vector<std::string> one(1);
   const NcclApi* nc = nccl_api();
+  const bool trace = plan_trace();
+  int idx = 0;
   for (const Op& o : ops_) {
     hipStream_t s = stream(o.stream, main);
+    if (trace) {
+      const auto t = std::chrono::steady_clock::now().time_since_epoch();
+      std::fprintf(stderr, "plan seq %llu op %d kind %d stream %d t_us %lld\n",
+                   (unsigned long long)seq_, idx, (int)o.kind, o.stream,
+                   (long long)std::chrono::duration_cast<std::chrono::microseconds>(t).count());
+    }
+    ++idx;
     switch (o.kind) {
       case SEG:
         one[0] = o.seg;
@@ -140,15 +164,11 @@ void StepPlan::run(hipStream_t main) {
                            o.count, o.dtype, o.comm, s),
             "ncclAllGather");
         break;
-      case COPY:
-        ck(hipMemcpyAsync(reinterpret_cast<void*>(o.b), reinterpret_cast<const void*>(o.a),
-                          o.count, hipMemcpyDeviceToDevice, s),
-           "hipMemcpyAsync");
+      case COPY:  // kernels, not hipMemcpyAsync / hipStreamWriteValue32 (runtime/p2p.cpp)
+        copy_async(reinterpret_cast<void*>(o.b), reinterpret_cast<const void*>(o.a), o.count, s);
         break;
       case SIGNAL:
-        ck(hipStreamWriteValue32(s, reinterpret_cast<void*>(o.a),
-                                 (uint32_t)((int64_t)seq_ + o.delta), 0),
-           "hipStreamWriteValue32");
+        signal_u32(s, reinterpret_cast<void*>(o.a), (uint32_t)((int64_t)seq_ + o.delta));
         break;
       case WAITV:
         ck(hipStreamWaitValue32(s, reinterpret_cast<void*>(o.a),

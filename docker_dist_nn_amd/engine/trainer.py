@@ -117,7 +117,8 @@ class Trainer:
             # DNN_PIPE=ipc: xGMI peer writes into IPC-mapped buffers instead of RCCL P2P
             use_ipc = (switches.get("DNN_PIPE") == "ipc" and
                        self.device.type == "cuda" and mesh.pp > 1)
-            self.pipe = IpcPipe(mesh, st) if use_ipc else DistPipe(mesh, st)
+            self.pipe = (IpcPipe(mesh, st, relays=int(switches.get("DNN_IPC_RELAYS")))
+                         if use_ipc else DistPipe(mesh, st))
             ids = [mesh.stage]
             sync = (GradSync(mesh.dp_group, mesh.dp, shard=self.dp_reduce == "shard")
                     if mesh.dp > 1 or self.dp_reduce == "shard" else None)

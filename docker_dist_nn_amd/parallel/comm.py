@@ -167,6 +167,38 @@ class DistPipe:
             raise RuntimeError("step ended with unconsumed pipeline receives")
 
 
+def relay_assignment(pp: int, dp: int, k: int) -> dict:
+    """Relay ranks of every directed pipeline hop of a pp x dp mesh (rank = replica * pp +
+    stage, parallel/groups.build_mesh): {(src, dst, "f" | "b"): [k relay ranks]}. A hop's rows
+    are striped over the direct link and k two-link paths src -> relay -> dst, so one hop
+    draws on k + 1 of the source's xGMI links instead of one. Relays are picked least-loaded
+    first (then by distance from the source), so duties spread over the node; the result is
+    a pure function of (pp, dp, k): every rank computes the same table."""
+    world = pp * dp
+    hops = []
+    for r in range(dp):
+        for s in range(pp - 1):
+            a, b = r * pp + s, r * pp + s + 1
+            hops += [(a, b, "f"), (b, a, "b")]
+    if k and world - 2 < k:
+        raise ValueError(f"{k} relays per hop need >= {k + 2} ranks (world {world})")
+    load = [0] * world
+    out = {}
+    for src, dst, d in hops:
+        cands = sorted((x for x in range(world) if x not in (src, dst)),
+                       key=lambda x: (load[x], (x - src) % world))
+        out[(src, dst, d)] = cands[:k]
+        for x in cands[:k]:
+            load[x] += 1
+    return out
+
+
+def relay_parts(r0: int, r1: int, k: int) -> list[int]:
+    """Row bounds of the k + 1 stripes of rows [r0, r1) (stripe 0 = the direct link)."""
+    n = r1 - r0
+    return [r0 + (n * p // (k + 1)) // 8 * 8 for p in range(k + 1)] + [r1]
+
+
 class IpcPipe:
     """Pipeline hops as direct writes into IPC-mapped peer buffers (one stage per rank).
 
@@ -183,9 +215,16 @@ class IpcPipe:
                   resume (prev.ack_f = s) and the next rank likewise (next.ack_b = s)
 
     All waits/signals are stream-ordered on the compute stream: the signal follows the copy,
-    the acks follow every kernel of the step that reads the buffers (wgrad included)."""
+    the acks follow every kernel of the step that reads the buffers (wgrad included).
 
-    def __init__(self, mesh: Mesh, stage):
+    ``relays`` = k > 0 (native step only, parallel/native_step.py): every hop's rows are
+    striped over the direct link and k relay ranks (relay_assignment). Stripe p >= 1 is copied
+    into a relay rank's staging slot, whose own relay stream waits for it, copies it into the
+    consumer's rows and raises the consumer's per-stripe flag; the consumer waits for all k + 1
+    stripe flags. The consumer's end-of-step ack also covers the relay slots (it follows the
+    relay copies it waited for). Flag block: [f[j][p], b[j][p], ack_f, ack_b, relay[d][j]]."""
+
+    def __init__(self, mesh: Mesh, stage, relays: int = 0):
         import torch.distributed as dist
 
         from ..utils.native import native
@@ -197,22 +236,69 @@ class IpcPipe:
         self.stage = stage
         nm = stage.nm
         self.nm = nm
-        # flag block: [f[0..nm), b[0..nm), ack_f, ack_b]
-        self.flags = torch.zeros(2 * nm + 2, dtype=torch.int32, device=stage.device)
-        torch.cuda.synchronize(stage.device)
-        mine = {"x_in": self.n.ipc_export(stage.x_in.data_ptr()),
-                "grad_out": self.n.ipc_export(stage.grad_out.data_ptr()),
-                "flags": self.n.ipc_export(self.flags.data_ptr())}
-        everyone = [None] * dist.get_world_size()
-        dist.all_gather_object(everyone, mine)
-        self.seq = 0
-        self.prev = self._peer(everyone, mesh.prev_rank)
-        self.next = self._peer(everyone, mesh.next_rank)
+        self.k = k = int(relays)
+        me = mesh.rank
+        assign = relay_assignment(mesh.pp, mesh.dp, k) if k else {}
+        # my relay duties, in table order: (src, dst, direction, stripe index)
+        self.duties = [(h[0], h[1], h[2], rl.index(me) + 1) for h, rl in assign.items()
+                       if me in rl]
+        self.ackf = 2 * nm * (k + 1)
+        self.ackb = self.ackf + 1
+        self.flags = torch.zeros(self.ackf + 2 + len(self.duties) * nm, dtype=torch.int32,
+                                 device=stage.device)
         # destination rows have the source's width: my output == the consumer's input, my
         # dx_send == the producer's grad_out
         self.row_bytes_f = stage.output.stride(0) * stage.output.element_size()
         self.row_bytes_b = (stage.dx_send.stride(0) * stage.dx_send.element_size()
                             if stage.dx_send is not None else 0)
+        self.part_max = max(b - a for a, b in zip(relay_parts(0, stage.mb, k),
+                                                  relay_parts(0, stage.mb, k)[1:]))
+        everyone_rb = [None] * dist.get_world_size()
+        dist.all_gather_object(everyone_rb, (self.row_bytes_f, self.row_bytes_b))
+        # a relay slot holds one stripe of one micro-batch of the hop's rows
+        self.relay_bufs = []
+        for src, dst, d, _p in self.duties:
+            rb = everyone_rb[src][0] if d == "f" else everyone_rb[src][1]
+            self.relay_bufs.append((torch.zeros(nm * self.part_max * rb, dtype=torch.uint8,
+                                                device=stage.device), rb))
+        torch.cuda.synchronize(stage.device)
+        mine = {"x_in": self.n.ipc_export(stage.x_in.data_ptr()),
+                "grad_out": self.n.ipc_export(stage.grad_out.data_ptr()),
+                "flags": self.n.ipc_export(self.flags.data_ptr()),
+                "relay": [self.n.ipc_export(b.data_ptr()) for b, _ in self.relay_bufs]}
+        everyone = [None] * dist.get_world_size()
+        dist.all_gather_object(everyone, mine)
+        self.seq = 0
+        self.prev = self._peer(everyone, mesh.prev_rank)
+        self.next = self._peer(everyone, mesh.next_rank)
+        imp = lambda r, key: self.n.ipc_import(*everyone[r][key])  # noqa: E731
+
+        def duty_index(r, hop):
+            ds = [h for h, rl in assign.items() if r in rl]
+            return ds.index(hop)
+
+        # my hops' relays: where stripe p >= 1 goes
+        self.relay_out = {"f": [], "b": []}
+        for d, peer in (("f", mesh.next_rank), ("b", mesh.prev_rank)):
+            if peer is None:
+                continue
+            for r in assign.get((me, peer, d), []):
+                di = duty_index(r, (me, peer, d))
+                self.relay_out[d].append({
+                    "buf": self.n.ipc_import(*everyone[r]["relay"][di]),
+                    "flags": imp(r, "flags"), "d": di})
+        # my duties' consumers: where my relay slots go
+        self.relay_dst = [{"buf": imp(dst, "x_in" if d == "f" else "grad_out"),
+                           "flags": imp(dst, "flags")} for _s, dst, d, _p in self.duties]
+
+    def fidx(self, j: int, p: int = 0) -> int:
+        return j * (self.k + 1) + p
+
+    def bidx(self, j: int, p: int = 0) -> int:
+        return self.nm * (self.k + 1) + j * (self.k + 1) + p
+
+    def ridx(self, d: int, j: int) -> int:
+        return self.ackf + 2 + d * self.nm + j
 
     def _peer(self, everyone, rank):
         if rank is None:
@@ -228,45 +314,49 @@ class IpcPipe:
         return base + 4 * i
 
     def begin_step(self):
+        if self.k:
+            raise RuntimeError("relayed IPC hops run in the native step only "
+                               "(parallel/native_step.py)")
         self.seq += 1
 
     def recv_fwd(self, stage, j):
         if self.prev is not None:
-            self.n.wait_geq_u32(self._stream(), self._flag(self.flags.data_ptr(), j), self.seq)
+            self.n.wait_geq_u32(self._stream(), self._flag(self.flags.data_ptr(), self.fidx(j)),
+                                self.seq)
 
     def send_fwd(self, stage, j):
         if self.next is None:
             return
-        s, nm = self._stream(), self.nm
+        s = self._stream()
         if j == 0:  # the consumer finished every read of its x_in for the previous step
-            self.n.wait_geq_u32(s, self._flag(self.flags.data_ptr(), 2 * nm), self.seq - 1)
+            self.n.wait_geq_u32(s, self._flag(self.flags.data_ptr(), self.ackf), self.seq - 1)
         r = stage.rows_of(j)
         src = stage.output[r]
         off = r.start * self.row_bytes_f
         self.n.copy_async(self.next["x_in"] + off, src.data_ptr(), src.numel() * src.element_size(), s)
-        self.n.signal_u32(s, self._flag(self.next["flags"], j), self.seq)
+        self.n.signal_u32(s, self._flag(self.next["flags"], self.fidx(j)), self.seq)
 
     def recv_bwd(self, stage, j):
         if self.next is not None:
-            self.n.wait_geq_u32(self._stream(), self._flag(self.flags.data_ptr(), self.nm + j),
+            self.n.wait_geq_u32(self._stream(), self._flag(self.flags.data_ptr(), self.bidx(j)),
                                 self.seq)
 
     def send_bwd(self, stage, j):
         if self.prev is None:
             return
-        s, nm = self._stream(), self.nm
+        s = self._stream()
         if j == 0:
-            self.n.wait_geq_u32(s, self._flag(self.flags.data_ptr(), 2 * nm + 1), self.seq - 1)
+            self.n.wait_geq_u32(s, self._flag(self.flags.data_ptr(), self.ackb), self.seq - 1)
         r = stage.rows_of(j)
         src = stage.dx_send[r]
         off = r.start * self.row_bytes_b
         self.n.copy_async(self.prev["grad_out"] + off, src.data_ptr(),
                           src.numel() * src.element_size(), s)
-        self.n.signal_u32(s, self._flag(self.prev["flags"], nm + j), self.seq)
+        self.n.signal_u32(s, self._flag(self.prev["flags"], self.bidx(j)), self.seq)
 
     def end_step(self):
-        s, nm = self._stream(), self.nm
+        s = self._stream()
         if self.prev is not None:  # my x_in is free for the previous rank's next step
-            self.n.signal_u32(s, self._flag(self.prev["flags"], 2 * nm), self.seq)
+            self.n.signal_u32(s, self._flag(self.prev["flags"], self.ackf), self.seq)
         if self.next is not None:  # my grad_out is free for the next rank's next step
-            self.n.signal_u32(s, self._flag(self.next["flags"], 2 * nm + 1), self.seq)
+            self.n.signal_u32(s, self._flag(self.next["flags"], self.ackb), self.seq)

@@ -32,6 +32,7 @@ from typing import Optional
 import torch
 
 from ..utils.native import native
+from .comm import relay_parts
 from .pipeline import dp_buckets
 
 SEG, SEND, RECV, ALLREDUCE, REDUCE_SCATTER, ALL_GATHER, COPY, SIGNAL, WAITV, REC, WAIT = range(11)
@@ -81,7 +82,16 @@ class NativeStep:
         self._ev = 0
         self.ops: list[tuple] = []
         self._build()
-        self.plan = self.n.StepPlan(4, max(1, self._ev))
+        n_streams = 4 + (len(ipc.duties) if transport == "ipc" and ipc is not None else 0)
+        # streams of a plan block on flags / peers: each needs its own hardware queue (HIP maps
+        # streams beyond GPU_MAX_HW_QUEUES onto shared queues, where one blocked wait stalls
+        # the streams behind it -- a cross-rank deadlock); stream 0 is the caller's
+        hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+        if n_streams > hwq:
+            raise RuntimeError(f"native step needs {n_streams} hardware queues, "
+                               f"GPU_MAX_HW_QUEUES={hwq}: set it (before the GPU is "
+                               f"initialised) to >= {n_streams}")
+        self.plan = self.n.StepPlan(n_streams, max(1, self._ev))
         for o in self.ops:
             self.plan.add(**o)
 
@@ -119,10 +129,12 @@ class NativeStep:
             self._seg(f"DQF{j}" if direction == "f" else f"DQB{j}")
             return
         t = st.x_in if direction == "f" else st.grad_out
-        if self.transport == "ipc":  # the producer's copy + flag: wait on the compute stream
-            base = self.ipc.flags.data_ptr()
-            idx = j if direction == "f" else st.nm + j
-            self.ops.append(dict(kind=WAITV, stream=MAIN, a=base + 4 * idx, delta=0))
+        if self.transport == "ipc":  # the producer's copies + flags: wait on the compute stream
+            p = self.ipc
+            base = p.flags.data_ptr()
+            for part in range(p.k + 1):  # the direct stripe and every relayed one
+                idx = p.fidx(j, part) if direction == "f" else p.bidx(j, part)
+                self.ops.append(dict(kind=WAITV, stream=MAIN, a=base + 4 * idx, delta=0))
             return
         ptr, cnt = self._rows(t, j)
         s = FWD if direction == "f" else BWD
@@ -152,19 +164,30 @@ class NativeStep:
         if self.transport == "ipc":
             p = self.ipc
             peer = p.next if direction == "f" else p.prev
-            nm = st.nm
             if j == 0:  # the peer finished reading that buffer in the previous step (ack)
-                self.ops.append(dict(kind=WAITV, stream=s,
-                                     a=p.flags.data_ptr() + 4 * (2 * nm + (0 if direction == "f"
-                                                                          else 1)),
+                ack = p.ackf if direction == "f" else p.ackb
+                self.ops.append(dict(kind=WAITV, stream=s, a=p.flags.data_ptr() + 4 * ack,
                                      delta=-1))
             dst_base = peer["x_in"] if direction == "f" else peer["grad_out"]
             row_bytes = p.row_bytes_f if direction == "f" else p.row_bytes_b
-            off = st.rows_of(j).start * row_bytes
-            self.ops.append(dict(kind=COPY, stream=s, a=ptr, b=dst_base + off,
-                                 count=cnt * t.element_size()))
-            idx = j if direction == "f" else nm + j
-            self.ops.append(dict(kind=SIGNAL, stream=s, a=peer["flags"] + 4 * idx, delta=0))
+            r = st.rows_of(j)
+            bounds = relay_parts(r.start, r.stop, p.k)
+            for part in range(p.k + 1):  # stripe 0 direct, stripe q via relay q - 1
+                a0, a1 = bounds[part], bounds[part + 1]
+                src = ptr + (a0 - r.start) * row_bytes
+                if part == 0:
+                    self.ops.append(dict(kind=COPY, stream=s, a=src, b=dst_base + a0 * row_bytes,
+                                         count=(a1 - a0) * row_bytes))
+                    idx = p.fidx(j, 0) if direction == "f" else p.bidx(j, 0)
+                    self.ops.append(dict(kind=SIGNAL, stream=s, a=peer["flags"] + 4 * idx,
+                                         delta=0))
+                else:
+                    rel = p.relay_out[direction][part - 1]
+                    slot = rel["buf"] + j * p.part_max * row_bytes
+                    self.ops.append(dict(kind=COPY, stream=s, a=src, b=slot,
+                                         count=(a1 - a0) * row_bytes))
+                    self.ops.append(dict(kind=SIGNAL, stream=s,
+                                         a=rel["flags"] + 4 * p.ridx(rel["d"], j), delta=0))
             return
         peer = m.stage + 1 if direction == "f" else m.stage - 1
         self.ops.append(dict(kind=SEND, stream=s, comm=self.comm_f if s == FWD else self.comm_b,
@@ -267,13 +290,36 @@ class NativeStep:
             elif op == "O":
                 pass  # emitted with the batched W
         if self.transport == "ipc":  # release the buffers I receive into for the next step
-            p, nm = self.ipc, st.nm
+            p = self.ipc
             if p.prev is not None:
-                self.ops.append(dict(kind=SIGNAL, stream=MAIN, a=p.prev["flags"] + 4 * (2 * nm),
+                self.ops.append(dict(kind=SIGNAL, stream=MAIN, a=p.prev["flags"] + 4 * p.ackf,
                                      delta=0))
             if p.next is not None:
-                self.ops.append(dict(kind=SIGNAL, stream=MAIN,
-                                     a=p.next["flags"] + 4 * (2 * nm + 1), delta=0))
+                self.ops.append(dict(kind=SIGNAL, stream=MAIN, a=p.next["flags"] + 4 * p.ackb,
+                                     delta=0))
+            self._relay_duties()
+
+    def _relay_duties(self) -> None:
+        """My relay work for other ranks' hops, one stream per duty (a duty's stripes arrive
+        in micro-batch order, and separate streams keep one hop from blocking another):
+        wait for the producer's stripe j in my slot -> copy it into the consumer's rows ->
+        raise the consumer's stripe flag."""
+        p, st = self.ipc, self.st
+        for d, ((src, dst, direction, part), dst_ptrs) in enumerate(zip(p.duties, p.relay_dst)):
+            stream = 4 + d
+            buf, rb = p.relay_bufs[d]
+            for j in range(st.nm):
+                r = st.rows_of(j)  # every stage shares the micro-batch row layout
+                bounds = relay_parts(r.start, r.stop, p.k)
+                a0, a1 = bounds[part], bounds[part + 1]
+                self.ops.append(dict(kind=WAITV, stream=stream,
+                                     a=p.flags.data_ptr() + 4 * p.ridx(d, j), delta=0))
+                self.ops.append(dict(kind=COPY, stream=stream,
+                                     a=buf.data_ptr() + j * p.part_max * rb,
+                                     b=dst_ptrs["buf"] + a0 * rb, count=(a1 - a0) * rb))
+                idx = p.fidx(j, part) if direction == "f" else p.bidx(j, part)
+                self.ops.append(dict(kind=SIGNAL, stream=stream, a=dst_ptrs["flags"] + 4 * idx,
+                                     delta=0))
 
     # ---- execution -----------------------------------------------------------------------
     def run(self, stream: int) -> None:

@@ -82,7 +82,7 @@ class Planner:
     def __init__(self, tflops: float = 550.0, link_gbps: float = 64.0,
                  hop_latency_us: float = 15.0, allreduce_gbps: float = 150.0,
                  step_overhead_us: float = 20.0, boundary_bytes: float = 2.0,
-                 dp_grad_bytes: float = 2.0):
+                 dp_grad_bytes: float = 2.0, relays: int = 0, relay_eff: float = 0.8):
         self.rate = tflops * 1e12
         self.link = link_gbps * 1e9
         self.lat = hop_latency_us * 1e-6
@@ -90,6 +90,10 @@ class Planner:
         self.ovh = step_overhead_us * 1e-6
         self.bb = boundary_bytes  # bytes per boundary element on the wire (bf16 = 2)
         self.gb = dp_grad_bytes   # bytes per parameter per DP collective (shard bf16 = 2)
+        # relayed IPC hops (parallel/comm.relay_assignment): a hop's rows striped over the
+        # direct link and `relays` two-link paths, each path worth `relay_eff` of a link (the
+        # relay's second copy adds latency and HBM traffic on the relay GPU)
+        self.hop_bw = self.link * (1.0 + relays * relay_eff)
 
     @classmethod
     def calibrated(cls, spec: MLPSpec, **kw) -> "Planner":
@@ -108,7 +112,7 @@ class Planner:
             comp.append(sum(fl[g:g + k]) * mb / self.rate)
             g += k
             if g < len(spec.layers):
-                hops.append(self.lat + mb * spec.layers[g - 1].out_dim * self.bb / self.link)
+                hops.append(self.lat + mb * spec.layers[g - 1].out_dim * self.bb / self.hop_bw)
         return comp, hops
 
     def best_distribution(self, spec: MLPSpec, pp: int, mb: int) -> list[int]:

@@ -40,6 +40,8 @@ SWITCHES: dict[str, tuple[str, str]] = {
     "DNN_BW_OVERLAP": ("0", "wgrad_i on a side stream concurrent with dgrad_i (1 stage)"),
     "DNN_DP_DEFER": ("1", "deferred data-parallel update (Python executor path)"),
     "DNN_PIPE": ("rccl", "pipeline transport: rccl | ipc (xGMI peer copies + stream flags)"),
+    "DNN_IPC_RELAYS": ("0", "ipc transport: stripe every hop over the direct link + this many "
+                            "relay ranks (two-link paths; native step only)"),
     "DNN_SERVE_REPLAY": ("graph", "serving engine replay: graph | native | eager"),
     "DNN_SYNC_DEBUG": ("0", "synchronise + check after every kernel (race / fault hunting)"),
     "DNN_AUTOBUILD": ("1", "build the native extension on import if it is missing"),

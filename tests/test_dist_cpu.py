@@ -124,3 +124,19 @@ def test_dp_split_balances_gradient_bytes():
     assert dp_split(stage([784] + [1024] * 7 + [10])) == 4
     assert dp_split(stage([784, 8192, 8192, 10])) == 2
     assert dp_split(stage([784, 10])) == 0  # one layer: nothing to defer
+
+
+def test_relay_assignment_balances_duties():
+    from docker_dist_nn_amd.parallel.comm import relay_assignment, relay_parts
+
+    a = relay_assignment(4, 2, 2)
+    assert len(a) == 12  # 3 boundaries x 2 directions x 2 replicas
+    load = {}
+    for (src, dst, _), rl in a.items():
+        assert len(rl) == 2 and src not in rl and dst not in rl and len(set(rl)) == 2
+        for r in rl:
+            load[r] = load.get(r, 0) + 1
+    assert sum(load.values()) == 24 and max(load.values()) <= 4  # 3 per rank on average
+    b = relay_parts(4096, 8192, 2)
+    assert b[0] == 4096 and b[-1] == 8192 and all(x % 8 == 0 for x in b)
+    assert sorted(b) == b

@@ -131,9 +131,14 @@ def test_pp2_ipc_pipe_bitwise_equals_rccl_path(dev):
             assert np.array_equal(a, b), k
 
 
-def _native_worker(rank, world, port, native_dist, steps, nm, out_dir):
+def _native_worker(rank, world, port, native_dist, steps, nm, out_dir, relays=0, tag=None):
+    # every stream of a plan that waits on a flag needs a hardware queue of its own (HIP
+    # multiplexes streams beyond GPU_MAX_HW_QUEUES onto shared queues, where one blocked wait
+    # would stall the others): 4 plan streams + the relay duties + the default stream
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DNN_PIPE="ipc",
-                      DNN_NATIVE_DIST=native_dist)
+                      DNN_NATIVE_DIST=native_dist, DNN_IPC_RELAYS=str(relays),
+                      GPU_MAX_HW_QUEUES="8")
+    tag = native_dist if tag is None else tag
     import time
 
     import torch.distributed as dist
@@ -159,10 +164,10 @@ def _native_worker(rank, world, port, native_dist, steps, nm, out_dir):
         host.append(time.perf_counter() - t0)
     torch.cuda.synchronize()
     for k, (w, _b) in tr.local_weights().items():
-        np.save(os.path.join(out_dir, f"n{native_dist}_w{k}.npy"), w)
-    np.save(os.path.join(out_dir, f"n{native_dist}_host_r{rank}.npy"), np.array(host))
+        np.save(os.path.join(out_dir, f"n{tag}_w{k}.npy"), w)
+    np.save(os.path.join(out_dir, f"n{tag}_host_r{rank}.npy"), np.array(host))
     if tr.last is not None:
-        np.save(os.path.join(out_dir, f"n{native_dist}_loss.npy"), np.array([tr.loss()]))
+        np.save(os.path.join(out_dir, f"n{tag}_loss.npy"), np.array([tr.loss()]))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -189,6 +194,26 @@ def test_native_multirank_step_bitwise_equals_python(dev, world, nm):
                 for r in range(world)]
         print("native host s/step per rank:", host)
         assert max(host) < 2e-3, host
+
+
+@pytest.mark.parametrize("world,relays", [(3, 1), (4, 2)])
+def test_relayed_ipc_hops_bitwise_equal_direct(dev, world, relays):
+    """Relayed xGMI hops (DNN_IPC_RELAYS, parallel/comm.relay_assignment): every hop's rows
+    striped over the direct copy and `relays` two-hop copies through other ranks' staging
+    slots and relay streams give bit-identical training to direct hops (ranks = processes
+    sharing cuda:0; the data moved is the same, only its route differs)."""
+    steps, nm = 3, 4
+    with tempfile.TemporaryDirectory() as d:
+        for k, tag in ((0, "direct"), (relays, "relay")):
+            mp.start_processes(_native_worker,
+                               args=(world, _free_port(), "1", steps, nm, d, k, tag),
+                               nprocs=world, join=True, start_method="spawn")
+        for k in range(4):
+            a = np.load(os.path.join(d, f"ndirect_w{k}.npy"))
+            b = np.load(os.path.join(d, f"nrelay_w{k}.npy"))
+            assert np.array_equal(a, b), k
+        assert np.array_equal(np.load(os.path.join(d, "ndirect_loss.npy")),
+                              np.load(os.path.join(d, "nrelay_loss.npy")))
 
 
 def test_step_plan_rccl_allreduce_one_rank(dev):
