@@ -562,6 +562,75 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&a
       // stage (issued before them) with vmcnt(#stores) -- see epilogue_direct_stores.
       // Two instantiations of the store loop (activation derivative from `aux`, or bias +
       // activation), so only one kind of hoisted operand is live at a time.
+      // ReLU dgrad: the derivative is a mask, and masking commutes with the bf16 rounding, so
+      // it is applied AFTER the 16-lane swap, to the 8 consecutive columns a lane stores: the
+      // activation rows are then read as 16-byte chunks (64 contiguous bytes per row and
+      // instruction) instead of 8-byte ones. Column sums of the stored values are taken in the
+      // same layout; per column they add the same rows in the same order (the swap keeps a
+      // lane's row), so the result is bitwise that of the generic path.
+      auto relu_body = [&]() {
+      uint4 yv[FN / 2][FM];
+#pragma unroll
+      for (int jj = 0; jj < FN / 2; ++jj) {
+        const u16* ya = p.aux + min(scol0 + 32 * jj, p.N - 8);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+          yv[jj][i] = *(const uint4*)(ya + min(row0 + 16 * i, p.M - 1) * p.ld_aux);
+      }
+#pragma unroll
+      for (int j = 0; j < FN; j += 2) {
+        f32x4_t b0 = {0.f, 0.f, 0.f, 0.f}, b1 = {0.f, 0.f, 0.f, 0.f};
+        if (p.bias) {  // (no caller combines bias and aux; kept correct, not hoisted)
+          const int c0 = col0 + 16 * j;
+          if (c0 < p.N) b0 = *(const f32x4_t*)(p.bias + c0);
+          if (c0 + 16 < p.N) b1 = *(const f32x4_t*)(p.bias + c0 + 16);
+        }
+        float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        const int scol = scol0 + 16 * j;
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int row = row0 + 16 * i;
+          const unsigned x0 = pack_bf16x2(acc[i][j][0] + b0[0], acc[i][j][1] + b0[1]);
+          const unsigned x1 = pack_bf16x2(acc[i][j][2] + b0[2], acc[i][j][3] + b0[3]);
+          const unsigned z0 = pack_bf16x2(acc[i][j + 1][0] + b1[0], acc[i][j + 1][1] + b1[1]);
+          const unsigned z1 = pack_bf16x2(acc[i][j + 1][2] + b1[2], acc[i][j + 1][3] + b1[3]);
+          const auto s0 = __builtin_amdgcn_permlane16_swap(x0, z0, false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(x1, z1, false, false);
+          unsigned w[4] = {s0[0], s1[0], s0[1], s1[1]};
+          const uint4 y = yv[j / 2][i];
+          const unsigned ys[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {  // keep a bf16 where its activation is > 0
+            const unsigned lo = ys[q] & 0xffffu, hi = ys[q] >> 16;
+            const unsigned keep = ((lo & 0x8000u) == 0u && lo != 0u ? 0x0000ffffu : 0u) |
+                                  ((hi & 0x8000u) == 0u && hi != 0u ? 0xffff0000u : 0u);
+            w[q] &= keep;
+          }
+          if (want_sum && row < p.M) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              cs[2 * q] += __uint_as_float(w[q] << 16);
+              cs[2 * q + 1] += __uint_as_float(w[q] & 0xffff0000u);
+            }
+          }
+          if (row < p.M && scol < p.N)
+            *(uint4*)((u16*)p.C + (long)row * p.ldc + scol) = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+        if (want_sum) {  // the 8 columns this lane stores, summed over the wave's rows
+          f32x4_t r0, r1;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            r0[e] = row16_sum(cs[e]);
+            r1[e] = row16_sum(cs[4 + e]);
+          }
+          if (frow == 0) {
+            float LDS_AS* d = red + wm * BN + (scol - tn * BN);
+            *(f32x4_t LDS_AS*)d = r0;
+            *(f32x4_t LDS_AS*)(d + 4) = r1;
+          }
+        }
+      }
+      };
       auto body = [&](auto has_aux) {
       constexpr bool AUX = decltype(has_aux)::value;
       [[maybe_unused]] f32x4_t bv[AUX ? 1 : FN];
@@ -657,7 +726,8 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&a
         }
       }
       };
-      if (p.aux) body(std::true_type{});
+      if (p.aux && p.act == ACT_RELU) relu_body();
+      else if (p.aux) body(std::true_type{});
       else body(std::false_type{});
       if (want_sum) {
         lds_barrier();

@@ -69,9 +69,12 @@ def test_persist_exact(dev, la, lb, bm, bn, persist):
 
 @pytest.mark.parametrize("bm,bn", [(256, 256), (128, 128), (256, 64)])
 @pytest.mark.parametrize("act", ["relu", "sigmoid"])
-def test_persist_dgrad_mask_equals_classic(dev, bm, bn, act):
+@pytest.mark.parametrize("wt", [False, True])
+def test_persist_dgrad_mask_equals_classic(dev, bm, bn, act, wt):
     """dgrad epilogue (activation derivative from the stored output) on random data: the
-    persistent form rounds the same fp32 values as the one-tile form."""
+    persistent form rounds the same fp32 values as the one-tile form (ReLU: the mask applied
+    after the 16-lane swap, 16-byte activation reads). ``wt``: B is the transposed weight
+    copy (K-major, the engine's default dgrad operand)."""
     gen = torch.Generator().manual_seed(3 + bm + bn)
     M, N, K = 1024, 512, 256  # dx[M][N] = dz[M][K] . w[K][N]
     dz = torch.randn(M, K, generator=gen).to(torch.bfloat16).to(dev)
@@ -83,7 +86,8 @@ def test_persist_dgrad_mask_equals_classic(dev, bm, bn, act):
     for persist in (0, -1):
         dx = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         cs = torch.empty(M // bm, N, device=dev)
-        ops.gemm(dz, w, dx, layout_a=KMAJ, layout_b=MNMAJ, M=M, N=N, K=K, aux=y, act=act,
+        b, lb = (w.t().contiguous(), KMAJ) if wt else (w, MNMAJ)
+        ops.gemm(dz, b, dx, layout_a=KMAJ, layout_b=lb, M=M, N=N, K=K, aux=y, act=act,
                  tiles=(bm, bn), colsum=cs, persist=persist)
         outs.append((dx, cs))
     ref = dz.float() @ w.float()
