@@ -75,8 +75,15 @@ PYBIND11_MODULE(_native, m) {
          uintptr_t colsum, long ld_colsum, uintptr_t xent_labels, int n_cls, float xent_scale,
          uintptr_t loss_part, uintptr_t correct, int k_total, int stages, int group_m,
          int persist, uintptr_t mask_out, uintptr_t mask_in, long ld_mask, uintptr_t ct,
-         long ld_ct) {
+         long ld_ct, uintptr_t upd_master, uintptr_t upd_mom, uintptr_t upd_shadow,
+         uintptr_t upd_lr, float upd_mu, float upd_wd) {
         GemmParams p{};
+        p.upd_master = P<float>(upd_master);
+        p.upd_mom = P<float>(upd_mom);
+        p.upd_shadow = P<uint16_t>(upd_shadow);
+        p.upd_lr = P<const float>(upd_lr);
+        p.upd_mu = upd_mu;
+        p.upd_wd = upd_wd;
         p.ct = P<uint16_t>(ct);
         p.ld_ct = ld_ct;
         p.group_m = group_m;
@@ -122,6 +129,10 @@ PYBIND11_MODULE(_native, m) {
               q.mask_out = R.fix(q.mask_out);
               q.mask_in = R.fix(q.mask_in);
               q.ct = R.fix(q.ct);
+              q.upd_master = R.fix(q.upd_master);
+              q.upd_mom = R.fix(q.upd_mom);
+              q.upd_shadow = R.fix(q.upd_shadow);
+              q.upd_lr = R.fix(q.upd_lr);
               return dnn::gemm_bf16(q, layout_a, layout_b, out_f32, bm, bn, splits, s, stages,
                                     persist);
             },
@@ -136,7 +147,9 @@ PYBIND11_MODULE(_native, m) {
       py::arg("loss_part") = 0, py::arg("correct") = 0, py::arg("k_total") = 0,
       py::arg("stages") = 0, py::arg("group_m") = 0, py::arg("persist") = 0,
       py::arg("mask_out") = 0, py::arg("mask_in") = 0, py::arg("ld_mask") = 0,
-      py::arg("ct") = 0, py::arg("ld_ct") = 0);
+      py::arg("ct") = 0, py::arg("ld_ct") = 0, py::arg("upd_master") = 0,
+      py::arg("upd_mom") = 0, py::arg("upd_shadow") = 0, py::arg("upd_lr") = 0,
+      py::arg("upd_mu") = 0.f, py::arg("upd_wd") = 0.f);
   m.def("gemm_default_stages", &dnn::default_stages);
 
   m.def("gemv_max_rows", []() { return dnn::GEMV_MAX_ROWS; });

@@ -52,4 +52,29 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// One SGD step on 4 elements (weight decay, optional momentum, optional bf16 shadow): shared
+// by sgd_kernel, the fused reduction (reduce_multi) and the fused-update weight-gradient
+// epilogue (gemm_tile.hpp), so every path produces the same bits.
+__device__ __forceinline__ f32x4_t sgd4(float* __restrict__ p, f32x4_t gv,
+                                        float* __restrict__ mom, u16* __restrict__ shadow,
+                                        float lr, float mu, float wd) {
+  f32x4_t pv = *(const f32x4_t*)p;
+  gv += wd * pv;
+  if (mom) {
+    f32x4_t m = *(const f32x4_t*)mom;
+    m = mu * m + gv;
+    *(f32x4_t*)mom = m;
+    gv = m;
+  }
+  pv -= lr * gv;
+  *(f32x4_t*)p = pv;
+  if (shadow) {
+    bf16x4_t o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (short)f2bf(pv[e]);
+    *(bf16x4_t*)shadow = o;
+  }
+  return pv;  // the updated weights
+}
+
 }  // namespace dnn

@@ -356,26 +356,7 @@ int reduce_slabs(const float* src, long stride, int n_src, long n, float scale, 
 // job runs the TX x TY scheme of reduce_slabs_kernel with its own TY (same fixed summation
 // order, so results are bitwise identical to reduce_slabs).
 // ------------------------------------------------------------------------------------------
-// One SGD step on 4 consecutive parameters (shared by sgd_kernel and the fused reduce).
-__device__ __forceinline__ void sgd4(float* __restrict__ p, f32x4_t gv, float* __restrict__ mom,
-                                     u16* __restrict__ shadow, float lr, float mu, float wd) {
-  f32x4_t pv = *(const f32x4_t*)p;
-  gv += wd * pv;
-  if (mom) {
-    f32x4_t m = *(const f32x4_t*)mom;
-    m = mu * m + gv;
-    *(f32x4_t*)mom = m;
-    gv = m;
-  }
-  pv -= lr * gv;
-  *(f32x4_t*)p = pv;
-  if (shadow) {
-    bf16x4_t o;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = (short)f2bf(pv[e]);
-    *(bf16x4_t*)shadow = o;
-  }
-}
+// sgd4 (one SGD step on 4 parameters) lives in common.hpp: shared with the GEMM epilogue.
 
 // One Adam / AdamW step on 4 elements (torch.optim semantics): shared by adam_kernel and the
 // fused reduction, so both paths produce the same bits.

@@ -235,7 +235,8 @@ const char* gemm_error_string(int code) {
     case -11: return "fused cross-entropy needs bf16 output, N == bn <= 128, a bias and 0 < n_cls <= N";
     case -13: return "relu bit masks need bf16 output, act = relu, ld_mask >= N/8, no aux/xent, one-tile form";
     case -12: return "pipeline stages must be 2..4 (8-wave tiles: 2..3, 256x256: 2 or 8 = ping-pong)";
-    case -14: return "transposed output ct needs bf16 output, no xent, one split, one-tile form, ld_ct >= M, 16-byte alignment";
+    case -14: return "transposed output ct needs bf16 output (or the fused update), no xent, one split, one-tile form, ld_ct >= M, 16-byte alignment";
+    case -15: return "fused SGD epilogue needs f32 output, one split, no accumulate/bias/xent, a device lr, 16-byte aligned buffers, N % 8 == 0, one-tile form";
     default: return "unknown gemm error";
   }
 }
@@ -270,9 +271,14 @@ int gemm_check(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn,
   const long a_row = la == KMAJ ? ktot : p.M;
   const long b_row = lb == KMAJ ? ktot : p.N;
   if (p.lda < a_row || p.ldb < b_row || p.ldc < p.N || (p.aux && p.ld_aux < p.N)) return -8;
-  if (p.ct && (out_f32 || p.xent_labels || splits != 1 || p.ld_ct < p.M || p.ld_ct % 8 ||
-               ((uintptr_t)p.ct & 15)))
+  if (p.ct && ((out_f32 && !p.upd_master) || p.xent_labels || splits != 1 || p.ld_ct < p.M ||
+               p.ld_ct % 8 || ((uintptr_t)p.ct & 15)))
     return -14;
+  // fused SGD epilogue: the f32 weight gradient of ONE split is consumed in place
+  if (p.upd_master && (!out_f32 || splits != 1 || p.accumulate || p.bias || p.xent_labels ||
+                       !p.upd_lr || mis(p.upd_master) || (p.upd_mom && mis(p.upd_mom)) ||
+                       (p.upd_shadow && ((uintptr_t)p.upd_shadow & 15)) || p.N % 8))
+    return -15;
   if ((p.mask_out || p.mask_in) &&
       (out_f32 || p.act != ACT_RELU || (p.mask_in && p.aux) || (p.mask_out && p.mask_in) ||
        p.xent_labels || p.ld_mask < (p.N + 7) / 8))
@@ -284,11 +290,9 @@ int gemm_bf16(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, 
               hipStream_t stream, int stages, int persist) {
   const int rc = gemm_check(p, la, lb, out_f32, bm, bn, splits);
   if (rc) return rc;
-  if (p.ct && (out_f32 || p.xent_labels || splits != 1 || p.ld_ct < p.M || p.ld_ct % 8 ||
-               ((uintptr_t)p.ct & 15)))
-    return -14;
   if ((p.mask_out || p.mask_in) && persist) return -13;
   if (p.ct && persist) return -14;
+  if (p.upd_master && persist) return -15;
 
   // (A 4-wave 256x256 form -- 128x128 per wave, one wave per SIMD, accumulators in AGPRs,
   // hipBLASLt's MT256x256 MIWT8_8 shape -- was built and measured: 7 % slower on 8192^3 fwd,

@@ -56,6 +56,15 @@ struct GemmParams {
   // wgrad reads both operands contraction-contiguous (ds_read_b128, no per-tile transpose).
   uint16_t* ct;
   long ld_ct;
+  // Optional fused SGD update (f32 output, one split, no accumulation): instead of storing the
+  // weight gradient C[m][n], the epilogue applies sgd4 to the fp32 master weights at the same
+  // [m][n] (row stride ldc), momentum, and the bf16 shadow, and (with ct) writes the new bf16
+  // weights transposed: W^T for the dgrad. lr from device memory.
+  float* upd_master;
+  float* upd_mom;
+  uint16_t* upd_shadow;
+  const float* upd_lr;
+  float upd_mu, upd_wd;
 };
 
 // Returns 0 on success, a negative code when a shape/alignment precondition fails

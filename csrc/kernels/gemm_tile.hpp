@@ -386,6 +386,24 @@ __device__ __forceinline__ void epilogue_staged(const GemmParams& p,
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] += bias_r[e];
       if constexpr (OUT_F32) {
+        if (p.upd_master) {  // uniform: fused SGD of the weights this gradient belongs to
+          const long off = gm * p.ldc + gn;
+          const float lr = *p.upd_lr;
+          const f32x4_t w0 = sgd4(p.upd_master + off, f32x4_t{v[0], v[1], v[2], v[3]},
+                                  p.upd_mom ? p.upd_mom + off : nullptr,
+                                  p.upd_shadow ? p.upd_shadow + off : nullptr, lr, p.upd_mu,
+                                  p.upd_wd);
+          const f32x4_t w1 = sgd4(p.upd_master + off + 4, f32x4_t{v[4], v[5], v[6], v[7]},
+                                  p.upd_mom ? p.upd_mom + off + 4 : nullptr,
+                                  p.upd_shadow ? p.upd_shadow + off + 4 : nullptr, lr,
+                                  p.upd_mu, p.upd_wd);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            ov[it][e] = (short)f2bf(w0[e]);
+            ov[it][e + 4] = (short)f2bf(w1[e]);
+          }
+          continue;
+        }
         float* c = (float*)p.C + (long)split * p.c_split_stride + gm * p.ldc + gn;
         if (!p.accumulate && p.act != ACT_LINEAR) {
 #pragma unroll
@@ -425,8 +443,9 @@ __device__ __forceinline__ void epilogue_staged(const GemmParams& p,
         if (p.mask_out) p.mask_out[gm * p.ld_mask + (gn >> 3)] = (unsigned char)bits;
       }
     }
-    if constexpr (!OUT_F32) {
-      if (p.ct) {  // uniform: transposed copy of this chunk through LDS (bf16 [BN][rows])
+    {
+      if (p.ct) {  // uniform: transposed copy of this chunk through LDS (bf16 [BN][rows]):
+                   // the stored bf16 output, or (fused update) the new bf16 weights
         // bf16 [BN][TLD] transposed tile. The 8-row block of a row index is XOR-swizzled by
         // the column's 8-column group (sw): together with the +8 pad, the 2-byte writes of a
         // half-wave (32 column groups, one row) spread over 16 banks instead of 2, and every

@@ -92,6 +92,9 @@ class StageParams:
         # transposed bf16 weight shadows W^T[Kp][Np] of the layers whose dgrad reads them
         # (enable_wt); refreshed after every update of their layer (refresh_t)
         self.wt: dict[int, torch.Tensor] = {}
+        # layers whose weight gradient GEMM applies the SGD step itself (Stage.enable_fused_
+        # wgrad_update): the per-step update paths below skip their weights and W^T
+        self.fused_layers: set[int] = set()
         self._init_state()
 
     def _init_state(self):
@@ -166,10 +169,13 @@ class StageParams:
             self.wt[i] = torch.zeros(g.kp, g.np_, dtype=torch.bfloat16, device=self.device)
             ops.transpose_bf16(self.wbf(i), self.wt[i])
 
-    def refresh_t(self, a: int = 0, b: Optional[int] = None) -> None:
-        """Re-derive W^T of the local layers [a, b) that keep one (after their update)."""
+    def refresh_t(self, a: int = 0, b: Optional[int] = None, step: bool = False) -> None:
+        """Re-derive W^T of the local layers [a, b) that keep one (after their update).
+        ``step``: a per-step update -- layers updated by their wgrad epilogue (which writes
+        W^T itself) are skipped."""
         b = len(self.geoms) if b is None else b
-        ops.transpose_multi([(self.wbf(i), self.wt[i]) for i in range(a, b) if i in self.wt])
+        ops.transpose_multi([(self.wbf(i), self.wt[i]) for i in range(a, b) if i in self.wt and
+                             not (step and i in self.fused_layers)])
 
     def _layers_of(self, e0: int, e1: int) -> tuple[int, int]:
         """Local layers whose parameters lie in the flat element range [e0, e1)."""
@@ -230,11 +236,33 @@ class StageParams:
         if getattr(self, "step_dev", None) is not None:
             self.step_dev.fill_(int(n))
 
+    def _unfused_ranges(self) -> list[tuple[int, int]]:
+        """[0, numel) minus the weight regions of fused_layers (updated by their wgrad)."""
+        cuts = sorted((self.w_off[i], self.w_off[i] + self.geoms[i].np_ * self.geoms[i].kp)
+                      for i in self.fused_layers)
+        out, lo = [], 0
+        for a, b in cuts:
+            if a > lo:
+                out.append((lo, a))
+            lo = b
+        if lo < self.numel:
+            out.append((lo, self.numel))
+        return out
+
     def record_update(self) -> None:
         """The launches of one optimizer update reading lr / step from device memory (for
         recording into a native Program: no per-step host values)."""
         self._device_scalars()
         o = self.optim
+        if self.fused_layers:  # SGD only (Stage.enable_fused_wgrad_update)
+            for a, b in self._unfused_ranges():
+                sl = slice(a, b)
+                ops.sgd_update(self.master[sl], self.grad[sl],
+                               self.state[0][sl] if self.state else None, self.shadow[sl],
+                               lr=o.lr, momentum=o.momentum, weight_decay=o.weight_decay,
+                               lr_dev=self.lr_dev)
+            self.refresh_t(step=True)
+            return
         if o.name == "sgd":
             ops.sgd_update(self.master, self.grad, self.state[0] if self.state else None,
                            self.shadow, lr=o.lr, momentum=o.momentum,
@@ -245,7 +273,7 @@ class StageParams:
                             decoupled=o.decoupled or o.name == "adamw", lr_dev=self.lr_dev,
                             step_dev=self.step_dev)
             ops.step_advance(self.step_dev)
-        self.refresh_t()
+        self.refresh_t(step=True)
 
     def record_update_range(self, a: int, b: int, advance: bool, refresh: bool = True) -> None:
         """record_update over the flat element range [a, b) only (a DP bucket of whole layers);
@@ -356,7 +384,7 @@ class StageParams:
             ops.adam_update(self.master, self.grad, self.state[0], self.state[1], self.shadow,
                             lr=lr, betas=o.betas, eps=o.eps, weight_decay=o.weight_decay,
                             decoupled=o.decoupled or o.name == "adamw", step=self.step_count)
-        self.refresh_t()
+        self.refresh_t(step=True)
 
 
 class Stage:
@@ -706,9 +734,13 @@ class Stage:
             else:
                 r, acc = self.rows_of(j), self._w_done > 0
             if j < 0 or self.wgrad_mode != "batched":
+                fused = self.params.fused_layers
+                idx = [i for i in range(len(self.geoms)) if i not in fused]
                 items = [(self.dz[i][r], self.input_of(i)[r], self.slabs[i], self.w_splits[i],
-                          acc) for i in range(len(self.geoms))]
-                for i in ops.linear_wgrad_group(items):
+                          acc) for i in idx]
+                for k in ops.linear_wgrad_group(items):
+                    self.wgrad_layer(idx[k], j)
+                for i in sorted(fused):
                     self.wgrad_layer(i, j)
                 return
         for i in range(len(self.geoms)):
@@ -734,10 +766,22 @@ class Stage:
                                      accumulate=accumulate)
         else:
             kk = j < 0 and i in self.dzT
+            upd = wt = None
+            p = self.params
+            if i in p.fused_layers:  # the epilogue applies SGD to W_i and writes W_i^T
+                if j >= 0:
+                    raise RuntimeError("fused weight update runs on the batched wgrad only")
+                p._device_scalars()
+                g, o = self.geoms[i], p.optim
+                w0, w1 = p.w_off[i], p.w_off[i] + g.np_ * g.kp
+                upd = dict(master=p.w32(i), shadow=p.wbf(i), lr_dev=p.lr_dev,
+                           mom=p.state[0][w0:w1].view(g.np_, g.kp) if p.state else None,
+                           momentum=o.momentum, weight_decay=o.weight_decay)
+                wt = p.wt.get(i)
             ops.linear_wgrad(self.dz[i][r], self.input_of(i)[r], self.slabs[i],
                              splits=self.w_splits[i], accumulate=accumulate,
                              dzt=self.dzT[i] if kk else None,
-                             xt=self.actT[i - 1] if kk else None)
+                             xt=self.actT[i - 1] if kk else None, upd=upd, wt=wt)
 
     def finalize_grads(self, layers: Optional[Sequence[int]] = None) -> None:
         """Reduce bias partials (and, for split-K, weight slabs) into the flat gradient."""
@@ -762,7 +806,7 @@ class Stage:
             for i in key:
                 g = self.geoms[i]
                 n = g.np_ * g.kp
-                if self.wgrad_algo != "streamk":
+                if self.wgrad_algo != "streamk" and i not in p.fused_layers:
                     jobs.append((self.slabs[i], self.w_splits[i], n, n, p.gw(i), 1.0, False))
                 jobs.append((self.bpart[i], self.bpart[i].shape[0], g.np_, g.np_, p.gb(i), 1.0,
                              False))
@@ -788,7 +832,7 @@ class Stage:
                                             mom=p.state[0] if p.state else None,
                                             shadow=p.shadow, lr=o.lr, momentum=o.momentum,
                                             weight_decay=o.weight_decay, lr_dev=p.lr_dev))
-            p.refresh_t()
+            p.refresh_t(step=True)
             return
         ops.reduce_multi(jobs, sgd=dict(grad=p.grad, master=p.master, mom=p.state[0],
                                         v=p.state[1], shadow=p.shadow, lr=o.lr,
@@ -797,7 +841,7 @@ class Stage:
                                         decoupled=o.decoupled or o.name == "adamw",
                                         step_dev=p.step_dev))
         ops.step_advance(p.step_dev)  # as record_update: the segment replaces FIN + O
-        p.refresh_t()
+        p.refresh_t(step=True)
 
     def update_then_forward(self, j: int, s: int, lr: Optional[float] = None) -> None:
         """Deferred DP update of layers [s, L) (completing the step: advance) followed by the
@@ -827,6 +871,22 @@ class Stage:
         for i in ls:
             self.wgrad_layer(i)
         self.finalize_grads(sorted(ls))
+
+    def enable_fused_wgrad_update(self) -> list[int]:
+        """Layers whose weight gradient is ONE split (big layers: the wide model's 8192x8192)
+        apply the SGD step in their wgrad GEMM's epilogue (ops.linear_wgrad upd): no fp32
+        gradient round trip through HBM, no separate update pass over those weights, and W^T
+        written by the same epilogue instead of a transpose launch. Only without data
+        parallelism (the gradient must be complete where it is produced) and for SGD; call
+        before compile_native. Returns the layers."""
+        p = self.params
+        if (self.device.type != "cuda" or self.wgrad_mode != "batched" or
+                self.wgrad_algo != "splitk" or p.optim.name != "sgd" or p.sharded or
+                switches.get("DNN_WGRAD_FUSED_UPDATE") == "0" or self._prog is not None):
+            return []
+        p.fused_layers = {i for i in range(len(self.geoms)) if self.w_splits[i] == 1}
+        self._reduce_jobs.clear()
+        return sorted(p.fused_layers)
 
     def shard_update(self, e0: int, e1: int, lr: Optional[float] = None) -> None:
         """Sharded DP: unpack this rank's reduced piece of bucket [e0, e1) and update it (no
@@ -934,7 +994,7 @@ class Stage:
                 self._record_fin_sgd()
             prog.mark("O")
             self.params.record_update()
-            for a in range(L if not self.params.sharded else 0):
+            for a in range(L if not (self.params.sharded or self.params.fused_layers) else 0):
                 # split updates: every contiguous layer range, no step advance
                 for b in range(a + 1, L + 1):
                     prog.mark(f"O{a}-{b}")

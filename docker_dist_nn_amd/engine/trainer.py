@@ -123,6 +123,11 @@ class Trainer:
             sync = (GradSync(mesh.dp_group, mesh.dp, shard=self.dp_reduce == "shard")
                     if mesh.dp > 1 or self.dp_reduce == "shard" else None)
         self.executor = PipelineExecutor(self.stages, self.pipe, schedule, pp, ids, sync)
+        # one-split weight gradients update their weights in the GEMM epilogue (no DP: the
+        # gradient is complete where it is produced)
+        if mesh is None or (mesh.dp == 1 and self.dp_reduce != "shard"):
+            for st in self.stages:
+                st.enable_fused_wgrad_update()
         # native step executor: record each stage's launches once, replay from C++ (after the
         # pipe has aliased loopback buffers, so the recorded pointers are the final ones)
         if native_exec is None:

@@ -223,7 +223,7 @@ def wgrad_config(M: int, N: int, K_total: int, max_splits: int = 48) -> tuple[in
 def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=None, aux=None,
          act=0, accumulate: bool = False, splits: int = 1, tiles: tuple[int, int] | None = None,
          colsum=None, k_total: int = 0, stages: int = 0, group_m: int = 0, persist: int = 0,
-         mask_out=None, mask_in=None, ct=None):
+         mask_out=None, mask_in=None, ct=None, upd=None):
     """C (+)= epilogue(A.B). See csrc/kernels/gemm.hpp for the layout/epilogue contract.
 
     ``persist`` != 0 runs the persistent-workgroup form with the register-direct epilogue
@@ -251,12 +251,34 @@ def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=
                               m.shape[0] < M or m.shape[1] < -(-N // 8)):
             raise ValueError(f"relu mask must be uint8 [{M}][>={-(-N // 8)}] row-major")
     if ct is not None and (ct.dtype != torch.bfloat16 or ct.dim() != 2 or ct.stride(1) != 1 or
-                           ct.shape[0] < N or ct.shape[1] < M or out_f32):
+                           ct.shape[0] < N or ct.shape[1] < M or (out_f32 and upd is None)):
         raise ValueError(f"ct must be a bf16 [>={N}][>={M}] row-major transposed output")
+    if upd is not None:
+        # fused SGD epilogue (f32 output of one split): the gradient updates the weights in place
+        # -- upd = dict(master=fp32 [M][N] view (row stride = C's), mom=None | same shape,
+        # shadow=None | bf16 same shape, lr_dev=fp32 [1], momentum, weight_decay); ct = W^T
+        if not out_f32 or splits != 1 or accumulate or bias is not None:
+            raise ValueError("fused update: f32 output, one split, no accumulation / bias")
+        for k in ("master", "mom", "shadow"):
+            t = upd.get(k)
+            if t is not None and (t.dim() != 2 or t.stride(1) != 1 or t.shape[0] < M or
+                                  t.shape[1] < N or t.stride(0) != (c if c.dim() == 2
+                                                                    else c[0]).stride(0)):
+                raise ValueError(f"fused update: {k} must be [M][N] with C's row stride")
     if not a.is_cuda:
         ref.gemm(a, b, c, layout_a=layout_a, layout_b=layout_b, M=M, N=N, K=K, bias=bias,
                  aux=aux, act=act, accumulate=accumulate, splits=splits, colsum=colsum,
                  colsum_rows=tiles[0] if tiles else 0, k_total=k_total)
+        if upd is not None:
+            g = (c if c.dim() == 2 else c[0])[:M, :N]
+            mom = upd.get("mom")
+            sh = upd.get("shadow")
+            ref.sgd_update(upd["master"][:M, :N], g, mom[:M, :N] if mom is not None else None,
+                           sh[:M, :N] if sh is not None else None, float(upd["lr_dev"][0]),
+                           upd.get("momentum", 0.0), upd.get("weight_decay", 0.0))
+            if ct is not None:
+                ct[:N, :M] = upd["master"][:M, :N].t().to(torch.bfloat16)
+            return c
         if ct is not None:
             ct[:N, :M] = c[:M, :N].t()
         return c
@@ -297,7 +319,12 @@ def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=
                        mask_out=_p(mask_out), mask_in=_p(mask_in),
                        ld_mask=(mask_out if mask_out is not None else mask_in).stride(0)
                        if (mask_out is not None or mask_in is not None) else 0,
-                       ct=_p(ct), ld_ct=ct.stride(0) if ct is not None else 0)
+                       ct=_p(ct), ld_ct=ct.stride(0) if ct is not None else 0,
+                       **({} if upd is None else dict(
+                           upd_master=_p(upd["master"]), upd_mom=_p(upd.get("mom")),
+                           upd_shadow=_p(upd.get("shadow")), upd_lr=_p(upd["lr_dev"]),
+                           upd_mu=float(upd.get("momentum", 0.0)),
+                           upd_wd=float(upd.get("weight_decay", 0.0)))))
     return c
 
 
@@ -509,13 +536,18 @@ def linear_dgrad(dz, w, dx, y_prev=None, act_prev="linear", colsum=None, mask_pr
                 else _persist("dgrad", t), mask_in=mask_prev, ct=dxt)
 
 
-def linear_wgrad(dz, x, slabs, splits=1, accumulate=False, dzt=None, xt=None):
+def linear_wgrad(dz, x, slabs, splits=1, accumulate=False, dzt=None, xt=None, upd=None,
+                 wt=None):
     """slabs[s][Np][Kp] (+)= dz[rows_s]^T . x[rows_s] over the batch rows of split s (fp32).
     ``dzt`` / ``xt`` (bf16 [Np][R] / [Kp][R], written transposed by the producing GEMMs'
     epilogues): the contraction runs K-major on both operands (the forward's main loop,
-    bench/layout_ab.py: 1.2x on 8192x8192 weights); same k order, same result bits."""
+    bench/layout_ab.py: 1.2x on 8192x8192 weights); same k order, same result bits.
+    ``upd`` (one split): the epilogue applies the SGD step to the layer's weights instead of
+    storing the gradient (ops.gemm), and writes the new bf16 weights transposed into ``wt``."""
     R, N = dz.shape
     K = x.shape[1]
+    if upd is not None and (splits != 1 or accumulate):
+        raise ValueError("the fused weight update needs one split and no accumulation")
     if dzt is not None and xt is not None and dz.is_cuda:
         bm, bn, s = wgrad_config(N, K, R)
         tiles = (bm, bn) if s == splits else pick_tiles(N, K, splits)
@@ -523,13 +555,14 @@ def linear_wgrad(dz, x, slabs, splits=1, accumulate=False, dzt=None, xt=None):
         return gemm(dzt, xt, slabs, layout_a=KMAJ, layout_b=KMAJ, M=N, N=K, K=R, k_total=R,
                     accumulate=accumulate, splits=splits, tiles=tiles,
                     stages=STAGES["wgrad"] or (t or {}).get("stages", 0),
-                    persist=_persist("wgrad", t))
+                    persist=0 if upd is not None else _persist("wgrad", t), upd=upd, ct=wt)
     if R % 64 or splits > R // 64:
         raise ValueError("rows must be a multiple of 64 with at least 64 rows per split")
     bm, bn, s = wgrad_config(N, K, R)
     tiles = (bm, bn) if s == splits else pick_tiles(N, K, splits)
     t = tuning.lookup("wgrad", N, K, R) if s == splits else None
-    if splits == 1 and dz.is_cuda and _blas("wgrad", tuning.lookup("wgrad", N, K, R)) and \
+    if upd is None and splits == 1 and dz.is_cuda and \
+            _blas("wgrad", tuning.lookup("wgrad", N, K, R)) and \
             _blas_ok(dz, x, slabs[0], True, False, N, K, R, None, False, accumulate):
         return blas_gemm(dz, x, slabs[0], trans_a=True, trans_b=False, M=N, N=K, K=R,
                          accumulate=accumulate,
@@ -537,7 +570,7 @@ def linear_wgrad(dz, x, slabs, splits=1, accumulate=False, dzt=None, xt=None):
     return gemm(dz, x, slabs, layout_a=MNMAJ, layout_b=MNMAJ, M=N, N=K, K=R, k_total=R,
                 accumulate=accumulate, splits=splits, tiles=tiles,
                 stages=STAGES["wgrad"] or (t or {}).get("stages", 0),
-                persist=_persist("wgrad", t))
+                persist=0 if upd is not None else _persist("wgrad", t), upd=upd, ct=wt)
 
 
 def linear_wgrad_group(items) -> list:

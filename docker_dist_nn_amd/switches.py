@@ -31,6 +31,8 @@ SWITCHES: dict[str, tuple[str, str]] = {
     "DNN_WGRAD_ALGO": ("splitk", "weight-gradient algorithm: splitk | streamk"),
     "DNN_WGRAD_GROUP": ("1", "one grouped launch for small split-K weight gradients"),
     "DNN_FUSE_FIN_SGD": ("1", "gradient reduction and optimizer step in one launch (FINO)"),
+    "DNN_WGRAD_FUSED_UPDATE": ("1", "one-split weight gradients apply SGD (and write W^T) in "
+                                    "their GEMM epilogue; no data parallelism"),
     "DNN_NATIVE_EXEC": ("1", "record each stage's launches once and replay them from C++"),
     "DNN_NATIVE_PLAN": ("1", "single-process pipeline step as one native call"),
     "DNN_LOOPBACK_STREAMS": ("1", "single-process pipeline: one stream per stage, event edges "

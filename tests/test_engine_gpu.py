@@ -192,3 +192,41 @@ def test_kmajor_wgrad_training_bitwise(dev, monkeypatch, model):
         out.append(tr.local_weights())
     for k in out[0]:
         assert np.array_equal(out[0][k][0], out[1][k][0]), k
+
+
+def test_fused_wgrad_update_bitwise(dev, monkeypatch):
+    """One-split weight gradients that apply SGD (momentum + weight decay) and write W^T in
+    their GEMM epilogue (Stage.enable_fused_wgrad_update) train bit-identically to the
+    separate reduction + update + transpose."""
+    import numpy as np
+
+    from docker_dist_nn_amd import MLPSpec
+    from docker_dist_nn_amd.data import synthetic_mnist
+    from docker_dist_nn_amd.engine import OptimConfig, Trainer
+
+    rows = 2048
+    x, y = synthetic_mnist(rows, seed=3)
+    xb = torch.zeros(rows, 832, dtype=torch.bfloat16)
+    xb[:, :784] = torch.from_numpy(x).to(torch.bfloat16)
+    xd, yd = xb.to(dev), torch.from_numpy(y).to(dev)
+    out = {}
+    for fused in ("0", "1"):
+        monkeypatch.setenv("DNN_WGRAD_FUSED_UPDATE", fused)
+        tr = Trainer(MLPSpec.parse("784-8192-8192-10"), micro_batch=rows, num_micro=1,
+                     device=dev, optim=OptimConfig(lr=0.02, momentum=0.9, weight_decay=1e-4))
+        p = tr.stages[0].params
+        assert bool(p.fused_layers) == (fused == "1")
+        if fused == "1":
+            assert 1 in p.fused_layers and 1 in p.wt
+        for _ in range(3):
+            tr.set_batch(xd, yd)
+            tr.step()
+        torch.cuda.synchronize(dev)
+        out[fused] = (tr.local_weights(), tr.loss(), p.wt[1].cpu().clone(),
+                      p.state[0].cpu().clone())
+    for k, (w, b) in out["0"][0].items():
+        assert np.array_equal(w, out["1"][0][k][0]), k
+        assert np.array_equal(b, out["1"][0][k][1]), k
+    assert out["0"][1] == out["1"][1]
+    assert torch.equal(out["0"][2], out["1"][2])  # W^T written by the epilogue
+    assert torch.equal(out["0"][3], out["1"][3])  # momentum
