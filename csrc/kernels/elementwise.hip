@@ -761,6 +761,67 @@ __global__ void p2p_signal_kernel(unsigned* flag, unsigned value) {
   if (l == 0) __hip_atomic_store(flag + l, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Device-sequence forms (graph-capturable step plans): the step number lives in device memory
+// and is advanced by a kernel at the start of every step, so a captured plan replays with the
+// right flag values. The wait spins ONE lane on the flag (system-scope acquire loads, s_sleep
+// between polls) and gives up after `timeout_ns`, recording the failure in *err instead of
+// hanging the queue: every wave of the kernel always finishes.
+__global__ void p2p_seq_advance_kernel(unsigned* seq) {
+  const unsigned l = threadIdx.x;
+  if (l == 0) seq[l] = seq[l] + 1u;
+}
+
+__global__ void p2p_signal_seq_kernel(unsigned* flag, const unsigned* seq, int delta) {
+  const unsigned l = threadIdx.x;
+  if (l == 0)
+    __hip_atomic_store(flag + l, seq[l] + (unsigned)delta, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void p2p_wait_seq_kernel(const unsigned* flag, const unsigned* seq, int delta,
+                                    unsigned* err, unsigned long long timeout_ticks) {
+  const unsigned l = threadIdx.x;
+  if (l != 0) return;
+  const unsigned target = seq[l] + (unsigned)delta;
+  const unsigned long long t0 = wall_clock64();
+  // wrapping step counters: "reached" = (int)(flag - target) >= 0
+  while ((int)(__hip_atomic_load(flag + l, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) -
+               target) < 0) {
+    __builtin_amdgcn_s_sleep(4);
+    if (wall_clock64() - t0 > timeout_ticks) {
+      __hip_atomic_store(err + l, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+  }
+}
+
+int p2p_seq_advance(uint32_t* seq, hipStream_t stream) {
+  hipLaunchKernelGGL(p2p_seq_advance_kernel, dim3(1), dim3(64), 0, stream, seq);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
+int p2p_signal_seq(uint32_t* flag, const uint32_t* seq, int delta, hipStream_t stream) {
+  if (reinterpret_cast<uintptr_t>(flag) & 3) return -1;
+  hipLaunchKernelGGL(p2p_signal_seq_kernel, dim3(1), dim3(64), 0, stream, flag, seq, delta);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
+int p2p_wait_seq(const uint32_t* flag, const uint32_t* seq, int delta, uint32_t* err,
+                 double timeout_s, hipStream_t stream) {
+  if (reinterpret_cast<uintptr_t>(flag) & 3) return -1;
+  static int rate_khz = [] {  // wall_clock64 ticks per ms (100 MHz on gfx9)
+    int r = 0, dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess)
+      (void)hipDeviceGetAttribute(&r, hipDeviceAttributeWallClockRate, dev);
+    return r > 0 ? r : 100000;
+  }();
+  const unsigned long long ticks =
+      (unsigned long long)(timeout_s * 1e3 * (double)rate_khz);
+  hipLaunchKernelGGL(p2p_wait_seq_kernel, dim3(1), dim3(64), 0, stream, flag, seq, delta, err,
+                     ticks);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
 int p2p_copy(void* dst, const void* src, size_t bytes, hipStream_t stream) {
   if (bytes == 0) return 0;
   if ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) return -1;

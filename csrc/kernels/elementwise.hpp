@@ -99,5 +99,11 @@ int dequant_rows_fp8(const unsigned char* q, long ldq, const float* scale, int r
 // Peer copy (16-byte aligned) and flag write as kernels: never block the issuing host thread.
 int p2p_copy(void* dst, const void* src, size_t bytes, hipStream_t stream);
 int p2p_signal(uint32_t* flag, uint32_t value, hipStream_t stream);
+// Device-sequence flag protocol (graph-capturable): seq advanced in-stream, signal writes
+// *seq + delta, wait spins until flag >= *seq + delta or times out (sets *err).
+int p2p_seq_advance(uint32_t* seq, hipStream_t stream);
+int p2p_signal_seq(uint32_t* flag, const uint32_t* seq, int delta, hipStream_t stream);
+int p2p_wait_seq(const uint32_t* flag, const uint32_t* seq, int delta, uint32_t* err,
+                 double timeout_s, hipStream_t stream);
 
 }  // namespace dnn

@@ -1,5 +1,6 @@
 #include "runtime/step_plan.hpp"
 #include "runtime/p2p.hpp"
+#include "kernels/elementwise.hpp"
 
 #include <dlfcn.h>
 
@@ -76,6 +77,33 @@ StepPlan::StepPlan(int n_streams, int n_events) {
     events_.push_back(e);
   }
   ck(hipEventCreateWithFlags(&fork_, hipEventDisableTiming), "hipEventCreate");
+  ck(hipMalloc(&dev_, 2 * sizeof(uint32_t)), "hipMalloc");
+  ck(hipMemset(dev_, 0, 2 * sizeof(uint32_t)), "hipMemset");
+  ck(hipDeviceSynchronize(), "hipDeviceSynchronize");
+}
+
+void StepPlan::set_seq(uint32_t s) {
+  if (s == seq_) return;
+  seq_ = s;
+  ck(hipMemcpy(dev_, &s, sizeof(s), hipMemcpyHostToDevice), "hipMemcpy");
+}
+
+void StepPlan::sync_seq() {
+  ck(hipMemcpy(&seq_, dev_, sizeof(seq_), hipMemcpyDeviceToHost), "hipMemcpy");
+}
+
+uint32_t StepPlan::flag_timeouts() const {
+  uint32_t e = 0;
+  ck(hipMemcpy(&e, dev_ + 1, sizeof(e), hipMemcpyDeviceToHost), "hipMemcpy");
+  return e;
+}
+
+static double wait_timeout_s() {
+  static const double t = [] {
+    const char* e = std::getenv("DNN_FLAG_TIMEOUT");
+    return e ? std::atof(e) : 120.0;
+  }();
+  return t;
 }
 
 StepPlan::~StepPlan() {
@@ -83,6 +111,7 @@ StepPlan::~StepPlan() {
   for (auto e : join_) (void)hipEventDestroy(e);
   if (fork_) (void)hipEventDestroy(fork_);
   for (auto s : streams_) (void)hipStreamDestroy(s);
+  if (dev_) (void)hipFree(dev_);
 }
 
 void StepPlan::add(const Op& op) {
@@ -121,6 +150,7 @@ static bool plan_trace() {
 
 void StepPlan::run(hipStream_t main) {
   ++seq_;
+  if (p2p_seq_advance(dev_, main) != 0) throw std::runtime_error("p2p_seq_advance failed");
   ck(hipEventRecord(fork_, main), "hipEventRecord");
   for (auto s : streams_) ck(hipStreamWaitEvent(s, fork_, 0), "hipStreamWaitEvent");
   std::vector<std::string> one(1);
@@ -167,14 +197,14 @@ void StepPlan::run(hipStream_t main) {
       case COPY:  // kernels, not hipMemcpyAsync / hipStreamWriteValue32 (runtime/p2p.cpp)
         copy_async(reinterpret_cast<void*>(o.b), reinterpret_cast<const void*>(o.a), o.count, s);
         break;
-      case SIGNAL:
-        signal_u32(s, reinterpret_cast<void*>(o.a), (uint32_t)((int64_t)seq_ + o.delta));
+      case SIGNAL:  // flag = device step number + delta (kernels: capturable, non-blocking)
+        if (p2p_signal_seq(reinterpret_cast<uint32_t*>(o.a), dev_, (int)o.delta, s) != 0)
+          throw std::runtime_error("p2p_signal_seq failed");
         break;
       case WAITV:
-        ck(hipStreamWaitValue32(s, reinterpret_cast<void*>(o.a),
-                                (uint32_t)((int64_t)seq_ + o.delta), hipStreamWaitValueGte,
-                                0xFFFFFFFFu),
-           "hipStreamWaitValue32");
+        if (p2p_wait_seq(reinterpret_cast<const uint32_t*>(o.a), dev_, (int)o.delta, dev_ + 1,
+                         wait_timeout_s(), s) != 0)
+          throw std::runtime_error("p2p_wait_seq failed");
         break;
       case REC:
         ck(hipEventRecord(events_[o.event], s), "hipEventRecord");

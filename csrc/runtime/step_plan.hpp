@@ -76,7 +76,13 @@ class StepPlan {
   // One step on `main`; advances the sequence number first (seq() = 1 in the first step).
   void run(hipStream_t main);
   uint32_t seq() const { return seq_; }
-  void set_seq(uint32_t s) { seq_ = s; }
+  // Sets the step number (host mirror and the device counter the flag kernels read); not
+  // during a capture.
+  void set_seq(uint32_t s);
+  // Flag waits that timed out (device error word; reading it synchronises the device).
+  uint32_t flag_timeouts() const;
+  // Host mirror := device step number (after graph replays advanced it on the device).
+  void sync_seq();
   size_t size() const { return ops_.size(); }
   int n_streams() const { return (int)streams_.size() + 1; }
   // RCCL async-error poll over every communicator the plan uses (0 = healthy).
@@ -90,6 +96,8 @@ class StepPlan {
   std::vector<hipEvent_t> join_;
   std::vector<Op> ops_;
   uint32_t seq_ = 0;
+  // [0] = step number read by the SIGNAL / WAITV kernels, [1] = wait-timeout error word
+  uint32_t* dev_ = nullptr;
 };
 
 }  // namespace dnn

@@ -220,8 +220,9 @@ class Trainer:
         Every buffer is allocated up front, so replay touches fixed pointers. The capture runs
         on a private stream (the legacy null stream cannot be captured); replay is ordered
         against the caller's stream with events. Capturing executes the step once for real."""
-        if self.mesh is not None or self.device.type != "cuda":
-            raise RuntimeError("graph capture is for the local GPU path")
+        if self.device.type != "cuda" or (self.mesh is not None and self.native_step is None):
+            raise RuntimeError("graph capture needs the local GPU path or a native "
+                               "multi-rank step (parallel/native_step.py)")
         cur = torch.cuda.current_stream(self.device)
         self._stream = torch.cuda.Stream(self.device)
         self._stream.wait_stream(cur)
@@ -250,10 +251,21 @@ class Trainer:
         self._graph = graphs[0]
         self.graph_nodes = graphs[0].num_nodes
         torch.cuda.synchronize(self.device)
+        ns = self.native_step
+        if ns is not None:  # captures advanced only the host mirror of the step number
+            ns.plan.sync_seq()
+            if ns.ipc is not None:
+                ns.ipc.seq = ns.plan.seq
 
     def release_graph(self) -> None:
         self._graph = None
         self._graphs = []
+        ns = self.native_step
+        if ns is not None:  # replays advanced the device step number only
+            torch.cuda.synchronize(self.device)
+            ns.plan.sync_seq()
+            if ns.ipc is not None:
+                ns.ipc.seq = ns.plan.seq
 
     # -------------------------------------------------------------------------------------
     def loss(self) -> Optional[float]:

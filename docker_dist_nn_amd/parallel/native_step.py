@@ -333,7 +333,12 @@ class NativeStep:
         p.step_count += 1
 
     def comm_error(self) -> int:
-        return self.plan.comm_error()
+        """RCCL async error of any communicator of the plan, or -1 if a flag wait (IPC hop)
+        timed out (DNN_FLAG_TIMEOUT seconds)."""
+        rc = self.plan.comm_error()
+        if rc == 0 and self.transport == "ipc" and self.plan.flag_timeouts():
+            return -1
+        return rc
 
     def describe(self) -> dict:
         kinds = {}

@@ -131,7 +131,8 @@ def test_pp2_ipc_pipe_bitwise_equals_rccl_path(dev):
             assert np.array_equal(a, b), k
 
 
-def _native_worker(rank, world, port, native_dist, steps, nm, out_dir, relays=0, tag=None):
+def _native_worker(rank, world, port, native_dist, steps, nm, out_dir, relays=0, tag=None,
+                   graph=False):
     # every stream of a plan that waits on a flag needs a hardware queue of its own (HIP
     # multiplexes streams beyond GPU_MAX_HW_QUEUES onto shared queues, where one blocked wait
     # would stall the others): 4 plan streams + the relay duties + the default stream
@@ -157,8 +158,13 @@ def _native_worker(rank, world, port, native_dist, steps, nm, out_dir, relays=0,
     xt, yt = _batch(256 * nm)
     xd, yd = xt.to(dev), yt.to(dev)
     host = []
-    for _ in range(steps):
-        tr.set_batch(xd if tr.first else None, yd if tr.last else None, zero_copy=True)
+    done = 0
+    if graph:  # one eager warm-up step + the capture's executed step, then replays
+        tr.set_batch(xd if tr.first else None, yd if tr.last else None)
+        tr.capture(warmup=1)
+        done = 2
+    for _ in range(steps - done):
+        tr.set_batch(xd if tr.first else None, yd if tr.last else None, zero_copy=not graph)
         t0 = time.perf_counter()
         tr.step()
         host.append(time.perf_counter() - t0)
@@ -214,6 +220,29 @@ def test_relayed_ipc_hops_bitwise_equal_direct(dev, world, relays):
             assert np.array_equal(a, b), k
         assert np.array_equal(np.load(os.path.join(d, "ndirect_loss.npy")),
                               np.load(os.path.join(d, "nrelay_loss.npy")))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_native_multirank_step_graph_capture(dev, world):
+    """The native multi-rank step (IPC hops: device step-number flag kernels) captured into a
+    HIP graph and replayed gives bit-identical training to eager plan runs, and a replayed
+    step costs the host only the graph launch."""
+    steps, nm = 6, 4
+    with tempfile.TemporaryDirectory() as d:
+        for tag, graph in (("eager", False), ("graph", True)):
+            mp.start_processes(_native_worker,
+                               args=(world, _free_port(), "1", steps, nm, d, 0, tag, graph),
+                               nprocs=world, join=True, start_method="spawn")
+        for k in range(4):
+            a = np.load(os.path.join(d, f"neager_w{k}.npy"))
+            b = np.load(os.path.join(d, f"ngraph_w{k}.npy"))
+            assert np.array_equal(a, b), k
+        assert np.array_equal(np.load(os.path.join(d, "neager_loss.npy")),
+                              np.load(os.path.join(d, "ngraph_loss.npy")))
+        host = [float(np.median(np.load(os.path.join(d, f"ngraph_host_r{r}.npy"))))
+                for r in range(world)]
+        print("graph replay host s/step per rank:", host)
+        assert max(host) < 5e-4, host
 
 
 def test_step_plan_rccl_allreduce_one_rank(dev):
