@@ -36,8 +36,11 @@ import time
 # onto GPU_MAX_HW_QUEUES hardware queues (default 4) in order, so two streams sharing a queue
 # would serialise a spinning RCCL receive in one direction with a send in the other. Give
 # every stream its own queue (set before the HIP runtime initialises; <= 32 by pool policy).
-if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+# The box exports GPU_MAX_HW_QUEUES=4 (HIP's default), so raise it rather than setdefault;
+# one-GPU rehearsals (DNN_FORCE_DEVICE: many ranks share one GPU) keep what the caller set.
+if int(os.environ.get("WORLD_SIZE", "1")) > 1 and not os.environ.get("DNN_FORCE_DEVICE"):
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 16:
+        os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 import torch  # noqa: E402
 
@@ -73,7 +76,8 @@ def parse_args(argv=None):
     ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--optimizer", default="sgd", choices=["sgd", "adam", "adamw"])
     ap.add_argument("--graph", action="store_true",
-                    help="replay the step as a HIP graph (1 GPU); eager is faster at large batch")
+                    help="replay the step as a HIP graph (1 GPU, or N > 1 with the native step); "
+                         "eager is as fast at large batch")
     ap.add_argument("--graph-copies", type=int, default=2,
                     help="alternate between this many instantiations of the step graph")
     ap.add_argument("--boundary", default="bf16", choices=["bf16", "fp8"],
@@ -132,7 +136,9 @@ def measure(a, spec, n, world, dev, text):
     x, y = synthetic_mnist(max(60000, 2 * rows), seed=a.seed + 1000 * replica)
     data = DeviceDataset(x, y, rows, dev, kp=tr.stages[0].x_in.shape[1] if tr.first else None)
 
-    use_graph = world == 1 and a.graph
+    # --graph: the step as a HIP graph (one GPU, or a native multi-rank step: opt-in, the
+    # plan's flag waits are kernels so the whole rank step -- hops included -- is captured)
+    use_graph = a.graph and (world == 1 or tr.native_step is not None)
     step_i = 0
 
     def one_step():
@@ -143,7 +149,8 @@ def measure(a, spec, n, world, dev, text):
         step_i += 1
 
     if use_graph:
-        tr.set_batch(*data.batch(0))
+        xb, yb = data.batch(0)
+        tr.set_batch(xb if tr.first else None, yb if tr.last else None)
         tr.capture(copies=a.graph_copies)
     for _ in range(a.warmup):
         one_step()
