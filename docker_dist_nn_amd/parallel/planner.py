@@ -132,8 +132,10 @@ class Planner:
         L = spec.layers
         if loopback and pp > 1 and not micro_batch:
             # every stage on ONE GPU: the stages overlap only through their streams, so the
-            # micro-batch GEMMs must stay big enough to fill the chip (>= 8192 rows), 2 per stage
-            micro_batch = max(8192, rows_per_replica // (2 * pp)) // 64 * 64
+            # micro-batch GEMMs must stay big enough to fill the chip: >= 16384 rows measured
+            # best (profiles/r2_own_kernels/loopback_micro_ab.jsonl: pp4 0.72 -> 0.59-0.63 ms,
+            # pp8 4.55 -> 4.37 ms against 8192-row micro-batches)
+            micro_batch = max(16384, rows_per_replica // (2 * pp)) // 64 * 64
             micro_batch = min(micro_batch, rows_per_replica)
         mb = micro_batch or (rows_per_replica if pp == 1 else
                              max(64, rows_per_replica // (4 * pp) // 64 * 64))
