@@ -195,6 +195,41 @@ def measure(a, spec, n, world, dev, text):
     return out
 
 
+def measure_tp(a, spec, n, world, dev):
+    """--parallelism tpN: Megatron column/row tensor parallelism over all N ranks
+    (parallel/tensor.py) on ONE replicated batch of --batch rows (opt-in; not the pipeline
+    metric's layout)."""
+    from docker_dist_nn_amd.parallel.tensor import TensorParallelMLP
+
+    tp = int(a.parallelism[2:])
+    if world != tp:
+        raise SystemExit(f"--parallelism tp{tp} needs WORLD_SIZE={tp}")
+    rank = int(os.environ.get("RANK", "0"))
+    m = TensorParallelMLP(spec, rows=a.batch, tp=tp, rank=rank, device=dev,
+                          optim=OptimConfig(name=a.optimizer, lr=a.lr), seed=a.seed)
+    x, y = synthetic_mnist(a.batch, seed=a.seed + 1000)
+    m.set_batch(torch.from_numpy(x), torch.from_numpy(y))
+    for _ in range(a.warmup):
+        m.step()
+    torch.distributed.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        m.step()
+    torch.distributed.barrier()
+    torch.cuda.synchronize(dev)
+    t = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    elapsed = float(t.item())
+    return {"value": round(a.batch * a.steps / elapsed, 1),
+            "ms_per_step": round(elapsed / a.steps * 1e3, 4), "global_batch": a.batch,
+            "parallelism": f"tp{tp}", "layer_distribution": [len(spec.layers)],
+            "micro_batch": a.batch, "num_micro": 1, "schedule": "none",
+            "transport": "rccl" if torch.distributed.get_backend() == "nccl" else "gloo",
+            "native_step": False, "boundary": "bf16", "dp_reduce": None, "hip_graph": False,
+            "graph_copies": 0, "loss": m.loss(), "planner_predicted": None}
+
+
 def main(argv=None):
     a = parse_args(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -213,9 +248,12 @@ def main(argv=None):
 
         init_distributed(switches.get("DNN_DIST_BACKEND"))
 
-    m = measure(a, spec, n, world, dev, a.parallelism)
+    if a.parallelism.startswith("tp"):
+        m = measure_tp(a, spec, n, world, dev)
+    else:
+        m = measure(a, spec, n, world, dev, a.parallelism)
     dp_only = None
-    if world > 1 and not a.no_dp_compare and not m["parallelism"].startswith("dp"):
+    if world > 1 and not a.no_dp_compare and not m["parallelism"].startswith(("dp", "tp")):
         d = measure(a, spec, n, world, dev, f"dp{n}")
         dp_only = {k: d[k] for k in ("value", "ms_per_step", "parallelism", "global_batch",
                                      "transport", "native_step", "dp_reduce")}

@@ -596,6 +596,18 @@ PYBIND11_MODULE(_native, m) {
         stream);
   });
 
+  m.def("bias_act_cast", [](uintptr_t in, long ld_in, uintptr_t bias, int act, uintptr_t out,
+                            long ld_out, int rows, int cols, uintptr_t stream) {
+    launch(
+        "bias_act_cast",
+        [=](hipStream_t s, const dnn::Program& R) {
+          return dnn::bias_act_cast(R.fix(P<const float>(in)), ld_in,
+                                    R.fix(P<const float>(bias)), act, R.fix(P<uint16_t>(out)),
+                                    ld_out, rows, cols, s);
+        },
+        stream);
+  });
+
   // ---- runtime: native step executor (recorded launch programs) ---------------------------
   py::class_<dnn::Program>(m, "Program",
                            "Recorded kernel launches in named segments, replayed from C++.")

@@ -585,6 +585,36 @@ int unpack_bf16(const uint16_t* in, long ld_in, int rows, int cols, float* out, 
 }
 
 // ------------------------------------------------------------------------------------------
+// out[r][c] = act(in[r][c] + bias[c]) as bf16: the epilogue of a row-parallel (tensor-parallel)
+// layer, applied after the all-reduce of its fp32 partial sums (parallel/tensor.py).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void bias_act_cast_kernel(const float* __restrict__ in,
+                                                            long ld_in,
+                                                            const float* __restrict__ bias,
+                                                            int act, u16* __restrict__ out,
+                                                            long ld_out, int rows, int cols4) {
+  const long total = (long)rows * cols4;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int r = (int)(i / cols4), c = (int)(i % cols4) * 4;
+    f32x4_t v = *(const f32x4_t*)(in + (long)r * ld_in + c);
+    if (bias) v += *(const f32x4_t*)(bias + c);
+    bf16x4_t o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (short)f2bf(act_fwd(v[e], act));
+    *(bf16x4_t*)(out + (long)r * ld_out + c) = o;
+  }
+}
+
+int bias_act_cast(const float* in, long ld_in, const float* bias, int act, uint16_t* out,
+                  long ld_out, int rows, int cols, hipStream_t stream) {
+  if (rows <= 0 || cols <= 0 || cols % 4 || ld_in % 4 || ld_out % 4) return -1;
+  const long total = (long)rows * (cols / 4);
+  hipLaunchKernelGGL(bias_act_cast_kernel, dim3(grid_for(total)), dim3(256), 0, stream, in,
+                     ld_in, bias, act, out, ld_out, rows, cols / 4);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
+// ------------------------------------------------------------------------------------------
 // bf16 transpose: dst[c][r] = src[r][c], 64x64 tiles through LDS (16-byte loads and stores).
 // Refreshes the transposed weight shadow W^T[Kp][Np] after an optimizer update, so the dgrad
 // GEMM reads both operands contraction-contiguous (ds_read_b128 fragments, the forward's main

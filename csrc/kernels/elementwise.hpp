@@ -96,6 +96,9 @@ int quant_rows_fp8(const uint16_t* x, long ldx, int rows, int cols, unsigned cha
 int dequant_rows_fp8(const unsigned char* q, long ldq, const float* scale, int rows, int cols,
                      uint16_t* x, long ldx, hipStream_t stream);
 
+// out = act(in + bias) as bf16 (row-parallel layer epilogue after the all-reduce).
+int bias_act_cast(const float* in, long ld_in, const float* bias, int act, uint16_t* out,
+                  long ld_out, int rows, int cols, hipStream_t stream);
 // Peer copy (16-byte aligned) and flag write as kernels: never block the issuing host thread.
 int p2p_copy(void* dst, const void* src, size_t bytes, hipStream_t stream);
 int p2p_signal(uint32_t* flag, uint32_t value, hipStream_t stream);

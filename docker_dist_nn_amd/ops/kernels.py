@@ -125,6 +125,11 @@ def dact_colsum(x, aux, act, part=None, n_part: int = 1):
     """x = act'(aux) * x in place (bf16), and (optional) part[n_part][cols] = column sums of the
     result over n_part row blocks: the epilogue of a library-GEMM dgrad."""
     rows, cols = x.shape
+    if not x.is_cuda:
+        x.copy_(ref.act_bwd(x.float(), aux[:rows, :cols].float(), _act(act)).to(x.dtype))
+        if part is not None:
+            ref.colsum_partial(x, part, n_part)
+        return
     native().dact_colsum(_p(x), x.stride(0), _p(aux), aux.stride(0), _act(act), rows, cols,
                          n_part, _p(part), _stream(x))
 
@@ -925,6 +930,22 @@ def pack_bf16(src, out):
         raise ValueError("pack_bf16 needs row-major tensors")
     native().pack_bf16(_p(src), src.stride(0), rows, cols, _p(out), out.stride(0), rows_p, cols_p,
                        _stream(out))
+
+
+def bias_act_cast(x, bias, y, act="relu"):
+    """y (bf16) = act(x (fp32) + bias): a row-parallel layer's epilogue after its all-reduce."""
+    rows, cols = y.shape
+    if not x.is_cuda:
+        v = x[:rows, :cols] + (bias[:cols] if bias is not None else 0.0)
+        y.copy_(ref.act_fwd(v, _act(act)).to(torch.bfloat16))
+        return y
+    _rows(x, "x", torch.float32)
+    _rows(y, "y", torch.bfloat16)
+    if bias is not None and (bias.dtype != torch.float32 or bias.numel() < cols):
+        raise ValueError("bias must be fp32 with >= cols entries")
+    native().bias_act_cast(_p(x), x.stride(0), _p(bias), _act(act), _p(y), y.stride(0), rows,
+                           cols, _stream(x))
+    return y
 
 
 def unpack_bf16(src, out):

@@ -317,3 +317,53 @@ def test_native_sharded_dp_one_rank_equals_python(dev, optim, monkeypatch):
         assert out["0"][1] == out["1"][1]
     finally:
         dist.destroy_process_group()
+
+
+def _tp_worker(rank, world, port, spec, rows, steps, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from docker_dist_nn_amd import MLPSpec
+    from docker_dist_nn_amd.engine import OptimConfig
+    from docker_dist_nn_amd.parallel.tensor import TensorParallelMLP
+
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    tp = TensorParallelMLP(MLPSpec.parse(spec), rows=rows, tp=world, rank=rank, device=dev,
+                           optim=OptimConfig(lr=0.05, momentum=0.9))
+    xt, yt = _batch(rows)
+    for _ in range(steps):
+        tp.set_batch(xt[:, :784].float(), yt)
+        tp.step()
+    ws = tp.full_weights()
+    if rank == 0:
+        for k, (w, b) in enumerate(ws):
+            np.save(os.path.join(out_dir, f"tp_w{k}.npy"), w)
+        np.save(os.path.join(out_dir, "tp_loss.npy"), np.array([tp.loss()]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_tensor_parallel_gpu_matches_single_process(dev, world):
+    """Megatron column/row tensor parallelism (parallel/tensor.py) on the gfx950 kernels --
+    ranks = processes sharing cuda:0, gloo all-reduces -- reproduces single-GPU training."""
+    from docker_dist_nn_amd import MLPSpec
+    from docker_dist_nn_amd.engine import OptimConfig, Trainer
+
+    rows, steps = 1024, 3
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_tp_worker, args=(world, _free_port(), SPEC, rows, steps, d),
+                           nprocs=world, join=True, start_method="spawn")
+        tr = Trainer(MLPSpec.parse(SPEC), micro_batch=rows, num_micro=1, device=dev,
+                     optim=OptimConfig(lr=0.05, momentum=0.9))
+        xt, yt = _batch(rows)
+        for _ in range(steps):
+            tr.set_batch(xt.to(dev), yt.to(dev))
+            tr.step()
+        for k, (w, _b) in tr.local_weights().items():
+            np.testing.assert_allclose(np.load(os.path.join(d, f"tp_w{k}.npy")), w,
+                                       rtol=1e-2, atol=1e-3)
+        np.testing.assert_allclose(np.load(os.path.join(d, "tp_loss.npy"))[0], tr.loss(),
+                                   rtol=1e-2)
