@@ -381,10 +381,16 @@ class PipelineExecutor:
         if st.nm != 1 or not st.first or not st.last or "W0" not in segs:
             return None
         L = len(st.geoms)
+        fused = st.params.fused_layers  # their wgrad also UPDATES W_i and W_i^T
         plan = [(st, "F0", 0), (None, "@fork", 0)]
         for i in range(L - 1, 0, -1):
-            plan += [(st, f"W{i}", 1), (st, f"B0.L{i}", 0), (None, "@fork", 0)]
-        plan = plan[:-1] + [(st, "W0", 0), (None, "@join", 0)]
+            if i in fused:  # dgrad_i reads the old W_i^T: the updating wgrad_i starts after it
+                plan += [(st, f"B0.L{i}", 0), (None, "@fork", 0), (st, f"W{i}", 1)]
+            else:
+                plan += [(st, f"W{i}", 1), (st, f"B0.L{i}", 0), (None, "@fork", 0)]
+        if plan[-1][1] == "@fork":
+            plan = plan[:-1]
+        plan += [(st, "W0", 0), (None, "@join", 0)]
         plan.append((st, "FINO", 0) if "FINO" in segs else (st, "FIN", 0))
         if "FINO" not in segs:
             plan.append((st, "O", 0))

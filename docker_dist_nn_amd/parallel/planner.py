@@ -69,9 +69,9 @@ def compositions(n: int, k: int):
 # Measured one-GPU training steps on MI355X with the round-2 own-kernel table
 # (profiles/r2_own_kernels, profiles/r2_epilogue): widths -> (rows, ms per step).
 MEASURED_STEP_MS = {
-    (784, 512, 256, 128, 10): (65536, 0.374),
-    (784, 1024, 1024, 1024, 1024, 1024, 1024, 1024, 10): (65536, 3.424),
-    (784, 8192, 8192, 10): (16384, 6.36),
+    (784, 512, 256, 128, 10): (65536, 0.373),
+    (784, 1024, 1024, 1024, 1024, 1024, 1024, 1024, 10): (65536, 3.31),
+    (784, 8192, 8192, 10): (16384, 6.27),
 }
 
 

@@ -6,19 +6,23 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def test_overlap_plan_bitwise(dev, monkeypatch):
-    from docker_dist_nn_amd import NAMED_MODELS
+@pytest.mark.parametrize("model,rows", [("mnist-fcnn", 8192), ("784-8192-8192-10", 2048)])
+def test_overlap_plan_bitwise(dev, monkeypatch, model, rows):
+    """784-8192-8192-10 at 2048 rows: layer 1's one-split wgrad updates W_1 / W_1^T in its
+    epilogue (fused update), so the plan must start it only after dgrad_1 has read W_1^T."""
+    from docker_dist_nn_amd import NAMED_MODELS, MLPSpec
     from docker_dist_nn_amd.data import synthetic_mnist
     from docker_dist_nn_amd.engine import OptimConfig, Trainer
 
-    x, y = synthetic_mnist(8192, seed=4)
-    xb = torch.zeros(8192, 832, dtype=torch.bfloat16)
+    spec = NAMED_MODELS.get(model) or MLPSpec.parse(model)
+    x, y = synthetic_mnist(rows, seed=4)
+    xb = torch.zeros(rows, 832, dtype=torch.bfloat16)
     xb[:, :784] = torch.from_numpy(x).to(torch.bfloat16)
     xb, yb = xb.to(dev), torch.from_numpy(y).to(dev)
     res = []
     for flag in ("0", "1"):
         monkeypatch.setenv("DNN_BW_OVERLAP", flag)
-        tr = Trainer(NAMED_MODELS["mnist-fcnn"], micro_batch=8192, num_micro=1,
+        tr = Trainer(spec, micro_batch=rows, num_micro=1,
                      optim=OptimConfig(lr=0.1, momentum=0.9), device=dev)
         losses = []
         for _ in range(4):
