@@ -120,7 +120,11 @@ def build(force: bool = False, jobs: int | None = None, sanitize: bool = False,
                     raise RuntimeError(f"native build failed compiling {cmd[-3]}")
 
     newest = max(o.stat().st_mtime for o in objs)
-    if force or jobs_to_run or not out.exists() or out.stat().st_mtime < newest:
+    # the .so records which object set it was linked from: switching back to an older header
+    # set (its objects exist and are OLDER than the .so) must still relink
+    stamp = out.with_suffix(".objset")
+    stale_set = not stamp.exists() or stamp.read_text().strip() != obj_dir.name
+    if force or jobs_to_run or stale_set or not out.exists() or out.stat().st_mtime < newest:
         link = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(out),
                 *map(str, objs), f"-L{ROCM / 'lib'}", "-lamdhip64", "-lhipblaslt"]
         if sanitize:
@@ -130,6 +134,7 @@ def build(force: bool = False, jobs: int | None = None, sanitize: bool = False,
             sys.stderr.write(" ".join(cmd) + "\n" + log)
         if rc:
             raise RuntimeError("native link failed")
+        stamp.write_text(obj_dir.name + "\n")
     return out
 
 
