@@ -328,24 +328,35 @@ static int grid_for(long n4) {
   return (int)(g < 2048 ? (g > 0 ? g : 1) : 2048);
 }
 
+// Source groups per block: about 4 loads per thread (one batch of independent loads in
+// flight, then the LDS combine). Few sources -> wide blocks over many columns; many sources
+// over few columns (bias partials: 256 x 512) -> up to 64 groups, so no thread walks a long
+// dependent chain of load rounds (16 groups left 16 loads per thread on those jobs and 1-2 on
+// the 18-slab weight jobs, i.e. 4x the blocks with one load each).
+static __host__ __device__ int reduce_ty(int n_src) {
+  int ty = 1;
+  while (ty < 64 && ty * 8 <= n_src) ty *= 2;
+  return ty;
+}
+
 int reduce_slabs(const float* src, long stride, int n_src, long n, float scale, float* out,
                  int accumulate, hipStream_t stream) {
   if (n <= 0 || n % 4 || n_src <= 0 || (n_src > 1 && stride % 4)) return -1;
   if ((((uintptr_t)src) | ((uintptr_t)out)) & 15) return -5;
   const long n4 = n / 4;
-  auto grid = [&](int tx) {
-    long g = (n4 + tx - 1) / tx;
-    return dim3((unsigned)(g < 8192 ? g : 8192));
-  };
-  if (n_src >= 16)
-    hipLaunchKernelGGL(reduce_slabs_kernel<16>, grid(16), dim3(256), 0, stream, src, stride, n_src,
-                       n4, scale, out, accumulate);
-  else if (n_src >= 4)
-    hipLaunchKernelGGL(reduce_slabs_kernel<4>, grid(64), dim3(256), 0, stream, src, stride, n_src,
-                       n4, scale, out, accumulate);
-  else
-    hipLaunchKernelGGL(reduce_slabs_kernel<1>, grid(256), dim3(256), 0, stream, src, stride, n_src,
-                       n4, scale, out, accumulate);
+  const int ty = reduce_ty(n_src);
+  long g = (n4 + 256 / ty - 1) / (256 / ty);
+  const dim3 grid((unsigned)(g < 8192 ? g : 8192));
+#define DNN_SLABS(TY)                                                                          \
+  case TY:                                                                                     \
+    hipLaunchKernelGGL(reduce_slabs_kernel<TY>, grid, dim3(256), 0, stream, src, stride, n_src, \
+                       n4, scale, out, accumulate);                                            \
+    break;
+  switch (ty) {
+    DNN_SLABS(64) DNN_SLABS(32) DNN_SLABS(16) DNN_SLABS(8) DNN_SLABS(4) DNN_SLABS(2)
+    default: DNN_SLABS(1)
+  }
+#undef DNN_SLABS
   return hipGetLastError() == hipSuccess ? 0 : -9;
 }
 
@@ -435,8 +446,6 @@ __device__ __forceinline__ void reduce_block(const ReduceJob& jb, long blk, f32x
   }
 }
 
-static __host__ __device__ int reduce_ty(int n_src) { return n_src >= 16 ? 16 : n_src >= 4 ? 4 : 1; }
-
 __global__ __launch_bounds__(256) void reduce_multi_kernel(ReduceJobs jobs, FusedSgd sg) {
   __shared__ f32x4_t red_s[256];
   f32x4_t LDS_AS* red = (f32x4_t LDS_AS*)red_s;
@@ -445,8 +454,12 @@ __global__ __launch_bounds__(256) void reduce_multi_kernel(ReduceJobs jobs, Fuse
   const ReduceJob& jb = jobs.job[j];
   const long blk = (long)blockIdx.x - jobs.block_start[j];
   switch (reduce_ty(jb.n_src)) {
+    case 64: reduce_block<64>(jb, blk, red, sg); break;
+    case 32: reduce_block<32>(jb, blk, red, sg); break;
     case 16: reduce_block<16>(jb, blk, red, sg); break;
+    case 8: reduce_block<8>(jb, blk, red, sg); break;
     case 4: reduce_block<4>(jb, blk, red, sg); break;
+    case 2: reduce_block<2>(jb, blk, red, sg); break;
     default: reduce_block<1>(jb, blk, red, sg); break;
   }
 }

@@ -322,8 +322,9 @@ class PipelineExecutor:
             return None
         if any(st._prog is None or not st._has_w or not st._o_native for st in self.stages):
             return None
-        if switches.get("DNN_BW_OVERLAP") == "1" and len(self.stages) == 1:
-            ov = self._overlap_plan(self.stages[0])
+        mode = switches.get("DNN_BW_OVERLAP")
+        if mode in ("1", "2") and len(self.stages) == 1:
+            ov = self._overlap_plan(self.stages[0], mode)
             if ov is not None:
                 self._plan = ov
                 return ov
@@ -372,16 +373,32 @@ class PipelineExecutor:
                       if not e[1].startswith("#")]
         return self._plan
 
-    def _overlap_plan(self, st):
+    def _overlap_plan(self, st, mode: str = "1"):
         """Single stage, one micro-batch: each layer's weight-gradient GEMM runs on the side
         stream while the main stream computes the next dgrad (wgrad_i needs dZ_i, which is
         ready before dgrad_i starts), so a memory-bound dgrad and a wgrad fill each other's
-        tails. Ends with a join, the first layer's wgrad and the gradient reduction/update."""
+        tails. Ends with a join, the first layer's wgrad and the gradient reduction/update.
+
+        mode "2" (opt-in A/B): ONE fork after the forward; the side stream runs the small
+        wgrads of layers L-1 .. 2 under the remaining dgrads, and the main stream runs the
+        dgrads and then W1, W0 itself (fewer ~6 us event packets, no large wgrad competing
+        with W0). Measured SLOWER on the headline (0.377 vs 0.372 ms): concurrent kernels
+        slow each other about in proportion, and the stagger the extra packets add helps
+        (profiles/r2_sched)."""
         segs = st._prog.segments()
         if st.nm != 1 or not st.first or not st.last or "W0" not in segs:
             return None
         L = len(st.geoms)
         fused = st.params.fused_layers  # their wgrad also UPDATES W_i and W_i^T
+        if mode == "2" and L >= 3 and not fused:
+            plan = [(st, "F0", 0), (None, "@fork", 0)]
+            plan += [(st, f"W{i}", 1) for i in range(L - 1, 1, -1)]
+            plan += [(st, f"B0.L{i}", 0) for i in range(L - 1, 0, -1)]
+            plan += [(st, "W1", 0), (st, "W0", 0), (None, "@join", 0)]
+            plan.append((st, "FINO", 0) if "FINO" in segs else (st, "FIN", 0))
+            if "FINO" not in segs:
+                plan.append((st, "O", 0))
+            return plan
         plan = [(st, "F0", 0), (None, "@fork", 0)]
         for i in range(L - 1, 0, -1):
             if i in fused:  # dgrad_i reads the old W_i^T: the updating wgrad_i starts after it
@@ -390,11 +407,31 @@ class PipelineExecutor:
                 plan += [(st, f"W{i}", 1), (st, f"B0.L{i}", 0), (None, "@fork", 0)]
         if plan[-1][1] == "@fork":
             plan = plan[:-1]
+        if switches.get("DNN_FORK_ELIDE") == "1":
+            plan = self._elide_forks(st, plan)
         plan += [(st, "W0", 0), (None, "@join", 0)]
         plan.append((st, "FINO", 0) if "FINO" in segs else (st, "FIN", 0))
         if "FINO" not in segs:
             plan.append((st, "O", 0))
         return plan
+
+    @staticmethod
+    def _elide_forks(st, plan):
+        """Drop a fork when the main stream enqueued nothing since the previous one (an empty
+        segment, e.g. the dgrads the fused classifier tail already ran): the side stream is
+        ordered after that earlier fork already. Each event record + wait is a barrier packet
+        that costs ~6 us of queue time on the main stream (kernel trace:
+        profiles/r2_sched), three of them sat between the tail and the next dgrad."""
+        out, main_work = [], True  # the first fork always follows real work (F0)
+        for e in plan:
+            if e[1] == "@fork":
+                if not main_work:
+                    continue
+                main_work = False
+            elif e[0] is not None and e[2] == 0 and st._prog.segment_size(e[1]) > 0:
+                main_work = True
+            out.append(e)
+        return out
 
     def _loopback_step_plan(self, plan):
         """Several stages in one process (loopback): run each stage on ITS OWN stream, with an
