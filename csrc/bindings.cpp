@@ -419,7 +419,7 @@ PYBIND11_MODULE(_native, m) {
   // jobs: sequence of (src, stride, n_src, n, out, scale, accumulate); > 16 jobs -> several
   // launches
   m.def("reduce_multi", [](const std::vector<std::tuple<uintptr_t, long, int, long, uintptr_t,
-                                                        float, int>>& jobs,
+                                                        float, int, uintptr_t, int>>& jobs,
                            uintptr_t stream, uintptr_t grad_base, uintptr_t master,
                            uintptr_t mom, uintptr_t shadow, float lr, float mu, float wd,
                            uintptr_t lr_dev, int adam, uintptr_t v, float b1, float b2,
@@ -429,7 +429,8 @@ PYBIND11_MODULE(_native, m) {
     J.reserve(jobs.size());
     for (const auto& t : jobs)
       J.push_back({P<const float>(std::get<0>(t)), std::get<1>(t), std::get<3>(t),
-                   P<float>(std::get<4>(t)), std::get<2>(t), std::get<5>(t), std::get<6>(t)});
+                   P<float>(std::get<4>(t)), std::get<2>(t), std::get<5>(t), std::get<6>(t),
+                   P<uint16_t>(std::get<7>(t)), std::get<8>(t)});
     const bool fused = master != 0;
     dnn::FusedSgd sg{P<const float>(grad_base), P<float>(master), P<float>(mom),
                      P<uint16_t>(shadow), lr, mu, wd, P<const float>(lr_dev)};
@@ -455,6 +456,7 @@ PYBIND11_MODULE(_native, m) {
             for (auto& j : q) {
               j.src = R.fix(j.src);
               j.out = R.fix(j.out);
+              j.wt = R.fix(j.wt);
             }
             dnn::FusedSgd f = sg;
             f.grad_base = R.fix(f.grad_base);

@@ -442,6 +442,13 @@ __device__ __forceinline__ void reduce_block(const ReduceJob& jb, long blk, f32x
         sgd4(sg.master + off, t, sg.mom ? sg.mom + off : nullptr,
              sg.shadow ? sg.shadow + off : nullptr, lr, sg.mu, sg.wd);
       }
+      if (jb.wt) {  // W^T refresh: this thread's 4 updated weights, read back in bf16
+        const bf16x4_t w = *(const bf16x4_t*)(sg.shadow + off);
+        const long k = i * 4, rows = jb.n / jb.wt_cols;
+        const long r = k / jb.wt_cols, c = k % jb.wt_cols;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) jb.wt[(c + e) * rows + r] = (u16)w[e];
+      }
     }
   }
 }
@@ -487,6 +494,10 @@ int reduce_multi(const ReduceJob* job, int n_jobs, hipStream_t stream, const Fus
     for (int k = 0; k < n_jobs; ++k)  // every output must lie in the flat gradient, 16-B aligned
       if (job[k].out < sg.grad_base || ((job[k].out - sg.grad_base) & 3)) return -1;
   }
+  for (int k = 0; k < n_jobs; ++k)  // W^T needs the fused update (its shadow) and whole rows
+    if (job[k].wt && (!sgd || !sg.shadow || job[k].wt_cols <= 0 || job[k].wt_cols % 4 ||
+                      job[k].n % job[k].wt_cols))
+      return -1;
   hipLaunchKernelGGL(reduce_multi_kernel, dim3(blocks), dim3(256), 0, stream, J, sg);
   return hipGetLastError() == hipSuccess ? 0 : -9;
 }

@@ -30,6 +30,12 @@ struct ReduceJob {
   int n_src;
   float scale;
   int accumulate;
+  // Optional (fused-SGD launches only): the job's output is a [n / wt_cols][wt_cols] weight
+  // gradient whose layer keeps a transposed bf16 shadow W^T[wt_cols][n / wt_cols]; the update
+  // writes it too (bitwise the transpose of the refreshed shadow), so no transpose launch
+  // follows the step's update.
+  uint16_t* wt;
+  int wt_cols;
 };
 constexpr int REDUCE_MAX_JOBS = 16;
 struct ReduceJobs {  // passed by value as the kernel argument

@@ -169,13 +169,14 @@ class StageParams:
             self.wt[i] = torch.zeros(g.kp, g.np_, dtype=torch.bfloat16, device=self.device)
             ops.transpose_bf16(self.wbf(i), self.wt[i])
 
-    def refresh_t(self, a: int = 0, b: Optional[int] = None, step: bool = False) -> None:
+    def refresh_t(self, a: int = 0, b: Optional[int] = None, step: bool = False,
+                  skip: frozenset = frozenset()) -> None:
         """Re-derive W^T of the local layers [a, b) that keep one (after their update).
         ``step``: a per-step update -- layers updated by their wgrad epilogue (which writes
-        W^T itself) are skipped."""
+        W^T itself) are skipped; so are the ``skip`` layers (W^T written by the update)."""
         b = len(self.geoms) if b is None else b
         ops.transpose_multi([(self.wbf(i), self.wt[i]) for i in range(a, b) if i in self.wt and
-                             not (step and i in self.fused_layers)])
+                             i not in skip and not (step and i in self.fused_layers)])
 
     def _layers_of(self, e0: int, e1: int) -> tuple[int, int]:
         """Local layers whose parameters lie in the flat element range [e0, e1)."""
@@ -796,10 +797,24 @@ class Stage:
         key = tuple(range(len(self.geoms))) if layers is None else tuple(layers)
         ops.reduce_multi(self._jobs(key))  # one launch for every slab set and bias-partial set
 
-    def _jobs(self, key: tuple) -> list:
+    # W^T written by the fused update for layers up to this many weights: its transposed
+    # stores are 2-byte scatters, cheaper than a transpose launch for the headline's 256x512
+    # (step 0.3724 -> 0.3678 ms) but not measurably for mlp8's 1024x1024 layers (3.318 vs
+    # 3.329 ms), which keep the coalesced LDS transpose (profiles/r2_sched/fin_wt_*)
+    WT_BY_UPDATE_MAX = 1 << 19
+
+    def _wt_by_update_layers(self) -> list:
+        p = self.params
+        if self.wgrad_algo == "streamk":
+            return []
+        return [i for i in p.wt if i not in p.fused_layers and
+                self.geoms[i].np_ * self.geoms[i].kp <= self.WT_BY_UPDATE_MAX]
+
+    def _jobs(self, key: tuple, with_wt: bool = False) -> list:
         """reduce_multi job table of the layers in ``key`` (buffers are fixed for the stage's
-        lifetime: built once)."""
-        jobs = self._reduce_jobs.get(key)
+        lifetime: built once). ``with_wt`` (fused update only): the weight jobs of layers that
+        keep a W^T shadow also write it (no transpose launch after the update)."""
+        jobs = self._reduce_jobs.get((key, with_wt))
         if jobs is None:
             p = self.params
             jobs = []
@@ -807,10 +822,12 @@ class Stage:
                 g = self.geoms[i]
                 n = g.np_ * g.kp
                 if self.wgrad_algo != "streamk" and i not in p.fused_layers:
-                    jobs.append((self.slabs[i], self.w_splits[i], n, n, p.gw(i), 1.0, False))
+                    jobs.append((self.slabs[i], self.w_splits[i], n, n, p.gw(i), 1.0, False,
+                                 p.wt[i] if with_wt and i in self._wt_by_update_layers()
+                                 else None))
                 jobs.append((self.bpart[i], self.bpart[i].shape[0], g.np_, g.np_, p.gb(i), 1.0,
                              False))
-            self._reduce_jobs[key] = jobs
+            self._reduce_jobs[(key, with_wt)] = jobs
         return jobs
 
     def fused_fin_sgd_ok(self) -> bool:
@@ -826,13 +843,16 @@ class Stage:
         p = self.params
         p._device_scalars()
         o = p.optim
-        jobs = self._jobs(tuple(range(len(self.geoms))))
+        wt_fused = switches.get("DNN_FIN_WT") == "1" and p.shadow is not None
+        jobs = self._jobs(tuple(range(len(self.geoms))), with_wt=wt_fused)
+        # layers whose W^T comes out of the update launch itself (no transpose launch after it)
+        skip = frozenset(i for i in self._wt_by_update_layers()) if wt_fused else frozenset()
         if o.name == "sgd":
             ops.reduce_multi(jobs, sgd=dict(grad=p.grad, master=p.master,
                                             mom=p.state[0] if p.state else None,
                                             shadow=p.shadow, lr=o.lr, momentum=o.momentum,
                                             weight_decay=o.weight_decay, lr_dev=p.lr_dev))
-            p.refresh_t(step=True)
+            p.refresh_t(step=True, skip=skip)
             return
         ops.reduce_multi(jobs, sgd=dict(grad=p.grad, master=p.master, mom=p.state[0],
                                         v=p.state[1], shadow=p.shadow, lr=o.lr,
@@ -841,7 +861,7 @@ class Stage:
                                         decoupled=o.decoupled or o.name == "adamw",
                                         step_dev=p.step_dev))
         ops.step_advance(p.step_dev)  # as record_update: the segment replaces FIN + O
-        p.refresh_t(step=True)
+        p.refresh_t(step=True, skip=skip)
 
     def update_then_forward(self, j: int, s: int, lr: Optional[float] = None) -> None:
         """Deferred DP update of layers [s, L) (completing the step: advance) followed by the

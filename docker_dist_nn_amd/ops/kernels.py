@@ -807,12 +807,16 @@ def reduce_multi(jobs, sgd=None):
     the SGD step to every reduced element (bitwise equal to a following sgd_update over them).
     With adam=True (and v=, betas=, eps=, decoupled=, step_dev= as for adam_update; mom = the
     first moment) it applies the Adam / AdamW step instead, bitwise equal to adam_update; the
-    caller advances step_dev afterwards."""
-    jobs = list(jobs)
+    caller advances step_dev afterwards.
+
+    A job may carry an 8th element ``wt`` (GPU, fused update with a shadow only): the bf16
+    W^T[cols][rows] of the layer whose [rows][cols] weight gradient the job reduces; the update
+    writes it too (bitwise the transpose of the refreshed shadow)."""
+    jobs = [tuple(j) + (None,) * (8 - len(j)) for j in jobs]
     if not jobs:
         return
     if not jobs[0][0].is_cuda:
-        for (src, n_src, stride, n, out, scale, acc) in jobs:
+        for (src, n_src, stride, n, out, scale, acc, _wt) in jobs:
             ref.reduce_slabs(src, n_src, stride, n, out, scale, acc)
         if sgd is not None and sgd.get("adam"):
             adam_update(sgd["master"], sgd["grad"], sgd["mom"], sgd["v"], sgd.get("shadow"),
@@ -826,15 +830,22 @@ def reduce_multi(jobs, sgd=None):
                        weight_decay=sgd.get("weight_decay", 0.0), lr_dev=sgd.get("lr_dev"))
         return
     packed = []
-    for (src, n_src, stride, n, out, scale, acc) in jobs:
+    for (src, n_src, stride, n, out, scale, acc, wt) in jobs:
         if src.dtype != torch.float32 or out.dtype != torch.float32:
             raise TypeError("reduce_multi works on fp32")
         if not (src.is_contiguous() and out.is_contiguous()):
             raise ValueError("reduce_multi needs contiguous buffers")
         if (n_src - 1) * stride + n > src.numel() or out.numel() < n:
             raise ValueError("reduce_multi range out of bounds")
+        if wt is not None:
+            if sgd is None or sgd.get("shadow") is None:
+                raise ValueError("reduce_multi: W^T output needs the fused update with a shadow")
+            if wt.dtype != torch.bfloat16 or wt.dim() != 2 or not wt.is_contiguous() or \
+                    wt.numel() != n or wt.shape[0] % 4:
+                raise ValueError("reduce_multi: W^T must be contiguous bf16 [cols][rows] of the "
+                                 "job's n elements, cols a multiple of 4")
         packed.append((_p(src), int(stride), int(n_src), int(n), _p(out), float(scale),
-                       int(acc)))
+                       int(acc), _p(wt), int(wt.shape[0]) if wt is not None else 0))
     if sgd is None:
         native().reduce_multi(packed, _stream(jobs[0][0]))
         return

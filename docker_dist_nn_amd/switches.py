@@ -42,6 +42,8 @@ SWITCHES: dict[str, tuple[str, str]] = {
     "DNN_BW_OVERLAP": ("1", "wgrad_i on a side stream concurrent with dgrad_i (1 stage, one "
                             "micro-batch): mlp8 3.43 -> 3.31 ms; 2 = only the small wgrads "
                             "on the side (headline 0.377 vs 0.372 ms, rejected); 0 = off"),
+    "DNN_FIN_WT": ("1", "the fused reduce + SGD/Adam launch (FINO) also writes the W^T "
+                        "shadows of the layers it updates (no transpose launch per step)"),
     "DNN_FORK_ELIDE": ("0", "overlap plans: drop a side-stream fork when the main stream "
                             "enqueued nothing since the previous one (~6 us per event "
                             "packet); headline 0.403 vs 0.373 ms: the wgrads then all start "
