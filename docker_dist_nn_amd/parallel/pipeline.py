@@ -323,7 +323,7 @@ class PipelineExecutor:
         if any(st._prog is None or not st._has_w or not st._o_native for st in self.stages):
             return None
         mode = switches.get("DNN_BW_OVERLAP")
-        if mode in ("1", "2") and len(self.stages) == 1:
+        if mode in ("1", "2", "3") and len(self.stages) == 1:
             ov = self._overlap_plan(self.stages[0], mode)
             if ov is not None:
                 self._plan = ov
@@ -384,17 +384,22 @@ class PipelineExecutor:
         dgrads and then W1, W0 itself (fewer ~6 us event packets, no large wgrad competing
         with W0). Measured SLOWER on the headline (0.377 vs 0.372 ms): concurrent kernels
         slow each other about in proportion, and the stagger the extra packets add helps
-        (profiles/r2_sched)."""
+        (profiles/r2_sched). mode "3" (opt-in A/B): the same side wgrads forked after W1, under
+        W0 -- slower still (0.386 ms): W0's workgroups hold the CUs and the side GEMMs wait."""
         segs = st._prog.segments()
         if st.nm != 1 or not st.first or not st.last or "W0" not in segs:
             return None
         L = len(st.geoms)
         fused = st.params.fused_layers  # their wgrad also UPDATES W_i and W_i^T
-        if mode == "2" and L >= 3 and not fused:
-            plan = [(st, "F0", 0), (None, "@fork", 0)]
-            plan += [(st, f"W{i}", 1) for i in range(L - 1, 1, -1)]
-            plan += [(st, f"B0.L{i}", 0) for i in range(L - 1, 0, -1)]
-            plan += [(st, "W1", 0), (st, "W0", 0), (None, "@join", 0)]
+        if mode in ("2", "3") and L >= 3 and not fused:
+            plan = [(st, "F0", 0)]
+            side = [(None, "@fork", 0)] + [(st, f"W{i}", 1) for i in range(L - 1, 1, -1)]
+            if mode == "2":  # small wgrads under the dgrads
+                plan += side
+            plan += [(st, f"B0.L{i}", 0) for i in range(L - 1, 0, -1)] + [(st, "W1", 0)]
+            if mode == "3":  # small wgrads under W0 (room for their workgroups next to it)
+                plan += side
+            plan += [(st, "W0", 0), (None, "@join", 0)]
             plan.append((st, "FINO", 0) if "FINO" in segs else (st, "FIN", 0))
             if "FINO" not in segs:
                 plan.append((st, "O", 0))

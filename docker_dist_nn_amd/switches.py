@@ -41,7 +41,8 @@ SWITCHES: dict[str, tuple[str, str]] = {
     "DNN_WGRAD_STREAMS": ("1", "concurrent wgrad streams in native single-process plans"),
     "DNN_BW_OVERLAP": ("1", "wgrad_i on a side stream concurrent with dgrad_i (1 stage, one "
                             "micro-batch): mlp8 3.43 -> 3.31 ms; 2 = only the small wgrads "
-                            "on the side (headline 0.377 vs 0.372 ms, rejected); 0 = off"),
+                            "on the side (headline 0.377 vs 0.372 ms, rejected); 3 = those under "
+                            "W0 (0.386 ms, rejected); 0 = off"),
     "DNN_FIN_WT": ("1", "the fused reduce + SGD/Adam launch (FINO) also writes the W^T "
                         "shadows of the layers it updates (no transpose launch per step)"),
     "DNN_FORK_ELIDE": ("0", "overlap plans: drop a side-stream fork when the main stream "
