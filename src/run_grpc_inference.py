@@ -9,4 +9,4 @@ sys.path.insert(0, os.path.dirname(SCRIPT_DIR))
 from docker_dist_nn_amd.cli.inference import main  # noqa: E402
 
 if __name__ == "__main__":
-    sys.exit(main(script_dir=SCRIPT_DIR) if "inference" != "manual_nn" else main())
+    sys.exit(main(script_dir=SCRIPT_DIR))
