@@ -640,7 +640,8 @@ PYBIND11_MODULE(_native, m) {
   // schedule order, one call, GIL released.
   // A whole step of a single-process (loopback) pipeline: (program, segment, stream) triples
   // in schedule order, one call, GIL released. stream 0 = `stream`, 1 = `side`; the pseudo
-  // segments "@fork" (side waits for main) and "@join" (main waits for side) order the two.
+  // segments "@fork" (side waits for main) and "@join" (main waits for side) order the two;
+  // "@rewait" makes the side wait on the last fork's record again (no packet on `stream`).
   m.def(
       "run_plan",
       [](const std::vector<std::tuple<const dnn::Program*, std::string, int>>& plan,
@@ -654,6 +655,11 @@ PYBIND11_MODULE(_native, m) {
         }
         std::vector<std::string> one(1);
         for (const auto& [pr, seg, si] : plan) {
+          if (seg == "@rewait") {  // side waits on the last fork again: a side-queue packet only
+            if (!side || hipStreamWaitEvent(S(side), ev_fork, 0) != hipSuccess)
+              throw std::runtime_error("run_plan: @rewait failed");
+            continue;
+          }
           if (seg == "@fork" || seg == "@join") {
             if (!side) throw std::invalid_argument("run_plan: fork/join without a side stream");
             hipEvent_t ev = seg == "@fork" ? ev_fork : ev_join;

@@ -323,7 +323,7 @@ class PipelineExecutor:
         if any(st._prog is None or not st._has_w or not st._o_native for st in self.stages):
             return None
         mode = switches.get("DNN_BW_OVERLAP")
-        if mode in ("1", "2", "3") and len(self.stages) == 1:
+        if mode in ("1", "2", "3", "4") and len(self.stages) == 1:
             ov = self._overlap_plan(self.stages[0], mode)
             if ov is not None:
                 self._plan = ov
@@ -391,6 +391,15 @@ class PipelineExecutor:
             return None
         L = len(st.geoms)
         fused = st.params.fused_layers  # their wgrad also UPDATES W_i and W_i^T
+        if mode == "4" and L >= 2 and not fused:  # largest side wgrad first, one fork
+            plan = [(st, "F0", 0), (None, "@fork", 0)]
+            plan += [(st, f"W{i}", 1) for i in range(1, L)]
+            plan += [(st, f"B0.L{i}", 0) for i in range(L - 1, 0, -1)]
+            plan += [(st, "W0", 0), (None, "@join", 0)]
+            plan.append((st, "FINO", 0) if "FINO" in segs else (st, "FIN", 0))
+            if "FINO" not in segs:
+                plan.append((st, "O", 0))
+            return plan
         if mode in ("2", "3") and L >= 3 and not fused:
             plan = [(st, "F0", 0)]
             side = [(None, "@fork", 0)] + [(st, f"W{i}", 1) for i in range(L - 1, 1, -1)]
@@ -412,8 +421,8 @@ class PipelineExecutor:
                 plan += [(st, f"W{i}", 1), (st, f"B0.L{i}", 0), (None, "@fork", 0)]
         if plan[-1][1] == "@fork":
             plan = plan[:-1]
-        if switches.get("DNN_FORK_ELIDE") == "1":
-            plan = self._elide_forks(st, plan)
+        if switches.get("DNN_FORK_ELIDE") in ("1", "2"):
+            plan = self._elide_forks(st, plan, rewait=switches.get("DNN_FORK_ELIDE") == "2")
         plan += [(st, "W0", 0), (None, "@join", 0)]
         plan.append((st, "FINO", 0) if "FINO" in segs else (st, "FIN", 0))
         if "FINO" not in segs:
@@ -421,16 +430,21 @@ class PipelineExecutor:
         return plan
 
     @staticmethod
-    def _elide_forks(st, plan):
+    def _elide_forks(st, plan, rewait: bool = False):
         """Drop a fork when the main stream enqueued nothing since the previous one (an empty
         segment, e.g. the dgrads the fused classifier tail already ran): the side stream is
         ordered after that earlier fork already. Each event record + wait is a barrier packet
         that costs ~6 us of queue time on the main stream (kernel trace:
-        profiles/r2_sched), three of them sat between the tail and the next dgrad."""
+        profiles/r2_sched), three of them sat between the tail and the next dgrad.
+        ``rewait``: keep the side stream's wait there ("@rewait": the same event again, a
+        packet on the side queue only), so the side kernels keep their stagger while the main
+        stream loses the records."""
         out, main_work = [], True  # the first fork always follows real work (F0)
         for e in plan:
             if e[1] == "@fork":
                 if not main_work:
+                    if rewait:
+                        out.append((None, "@rewait", 0))
                     continue
                 main_work = False
             elif e[0] is not None and e[2] == 0 and st._prog.segment_size(e[1]) > 0:

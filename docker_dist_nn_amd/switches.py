@@ -42,13 +42,15 @@ SWITCHES: dict[str, tuple[str, str]] = {
     "DNN_BW_OVERLAP": ("1", "wgrad_i on a side stream concurrent with dgrad_i (1 stage, one "
                             "micro-batch): mlp8 3.43 -> 3.31 ms; 2 = only the small wgrads "
                             "on the side (headline 0.377 vs 0.372 ms, rejected); 3 = those under "
-                            "W0 (0.386 ms, rejected); 0 = off"),
+                            "W0 (0.386 ms, rejected); 4 = one fork, W1..W3 on the side (0.407 ms, "
+                            "rejected); 0 = off"),
     "DNN_FIN_WT": ("1", "the fused reduce + SGD/Adam launch (FINO) also writes the W^T "
                         "shadows of the layers it updates (no transpose launch per step)"),
     "DNN_FORK_ELIDE": ("0", "overlap plans: drop a side-stream fork when the main stream "
                             "enqueued nothing since the previous one (~6 us per event "
                             "packet); headline 0.403 vs 0.373 ms: the wgrads then all start "
-                            "together and contend, rejected"),
+                            "together and contend, rejected; 2 = side re-waits instead "
+                            "(0.406 ms, rejected)"),
     "DNN_DP_DEFER": ("1", "deferred data-parallel update (Python executor path)"),
     "DNN_PIPE": ("rccl", "pipeline transport: rccl | ipc (xGMI peer copies + stream flags)"),
     "DNN_IPC_RELAYS": ("0", "ipc transport: stripe every hop over the direct link + this many "
