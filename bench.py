@@ -185,6 +185,7 @@ def measure(a, spec, n, world, dev, text):
         "layer_distribution": plan.distribution, "micro_batch": mb, "num_micro": nm,
         "schedule": a.schedule if plan.pp > 1 else "none",
         "transport": tr.transport, "native_step": tr.native_step is not None or world == 1,
+        "native_fallback": tr.native_fallback,
         "boundary": tr.boundary, "dp_reduce": tr.dp_reduce if plan.dp > 1 else None,
         "hip_graph": use_graph, "graph_copies": a.graph_copies if use_graph else 0,
         "loss": loss, "planner_predicted": round(plan.samples_per_s, 1),
@@ -227,7 +228,8 @@ def measure_tp(a, spec, n, world, dev):
             "micro_batch": a.batch, "num_micro": 1, "schedule": "none",
             "transport": "rccl" if torch.distributed.get_backend() == "nccl" else "gloo",
             "native_step": False, "boundary": "bf16", "dp_reduce": None, "hip_graph": False,
-            "graph_copies": 0, "loss": m.loss(), "planner_predicted": None}
+            "graph_copies": 0, "loss": m.loss(), "planner_predicted": None,
+            "native_fallback": None}
 
 
 def main(argv=None):
@@ -284,6 +286,7 @@ def main(argv=None):
         "last_loss": None if m["loss"] is None else round(m["loss"], 5),
         "planner_predicted": m["planner_predicted"],
         "dp_only": dp_only,
+        "native_fallback": m["native_fallback"],  # why the Python executor ran, if it did
         "switches": switches.active(),  # non-default DNN_* switches of this run
     }
     rank = int(os.environ.get("RANK", "0"))

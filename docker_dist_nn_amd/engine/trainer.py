@@ -51,6 +51,16 @@ def _warm_groups(mesh: Mesh, device) -> None:
     torch.cuda.synchronize(device)
 
 
+def _any_rank(flag: bool, device) -> bool:
+    """True on every rank if ``flag`` is true on any rank (MAX all-reduce, world group)."""
+    import torch.distributed as dist
+
+    t = torch.tensor([1.0 if flag else 0.0],
+                     device=device if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return bool(t.item() > 0)
+
+
 class Trainer:
     def __init__(self, spec: MLPSpec, *, micro_batch: int, num_micro: int = 1, pp: int = 1,
                  dp: int = 1, distribution: Optional[Sequence[int]] = None,
@@ -140,6 +150,7 @@ class Trainer:
         # native multi-rank step (parallel/native_step.py): the rank's whole step -- segment
         # replays, RCCL hops / xGMI peer copies, DP buckets -- as ONE C++ call per step
         self.native_step = None
+        self.native_fallback = None
         self.transport = ("loopback" if mesh is None else
                           "ipc" if isinstance(self.pipe, IpcPipe) else
                           "rccl" if mesh.backend == "nccl" else mesh.backend)
@@ -148,11 +159,30 @@ class Trainer:
             from ..parallel.native_step import NativeStep, native_step_supported
 
             why = native_step_supported(self.executor, mesh)
+            err = None
             if why is None and self.transport in ("rccl", "ipc"):
                 if mesh.backend == "nccl":
                     _warm_groups(mesh, self.device)
-                self.native_step = NativeStep(self.executor, mesh, self.transport,
-                                              ipc=self.pipe if self.transport == "ipc" else None)
+                try:
+                    if str(mesh.rank) in switches.get("DNN_FAULT_NATIVE_STEP").split(","):
+                        raise RuntimeError("injected native-step construction fault")
+                    self.native_step = NativeStep(self.executor, mesh, self.transport,
+                                                  ipc=self.pipe if self.transport == "ipc"
+                                                  else None)
+                except Exception as e:  # agreed on below: every rank falls back together
+                    err = e
+            # A rank running the native step and one running the Python executor would post
+            # their hops on different communicators: all ranks agree (one collective over the
+            # world group) and, if any rank could not build its native step, all of them use
+            # the Python executor instead of failing the job.
+            if _any_rank(err is not None, self.device):
+                import sys
+                print(f"[trainer] rank {mesh.rank}: native multi-rank step unavailable "
+                      f"({err!r} on this rank); every rank uses the Python executor",
+                      file=sys.stderr, flush=True)
+                self.native_fallback = repr(err) if err is not None else "another rank"
+                self.native_step = None
+            if self.native_step is not None:
                 self.executor.native_step = self.native_step
         self._graph = None
         self._stream = None

@@ -46,6 +46,9 @@ SWITCHES: dict[str, tuple[str, str]] = {
                             "rejected); 0 = off"),
     "DNN_FIN_WT": ("1", "the fused reduce + SGD/Adam launch (FINO) also writes the W^T "
                         "shadows of the layers it updates (no transpose launch per step)"),
+    "DNN_FAULT_NATIVE_STEP": ("", "fault injection (tests): comma-separated ranks whose "
+                                   "native multi-rank step construction raises; all ranks "
+                                   "then fall back to the Python executor together"),
     "DNN_FORK_ELIDE": ("0", "overlap plans: drop a side-stream fork when the main stream "
                             "enqueued nothing since the previous one (~6 us per event "
                             "packet); headline 0.403 vs 0.373 ms: the wgrads then all start "

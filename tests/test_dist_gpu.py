@@ -132,13 +132,13 @@ def test_pp2_ipc_pipe_bitwise_equals_rccl_path(dev):
 
 
 def _native_worker(rank, world, port, native_dist, steps, nm, out_dir, relays=0, tag=None,
-                   graph=False):
+                   graph=False, fault=""):
     # every stream of a plan that waits on a flag needs a hardware queue of its own (HIP
     # multiplexes streams beyond GPU_MAX_HW_QUEUES onto shared queues, where one blocked wait
     # would stall the others): 4 plan streams + the relay duties + the default stream
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DNN_PIPE="ipc",
                       DNN_NATIVE_DIST=native_dist, DNN_IPC_RELAYS=str(relays),
-                      GPU_MAX_HW_QUEUES="8")
+                      GPU_MAX_HW_QUEUES="8", DNN_FAULT_NATIVE_STEP=fault)
     tag = native_dist if tag is None else tag
     import time
 
@@ -154,7 +154,8 @@ def _native_worker(rank, world, port, native_dist, steps, nm, out_dir, relays=0,
     mesh = build_mesh(world, 1)
     tr = Trainer(MLPSpec.parse(SPEC), micro_batch=256, num_micro=nm, mesh=mesh, device=dev,
                  schedule="1f1b", optim=OptimConfig(name="sgd", lr=0.05, momentum=0.9))
-    assert (tr.native_step is not None) == (native_dist == "1")
+    assert (tr.native_step is not None) == (native_dist == "1" and not fault)
+    assert (tr.native_fallback is not None) == bool(fault)
     xt, yt = _batch(256 * nm)
     xd, yd = xt.to(dev), yt.to(dev)
     host = []
@@ -200,6 +201,24 @@ def test_native_multirank_step_bitwise_equals_python(dev, world, nm):
                 for r in range(world)]
         print("native host s/step per rank:", host)
         assert max(host) < 2e-3, host
+
+
+def test_native_step_construction_fault_falls_back_on_every_rank(dev):
+    """One rank cannot build its native step (injected fault): the ranks agree over the world
+    group and ALL run the Python executor (mixing the two would post hops on different
+    communicators), training bit for bit like an all-Python run."""
+    world, steps, nm = 3, 3, 4
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_native_worker, args=(world, _free_port(), "0", steps, nm, d),
+                           nprocs=world, join=True, start_method="spawn")
+        mp.start_processes(_native_worker, args=(world, _free_port(), "1", steps, nm, d, 0,
+                                                 "f", False, "1"),
+                           nprocs=world, join=True, start_method="spawn")
+        for k in range(4):
+            assert np.array_equal(np.load(os.path.join(d, f"n0_w{k}.npy")),
+                                  np.load(os.path.join(d, f"nf_w{k}.npy"))), k
+        assert np.array_equal(np.load(os.path.join(d, "n0_loss.npy")),
+                              np.load(os.path.join(d, "nf_loss.npy")))
 
 
 @pytest.mark.parametrize("world,relays", [(3, 1), (4, 2)])
