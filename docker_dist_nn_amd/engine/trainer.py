@@ -160,9 +160,9 @@ class Trainer:
 
             why = native_step_supported(self.executor, mesh)
             err = None
+            if mesh.backend == "nccl":  # every rank (group collectives): before any handle
+                _warm_groups(mesh, self.device)
             if why is None and self.transport in ("rccl", "ipc"):
-                if mesh.backend == "nccl":
-                    _warm_groups(mesh, self.device)
                 try:
                     if str(mesh.rank) in switches.get("DNN_FAULT_NATIVE_STEP").split(","):
                         raise RuntimeError("injected native-step construction fault")
@@ -173,9 +173,11 @@ class Trainer:
                     err = e
             # A rank running the native step and one running the Python executor would post
             # their hops on different communicators: all ranks agree (one collective over the
-            # world group) and, if any rank could not build its native step, all of them use
-            # the Python executor instead of failing the job.
-            if _any_rank(err is not None, self.device):
+            # world group) and, if any rank could not build its native step (an error, or a
+            # configuration it does not support), all of them use the Python executor instead
+            # of failing or deadlocking the job.
+            if _any_rank(self.native_step is None, self.device) and \
+                    (self.native_step is not None or err is not None):
                 import sys
                 print(f"[trainer] rank {mesh.rank}: native multi-rank step unavailable "
                       f"({err!r} on this rank); every rank uses the Python executor",
