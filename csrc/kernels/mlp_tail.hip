@@ -121,8 +121,11 @@ __device__ __forceinline__ bf16x8_t row_frag(const char LDS_AS* img, int blk, in
 
 }  // namespace tail
 
+// The whole tail for the 16-row blocks rb = rb_first + wave, + rb_step, ... < rb_end of this
+// workgroup; its bias-gradient / loss partials go to row `wg` of the partial buffers.
 template <int K3, int N3, bool RELU>
-__global__ __launch_bounds__(64 * tail::waves<RELU>()) void mlp_tail_kernel(TailParams p) {
+__device__ __forceinline__ void tail_body(const TailParams& p, char LDS_AS* lds, int rb_first,
+                                          int rb_step, int rb_end, long wg) {
   using tail::act;
   using tail::dact;
   constexpr int NW = tail::waves<RELU>();
@@ -130,8 +133,6 @@ __global__ __launch_bounds__(64 * tail::waves<RELU>()) void mlp_tail_kernel(Tail
   using tail::hi_bf;
   using tail::lo_bf;
   constexpr int NK = K3 / 32, NJ = N3 / 16, NS3 = N3 / 32, NKK = K3 / 16;
-  __shared__ __attribute__((aligned(16))) char smem[G::SMEM];
-  char LDS_AS* lds = (char LDS_AS*)smem;
   char LDS_AS* w3 = lds;
   char LDS_AS* w4 = lds + G::W3_BYTES;
   const int lane = threadIdx.x & 63;
@@ -147,9 +148,9 @@ __global__ __launch_bounds__(64 * tail::waves<RELU>()) void mlp_tail_kernel(Tail
   stage_tile<MNMAJ, N3, NW>(p.W4, p.ldw4, 0, 0, w4, wave, lane, N3);
 
   const int i16 = lane & 15, q = lane >> 4;
-  const int nrb = p.M >> 4;
-  const int nw = gridDim.x * NW;
-  int rb = blockIdx.x * NW + wave;
+  const int nrb = rb_end;
+  const int nw = rb_step;
+  int rb = rb_first + wave;
 
   bf16x8_t xb[NK];
   if (rb < nrb) {
@@ -314,7 +315,6 @@ __global__ __launch_bounds__(64 * tail::waves<RELU>()) void mlp_tail_kernel(Tail
     rw[K3 + N3 + tail::MAX_CLS + 1] = (float)corr_a;
   }
   __syncthreads();
-  const long wg = blockIdx.x;
   for (int c = threadIdx.x; c < K3 + N3 + tail::MAX_CLS + 2; c += NW * 64) {
     float t = 0.f;
 #pragma unroll
@@ -330,6 +330,40 @@ __global__ __launch_bounds__(64 * tail::waves<RELU>()) void mlp_tail_kernel(Tail
   }
   for (int c = tail::MAX_CLS + (int)threadIdx.x; c < p.N4; c += NW * 64)
     p.cs4[wg * p.ld_cs4 + c] = 0.f;
+}
+
+template <int K3, int N3, bool RELU>
+__global__ __launch_bounds__(64 * tail::waves<RELU>()) void mlp_tail_kernel(TailParams p) {
+  constexpr int NW = tail::waves<RELU>();
+  __shared__ __attribute__((aligned(16))) char smem[tail::Geo<K3, N3, NW>::SMEM];
+  tail_body<K3, N3, RELU>(p, (char LDS_AS*)smem, blockIdx.x * NW, gridDim.x * NW, p.M >> 4,
+                          blockIdx.x);
+}
+
+// Forward of the layer BEFORE the tail fused in front of it (ReLU everywhere): workgroup t
+// first computes the 256-row tile t of X = relu(A . W^T + b) (K3 = 256 = one 256x256 tile,
+// 8 waves, the one-tile main loop and staged epilogue of gemm.hip) and stores it, then runs
+// the tail over exactly those 256 rows -- read back from L2, no kernel boundary in between, and
+// one launch fewer. The tail's per-row math is unchanged; its partials are per 256-row tile.
+template <int K3, int N3>
+__global__ __launch_bounds__(512) void mlp_fwd_tail_kernel(GemmParams g, TailParams p) {
+  using C = Cfg<256, 256, 4, 2, 2>;
+  static_assert(C::NT == 64 * tail::waves<true>() && K3 == C::BN, "one tile = the tail input");
+  constexpr int SM = cmax<C::SMEM, tail::Geo<K3, N3, 8>::SMEM>::v;
+  __shared__ __attribute__((aligned(16))) char smem[SM];
+  char LDS_AS* lds = (char LDS_AS*)smem;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tm = blockIdx.x;
+  f32x4_t acc[C::FM][C::FN];
+  mma_tile<C, KMAJ, KMAJ>(g, tm * C::BM, 0, 0, g.K >> 6, lds, acc, wave, lane);
+  epilogue_staged<C, false>(g, acc, lds, tm * C::BM, 0, tm, 0, wave, lane);
+  // workgroup-scope release/acquire + barrier: the tile's stores (this CU, never read here
+  // before, so no stale L1 lines) are visible to every wave, and the LDS is free for the
+  // tail's weight images. (An agent-scope __threadfence() writes back L2 per workgroup.)
+  __syncthreads();
+  tail_body<K3, N3, true>(p, lds, tm * (C::BM / 16), tail::waves<true>(),
+                          (tm + 1) * (C::BM / 16), tm);
 }
 
 int mlp_tail_blocks(int M) {
@@ -354,6 +388,22 @@ const char* mlp_tail_error(int code) {
     case -9: return "mlp_tail: kernel launch failed";
     default: return "mlp_tail: unknown error";
   }
+}
+
+int mlp_fwd_tail(const GemmParams& g, const TailParams& p, hipStream_t stream) {
+  if (p.M <= 0 || p.M % 256 || g.M != p.M || g.N != 256 || p.K3 != 256 || p.N3 != 128 ||
+      g.K <= 0 || g.K % 64 || g.act != ACT_RELU || p.act2 != ACT_RELU || p.act3 != ACT_RELU ||
+      !g.bias || g.aux || g.colsum || g.xent_labels || g.mask_out || g.mask_in || g.ct ||
+      g.accumulate || g.k_total || g.C != (const void*)p.X || g.ldc != p.ldx ||
+      mlp_tail_blocks(p.M) != p.M / 256)
+    return -2;
+  if (p.n_cls < 1 || p.n_cls > tail::MAX_CLS || (p.N4 != 64 && p.N4 != 128)) return -3;
+  const long lds[] = {g.lda, g.ldb, p.ldx, p.ldw3, p.ldw4, p.ldh3, p.lddz4, p.lddz3, p.lddz2};
+  for (long l : lds)
+    if (l % 8) return -4;
+  hipLaunchKernelGGL((mlp_fwd_tail_kernel<256, 128>), dim3(p.M / 256), dim3(512), 0, stream, g,
+                     p);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
 }
 
 int mlp_tail(const TailParams& p, hipStream_t stream) {

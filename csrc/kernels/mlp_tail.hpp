@@ -51,6 +51,11 @@ struct TailParams {
 int mlp_tail_blocks(int M);
 // 0, or < 0 on an unsupported geometry / launch failure (see mlp_tail_error).
 int mlp_tail(const TailParams& p, hipStream_t stream);
+// The forward of the layer before the tail (g: A [M][K] . W [256][K]^T + bias, ReLU, C == the
+// tail's X) fused in front of the tail: one workgroup per 256-row tile, M / 256 partials, which
+// must equal mlp_tail_blocks(M). -2 = unsupported geometry (the caller keeps two launches).
+struct GemmParams;
+int mlp_fwd_tail(const GemmParams& g, const TailParams& p, hipStream_t stream);
 const char* mlp_tail_error(int code);
 
 }  // namespace dnn

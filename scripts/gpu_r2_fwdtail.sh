@@ -1,0 +1,11 @@
+# Forward-before-tail fusion (DNN_FWD_TAIL): tests, headline A/B, kernel trace.
+set -o pipefail
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/r2_fwdtail; mkdir -p $O
+cd $R
+timeout -k 10 300 python -u -m pytest tests/test_mlp_tail_gpu.py -m gpu -x -v --timeout 120 \
+  --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+tail -4 $O/pytest.log
+timeout -k 10 900 bash scripts/gpu_sw_ab.sh r2_fwdtail "--steps 50 --warmup 10" 4 DNN_FWD_TAIL=0 DNN_FWD_TAIL=1 || exit 1
+cd /tmp && export TMPDIR=/tmp
+DNN_FWD_TAIL=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 5 > $O/prof.log 2>&1 || { tail -20 $O/prof.log; exit 1; }
+cd $R && python scripts/trace_summary.py $O/prof/run_kernel_trace.csv --steps 3 > $O/summary.txt; head -14 $O/summary.txt
