@@ -518,7 +518,10 @@ class PipelineExecutor:
                 st.params.set_lr(st.params.optim.lr)
             if self._side is None and (self.wgrad_streams > 1 or
                                        any(e[1] == "@fork" for e in plan)):
-                self._side = torch.cuda.Stream(dev)
+                # DNN_SIDE_PRIORITY=1: the side stream (small wgrads) at high priority, so
+                # its workgroups are dispatched ahead of the main stream's pending ones
+                self._side = torch.cuda.Stream(
+                    dev, priority=-1 if switches.get("DNN_SIDE_PRIORITY") == "1" else 0)
             native().run_plan([(st._prog if st is not None else None, seg, si)
                                for st, seg, si in plan],
                               torch.cuda.current_stream(dev).cuda_stream,

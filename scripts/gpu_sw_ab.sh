@@ -11,7 +11,7 @@ d = json.loads([l for l in open(sys.argv[2]) if l.startswith("{")][-1])
 print(json.dumps({"env": sys.argv[1], "model": d["config"]["model"], "ms": d["ms_per_step"]}))
 PY
 }
-for i in $(seq $N); do for e in "$@"; do b $e; done; done
+for i in $(seq $N); do for e in "$@"; do b "$e"; done; done
 python - $O/ab.jsonl <<'PY'
 import json, sys, collections
 d = collections.defaultdict(list)
