@@ -285,7 +285,7 @@ def test_pack_unpack(dev):
     assert torch.equal(back, x.to(torch.bfloat16).float())
 
 
-@pytest.mark.parametrize("n_src", [1, 3, 8, 17, 128])
+@pytest.mark.parametrize("n_src", [1, 3, 8, 17, 40, 64, 128, 300])  # every source-group class
 def test_reduce_slabs_many_sources(dev, n_src):
     gen = torch.Generator().manual_seed(n_src)
     n = 4096 + 64
@@ -296,10 +296,11 @@ def test_reduce_slabs_many_sources(dev, n_src):
 
 
 def test_reduce_multi_bitwise_equals_reduce_slabs(dev):
-    """One launch over jobs with every TY class (1, 4, 16 sources) and > 16 jobs (several
-    launches) must reproduce per-job reduce_slabs bit for bit."""
+    """One launch over jobs with every source-group class (1..64 groups of sources) and > 16
+    jobs (several launches) must reproduce per-job reduce_slabs bit for bit."""
     gen = torch.Generator().manual_seed(5)
-    shapes = [(1, 64), (3, 4096), (7, 832 * 512), (16, 256), (512, 128), (40, 1024)] * 3
+    shapes = [(1, 64), (3, 4096), (7, 832 * 512), (16, 256), (512, 128), (40, 1024),
+              (9, 2048), (18, 832 * 512), (64, 256 * 512), (128, 4096)] * 2
     jobs, expect = [], []
     for k, (ns, n) in enumerate(shapes):
         src = torch.randn(ns, n + 8, generator=gen).to(dev)
