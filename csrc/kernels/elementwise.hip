@@ -328,14 +328,14 @@ static int grid_for(long n4) {
   return (int)(g < 2048 ? (g > 0 ? g : 1) : 2048);
 }
 
-// Source groups per block: about DNN_REDUCE_LOADS (8) loads per thread, then the LDS
-// combine (8 vs 4: reduction 24.0 -> 21.7 us, headline 0.3735 -> 0.3661 ms, 4 alternating
-// rounds, profiles/r2_sched/reduce_loads_ab.jsonl). Few sources -> wide blocks over many columns; many sources
+// Source groups per block: about DNN_REDUCE_LOADS (16) loads per thread, then the LDS
+// combine (headline reduction 24.0 us at 4 loads, 21.7 at 8, 20.3 at 16; step 0.3735 ->
+// 0.3661 ms for 4 -> 8 in 4 alternating rounds: profiles/r2_sched/reduce_loads*_ab.jsonl). Few sources -> wide blocks over many columns; many sources
 // over few columns (bias partials: 256 x 512) -> up to 64 groups, so no thread walks a long
 // dependent chain of load rounds (16 groups left 16 loads per thread on those jobs and 1-2 on
 // the 18-slab weight jobs, i.e. 4x the blocks with one load each).
 #ifndef DNN_REDUCE_LOADS  // target loads per thread (A/B builds: DNN_HIP_DEFINES)
-#define DNN_REDUCE_LOADS 8
+#define DNN_REDUCE_LOADS 16
 #endif
 static __host__ __device__ int reduce_ty(int n_src) {
   int ty = 1;
