@@ -54,9 +54,11 @@ from docker_dist_nn_amd.engine import OptimConfig, Trainer  # noqa: E402
 from docker_dist_nn_amd.parallel.planner import Planner, parse_parallelism  # noqa: E402
 
 METRIC = "samples/sec (whole node) MNIST FCNN training at 1/2/4/8-stage pipeline"
-# Only published training throughput of the reference: centralized Keras 784-32-16-10,
-# batch 32, 54,000 samples in ~5 s/epoch (notebook …ipynb:302-361).
-BASELINE_SAMPLES_PER_S = 10_800.0
+# BASELINE.md publishes no number for this metric on this model: vs_baseline is null. The only
+# published training throughput of the reference is centralized Keras on a DIFFERENT model
+# (784-32-16-10, batch 32, 54,000 samples in ~5 s/epoch on Colab CPU; notebook
+# …ipynb:302-361); it is reported as a labelled reference frame, not as vs_baseline.
+KERAS_REF_SAMPLES_PER_S = 10_800.0
 MODEL_LABEL = {"mnist-fcnn": "784-512-256-128-10 MNIST FCNN",
                "mlp8": "784-1024x7-10 MLP (8 Linear)", "mlp7": "784-1024x6-10 MLP",
                "wide": "784-8192-8192-10 MLP"}
@@ -71,7 +73,9 @@ def parse_args(argv=None):
     ap.add_argument("--batch", type=int, default=65536,
                     help="rows per GPU per step (global batch = batch x N)")
     ap.add_argument("--parallelism", default="pipeline")
-    ap.add_argument("--schedule", default="1f1b")
+    ap.add_argument("--schedule", default="auto",
+                    help="pipeline schedule; auto = 1f1b_lh (latency-hiding 1F1B) for pipelines "
+                         "across GPUs, 1f1b for single-process (loopback) pipelines")
     ap.add_argument("--micro", type=int, default=0, help="micro-batch rows (0 = planner)")
     ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--optimizer", default="sgd", choices=["sgd", "adam", "adamw"])
@@ -108,6 +112,35 @@ def _plan(a, spec, n, world, text):
     return planner.evaluate(spec, pp, dp, rows, loopback=loopback)
 
 
+def first_step_guard(tr, one_step, dev, timeout_s):
+    """Run the first multi-rank step under a watchdog: if it has not completed on the device
+    within ``timeout_s`` (a cross-rank hang: a hop or collective whose partner never comes),
+    print this rank's plan and exit non-zero instead of hanging the job. The process exits
+    with os._exit (no exec, nothing re-launched)."""
+    import threading
+
+    done = threading.Event()
+
+    def watch():
+        if not done.wait(timeout_s):
+            ns = tr.native_step
+            rank = os.environ.get("RANK", "?")
+            print(f"[bench] rank {rank}: first step not done after {timeout_s:.0f} s; "
+                  f"transport {tr.transport}, plan "
+                  f"{ns.describe() if ns is not None else 'python executor'}",
+                  file=sys.stderr, flush=True)
+            if ns is not None:
+                print(ns.trace(), file=sys.stderr, flush=True)
+            os._exit(3)
+
+    th = threading.Thread(target=watch, daemon=True)
+    th.start()
+    one_step()
+    torch.cuda.synchronize(dev)
+    done.set()
+    th.join()
+
+
 def measure(a, spec, n, world, dev, text):
     """Build the trainer for one layout, W warm-up + K timed steps; returns the JSON fields."""
     plan = _plan(a, spec, n, world, text)
@@ -127,8 +160,11 @@ def measure(a, spec, n, world, dev, text):
         for g in (mesh.fwd_group, mesh.bwd_group, mesh.dp_group, None):
             torch.distributed.all_reduce(t, group=g)
         torch.cuda.synchronize(dev)
+    sched = a.schedule
+    if sched == "auto":
+        sched = "1f1b_lh" if world > 1 and plan.pp > 1 else "1f1b"
     tr = Trainer(spec, micro_batch=mb, num_micro=nm, distribution=plan.distribution,
-                 pp=plan.pp, dp=plan.dp, schedule=a.schedule,
+                 pp=plan.pp, dp=plan.dp, schedule=sched,
                  optim=OptimConfig(name=a.optimizer, lr=a.lr),
                  device=dev, seed=a.seed, mesh=mesh, boundary=a.boundary,
                  dp_reduce=a.dp_reduce)
@@ -148,6 +184,8 @@ def measure(a, spec, n, world, dev, text):
         tr.step()
         step_i += 1
 
+    if world > 1:  # the first multi-rank step is bounded: a hang prints the plan and exits
+        first_step_guard(tr, one_step, dev, float(switches.get("DNN_FIRST_STEP_TIMEOUT")))
     if use_graph:
         xb, yb = data.batch(0)
         tr.set_batch(xb if tr.first else None, yb if tr.last else None)
@@ -183,8 +221,9 @@ def measure(a, spec, n, world, dev, text):
         "global_batch": global_batch,
         "parallelism": plan.parallelism + ("-loopback" if world == 1 and plan.pp > 1 else ""),
         "layer_distribution": plan.distribution, "micro_batch": mb, "num_micro": nm,
-        "schedule": a.schedule if plan.pp > 1 else "none",
+        "schedule": sched if plan.pp > 1 else "none",
         "transport": tr.transport, "native_step": tr.native_step is not None or world == 1,
+        "rccl_plan": tr.native_step.mode if tr.native_step is not None else None,
         "native_fallback": tr.native_fallback,
         "boundary": tr.boundary, "dp_reduce": tr.dp_reduce if plan.dp > 1 else None,
         "hip_graph": use_graph, "graph_copies": a.graph_copies if use_graph else 0,
@@ -227,7 +266,8 @@ def measure_tp(a, spec, n, world, dev):
             "parallelism": f"tp{tp}", "layer_distribution": [len(spec.layers)],
             "micro_batch": a.batch, "num_micro": 1, "schedule": "none",
             "transport": "rccl" if torch.distributed.get_backend() == "nccl" else "gloo",
-            "native_step": False, "boundary": "bf16", "dp_reduce": None, "hip_graph": False,
+            "native_step": False, "rccl_plan": None, "boundary": "bf16", "dp_reduce": None,
+            "hip_graph": False,
             "graph_copies": 0, "loss": m.loss(), "planner_predicted": None,
             "native_fallback": None}
 
@@ -269,7 +309,11 @@ def main(argv=None):
         "ms_per_step": m["ms_per_step"],
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": round(m["value"] / BASELINE_SAMPLES_PER_S, 1),
+        "vs_baseline": None,
+        "reference_frame": {
+            "label": "vs Keras 784-32-16-10 CPU training (different model, BASELINE.md)",
+            "samples_per_s": KERAS_REF_SAMPLES_PER_S,
+            "ratio": round(m["value"] / KERAS_REF_SAMPLES_PER_S, 1)},
         "dtype": "bf16",
         "data": "synthetic (MNIST-shaped 784-feature inputs, teacher labels; random-init weights)",
         "config": {
@@ -277,8 +321,8 @@ def main(argv=None):
             "global_batch": m["global_batch"],
             "seq_len": None,
             **{k: m[k] for k in ("parallelism", "layer_distribution", "micro_batch", "num_micro",
-                                 "schedule", "transport", "native_step", "boundary",
-                                 "dp_reduce", "hip_graph", "graph_copies")},
+                                 "schedule", "transport", "native_step", "rccl_plan",
+                                 "boundary", "dp_reduce", "hip_graph", "graph_copies")},
             "optimizer": a.optimizer,
         },
         # EXECUTED FLOPs (no dgrad of the first layer: models/mlp.py)

@@ -22,10 +22,16 @@ std::vector<SchedOp> make_schedule(const std::string& kind, int S, int M, int s)
     for (int j = 0; j < M; ++j) F(j);
     for (int j = 0; j < M; ++j) B(j);
     W(-1);
-  } else if (kind == "1f1b" || kind == "1f1b_w" || kind == "zb") {
+  } else if (kind == "1f1b" || kind == "1f1b_w" || kind == "zb" || kind == "1f1b_lh") {
     const bool eager_w = kind == "1f1b_w";
     const bool zb = kind == "zb";
-    const int warm = std::min(S - s - 1, M);
+    // 1f1b_lh (latency hiding): 3x the warm-up forwards. Classic 1F1B keeps only S - s
+    // micro-batches in flight on stage s, which covers the round trip to the last stage only
+    // when hops are free; with a hop of about one micro-batch's compute that round trip is
+    // ~3x longer, and the extra in-flight micro-batches (their rows are allocated anyway) keep
+    // both link directions busy: per micro-batch max(compute, hop) instead of up to
+    // compute + 2 hops (parallel/plan_sim.py, tests/test_step_plan_sim_cpu.py).
+    const int warm = std::min((kind == "1f1b_lh" ? 3 : 1) * (S - s - 1), M);
     std::deque<int> pending_w;
     int f = 0, b = 0;
     for (; f < warm; ++f) F(f);
@@ -57,7 +63,7 @@ std::vector<SchedOp> make_schedule(const std::string& kind, int S, int M, int s)
     }
   } else {
     throw std::invalid_argument("unknown schedule kind '" + kind +
-                                "' (gpipe | 1f1b | 1f1b_w | zb)");
+                                "' (gpipe | 1f1b | 1f1b_lh | 1f1b_w | zb)");
   }
   ops.push_back({OpKind::OPT, -1});
   return ops;

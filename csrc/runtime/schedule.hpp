@@ -8,6 +8,7 @@
 // Kinds:
 //   "gpipe"  : all F, then all B (same micro order), then one batched W over every micro-batch
 //   "1f1b"   : warm-up F's, steady F/B pairs, cool-down B's, then one batched W
+//   "1f1b_lh": 1f1b with 3x the warm-up forwards: hides hop latency (multi-GPU default)
 //   "1f1b_w" : as 1f1b but W_j runs right after B_j (per-micro-batch wgrad, slab accumulation)
 //   "zb"     : 1f1b whose cool-down interleaves per-micro W's into the slots where the stage
 //              would wait for the next gradient (zero-bubble style W deferral)

@@ -127,6 +127,18 @@ void StepPlan::add(const Op& op) {
     throw std::invalid_argument("StepPlan op: RCCL op without a communicator / nccl_load");
   if ((op.kind == SIGNAL || op.kind == WAITV) && !op.a)
     throw std::invalid_argument("StepPlan op: flag address");
+  if (op.kind == GSTART || op.kind == GEND) {
+    if (!nccl_api()) throw std::invalid_argument("StepPlan op: RCCL group without nccl_load");
+    // a group holds RCCL ops of ONE stream only, and groups do not nest
+    if (op.kind == GSTART && group_open_ >= 0)
+      throw std::invalid_argument("StepPlan op: nested RCCL group");
+    if (op.kind == GEND && group_open_ != op.stream)
+      throw std::invalid_argument("StepPlan op: GEND without GSTART on its stream");
+    group_open_ = op.kind == GSTART ? op.stream : -1;
+  } else if (group_open_ >= 0 && (!(op.kind == SEND || op.kind == RECV) ||
+                                  op.stream != group_open_)) {
+    throw std::invalid_argument("StepPlan op: only SEND / RECV of the group's stream in a group");
+  }
   ops_.push_back(op);
 }
 
@@ -149,6 +161,7 @@ static bool plan_trace() {
 }
 
 void StepPlan::run(hipStream_t main) {
+  if (group_open_ >= 0) throw std::runtime_error("StepPlan::run: RCCL group left open");
   ++seq_;
   if (p2p_seq_advance(dev_, main) != 0) throw std::runtime_error("p2p_seq_advance failed");
   ck(hipEventRecord(fork_, main), "hipEventRecord");
@@ -211,6 +224,12 @@ void StepPlan::run(hipStream_t main) {
         break;
       case WAIT:
         ck(hipStreamWaitEvent(s, events_[o.event], 0), "hipStreamWaitEvent");
+        break;
+      case GSTART:
+        nck(nc->group_start(), "ncclGroupStart");
+        break;
+      case GEND:
+        nck(nc->group_end(), "ncclGroupEnd");
         break;
     }
   }

@@ -14,6 +14,8 @@
 //          peer buffer and stream-ordered 32-bit flags (hipStreamWriteValue32 /
 //          hipStreamWaitValue32) carrying the step sequence number (value = seq + delta)
 //   REC / WAIT  event record on one stream / another stream waits for it
+//   GSTART / GEND  ncclGroupStart / ncclGroupEnd around the RCCL ops between them (one kernel
+//          per group: its sends and receives progress together)
 // Streams: index 0 is the caller's stream; the plan owns the others (per-direction comm
 // streams, a data-parallel stream). Every run forks all plan streams from stream 0 first and
 // joins them back at the end, so a step is ordered like one kernel on the caller's stream and
@@ -52,7 +54,7 @@ const NcclApi* nccl_api();  // nullptr until nccl_load succeeded
 class StepPlan {
  public:
   enum Kind { SEG = 0, SEND, RECV, ALLREDUCE, REDUCE_SCATTER, ALL_GATHER, COPY, SIGNAL, WAITV,
-              REC, WAIT };
+              REC, WAIT, GSTART, GEND };
   struct Op {
     Kind kind;
     int stream = 0;
@@ -72,7 +74,10 @@ class StepPlan {
   StepPlan& operator=(const StepPlan&) = delete;
 
   void add(const Op& op);
-  void clear_ops() { ops_.clear(); }
+  void clear_ops() {
+    ops_.clear();
+    group_open_ = -1;
+  }
   // One step on `main`; advances the sequence number first (seq() = 1 in the first step).
   void run(hipStream_t main);
   uint32_t seq() const { return seq_; }
@@ -96,6 +101,7 @@ class StepPlan {
   std::vector<hipEvent_t> join_;
   std::vector<Op> ops_;
   uint32_t seq_ = 0;
+  int group_open_ = -1;  // stream of the RCCL group being added, -1 = none
   // [0] = step number read by the SIGNAL / WAITV kernels, [1] = wait-timeout error word
   uint32_t* dev_ = nullptr;
 };

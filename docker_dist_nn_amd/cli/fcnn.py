@@ -65,7 +65,7 @@ def build_parser(script_dir: str) -> argparse.ArgumentParser:
     ap.add_argument("--momentum", type=float, default=0.0)
     ap.add_argument("--micro-batch", type=int, default=256)
     ap.add_argument("--num-micro-batches", type=int, default=1)
-    ap.add_argument("--schedule", choices=["gpipe", "1f1b", "1f1b_w", "zb"], default="1f1b")
+    ap.add_argument("--schedule", choices=["gpipe", "1f1b", "1f1b_lh", "1f1b_w", "zb"], default="1f1b")
     ap.add_argument("--synthetic", type=int, default=0,
                     help="train on N synthetic MNIST-shaped samples instead of --inputs")
     ap.add_argument("--seed", type=int, default=0)

@@ -133,7 +133,7 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--num-micro-batches", type=int, default=1)
     ap.add_argument("--pp", type=int, default=0, help="pipeline stages (0 = planner)")
     ap.add_argument("--layer-distribution", default=None)
-    ap.add_argument("--schedule", choices=["gpipe", "1f1b", "1f1b_w", "zb"], default="1f1b")
+    ap.add_argument("--schedule", choices=["gpipe", "1f1b", "1f1b_lh", "1f1b_w", "zb"], default="1f1b")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--device", default="auto")
     ap.add_argument("--save", default=None, help="export trained model JSON (reference format)")

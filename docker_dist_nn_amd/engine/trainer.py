@@ -41,13 +41,15 @@ def default_distribution(spec: MLPSpec, pp: int) -> list[int]:
 
 def _warm_groups(mesh: Mesh, device) -> None:
     """Make sure the RCCL communicators of this rank's groups exist (one tiny collective each,
-    in the same group order on every rank) before their handles are taken."""
+    in global group-creation order: two ranks sharing groups meet them in the same order, so
+    the warm-up cannot deadlock) before their handles are taken."""
     import torch.distributed as dist
 
     t = torch.zeros(1, device=device)
-    for g in (mesh.fwd_group, mesh.bwd_group, mesh.dp_group):
-        if g is not None:
-            dist.all_reduce(t, group=g)
+    groups = mesh.member_groups or [g for g in (mesh.fwd_group, mesh.bwd_group, mesh.dp_group)
+                                    if g is not None]
+    for g in groups:
+        dist.all_reduce(t, group=g)
     torch.cuda.synchronize(device)
 
 

@@ -10,6 +10,11 @@ Groups created (all ranks call ``new_group`` in the same order, as torch require
     directions on separate communicators (separate RCCL streams) means a blocked send in one
     direction can never stall a receive in the other, which is what makes posting every
     receive of a step up front deadlock-free without grouping sends and receives.
+  * per link (stage s <-> s+1 of a replica), TWO 2-rank groups: the forward channel and the
+    backward channel of the native RCCL step (parallel/native_step.py, ``streams`` form).
+    RCCL orders the kernels of one communicator, so a channel with one sender and one receiver
+    per communicator is what lets a receive run concurrently with the same rank's send in the
+    same direction.
   * per stage, one data-parallel group over the replicas (gradient all-reduce).
 
 Backend: ``nccl`` (= RCCL on ROCm, over xGMI) for GPU tensors, ``gloo`` for CPU runs/tests.
@@ -39,6 +44,13 @@ class Mesh:
     dp_group: Optional[object] = None
     dp_ranks: list[int] = field(default_factory=list)
     backend: str = "gloo"
+    # link channels of the native RCCL step: from/to the previous / next stage
+    link_f_in: Optional[object] = None
+    link_f_out: Optional[object] = None
+    link_b_in: Optional[object] = None
+    link_b_out: Optional[object] = None
+    # this rank's groups in global creation order (communicator warm-up without deadlock)
+    member_groups: list = field(default_factory=list)
 
     @property
     def prev_rank(self) -> Optional[int]:
@@ -82,9 +94,24 @@ def build_mesh(pp: int, dp: int) -> Mesh:
         bg = dist.new_group(ranks) if pp > 1 else None
         if r == replica:
             m.pipe_ranks, m.fwd_group, m.bwd_group = ranks, fg, bg
+            if fg is not None:
+                m.member_groups += [fg, bg]
+    for r in range(dp):
+        for s in range(pp - 1):
+            a, b = r * pp + s, r * pp + s + 1
+            lf = dist.new_group([a, b])
+            lb = dist.new_group([a, b])
+            if rank == a:
+                m.link_f_out, m.link_b_in = lf, lb
+            elif rank == b:
+                m.link_f_in, m.link_b_out = lf, lb
+            if rank in (a, b):
+                m.member_groups += [lf, lb]
     for s in range(pp):
         ranks = [r * pp + s for r in range(dp)]
         g = dist.new_group(ranks) if dp > 1 else None
         if s == stage:
             m.dp_group, m.dp_ranks = g, ranks
+            if g is not None:
+                m.member_groups.append(g)
     return m

@@ -60,6 +60,11 @@ SWITCHES: dict[str, tuple[str, str]] = {
                             "together and contend, rejected; 2 = side re-waits instead "
                             "(0.406 ms, rejected)"),
     "DNN_DP_DEFER": ("1", "deferred data-parallel update (Python executor path)"),
+    "DNN_RCCL_PLAN": ("auto", "native RCCL step form: streams (one stream per hop channel) | "
+                      "slotted (one RCCL stream, per-slot groups: safe with one resident RCCL "
+                      "kernel) | auto (streams when GPU_MAX_HW_QUEUES >= 6)"),
+    "DNN_FIRST_STEP_TIMEOUT": ("60", "bench.py: seconds the first multi-rank step may take "
+                               "before the plan trace is printed and the run exits"),
     "DNN_PIPE": ("rccl", "pipeline transport: rccl | ipc (xGMI peer copies + stream flags)"),
     "DNN_IPC_RELAYS": ("0", "ipc transport: stripe every hop over the direct link + this many "
                             "relay ranks (two-link paths; native step only)"),

@@ -386,3 +386,79 @@ def test_tensor_parallel_gpu_matches_single_process(dev, world):
                                        rtol=1e-2, atol=1e-3)
         np.testing.assert_allclose(np.load(os.path.join(d, "tp_loss.npy"))[0], tr.loss(),
                                    rtol=1e-2)
+
+
+def _interp_worker(rank, world, port, pp, mode, boundary, dp_reduce, use_interp, steps, nm,
+                   out_dir, tag):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DNN_DP_DEFER="0")
+    import torch.distributed as dist
+
+    from docker_dist_nn_amd import MLPSpec
+    from docker_dist_nn_amd.engine import OptimConfig, Trainer
+    from docker_dist_nn_amd.parallel.groups import build_mesh
+    from docker_dist_nn_amd.parallel.native_step import NativeStep
+    from docker_dist_nn_amd.parallel.plan_interp import PlanInterpreter, interp_groups
+
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mesh = build_mesh(pp, world // pp)
+    mb = 256
+    tr = Trainer(MLPSpec.parse(SPEC), micro_batch=mb, num_micro=nm, mesh=mesh, device=dev,
+                 schedule="1f1b_lh", boundary=boundary, dp_reduce=dp_reduce,
+                 optim=OptimConfig(name="sgd", lr=0.05, momentum=0.9))
+    assert tr.native_step is None  # gloo: the Python executor, unless interpreted below
+    it = None
+    if use_interp:
+        comms, groups = interp_groups(mesh)
+        ns = NativeStep(tr.executor, mesh, "rccl", comms=comms, mode=mode, build_only=True)
+        it = PlanInterpreter(ns, groups, timeout_s=60)
+    rows = mb * nm
+    xt, yt = _batch(rows * mesh.dp)
+    xs = xt[mesh.replica * rows:(mesh.replica + 1) * rows].to(dev)
+    ys = yt[mesh.replica * rows:(mesh.replica + 1) * rows].to(dev)
+    for _ in range(steps):
+        tr.set_batch(xs if tr.first else None, ys if tr.last else None)
+        if it is None:
+            tr.step()
+        else:
+            for st in tr.stages:
+                st.begin_step()
+            it.run_step()
+    torch.cuda.synchronize()
+    for k, (w, b) in tr.local_weights().items():
+        if mesh.replica == 0:
+            np.save(os.path.join(out_dir, f"{tag}_w{k}.npy"), w)
+            np.save(os.path.join(out_dir, f"{tag}_b{k}.npy"), b)
+    if tr.last is not None and mesh.replica == 0:
+        np.save(os.path.join(out_dir, f"{tag}_loss.npy"), np.array([tr.loss()]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("pp,world,mode,boundary,dp_reduce", [
+    (2, 4, "streams", "bf16", "shard"),
+    (2, 4, "slotted", "fp8", "allreduce"),
+    (4, 4, "streams", "fp8", "allreduce"),
+    (3, 3, "slotted", "bf16", "allreduce"),
+])
+def test_rccl_plan_interpreted_bitwise_equals_python(dev, pp, world, mode, boundary, dp_reduce):
+    """The EXACT op list of the native RCCL step (NativeStep._build: streams or slotted form,
+    link-channel sends / receives, RCCL groups, sharded reduce-scatter into grad_piece + e0/d and
+    in-place all-gather, fp8 two-part hops), executed by the gloo plan interpreter
+    (parallel/plan_interp.py) on processes sharing cuda:0, trains bit for bit like the
+    op-by-op Python executor: every pointer, count, peer and event edge of the plan is right."""
+    steps, nm = 3, 2 * pp
+    with tempfile.TemporaryDirectory() as d:
+        for use, tag in ((False, "py"), (True, "plan")):
+            mp.start_processes(_interp_worker,
+                               args=(world, _free_port(), pp, mode, boundary, dp_reduce, use,
+                                     steps, nm, d, tag),
+                               nprocs=world, join=True, start_method="spawn")
+        for k in range(4):
+            for wb in ("w", "b"):
+                a = np.load(os.path.join(d, f"py_{wb}{k}.npy"))
+                b = np.load(os.path.join(d, f"plan_{wb}{k}.npy"))
+                assert np.array_equal(a, b), (wb, k)
+        assert np.array_equal(np.load(os.path.join(d, "py_loss.npy")),
+                              np.load(os.path.join(d, "plan_loss.npy")))

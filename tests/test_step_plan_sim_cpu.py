@@ -1,21 +1,36 @@
-"""Deadlock-freedom of the native multi-rank step plans (parallel/native_step.py) on the CPU.
+"""The native multi-rank step plans (parallel/native_step.py) on the CPU, for layouts the
+one-GPU pool cannot run.
 
 Every rank's StepPlan op list is built exactly as on a GPU (NativeStep._build over the real
-schedule and IpcPipe flag / relay layout), with fake device addresses instead of buffers, and
-then executed by a small event simulator with HIP stream semantics: per-stream FIFO order,
-hipStreamWaitValue32 (WAITV) blocks until the flag word reaches the step's sequence number,
-hipStreamWriteValue32 (SIGNAL) sets it, events (REC / WAIT) order streams of one rank, and
-every plan run forks its side streams from the caller's stream and joins them back. A plan
-set that can stall on some interleaving shows up as a simulator state in which no stream can
-make progress. This covers layouts the one-GPU pool cannot run (8 ranks, relayed hops).
+schedule, the real StageParams flat layout of the stage's layers, and the IpcPipe flag / relay
+layout), with fake device addresses for the activation buffers and fake communicator handles,
+then executed by the timed plan simulator (parallel/plan_sim.py): per-stream FIFO order, event
+edges, fork/join per plan run, RCCL point-to-point as blocking FIFO rendezvous per (communicator,
+src, dst), RCCL groups, collectives as barriers over their communicator, IPC flags.
+
+Checked, for every BASELINE layout (pp2, pp4, pp8, pp4dp2, pp2dp4) x hop format (bf16, fp8) x
+DP exchange (sharded, all-reduce):
+* deadlock freedom of both RCCL plan forms; the ``slotted`` form also with at most ONE RCCL
+  kernel resident per rank (``serial_rccl``);
+* the steady-state period per micro-batch of the ``streams`` form is max(compute, hop): the
+  hop-in of micro-batch j+1 overlaps j's compute and hop-out;
+* every WAIT is enqueued after the REC it names (a HIP event wait binds to the last record);
+* the sharded DP collectives' pointers and counts equal GradSync's tensor slices for every
+  replica (RS into grad_piece + e0/d, in-place AG shadow + p0 -> shadow + e0).
 """
 from types import SimpleNamespace as NS
 
 import pytest
+import torch
 
+from docker_dist_nn_amd import MLPSpec
+from docker_dist_nn_amd.engine.stage import OptimConfig, StageParams
+from docker_dist_nn_amd.models.mlp import LayerGeom
 from docker_dist_nn_amd.parallel import native_step as nsmod
+from docker_dist_nn_amd.parallel import plan_sim
 from docker_dist_nn_amd.parallel.comm import IpcPipe, relay_assignment, relay_parts
 from docker_dist_nn_amd.parallel.pipeline import schedule_ops
+from docker_dist_nn_amd.partition import plan_stages
 
 
 class FakeTensor:
@@ -39,27 +54,64 @@ class FakeTensor:
         return self.cols if d == 0 else 1
 
 
+KEYS = ["x_in", "grad_out", "output", "dx_send", "flags", "q_in", "s_in", "q_gin", "s_gin",
+        "q_out", "s_out", "q_dx", "s_dx"] + [f"relay{i}" for i in range(16)]
+
+
 def _addr(rank, key):
-    keys = ["x_in", "grad_out", "output", "dx_send", "flags"] + [f"relay{i}" for i in range(16)]
-    return (rank + 1) << 40 | (keys.index(key) + 1) << 32
+    return (rank + 1) << 40 | (KEYS.index(key) + 1) << 32
 
 
-def _build_rank(rank, pp, dp, nm, mb, k, width, sched):
+class FakeProg:
+    def segments(self):
+        return {"FINO", "W"}
+
+
+def _stage(rank, pp, dp, nm, mb, spec, dist, boundary, dp_reduce):
     stage, replica = rank % pp, rank // pp
+    plan = plan_stages(len(spec.layers), dist)[stage]
+    geoms = [LayerGeom(i, spec.layers[i]) for i in range(plan.layer_start, plan.layer_end)]
+    shard = (dp, replica) if dp_reduce == "shard" and dp > 1 else None
+    params = StageParams(geoms, torch.device("cpu"), OptimConfig(), shard=shard)
+    rows = mb * nm
+    w_in, w_out = geoms[0].kp, geoms[-1].np_
+    st = NS(nm=nm, mb=mb, boundary=boundary, _has_w=True, _o_native=True, _prog=FakeProg(),
+            params=params, geoms=geoms, rows_of=lambda j: slice(j * mb, (j + 1) * mb))
+    for key, w, es in (("x_in", w_in, 2), ("grad_out", w_out, 2), ("output", w_out, 2),
+                       ("dx_send", w_in, 2), ("q_in", w_in, 1), ("s_in", 1, 4),
+                       ("q_gin", w_out, 1), ("s_gin", 1, 4), ("q_out", w_out, 1),
+                       ("s_out", 1, 4), ("q_dx", w_in, 1), ("s_dx", 1, 4)):
+        setattr(st, key, FakeTensor(_addr(rank, key), rows, w, es))
     mesh = NS(rank=rank, pp=pp, dp=dp, stage=stage, replica=replica,
               prev_rank=rank - 1 if stage > 0 else None,
               next_rank=rank + 1 if stage + 1 < pp else None)
-    rows = mb * nm
-    st = NS(nm=nm, mb=mb, boundary="bf16", _has_w=True, _o_native=True,
-            _prog=NS(segments=lambda: {"FINO", "W"}),
-            params=NS(sharded=False, grad=FakeTensor(_addr(rank, "output") + (1 << 31), 1, 1, 4),
-                      layer_grad_range=lambda i: (i * 4096, (i + 1) * 4096)),
-            geoms=[NS(np_=64, kp=64), NS(np_=64, kp=64)],
-            x_in=FakeTensor(_addr(rank, "x_in"), rows, width),
-            grad_out=FakeTensor(_addr(rank, "grad_out"), rows, width),
-            output=FakeTensor(_addr(rank, "output"), rows, width),
-            dx_send=FakeTensor(_addr(rank, "dx_send"), rows, width),
-            rows_of=lambda j: slice(j * mb, (j + 1) * mb))
+    return st, mesh
+
+
+def _comms(mesh):
+    r = mesh.rank
+    c = {"dp": ("dp", mesh.stage)}
+    if mesh.prev_rank is not None:
+        c["f_in"], c["b_out"] = ("lf", mesh.prev_rank, r), ("lb", mesh.prev_rank, r)
+    if mesh.next_rank is not None:
+        c["f_out"], c["b_in"] = ("lf", r, mesh.next_rank), ("lb", r, mesh.next_rank)
+    return c
+
+
+def build_rccl(rank, pp, dp, nm, mb=256, spec="784-512-256-128-10", dist=None,
+               boundary="bf16", dp_reduce="shard", mode="streams", sched="1f1b"):
+    spec = MLPSpec.parse(spec)
+    dist = dist or [len(spec.layers) // pp] * (pp - 1) + [len(spec.layers) - (pp - 1) *
+                                                         (len(spec.layers) // pp)]
+    st, mesh = _stage(rank, pp, dp, nm, mb, spec, dist, boundary, dp_reduce)
+    ex = NS(stages=[st], ops=[schedule_ops(sched, pp, nm, mesh.stage)], kind=sched)
+    return nsmod.NativeStep(ex, mesh, "rccl", comms=_comms(mesh), mode=mode, build_only=True)
+
+
+def build_ipc(rank, pp, dp, nm, mb, k, width, sched):
+    spec = MLPSpec.parse("-".join([str(width)] * (pp + 1)))
+    st, mesh = _stage(rank, pp, dp, nm, mb, spec, [1] * pp, "bf16", "allreduce")
+    st._prog = NS(segments=lambda: {"FINO", "W"})
     assign = relay_assignment(pp, dp, k) if k else {}
     ipc = NS(k=k, nm=nm, seq=0)
     ipc.duties = [(h[0], h[1], h[2], rl.index(rank) + 1) for h, rl in assign.items()
@@ -96,94 +148,193 @@ def _build_rank(rank, pp, dp, nm, mb, k, width, sched):
                                      "d": di})
     ipc.relay_dst = [{"buf": _addr(dst, "x_in" if d == "f" else "grad_out"),
                       "flags": _addr(dst, "flags")} for _s, dst, d, _p in ipc.duties]
-    ex = NS(stages=[st], ops=[schedule_ops(sched, pp, nm, stage)])
-    ns = nsmod.NativeStep.__new__(nsmod.NativeStep)
-    ns.ex, ns.mesh, ns.st, ns.transport, ns.ipc = ex, mesh, st, "ipc", ipc
-    ns.dp, ns.sharded = dp, False
-    ns.comm_f = ns.comm_b = ns.comm_dp = 0
-    ns._ev, ns.ops = 0, []
-    ns._build()
-    return ns.ops, 4 + len(ipc.duties)
+    ex = NS(stages=[st], ops=[schedule_ops(sched, pp, nm, mesh.stage)], kind=sched)
+    return nsmod.NativeStep(ex, mesh, "ipc", ipc=ipc, build_only=True)
 
 
-def simulate(pp, dp, nm, k, steps=3, sched="1f1b", mb=64, width=64):
-    """Runs `steps` plan executions of every rank; returns the number of ops executed or
-    raises AssertionError with the blocked stream heads on a deadlock."""
-    world = pp * dp
-    mem = {}
-    queues = {}  # (rank, stream) -> list of (kind, payload, step)
-    arrivals = {}  # collective key -> set of ranks whose stream reached it
-    for r in range(world):
-        ops, ns = _build_rank(r, pp, dp, nm, mb, k, width, sched)
-        n_coll = 0
-        for o in ops:  # collectives: a barrier over the stage's DP group, in program order
-            if o["kind"] == nsmod.ALLREDUCE:
-                o["coll"] = n_coll
-                n_coll += 1
-        for s in range(1, steps + 1):
-            queues.setdefault((r, 0), []).append(("FORK", None, s))
-            for i in range(1, ns):
-                queues.setdefault((r, i), []).append(("WFORK", None, s))
-            for o in ops:
-                queues.setdefault((r, o["stream"]), []).append(("OP", o, s))
-            for i in range(1, ns):
-                queues[(r, i)].append(("JREC", i, s))
-                queues[(r, 0)].append(("JWAIT", i, s))
-    fork, join, ev = {}, {}, {}
-    heads = {q: 0 for q in queues}
-    done = 0
-    while True:
-        progress = False
-        for (r, si), q in queues.items():
-            while heads[(r, si)] < len(q):
-                kind, o, s = q[heads[(r, si)]]
-                if kind == "FORK":
-                    fork[r] = s
-                elif kind == "WFORK":
-                    if fork.get(r, 0) < s:
-                        break
-                elif kind == "JREC":
-                    join[(r, o)] = s
-                elif kind == "JWAIT":
-                    if join.get((r, o), 0) < s:
-                        break
-                else:
-                    kd = o["kind"]
-                    if kd == nsmod.WAITV:
-                        if mem.get(o["a"], 0) < s + o.get("delta", 0):
-                            break
-                    elif kd == nsmod.SIGNAL:
-                        mem[o["a"]] = s + o.get("delta", 0)
-                    elif kd == nsmod.REC:
-                        ev[(r, o["event"])] = s
-                    elif kd == nsmod.WAIT:
-                        if ev.get((r, o["event"]), 0) < s:
-                            break
-                    elif kd == nsmod.ALLREDUCE:
-                        key = (r % pp, s, o["coll"])
-                        arrivals.setdefault(key, set()).add(r)
-                        if len(arrivals[key]) < dp:
-                            break
-                    # SEG / COPY complete immediately
-                heads[(r, si)] += 1
-                done += 1
-                progress = True
-        if all(heads[q] == len(v) for q, v in queues.items()):
-            return done
-        if not progress:
-            blocked = {q: queues[q][heads[q]] for q in queues if heads[q] < len(queues[q])}
-            raise AssertionError(f"deadlock: {blocked}")
+def check_enqueue_order(ops):
+    """Every WAIT on an event is enqueued after a REC of it; every event id is recorded once."""
+    recorded = set()
+    for o in nsmod.flatten(ops):
+        if o["kind"] == nsmod.REC:
+            assert o["event"] not in recorded, f"event {o['event']} recorded twice"
+            recorded.add(o["event"])
+        elif o["kind"] == nsmod.WAIT:
+            assert o["event"] in recorded, f"WAIT on event {o['event']} before its REC"
 
 
+def sim(builds, steps=2, serial=False, f=1.0, b=2.0, hop=1.0, w=0.25, coll=0.5):
+    def seg_time(rank, seg):
+        if seg[0] == "F" and seg[1:].isdigit():
+            return f
+        if seg[0] == "B" and seg[1:].isdigit():
+            return b
+        if seg.startswith(("W", "FIN")):
+            return w
+        return 0.01
+
+    plans = {r: plan_sim.RankPlan(ns.ops, ns.n_streams) for r, ns in builds.items()}
+    return plan_sim.simulate(plans, steps=steps, seg_time=seg_time,
+                             p2p_time=lambda op: hop / (2 if op["dtype"] != nsmod.NCCL_BF16
+                                                         else 1),
+                             coll_time=lambda op: coll, serial_rccl=serial)
+
+
+LAYOUTS = [(2, 1), (4, 1), (8, 1), (4, 2), (2, 4)]
+
+
+def _spec(pp):
+    return "784-1024-1024-1024-1024-1024-1024-1024-10" if pp == 8 else "784-512-256-128-10"
+
+
+@pytest.mark.parametrize("pp,dp", LAYOUTS)
+@pytest.mark.parametrize("boundary", ["bf16", "fp8"])
+@pytest.mark.parametrize("dp_reduce", ["shard", "allreduce"])
+@pytest.mark.parametrize("mode", ["streams", "slotted"])
+def test_rccl_plans_deadlock_free(pp, dp, boundary, dp_reduce, mode):
+    nm = 2 * pp
+    builds = {r: build_rccl(r, pp, dp, nm, spec=_spec(pp), boundary=boundary,
+                            dp_reduce=dp_reduce, mode=mode) for r in range(pp * dp)}
+    for ns in builds.values():
+        check_enqueue_order(ns.ops)
+    assert sim(builds).makespan > 0
+    if mode == "slotted":  # safe with one resident RCCL kernel per rank
+        assert sim(builds, serial=True).makespan > 0
+
+
+def test_streams_form_needs_concurrent_rccl_kernels():
+    """The ``streams`` form relies on co-resident RCCL kernels (pre-posted receives): with one
+    resident kernel per rank it can deadlock -- why it needs one hardware queue per stream and
+    why ``auto`` falls back to ``slotted`` otherwise."""
+    pp = 4
+    builds = {r: build_rccl(r, pp, 1, 8, mode="streams") for r in range(pp)}
+    with pytest.raises(plan_sim.Deadlock):
+        sim(builds, serial=True)
+
+
+@pytest.mark.parametrize("sched", ["gpipe", "1f1b", "1f1b_lh"])
+@pytest.mark.parametrize("mode", ["streams", "slotted"])
+def test_rccl_plans_per_schedule(sched, mode):
+    builds = {r: build_rccl(r, 4, 2, 8, mode=mode, sched=sched) for r in range(8)}
+    assert sim(builds, serial=mode == "slotted").makespan > 0
+
+
+def _period(pp, mode, hop, sched="1f1b_lh", f=1.0, b=2.0):
+    """Steady-state time per micro-batch: slope of the step time in the micro-batch count."""
+    out = []
+    for nm in (16, 32):
+        builds = {r: build_rccl(r, pp, 1, nm, spec=_spec(pp), mode=mode, sched=sched)
+                  for r in range(pp)}
+        res = sim(builds, steps=1, hop=hop, f=f, b=b)
+        out.append(res.makespan)
+    return (out[1] - out[0]) / 16
+
+
+@pytest.mark.parametrize("pp", [2, 4, 8])
+@pytest.mark.parametrize("hop", [0.5, 3.0, 6.0])
+def test_streams_period_is_max_of_compute_and_hop(pp, hop):
+    """compute per micro-batch = F + B = 3; hop = one message per direction per micro-batch.
+    The streams form with the latency-hiding 1F1B (1f1b_lh) overlaps hop-in, compute and
+    hop-out: period = max(3, hop) (planner.Planner's model)."""
+    per = _period(pp, "streams", hop)
+    assert per <= 1.05 * max(3.0, hop) + 0.05, per
+
+
+def test_classic_1f1b_exposes_hop_latency():
+    """Why 1f1b_lh is the multi-GPU default: classic 1F1B keeps S - s micro-batches in flight,
+    which cannot cover a hop of one micro-batch's compute (2.5x slower here)."""
+    assert _period(4, "streams", 3.0, sched="1f1b") > 2 * _period(4, "streams", 3.0)
+
+
+@pytest.mark.parametrize("hop", [0.5, 3.0])
+def test_slotted_period_bounded(hop):
+    """The slotted form pays for its serial safety: a hop-in waits for the previous group, so
+    a micro-batch costs up to compute + hop (never more)."""
+    per = _period(4, "slotted", hop)
+    assert per <= 3.0 + hop + 0.1, per
+
+
+@pytest.mark.parametrize("dp", [2, 4])
+def test_sharded_collectives_match_gradsync_slices(dp):
+    """Every REDUCE_SCATTER / ALL_GATHER of the sharded native plan names exactly the bytes
+    GradSync (the Python executor) hands torch.distributed: RS input = grad16[e0:e1], output =
+    grad_piece[e0/d : e1/d]; AG input = shadow[p0:p1] (this replica's piece), output =
+    shadow[e0:e1] with sendbuff == recvbuff + rank * count (RCCL's in-place condition)."""
+    pp = 2
+    for r in range(pp * dp):
+        ns = build_rccl(r, pp, dp, 4, dp_reduce="shard")
+        p = ns.st.params
+        replica = r // pp
+        rs = [o for o in ns.ops if o["kind"] == nsmod.REDUCE_SCATTER]
+        ag = [o for o in ns.ops if o["kind"] == nsmod.ALL_GATHER]
+        assert len(rs) == len(ag) == len(p.shard_buckets) > 0
+        for o, (e0, e1) in zip(rs, p.shard_buckets):
+            src, dst = p.grad16[e0:e1], p.grad_piece[e0 // dp:e1 // dp]
+            assert o["a"] == src.data_ptr() and o["b"] == dst.data_ptr()
+            assert o["count"] == dst.numel() == src.numel() // dp
+        for o, (e0, e1) in zip(ag, p.shard_buckets):
+            p0, p1 = p.shard_piece(e0, e1)
+            assert (p0, p1) == (e0 + replica * o["count"], e0 + (replica + 1) * o["count"])
+            assert o["a"] == p.shadow[p0:p1].data_ptr()
+            assert o["b"] == p.shadow[e0:e1].data_ptr()
+            assert o["a"] == o["b"] + replica * o["count"] * 2  # bf16 bytes
+        ar = [o for o in ns.ops if o["kind"] == nsmod.ALLREDUCE]
+        assert len(ar) == 1 and ar[0]["a"] == p.grad[p.bias_lo:].data_ptr()
+        assert ar[0]["count"] == p.numel - p.bias_lo
+
+
+def test_link_channels_one_sender_one_receiver():
+    """In the streams form every link communicator carries ONE direction: its sends all come
+    from one rank and its receives all land on the other, in micro-batch order on both."""
+    pp, dp, nm = 4, 2, 8
+    chans = {}
+    for r in range(pp * dp):
+        ns = build_rccl(r, pp, dp, nm)
+        for o in nsmod.flatten(ns.ops):
+            if o["kind"] in (nsmod.SEND, nsmod.RECV):
+                chans.setdefault(o["comm"], []).append((o["kind"], r, o["tag"]))
+    for comm, lst in chans.items():
+        senders = {r for k, r, _ in lst if k == nsmod.SEND}
+        recvers = {r for k, r, _ in lst if k == nsmod.RECV}
+        assert len(senders) == len(recvers) == 1 and senders != recvers, comm
+        s_tags = [t for k, _, t in lst if k == nsmod.SEND]
+        r_tags = [t for k, _, t in lst if k == nsmod.RECV]
+        assert s_tags == r_tags, comm
+
+
+def test_slotted_groups_match_partner_slots():
+    """In the slotted form a rank's group t holds exactly the transfers whose partner op is in
+    the partner's group t (what makes it safe with one resident RCCL kernel)."""
+    pp, nm = 4, 8
+    groups = {}
+    for r in range(pp):
+        ns = build_rccl(r, pp, 1, nm, mode="slotted")
+        for o in ns.ops:
+            if o["kind"] == nsmod.GROUP:
+                for m in o["ops"]:
+                    groups.setdefault((o["tag"], m["tag"]), []).append(
+                        (r, m["kind"], m["gpeer"]))
+    for key, lst in groups.items():
+        assert len(lst) == 2, key
+        (r1, k1, p1), (r2, k2, p2) = lst
+        assert {k1, k2} == {nsmod.SEND, nsmod.RECV} and p1 == r2 and p2 == r1, key
+
+
+# ---- IPC transport (xGMI peer copies + flags) ------------------------------------------------
 @pytest.mark.parametrize("pp,dp,k", [(2, 1, 0), (3, 1, 0), (4, 1, 0), (3, 1, 1), (4, 1, 2),
                                      (4, 2, 0), (4, 2, 2), (8, 1, 2), (2, 4, 2), (4, 2, 6)])
 def test_ipc_plans_deadlock_free(pp, dp, k):
-    assert simulate(pp, dp, nm=2 * pp, k=k) > 0
+    nm = 2 * pp
+    builds = {r: build_ipc(r, pp, dp, nm, 64, k, 64, "1f1b") for r in range(pp * dp)}
+    for ns in builds.values():
+        check_enqueue_order(ns.ops)
+    assert sim(builds, steps=3).makespan > 0
 
 
 @pytest.mark.parametrize("sched", ["gpipe", "1f1b"])
 def test_ipc_relay_plans_deadlock_free_per_schedule(sched):
-    assert simulate(4, 2, nm=8, k=2, sched=sched) > 0
+    builds = {r: build_ipc(r, 4, 2, 8, 64, 2, 64, sched) for r in range(8)}
+    assert sim(builds, steps=3).makespan > 0
 
 
 def test_relay_stripes_reach_every_row_once():
@@ -193,8 +344,8 @@ def test_relay_stripes_reach_every_row_once():
     rb = width * 2
     writes = {}
     for r in range(pp * dp):
-        ops, _ = _build_rank(r, pp, dp, nm, mb, k, width, "1f1b")
-        for o in ops:
+        ns = build_ipc(r, pp, dp, nm, mb, k, width, "1f1b")
+        for o in ns.ops:
             if o["kind"] == nsmod.COPY and (o["b"] >> 32) & 0xff in (1, 2):  # x_in / grad_out
                 for row in range(o["count"] // rb):
                     key = (o["b"] >> 32, (o["b"] & 0xffffffff) // rb + row)
