@@ -203,11 +203,13 @@ static gemm_fn pick_layout(int la, int lb, int f32) {
 #undef DNN_G
 }
 
-// 4-wave tiles: any NS in 2..4; 8-wave tiles: NS = 2 (a third 64-KiB stage does not fit)
+// 4-wave tiles: any NS in 2..4, or 5 = the asymmetric ring (A 3 deep, B 2 deep); 8-wave tiles:
+// NS = 2, 3 where it fits, or 5 (256x256: 3 x 32 KiB A + 2 x 32 KiB B = all 160 KiB of LDS)
 template <int BM, int BN>
 static gemm_fn pick4(int ns, int la, int lb, int f32) {
   return ns == 2   ? pick_layout<Cfg<BM, BN, 2, 2, 2>>(la, lb, f32)
          : ns == 3 ? pick_layout<Cfg<BM, BN, 2, 2, 3>>(la, lb, f32)
+         : ns == 5 ? pick_layout<Cfg<BM, BN, 2, 2, 3, 2>>(la, lb, f32)
                    : pick_layout<Cfg<BM, BN, 2, 2, 4>>(la, lb, f32);
 }
 
@@ -234,7 +236,7 @@ const char* gemm_error_string(int code) {
     case -10: return "colsum needs bf16 output and ld_colsum >= N";
     case -11: return "fused cross-entropy needs bf16 output, N == bn <= 128, a bias and 0 < n_cls <= N";
     case -13: return "relu bit masks need bf16 output, act = relu, ld_mask >= N/8, no aux/xent, one-tile form";
-    case -12: return "pipeline stages must be 2..4 (8-wave tiles: 2..3, 256x256: 2 or 8 = ping-pong)";
+    case -12: return "pipeline stages must be 2..4 or 5 = A3/B2 ring (8-wave tiles: 2, 3, 5; 256x256: 2, 5 or 8 = ping-pong; 5: one-tile form, no fused xent)";
     case -14: return "transposed output ct needs bf16 output (or the fused update), no xent, one split, one-tile form, ld_ct >= M, 16-byte alignment";
     case -15: return "fused SGD epilogue needs f32 output, one split, no accumulate/bias/xent, a device lr, 16-byte aligned buffers, N % 8 == 0, one-tile form";
     default: return "unknown gemm error";
@@ -307,9 +309,10 @@ int gemm_bf16(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, 
   }
   const int nt = gemm_tile_threads(bm, bn);
   const int ns = stages ? stages : default_stages(bm, bn);
-  // 8-wave tiles: NS = 3 where three stages fit (not 256x256)
-  if (ns < 2 || ns > 4 || (nt == 512 && (ns > 3 || (ns == 3 && bm == 256 && bn == 256))))
+  // 8-wave tiles: NS = 3 where three stages fit (not 256x256); 5 = asymmetric A3/B2 ring
+  if (ns < 2 || ns > 5 || (nt == 512 && (ns == 4 || (ns == 3 && bm == 256 && bn == 256))))
     return -12;
+  if (ns == 5 && (persist || p.xent_labels)) return -12;
   if (persist && !p.xent_labels) {  // persistent form (gemm_persist.hip); NS <= 3
     if (ns > 3) return -12;
     GemmParams q = p;
@@ -321,16 +324,21 @@ int gemm_bf16(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, 
   else if (bm == 128 && bn == 64) fn = pick4<128, 64>(ns, la, lb, out_f32);
   else if (bm == 64 && bn == 128) fn = pick4<64, 128>(ns, la, lb, out_f32);
   else if (bm == 64 && bn == 64) fn = pick4<64, 64>(ns, la, lb, out_f32);
-  else if (bm == 256 && bn == 256) fn = pick_layout<Cfg<256, 256, 4, 2, 2>>(la, lb, out_f32);
+  else if (bm == 256 && bn == 256)
+    fn = ns == 5 ? pick_layout<Cfg<256, 256, 4, 2, 3, 2>>(la, lb, out_f32)
+                 : pick_layout<Cfg<256, 256, 4, 2, 2>>(la, lb, out_f32);
   else if (bm == 256 && bn == 128)
-    fn = ns == 2 ? pick_layout<Cfg<256, 128, 4, 2, 2>>(la, lb, out_f32)
-                 : pick_layout<Cfg<256, 128, 4, 2, 3>>(la, lb, out_f32);
+    fn = ns == 2   ? pick_layout<Cfg<256, 128, 4, 2, 2>>(la, lb, out_f32)
+         : ns == 5 ? pick_layout<Cfg<256, 128, 4, 2, 3, 2>>(la, lb, out_f32)
+                   : pick_layout<Cfg<256, 128, 4, 2, 3>>(la, lb, out_f32);
   else if (bm == 256 && bn == 64)
-    fn = ns == 2 ? pick_layout<Cfg<256, 64, 4, 2, 2>>(la, lb, out_f32)
-                 : pick_layout<Cfg<256, 64, 4, 2, 3>>(la, lb, out_f32);
+    fn = ns == 2   ? pick_layout<Cfg<256, 64, 4, 2, 2>>(la, lb, out_f32)
+         : ns == 5 ? pick_layout<Cfg<256, 64, 4, 2, 3, 2>>(la, lb, out_f32)
+                   : pick_layout<Cfg<256, 64, 4, 2, 3>>(la, lb, out_f32);
   else
-    fn = ns == 2 ? pick_layout<Cfg<128, 256, 2, 4, 2>>(la, lb, out_f32)
-                 : pick_layout<Cfg<128, 256, 2, 4, 3>>(la, lb, out_f32);
+    fn = ns == 2   ? pick_layout<Cfg<128, 256, 2, 4, 2>>(la, lb, out_f32)
+         : ns == 5 ? pick_layout<Cfg<128, 256, 2, 4, 3, 2>>(la, lb, out_f32)
+                   : pick_layout<Cfg<128, 256, 2, 4, 3>>(la, lb, out_f32);
 
   const int tiles_n = (p.N + bn - 1) / bn, tiles_m = (p.M + bm - 1) / bm;
   const int nwg = tiles_n * tiles_m * splits;

@@ -35,12 +35,22 @@ struct cmax {
   static constexpr int v = A > B ? A : B;
 };
 
-template <int BM_, int BN_, int WM_, int WN_, int NS_>
+//
+// NSB_ (default NS_): a B ring of its own depth. NS = 3, NSB = 2 keeps TWO A tiles in flight
+// behind the one being consumed and one B tile: the A operand of the forward / dgrad is the
+// streamed activation panel (HBM), B the weights (L2-resident after the first tiles), and what
+// limits those GEMMs is HBM bytes in flight per CU (profiles/r3_pmc: waves parked in vmcnt
+// waits 47-63 % of their cycles), not LDS. Only that asymmetric pair is implemented.
+template <int BM_, int BN_, int WM_, int WN_, int NS_, int NSB_ = NS_>
 struct Cfg {
-  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, NS = NS_;
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, NS = NS_, NSB = NSB_;
+  static_assert(NSB == NS || (NS == 3 && NSB == 2), "asymmetric ring: A 3 deep, B 2 deep only");
+  static constexpr bool ASYM = NSB != NS;
   static constexpr int NW = WM * WN, NT = 64 * NW;
   static constexpr int SM = BM / WM, SN = BN / WN, FM = SM / 16, FN = SN / 16;
   static constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
+  // asymmetric ring layout: [NS A slots][NSB B slots]
+  static constexpr int RING = ASYM ? NS * A_BYTES + NSB * B_BYTES : NS * STAGE;
   // LDS-DMA instructions one wave issues per stage (A + B): the vmcnt unit of the pipeline
   static constexpr int PER_STAGE = (BM + BN) / (8 * NW);
   // epilogue: fp32 staging of EPI_ROWS rows at a time (whole tile when it fits)
@@ -49,7 +59,9 @@ struct Cfg {
   static constexpr int CHUNKS = BM / EPI_ROWS, WPC = EPI_ROWS / SM;  // wave-rows per chunk
   static constexpr int CS_BYTES = EPI_ROWS * CS_LD * 4;
   static constexpr int RED_BYTES = NT * 32;  // colsum partial staging
-  static constexpr int SMEM = cmax<cmax<NS * STAGE, CS_BYTES + 64>::v, RED_BYTES>::v;
+  static constexpr int SMEM = cmax<cmax<RING, CS_BYTES + 64>::v, RED_BYTES>::v;
+  // per-wave LDS-DMA instructions of one A / one B tile (vmcnt units of the asymmetric ring)
+  static constexpr int PER_A = BM / (8 * NW), PER_B = BN / (8 * NW);
   static_assert(FM >= 1 && FN >= 1 && SM % 16 == 0 && SN % 16 == 0, "wave sub-tile");
   static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "LDS-DMA pieces per wave");
   static_assert(NT % (BN / 8) == 0 && (EPI_ROWS * (BN / 8)) % NT == 0, "epilogue mapping");
@@ -152,6 +164,63 @@ __device__ __forceinline__ void wait_stage(int after) {
 //   everyone finished step kt-1, so its buffer is free) -> issue tile kt+NS-1 into that
 //   buffer -> MFMA on tile kt.
 // acc is zeroed first; ends with every wave past a barrier, so the caller may reuse the LDS.
+// The k-step body shared by both rings: fragments of one staged A / B tile -> MFMAs.
+template <class C, int LA, int LB>
+__device__ __forceinline__ void mma_kstep(const char LDS_AS* sa, const char LDS_AS* sb,
+                                          f32x4_t (&acc)[C::FM][C::FN], int wm, int wn,
+                                          int lane) {
+  constexpr int FM = C::FM, FN = C::FN;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    bf16x8_t a[FM], b[FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) a[i] = load_frag<LA, C::BM>(sa, wm * FM + i, s, lane);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) b[j] = load_frag<LB, C::BN>(sb, wn * FN + j, s, lane);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+  }
+}
+
+// Asymmetric ring (Cfg NS = 3, NSB = 2): A slots kt % 3, B slots kt % 2. Issue order is
+// A0 B0 A1 | step kt: B(kt+1) A(kt+2), so at the top of step kt the only loads younger than
+// A(kt) and B(kt) are A(kt+1)'s: wait vmcnt(PER_A) (vmcnt(0) once A(kt+1) does not exist).
+// Bytes in flight while step kt computes: A(kt+1), A(kt+2), B(kt+1) -- two A tiles instead of
+// one. WAR: step kt restages A slot (kt+2)%3 and B slot (kt+1)%2, both last read in step kt-1,
+// which every wave finished before the barrier at the top of kt.
+template <class C, int LA, int LB>
+__device__ __forceinline__ void mma_tile_asym(const GemmParams& p, int m0, int n0, int kbase,
+                                              int nk, char LDS_AS* lds,
+                                              f32x4_t (&acc)[C::FM][C::FN], int wm, int wn,
+                                              int wave, int lane) {
+  constexpr int A_BYTES = C::A_BYTES, B_BYTES = C::B_BYTES;
+  char LDS_AS* ring_b = lds + 3 * A_BYTES;
+  auto stage_a = [&](int k) {
+    stage_tile<LA, C::BM, C::NW>(p.A, p.lda, m0, kbase + k * 64, lds + (k % 3) * A_BYTES, wave,
+                                 lane, p.M);
+  };
+  auto stage_b = [&](int k) {
+    stage_tile<LB, C::BN, C::NW>(p.B, p.ldb, n0, kbase + k * 64, ring_b + (k & 1) * B_BYTES,
+                                 wave, lane, p.N);
+  };
+  stage_a(0);
+  stage_b(0);
+  if (nk > 1) stage_a(1);
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) wait_vmcnt<C::PER_A>();
+    else wait_vmcnt<0>();
+    lds_barrier();
+    if (kt + 1 < nk) stage_b(kt + 1);
+    if (kt + 2 < nk) stage_a(kt + 2);
+    mma_kstep<C, LA, LB>(lds + (kt % 3) * A_BYTES, ring_b + (kt & 1) * B_BYTES, acc, wm, wn,
+                         lane);
+  }
+  __syncthreads();
+}
+
 template <class C, int LA, int LB>
 __device__ __forceinline__ void mma_tile(const GemmParams& p, int m0, int n0, int kbase, int nk,
                                          char LDS_AS* lds, f32x4_t (&acc)[C::FM][C::FN],
@@ -162,6 +231,10 @@ __device__ __forceinline__ void mma_tile(const GemmParams& p, int m0, int n0, in
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  if constexpr (C::ASYM) {
+    mma_tile_asym<C, LA, LB>(p, m0, n0, kbase, nk, lds, acc, wm, wn, wave, lane);
+    return;
+  }
 
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s) {

@@ -135,7 +135,15 @@ def read_meta(d: str) -> dict:
     with open(_meta_path(d)) as f:
         meta = json.load(f)
     if meta.get("format") != FORMAT or "shards" not in meta:
-        raise ValueError(f"{d}: not a format-{FORMAT} checkpoint (no shard list in meta.json)")
+        if meta.get("format") == 1 or "shards" not in meta:
+            raise ValueError(
+                f"{d}: format-1 checkpoint (per-stage stage{{s}}.safetensors, no shard list): "
+                f"this version reads format {FORMAT} only. Migrate by exporting the weights with "
+                f"the version that wrote it (neuron JSON) and starting from that JSON "
+                f"(cli/train.py --config), or train from scratch into a fresh directory; "
+                f"--resume on this directory would otherwise discard its shards on commit")
+        raise ValueError(f"{d}: not a format-{FORMAT} checkpoint (meta format "
+                         f"{meta.get('format')!r})")
     return meta
 
 
@@ -204,6 +212,9 @@ def restore_trainer(d: str, trainer) -> int:
     meta = st["meta"]
     if list(meta["widths"]) != list(trainer.spec.widths):
         raise ValueError(f"checkpoint widths {meta['widths']} != model {trainer.spec.widths}")
+    acts = [l.activation for l in trainer.spec.layers]
+    if meta.get("activations") is not None and list(meta["activations"]) != acts:
+        raise ValueError(f"checkpoint activations {meta['activations']} != model {acts}")
     same_opt = meta.get("optimizer") == trainer.optim.name
     for stage in trainer.stages:
         p = stage.params

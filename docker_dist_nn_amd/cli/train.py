@@ -221,7 +221,24 @@ def main(argv: Optional[list[str]] = None) -> int:
     done = False
     barrier = torch.distributed.barrier if world > 1 else None
 
+    def comm_healthy() -> bool:
+        """No RCCL async error and no timed-out IPC flag wait on ANY rank (a timed-out wait
+        lets the step consume rows that never arrived): agreed over the world group."""
+        bad = 0.0
+        if tr.native_step is not None:
+            bad = 1.0 if tr.native_step.comm_error() else 0.0
+        if world > 1:
+            t = torch.tensor([bad], device=dev if torch.distributed.get_backend() == "nccl"
+                             else "cpu")
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            bad = float(t.item())
+        return bad == 0.0
+
     def save(step_):
+        # never commit a checkpoint built from a step whose hops failed (ADVICE r2)
+        if not comm_healthy():
+            raise RuntimeError(f"rank {rank}: communication error or flag-wait timeout before "
+                               f"the step-{step_} checkpoint; not committing it")
         ckpt.save_trainer(a.checkpoint_dir, tr, step_, barrier=barrier, is_writer=replica == 0,
                           extra={"seed": a.seed, "rows_per_step": rows, "dp": dp})
 

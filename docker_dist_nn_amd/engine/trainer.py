@@ -188,6 +188,13 @@ class Trainer:
                 self.native_step = None
             if self.native_step is not None:
                 self.executor.native_step = self.native_step
+            elif isinstance(self.pipe, IpcPipe) and self.pipe.k:
+                # relayed IPC hops exist only in the native step: name the cause here instead
+                # of failing inside the first Python-executor step
+                raise RuntimeError(
+                    f"DNN_IPC_RELAYS={self.pipe.k} needs the native multi-rank step on every "
+                    f"rank, which is unavailable ({self.native_fallback or why}); run with "
+                    f"DNN_IPC_RELAYS=0 or fix the native step")
         self._graph = None
         self._stream = None
         self.graph_nodes = 0

@@ -499,6 +499,10 @@ class PipelineExecutor:
         self.pipe.begin_step()
         for st in self.stages:
             st.begin_step()
+            if st.params.fused_layers:
+                # one-split wgrads apply SGD in their epilogue (W, before O): they read the
+                # device lr, so this step's rate must be there before any W
+                st.params.set_lr(self.lr_fn() if self.lr_fn else st.params.optim.lr)
         plan = self._native_plan()
         if plan is not None and len(self.stages) > 1 and not getattr(self, "capturing", False) \
                 and switches.get("DNN_LOOPBACK_STREAMS") == "1":

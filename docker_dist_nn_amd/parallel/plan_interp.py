@@ -21,6 +21,7 @@ breaks bitwise equality with the Python executor (tests/test_dist_gpu.py).
 """
 from __future__ import annotations
 
+import threading
 import time
 from typing import Optional
 
@@ -40,7 +41,7 @@ class DeviceMemory:
         self.ranges = []
         seen = set()
         for t in tensors:
-            if not isinstance(t, torch.Tensor) or t.device.type != "cuda" or \
+            if not isinstance(t, torch.Tensor) or \
                     not t.is_contiguous() or t.numel() == 0 or t.data_ptr() in seen:
                 continue
             seen.add(t.data_ptr())
@@ -63,6 +64,28 @@ def stage_memory(st) -> DeviceMemory:
         elif isinstance(v, dict):
             ts += [x for x in v.values() if isinstance(x, torch.Tensor)]
     return DeviceMemory(ts)
+
+
+class _Done:
+    """Completion of a gloo work: gloo's send / receive works report is_completed() only after
+    wait(), so a helper thread waits and the interpreter polls the flag."""
+
+    def __init__(self, work):
+        self.work, self.err = work, None
+        self.ev = threading.Event()
+        threading.Thread(target=self._run, daemon=True).start()
+
+    def _run(self):
+        try:
+            self.work.wait()
+        except Exception as e:  # surfaced by the interpreter
+            self.err = e
+        self.ev.set()
+
+    def done(self) -> bool:
+        if self.ev.is_set() and self.err is not None:
+            raise self.err
+        return self.ev.is_set()
 
 
 class PlanInterpreter:
@@ -132,10 +155,9 @@ class PlanInterpreter:
                         k = o["kind"]
                         if s in inflight:
                             works = inflight[s]
-                            if not all(w.is_completed() for w, _ in works):
+                            if not all(w.done() for w, _ in works):
                                 break
-                            for w, fin in works:
-                                w.wait()
+                            for _, fin in works:
                                 if fin is not None:
                                     fin()
                             del inflight[s]
@@ -147,10 +169,11 @@ class PlanInterpreter:
                             if o["event"] not in events:
                                 break
                         elif k == GROUP:
-                            inflight[s] = [x for m in o["ops"] for x in self._start(m)]
+                            inflight[s] = [(_Done(w), f) for m in o["ops"]
+                                           for w, f in self._start(m)]
                             continue
                         else:
-                            inflight[s] = self._start(o)
+                            inflight[s] = [(_Done(w), f) for w, f in self._start(o)]
                             continue
                         head[s] += 1
                         progress = True

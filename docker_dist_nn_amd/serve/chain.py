@@ -22,6 +22,14 @@ and is reported as "Failed to forward request to <next>" (:136-140). Here:
   wrong caller;
 * a stage that fails turns the header status into an error code carrying its stage index;
   rank 0 raises ``StageFailure`` -> the reference's gRPC code + details;
+* blame on a timeout names the stage that actually stopped: every rank > 0 publishes the id of
+  the last request it has PROCESSED (received + computed) to the job's key-value store from a
+  background thread, and a payload receive that misses its per-hop deadline publishes an error
+  record; when a request's deadline expires, rank 0 blames the first stage that has not
+  processed it ("Failed to forward request to layer_container_k", as the reference's hop
+  before a dead stage reports it, grpc_node.py:136-140);
+* small requests (<= ops.GEMV_MAX_ROWS rows, the batch-1 serving path) travel as ONE fixed-size
+  packet per hop (header + rows); larger ones as a packet header then the payload;
 * ``STOP`` headers shut the chain down in order.
 
 Run by the launcher: ``python -m docker_dist_nn_amd.serve.chain --plan plan.json``.
@@ -58,9 +66,12 @@ from .. import switches
 
 log = logging.getLogger(__name__)
 
-ST_OK, ST_STOP, ST_VALUE, ST_INTERNAL = 0, 1, 2, 3
-_CODES = {ST_VALUE: grpc.StatusCode.INVALID_ARGUMENT, ST_INTERNAL: grpc.StatusCode.INTERNAL}
+ST_OK, ST_STOP, ST_VALUE, ST_INTERNAL, ST_DEADLINE = 0, 1, 2, 3, 4
+_CODES = {ST_VALUE: grpc.StatusCode.INVALID_ARGUMENT, ST_INTERNAL: grpc.StatusCode.INTERNAL,
+          ST_DEADLINE: grpc.StatusCode.DEADLINE_EXCEEDED}
 HOP_TIMEOUT_S = 10.0  # grpc_node.py:133
+HDR_BYTES = 64  # packet header: 5 int64 (request id, rows bucket, width, status, extra) + pad
+PUBLISH_S = 0.02  # progress publication period of ranks > 0
 
 
 def bucket(rows: int) -> int:
@@ -94,6 +105,14 @@ class ChainRank:
         self.fault_stage = switches.get("DNN_FAULT_STAGE")
         self.fault_kind = switches.get("DNN_FAULT_KIND")
         self.fault_after = int(switches.get("DNN_FAULT_AFTER"))
+        self.small = ops.GEMV_MAX_ROWS
+        self._packets: dict = {}
+        self.store = dist.distributed_c10d._get_default_store() if world > 1 else None
+        self._processed = 0
+        self._published = 0
+        if rank > 0 and world > 1:
+            t = threading.Thread(target=self._publisher, name="chain-progress", daemon=True)
+            t.start()
         if rank == 0 and world > 1:
             for fn, nm in ((self._sender, "chain-send"), (self._receiver, "chain-recv")):
                 t = threading.Thread(target=fn, name=nm, daemon=True)
@@ -119,6 +138,86 @@ class ChainRank:
     def _sync(self):
         if self.device.type == "cuda":
             torch.cuda.current_stream(self.device).synchronize()
+
+    def _packet(self, width: int) -> torch.Tensor:
+        """Fixed-size hop packet for activations of ``width`` bf16 columns: header bytes, then
+        up to ``small`` rows (reused per width; sends and receives of one rank are serial)."""
+        p = self._packets.get(width)
+        if p is None:
+            p = torch.zeros(HDR_BYTES + self.small * width * 2, dtype=torch.uint8,
+                            device=self.comm_dev)
+            self._packets[width] = p
+        return p
+
+    def _send_msg(self, hdr: list, payload: Optional[torch.Tensor], dst: int, group,
+                  width: int) -> None:
+        """One packet (header + the rows of a small request), then -- for a request of more
+        than ``small`` rows -- the payload as a second message."""
+        pk = self._packet(width)
+        h = torch.tensor(hdr, dtype=torch.int64)
+        pk[:40].copy_(h.view(torch.uint8))
+        R = hdr[1]
+        if payload is not None and hdr[3] == ST_OK and R <= self.small:
+            src = payload.reshape(-1).view(torch.uint8)
+            pk[HDR_BYTES:HDR_BYTES + src.numel()].copy_(src)
+            payload = None
+        self._send(pk, dst, group)
+        if payload is not None and hdr[3] == ST_OK:
+            self._send(payload, dst, group)
+
+    def _recv_hdr(self, src: int, group, width: int) -> tuple[list, torch.Tensor]:
+        pk = self._packet(width)
+        dist.recv(pk, src, group=group)
+        hdr = pk[:40].cpu().view(torch.int64).tolist()
+        return hdr, pk
+
+    def _recv_payload(self, dst: torch.Tensor, src: int, group, timeout_s: float) -> bool:
+        """Second message of a large request, bounded by the per-hop deadline."""
+        import datetime
+
+        t = dst if dst.device == self.comm_dev else torch.empty(dst.shape, dtype=dst.dtype,
+                                                                device=self.comm_dev)
+        w = dist.irecv(t, src, group=group)
+        try:
+            w.wait(timeout=datetime.timedelta(seconds=timeout_s))
+        except RuntimeError:
+            return False
+        if t is not dst:
+            dst.copy_(t)
+        return True
+
+    # -- progress / blame ---------------------------------------------------------------------
+    def _publisher(self) -> None:
+        """Ranks > 0: the id of the last request this stage processed, to the store."""
+        key = f"chain/processed/{self.rank}"
+        while True:
+            n = self._processed
+            if n != self._published:
+                try:
+                    self.store.set(key, str(n))
+                    self._published = n
+                except Exception:  # noqa: BLE001 -- the store went away at teardown
+                    return
+            time.sleep(PUBLISH_S)
+
+    def _progress(self, rank: int) -> int:
+        key = f"chain/processed/{rank}"
+        try:
+            if not self.store.check([key]):
+                return 0
+            return int(self.store.get(key))
+        except Exception:  # noqa: BLE001
+            return 0
+
+    def blame(self, rid: int) -> int:
+        """The stage a timed-out request is stuck at: the first rank > 0 that has not
+        processed it (every rank before it has, so the hop INTO it is where the request
+        stopped). Waits one publication period so a healthy stage's counter is current."""
+        time.sleep(2 * PUBLISH_S)
+        for k in range(1, self.world):
+            if self._progress(k) < rid:
+                return k
+        return self.world - 1
 
     # -- rank 0 -------------------------------------------------------------------------------
     def predict(self, x: np.ndarray, timeout: Optional[float] = None) -> np.ndarray:
@@ -152,9 +251,10 @@ class ChainRank:
         except FutureTimeout:
             with self._pending_lock:
                 self._pending.pop(rid, None)
-            raise StageFailure(self.names[1], grpc.StatusCode.DEADLINE_EXCEEDED,
-                               f"Deadline Exceeded (no answer from the chain within "
-                               f"{limit:.1f} s)") from None
+            k = self.blame(rid)
+            raise StageFailure(self.names[k], grpc.StatusCode.DEADLINE_EXCEEDED,
+                               f"Deadline Exceeded (request {rid} not processed by "
+                               f"{self.names[k]} within {limit:.1f} s)") from None
         status = hdr[3]
         if status != ST_OK:
             bad = self.names[hdr[4]] if 0 <= hdr[4] < len(self.names) else "stage"
@@ -166,12 +266,13 @@ class ChainRank:
         """Feeds the chain in request order (the only thread sending on the forward group)."""
         while True:
             item = self._sendq.get()
+            w = self.out_pad
             if item is None:
-                self._send(self._hdr(0, 0, 0, ST_STOP, 0), 1, self.fwd_group)
+                self._send_msg([0, 0, 0, ST_STOP, 0], None, 1, self.fwd_group, w)
                 return
             rid, R, rows, payload = item
-            self._send(self._hdr(rid, R, payload.shape[1], ST_OK, rows), 1, self.fwd_group)
-            self._send(payload, 1, self.fwd_group)
+            self._send_msg([rid, R, payload.shape[1], ST_OK, rows], payload, 1, self.fwd_group,
+                           w)
 
     def _receiver(self) -> None:
         """Collects results from the last rank and completes the waiting requests."""
@@ -186,6 +287,8 @@ class ChainRank:
                 res = torch.empty(R, n_out, dtype=torch.float32, device=self.comm_dev)
                 self._recv_into(res, last, self.ret_group)
                 res = res.cpu()
+            elif status == ST_DEADLINE:  # a stage's payload receive timed out: blame its hop
+                hdr = [rid, R, n_out, status, extra]
             with self._pending_lock:
                 fut = self._pending.pop(rid, None)
             if fut is not None:
@@ -212,47 +315,61 @@ class ChainRank:
     def loop(self) -> None:
         prev = self.rank - 1
         last = self.rank == self.world - 1
+        in_w = self.stage.in_pad
         served = 0
         while True:
-            hdr = self._recv_into(self._hdr(0, 0, 0, 0, 0), prev, self.fwd_group).tolist()
+            hdr, pk = self._recv_hdr(prev, self.fwd_group, in_w)
             req, R, width, status, extra = hdr
             if status == ST_STOP:
                 if last:
                     self._send(self._hdr(0, 0, 0, ST_STOP, 0), 0, self.ret_group)
                 else:
-                    self._send(self._hdr(0, 0, 0, ST_STOP, 0), self.rank + 1, self.fwd_group)
+                    self._send_msg([0, 0, 0, ST_STOP, 0], None, self.rank + 1, self.fwd_group,
+                                   self.out_pad)
                 return
             if status != ST_OK:  # propagate an upstream failure
+                self._processed = req
                 self._forward_hdr(last, req, R, 0, status, extra)
                 continue
             buf = self.stage.buffers(R)
-            self._recv_into(buf["x"], prev, self.fwd_group)
+            if R <= self.small:
+                buf["x"].reshape(-1).view(torch.uint8).copy_(
+                    pk[HDR_BYTES:HDR_BYTES + R * width * 2])
+            elif not self._recv_payload(buf["x"], prev, self.fwd_group, self.hop_timeout):
+                log.error(f"({self.names[self.rank]}) payload of request {req} did not arrive "
+                          f"within {self.hop_timeout:.1f} s")
+                self._forward_hdr(last, req, R, 0, ST_DEADLINE, prev)
+                continue
             try:
                 self._maybe_fault(served)
                 out = self.stage.forward(R)
-                self._sync()
+                if self.comm_dev.type == "cpu":
+                    self._sync()
             except ValueError:
+                self._processed = req
                 self._forward_hdr(last, req, R, 0, ST_VALUE, self.rank)
                 continue
             except Exception:  # noqa: BLE001
                 log.exception(f"({self.names[self.rank]}) stage failure")
+                self._processed = req
                 self._forward_hdr(last, req, R, 0, ST_INTERNAL, self.rank)
                 continue
             finally:
                 served += 1
+            self._processed = req  # received + computed: what rank 0's blame reads
             if last:
                 self._send(self._hdr(req, R, self.stage.out_dim, ST_OK, 0), 0, self.ret_group)
                 self._send(out[:, :self.stage.out_dim].contiguous(), 0, self.ret_group)
             else:
-                self._send(self._hdr(req, R, out.shape[1], ST_OK, 0), self.rank + 1,
-                           self.fwd_group)
-                self._send(out, self.rank + 1, self.fwd_group)
+                self._send_msg([req, R, out.shape[1], ST_OK, 0], out, self.rank + 1,
+                               self.fwd_group, self.out_pad)
 
     def _forward_hdr(self, last: bool, req, R, width, status, extra) -> None:
         if last:
             self._send(self._hdr(req, R, width, status, extra), 0, self.ret_group)
         else:
-            self._send(self._hdr(req, R, width, status, extra), self.rank + 1, self.fwd_group)
+            self._send_msg([req, R, width, status, extra], None, self.rank + 1, self.fwd_group,
+                           self.out_pad)
 
 
 def main(argv: Optional[list[str]] = None) -> int:

@@ -297,3 +297,45 @@ def test_worker_env_contract_and_forward_failure(model_files, tmp_path):
         c.close()
     finally:
         _stop(p)
+
+
+@pytest.fixture(scope="module")
+def model4_files(tmp_path_factory):
+    d = tmp_path_factory.mktemp("m4")
+    rng = np.random.default_rng(1)
+    dims = [784, 64, 48, 32, 10]
+    ws = [rng.standard_normal((dims[i + 1], dims[i])) * (2.0 / np.sqrt(dims[i])) for i in range(4)]
+    bs = [rng.standard_normal(dims[i + 1]) * 0.1 for i in range(4)]
+    cfg = d / "model4.json"
+    export_model_json(str(cfg), ws, bs, ["relu", "relu", "relu", "softmax"],
+                      layer_distribution=[1, 1, 1, 1])
+    x = rng.random((64, 784))
+    inp = d / "inputs4.json"
+    write_examples(str(inp), x, np.zeros(64, dtype=np.int64))
+    return cfg, inp, x
+
+
+@pytest.mark.parametrize("rows", [1, 40])  # one-packet serving path, packet + payload path
+def test_hung_stage_2_of_4_is_the_one_blamed(model4_files, tmp_path, rows):
+    """Stage 2 of a 4-rank chain hangs after one request: every later request fails with
+    DEADLINE_EXCEEDED "Failed to forward request to layer_container_2" -- the stage that
+    stopped, found from the per-rank progress each stage publishes -- not the first hop's
+    name (the round-2 chain always blamed names[1])."""
+    cfg, inp, x = model4_files
+    port = _port()
+    p = _start(cfg, inp, port, "ranks", tmp_path,
+               {"DNN_FAULT_STAGE": "2", "DNN_FAULT_KIND": "hang", "DNN_FAULT_AFTER": "1"},
+               args=("--hop-timeout", "1.0"))
+    try:
+        c = LayerClient(f"127.0.0.1:{port}", timeout=30)
+        ref = model_forward(load_model_config(str(cfg)).layers, x[:rows])
+        np.testing.assert_allclose(c.process(x[:rows]), ref, atol=2e-2)  # before the hang
+        for _ in range(2):
+            with pytest.raises(grpc.RpcError) as ei:
+                c.process(x[:rows])
+            assert ei.value.code() == grpc.StatusCode.DEADLINE_EXCEEDED, ei.value
+            assert "Failed to forward request to layer_container_2" in ei.value.details(), \
+                ei.value.details()
+        c.close()
+    finally:
+        _stop(p)

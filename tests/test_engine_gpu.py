@@ -144,7 +144,8 @@ def test_native_program_record_relocate(dev):
 def test_native_and_graph_optimizers_with_lr_schedule(dev, optim):
     """Adam/AdamW/SGD with a changing learning rate: native replay, HIP-graph replay and the
     Python path agree bit for bit (lr and the Adam step live in device memory, so recorded and
-    captured updates stay correct across steps)."""
+    captured updates stay correct across steps). SGD includes layers whose wgrad epilogue
+    applies the update (fused_layers): they must see this step's rate on every path."""
     import dataclasses
 
     spec = MLPSpec.parse("784-256-128-10")
@@ -154,6 +155,8 @@ def test_native_and_graph_optimizers_with_lr_schedule(dev, optim):
     for mode in ("python", "native", "graph"):
         tr = Trainer(spec, device=dev, micro_batch=512, num_micro=2,
                      optim=dataclasses.replace(optim), native_exec=mode != "python")
+        if optim.name == "sgd":  # one-split wgrads apply SGD in their epilogue (read lr_dev
+            assert tr.stages[0].params.fused_layers  # during W, before O: ADVICE r2)
         tr.set_batch(x, y)
         if mode == "graph":
             tr.capture(warmup=0)  # executes step 1 at lrs[0]

@@ -432,13 +432,17 @@ def test_sync_debug_mode(dev, monkeypatch):
 
 
 @pytest.mark.parametrize("la,lb", LAYOUTS)
-@pytest.mark.parametrize("ns", [3, 4])
+@pytest.mark.parametrize("ns", [3, 4, 5, "big5"])
 def test_pipeline_depth_bitwise(dev, la, lb, ns):
     """NS-stage LDS pipelines only change WHEN tiles are loaded, never the MFMA order: output
     must equal the 2-stage kernel bit for bit, including K shorter than the pipeline (nk < NS)
-    and uneven split-K ranges."""
+    and uneven split-K ranges. 5 = the asymmetric ring (A 3 deep, B 2 deep), also on the
+    8-wave tiles ("big5")."""
+    tiles = TILES
+    if ns == "big5":
+        ns, tiles = 5, BIG
     gen = torch.Generator().manual_seed(17 + ns + 4 * la + 2 * lb)
-    for (bm, bn) in TILES:
+    for (bm, bn) in tiles:
         for K in (64, 128, 192, 320):
             M, N = 256, 256
             a = _storage(la, M, K, gen, dev, False)
@@ -466,7 +470,7 @@ def test_pipeline_depth_rejects_bad_stages(dev):
     a = torch.zeros(128, 64, device=dev, dtype=torch.bfloat16)
     c = torch.zeros(128, 128, device=dev)
     with pytest.raises(ValueError, match="stages"):
-        ops.gemm(a, a, c, layout_a=KMAJ, layout_b=KMAJ, M=128, N=128, K=64, stages=5)
+        ops.gemm(a, a, c, layout_a=KMAJ, layout_b=KMAJ, M=128, N=128, K=64, stages=6)
 
 
 
