@@ -90,7 +90,7 @@ def step_ms(spec, R, x, y, dev, steps, reps):
 
 
 def tune_config(R, model, dev, table, steps, reps, log, only=None, verbose=False,
-                persist_opts=(0,), blas="1", margin=0.01):
+                persist_opts=(0,), blas="1", margin=0.01, stage_opts=(2,), tiles=None):
     spec = NAMED_MODELS.get(model) or MLPSpec.parse(model)
     kp0 = (spec.layers[0].in_dim + 63) // 64 * 64
     xs, ys = synthetic_mnist(min(R, 65536), seed=3)
@@ -109,25 +109,7 @@ def tune_config(R, model, dev, table, steps, reps, log, only=None, verbose=False
         prev = table.get(k)
         res = []
         trials = []  # (tile, splits, stages, persist, blas)
-        if cands == "logits":  # fused linear+CE (no table entry) vs library logits + CE kernel
-            if blas == "0":
-                continue
-            fused_ms = None
-            table.pop(k, None)
-            try:
-                fused_ms = step_ms(spec, R, x, y, dev, steps, reps)
-                table[k] = {"tile": [256, 64], "splits": 1, "stages": 2, "persist": 0, "blas": 1,
-                            "model": model}
-                lib_ms = step_ms(spec, R, x, y, dev, steps, reps)
-            except (ValueError, RuntimeError) as e:
-                log({"skip": k, "err": str(e)[:80]})
-                lib_ms = float("inf")
-            if fused_ms is None or lib_ms >= fused_ms * 0.995:
-                table.pop(k, None)
-            else:
-                table[k]["step_ms"] = round(lib_ms, 4)
-            log({"sig": k, "fused_ms": fused_ms and round(fused_ms, 4),
-                 "library_ms": round(lib_ms, 4), "library": k in table})
+        if cands == "logits":  # the fused linear+CE GEMM has a fixed tile: nothing to tune
             continue
         if blas == "only" and prev is not None:
             # incumbent vs the library GEMM only (csrc/runtime/blaslt.cpp)
@@ -135,9 +117,13 @@ def tune_config(R, model, dev, table, steps, reps, log, only=None, verbose=False
                            prev.get("persist", 0), 0))
         else:
             for (tile, s) in cands:
+                if tiles and tuple(tile) not in tiles:
+                    continue
+                # LDS ring forms (2 = 2-deep, 5 = asymmetric A3/B2 ring, one-tile form only);
                 # 256x256 tiles also run the ping-pong form (stages 8, gemm_pp.hip)
-                forms = [(2, pers) for pers in persist_opts]
-                if tuple(tile) == (256, 256):
+                forms = [(ns, pers) for ns in stage_opts for pers in persist_opts
+                         if not (ns == 5 and pers)]
+                if tuple(tile) == (256, 256) and 8 in stage_opts:
                     forms.append((8, 0))
                 trials += [(tuple(tile), s, ns, pers, 0) for ns, pers in forms]
         if blas in ("1", "only"):
@@ -186,11 +172,16 @@ def main():
     ap.add_argument("--persist", default="0,1",
                     help="GEMM forms to try: 0 = one tile per workgroup (gemm.hip), 1 = "
                     "persistent workgroups (gemm_persist.hip)")
+    ap.add_argument("--stages", default="2,5,8",
+                    help="LDS ring forms to try: 2, 3, 5 (asymmetric A3/B2), 8 (ping-pong)")
+    ap.add_argument("--tiles", default="",
+                    help="restrict candidates to these tiles, e.g. 256x256,256x128")
     ap.add_argument("--margin", type=float, default=0.01,
                     help="relative win a challenger needs over the incumbent entry")
     ap.add_argument("--blas", default="0", choices=["0", "1", "only"],
-                    help="hipBLASLt library GEMM as a candidate: 0 no, 1 yes, only = incumbent "
-                    "vs library per GEMM (quick)")
+                    help="hipBLASLt library GEMM as a candidate (COMPARISON build only, "
+                    "_build --blas; the product table never holds library entries): 0 no, "
+                    "1 yes, only = incumbent vs library per GEMM")
     a = ap.parse_args()
     os.environ.pop("DNN_BLAS", None)  # the table decides while tuning
     dev = torch.device("cuda")
@@ -213,7 +204,9 @@ def main():
         tune_config(int(rows), model, dev, table, a.steps, a.reps, log,
                     only=set(a.only.split(",")) if a.only else None, verbose=a.verbose,
                     persist_opts=tuple(int(v) for v in a.persist.split(",")), blas=a.blas,
-                    margin=a.margin)
+                    margin=a.margin, stage_opts=tuple(int(v) for v in a.stages.split(",")),
+                    tiles={tuple(int(v) for v in t.split("x")) for t in a.tiles.split(",")}
+                    if a.tiles else None)
         doc["entries"] = dict(table)
         with open(a.out, "w") as f:
             json.dump(doc, f, indent=1, sort_keys=True)

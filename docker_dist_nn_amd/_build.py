@@ -7,7 +7,12 @@ host objects only, GPU code untouched -- GPU ASan / xnack+ is not available on t
 The result is one shared object placed next to this file, so it travels with the repository
 snapshot to the GPU box and is what the driver sees loaded.
 
-Usage: ``python -m docker_dist_nn_amd._build [--force] [--jobs N] [--sanitize]``.
+The product build links NO vendor GEMM library: the library-GEMM entry points come from
+``csrc/runtime/blaslt_stub.cpp`` (unavailable). ``--blas`` makes the comparison build instead:
+``csrc/compare/blaslt.cpp`` + ``-lhipblaslt`` (hipBLASLt A/B runs, bench/gemm_vs_blas.py); it
+replaces the in-tree module until the next product build.
+
+Usage: ``python -m docker_dist_nn_amd._build [--force] [--jobs N] [--sanitize] [--blas]``.
 """
 from __future__ import annotations
 
@@ -48,9 +53,11 @@ def _pybind_includes() -> list[str]:
     return inc
 
 
-def _sources() -> tuple[list[Path], list[Path]]:
+def _sources(blas: bool = False) -> tuple[list[Path], list[Path]]:
     dev = sorted((CSRC / "kernels").glob("*.hip"))
     host = sorted((CSRC / "runtime").glob("*.cpp")) + [CSRC / "bindings.cpp"]
+    if blas:  # comparison build: the real hipBLASLt path instead of the stub
+        host = [h for h in host if h.name != "blaslt_stub.cpp"] + [CSRC / "compare" / "blaslt.cpp"]
     return dev, host
 
 
@@ -90,10 +97,10 @@ def _compile(cmd: list[str]) -> tuple[list[str], int, str]:
 
 
 def build(force: bool = False, jobs: int | None = None, sanitize: bool = False,
-          verbose: bool = False) -> Path:
+          verbose: bool = False, blas: bool = False) -> Path:
     """Compile (incrementally) and link the extension; returns the path of the .so."""
-    dev_src, host_src = _sources()
-    tag = "asan" if sanitize else "rel"
+    dev_src, host_src = _sources(blas)
+    tag = "asan" if sanitize else "rel"  # (stub and library objects have distinct names)
     extra = os.environ.get("DNN_HIP_DEFINES", "")
     if extra:
         tag += "-" + hashlib.sha1(extra.encode()).hexdigest()[:8]
@@ -123,10 +130,12 @@ def build(force: bool = False, jobs: int | None = None, sanitize: bool = False,
     # the .so records which object set it was linked from: switching back to an older header
     # set (its objects exist and are OLDER than the .so) must still relink
     stamp = out.with_suffix(".objset")
-    stale_set = not stamp.exists() or stamp.read_text().strip() != obj_dir.name
+    objset = obj_dir.name + ("+blas" if blas else "")
+    stale_set = not stamp.exists() or stamp.read_text().strip() != objset
     if force or jobs_to_run or stale_set or not out.exists() or out.stat().st_mtime < newest:
         link = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(out),
-                *map(str, objs), f"-L{ROCM / 'lib'}", "-lamdhip64", "-lhipblaslt"]
+                *map(str, objs), f"-L{ROCM / 'lib'}", "-lamdhip64",
+                *(["-lhipblaslt"] if blas else [])]
         if sanitize:
             link += ["-fsanitize=address,undefined"]
         cmd, rc, log = _compile(link)
@@ -134,7 +143,7 @@ def build(force: bool = False, jobs: int | None = None, sanitize: bool = False,
             sys.stderr.write(" ".join(cmd) + "\n" + log)
         if rc:
             raise RuntimeError("native link failed")
-        stamp.write_text(obj_dir.name + "\n")
+        stamp.write_text(objset + "\n")
     return out
 
 
@@ -144,8 +153,10 @@ def main(argv: list[str] | None = None) -> int:
     ap.add_argument("--jobs", type=int, default=None)
     ap.add_argument("--sanitize", action="store_true")
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--blas", action="store_true",
+                    help="comparison build: link hipBLASLt (library GEMM A/B runs only)")
     a = ap.parse_args(argv)
-    p = build(force=a.force, jobs=a.jobs, sanitize=a.sanitize, verbose=a.verbose)
+    p = build(force=a.force, jobs=a.jobs, sanitize=a.sanitize, verbose=a.verbose, blas=a.blas)
     print(p)
     return 0
 

@@ -83,6 +83,56 @@ def _device(name: str):
     return torch.device("cuda", 0)
 
 
+def train_ranks(mc, a, distribution, random_init: bool, n_st: int):
+    """``--train`` with one rank per non-empty stage (reference: one container per stage,
+    /root/reference/src/run_grpc_fcnn.py:83-155): the pipelined trainer (cli/train.py) under
+    launch.spawn_ranks -- RCCL hops on GPUs, gloo with ``--device cpu`` -- exporting the
+    trained model from its committed checkpoint; returns (weights, biases, report)."""
+    import tempfile
+
+    from ..config import load_model_config
+    from ..launch import spawn_ranks
+    from ..weights_io import export_model_json
+
+    with tempfile.TemporaryDirectory(prefix="fcnn_train_") as tmp:
+        args = ["--layer-distribution", json.dumps(list(distribution)), "--pp", str(n_st),
+                "--lr", str(a.lr), "--optimizer", a.optimizer, "--momentum", str(a.momentum),
+                "--micro-batch", str(a.micro_batch),
+                "--num-micro-batches", str(a.num_micro_batches), "--schedule", a.schedule,
+                "--seed", str(a.seed), "--epochs", str(a.epochs), "--steps", str(a.steps),
+                "--checkpoint-dir", os.path.join(tmp, "ckpt"),
+                "--save", os.path.join(tmp, "trained.json"),
+                "--device", "cpu" if a.device == "cpu" else "auto"]
+        if random_init:
+            args += ["--model", "-".join(str(w) for w in mc.spec().widths)]
+        else:
+            cfg = os.path.join(tmp, "start.json")
+            export_model_json(cfg, [L.weight for L in mc.layers], [L.bias for L in mc.layers],
+                              [L.activation for L in mc.layers],
+                              layer_distribution=list(distribution))
+            args += ["--config", cfg]
+        if a.synthetic:
+            args += ["--synthetic", str(a.synthetic)]
+        elif os.path.exists(a.inputs):
+            args += ["--inputs", os.path.abspath(a.inputs)]
+        if a.metrics:
+            args += ["--metrics", a.metrics]
+        log.info(f"training with {n_st} ranks (one per stage): {' '.join(args)}")
+        t0 = time.time()
+        job = spawn_ranks("docker_dist_nn_amd.cli.train", args, n_st,
+                          names=[f"train_stage{i}" for i in range(n_st)])
+        try:
+            codes = job.wait()
+        finally:
+            job.terminate()
+        if any(codes):
+            raise RuntimeError(f"training ranks exited with {codes}")
+        out = load_model_config(os.path.join(tmp, "trained.json"))
+    report = {"ranks": n_st, "train_seconds": time.time() - t0,
+              "layer_distribution": list(distribution)}
+    return [L.weight for L in out.layers], [L.bias for L in out.layers], report
+
+
 def main(argv: Optional[list[str]] = None, script_dir: str = SCRIPT_DIR_DEFAULT) -> int:
     logging.basicConfig(level=logging.INFO, format="%(asctime)s - %(levelname)s - %(message)s")
     a = build_parser(script_dir).parse_args(argv)
@@ -147,11 +197,19 @@ def main(argv: Optional[list[str]] = None, script_dir: str = SCRIPT_DIR_DEFAULT)
 
     # ---- optional training -----------------------------------------------------------------
     if a.train:
+        import torch
+
         from .train import train_model
 
+        n_st = len(plans)
+        ranks = n_st > 1 and (a.mode == "ranks" or (
+            a.mode == "auto" and a.device != "cpu" and torch.cuda.device_count() >= n_st))
         try:
-            ws, bs, report = train_model(mc, examples, a, distribution, random_init)
-        except ValueError as e:
+            if ranks:  # one process (GPU) per non-empty stage, like the reference's containers
+                ws, bs, report = train_ranks(mc, a, distribution, random_init, n_st)
+            else:
+                ws, bs, report = train_model(mc, examples, a, distribution, random_init)
+        except (ValueError, RuntimeError) as e:
             log.error(f"Training failed: {e}")
             return 1
         for L, w, b in zip(mc.layers, ws, bs):

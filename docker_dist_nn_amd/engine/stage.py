@@ -431,8 +431,7 @@ class Stage:
         # count is one 64/128-wide tile: logits then never exist in memory
         gl = self.geoms[-1]
         self.fused_xent = (self.last and gl.np_ in (64, 128) and
-                           switches.get("DNN_FUSED_XENT") == "1" and
-                           not self._logits_on_library(gl))
+                           switches.get("DNN_FUSED_XENT") == "1")
         self.acts: list[torch.Tensor] = []  # output of local layer i
         for i, g in enumerate(self.geoms):
             is_logits = self.last and i == len(self.geoms) - 1
@@ -537,16 +536,6 @@ class Stage:
         self._rx = self._rl = None
         self.boundary = "bf16"
         self._fp8_next = self._fp8_prev = False
-
-    def _logits_on_library(self, gl) -> bool:
-        """The tuned table routes the logits GEMM to hipBLASLt (long contractions, where the
-        one-row-tile fused cross-entropy GEMM cannot split K: the wide model's 8192-deep last
-        layer ran on 128 workgroups). Then logits are a library GEMM (fp32 out, bias epilogue)
-        followed by the softmax-CE kernel."""
-        if self.device.type != "cuda":
-            return False
-        t = ops.tuning.lookup("fwd", self.mb, gl.np_, gl.kp)
-        return ops.kernels._blas("fwd", t)
 
     def _tail_ok(self) -> bool:
         if not (self.fused_xent and self.device.type == "cuda" and len(self.geoms) >= 3 and

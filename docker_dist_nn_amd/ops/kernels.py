@@ -78,16 +78,40 @@ def _persist(kind: str, entry) -> int:
     return -1 if v == 1 else int(v)
 
 
-def _blas(kind: str, entry) -> bool:
-    """Library (hipBLASLt) GEMM for this product? DNN_BLAS: "" / "table" = the tuned table's
-    ``blas`` flag, "0" = never, "1" = every product the library path supports, or per kind
-    ("fwd=1,dgrad=0,wgrad=1")."""
+def _blas_requested(kind: str, entry) -> bool:
+    """Is the library (hipBLASLt) GEMM requested for this product? DNN_BLAS: "" / "table" = the
+    tuned table's ``blas`` flag, "0" = never, "1" = every product the library path supports,
+    or per kind ("fwd=1,dgrad=0,wgrad=1")."""
     spec = switches.get("DNN_BLAS").strip()
     if spec in ("", "table"):
         return bool((entry or {}).get("blas", 0))
     if "=" not in spec:
         return spec == "1"
     return dict(kv.split("=") for kv in spec.split(",")).get(kind, "0") == "1"
+
+
+_BLAS_WARNED = []
+
+
+def blas_built() -> bool:
+    """The library path exists only in the comparison build (``_build --blas``); the product
+    build links no vendor GEMM library."""
+    return bool(native().blas_available())
+
+
+def _blas(kind: str, entry) -> bool:
+    """Library GEMM for this product: requested (``_blas_requested``) AND built in."""
+    if not _blas_requested(kind, entry):
+        return False
+    if blas_built():
+        return True
+    if not _BLAS_WARNED:
+        _BLAS_WARNED.append(1)
+        import warnings
+
+        warnings.warn("DNN_BLAS asks for the hipBLASLt path, which is only in the comparison "
+                      "build (python -m docker_dist_nn_amd._build --blas): own kernels run")
+    return False
 
 
 _BLAS_OK: dict = {}

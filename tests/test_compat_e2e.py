@@ -339,3 +339,30 @@ def test_hung_stage_2_of_4_is_the_one_blamed(model4_files, tmp_path, rows):
         c.close()
     finally:
         _stop(p)
+
+
+def test_train_one_rank_per_stage_matches_single_process(model4_files, tmp_path):
+    """run_grpc_fcnn.py --train with one process per stage (--mode ranks: cli/train.py under
+    launch.spawn_ranks, gloo on CPU) trains [1,1,1,1] like the single-process (loopback)
+    trainer: the exported neuron-JSON weights agree within bf16 tolerance."""
+    cfg, inp, _ = model4_files
+    outs = {}
+    for mode in ("local", "ranks"):
+        out = tmp_path / f"trained_{mode}.json"
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "src", "run_grpc_fcnn.py"),
+                            "--config", str(cfg), "--inputs", str(inp), "--mode", mode,
+                            "--device", "cpu", "--train", "--steps", "4", "--synthetic", "2048",
+                            "--micro-batch", "128", "--num-micro-batches", "4", "--lr", "0.05",
+                            "--no-serve", "--save", str(out),
+                            "--cache-dir", str(tmp_path / f"c_{mode}")],
+                           capture_output=True, text=True, timeout=300,
+                           env=dict(os.environ, PYTHONPATH=ROOT))
+        assert r.returncode == 0, r.stdout + r.stderr
+        if mode == "ranks":
+            assert "training with 4 ranks" in r.stdout + r.stderr
+        outs[mode] = load_model_config(str(out)).layers
+    start = load_model_config(str(cfg)).layers
+    for a, b, s0 in zip(outs["local"], outs["ranks"], start):
+        assert not np.allclose(a.weight, s0.weight)  # it trained
+        np.testing.assert_allclose(a.weight, b.weight, rtol=2e-2, atol=2e-3)
+        np.testing.assert_allclose(a.bias, b.bias, rtol=2e-2, atol=2e-3)

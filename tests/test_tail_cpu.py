@@ -60,14 +60,14 @@ def test_build_reads_per_file_flags():
 
 def test_blas_switch(monkeypatch):
     monkeypatch.delenv("DNN_BLAS", raising=False)
-    assert K._blas("fwd", {"blas": 1}) and not K._blas("fwd", {"tile": [64, 64]})
-    assert not K._blas("fwd", None)
+    assert K._blas_requested("fwd", {"blas": 1}) and not K._blas_requested("fwd", {"tile": [64, 64]})
+    assert not K._blas_requested("fwd", None)
     monkeypatch.setenv("DNN_BLAS", "0")
-    assert not K._blas("fwd", {"blas": 1})
+    assert not K._blas_requested("fwd", {"blas": 1})
     monkeypatch.setenv("DNN_BLAS", "1")
-    assert K._blas("wgrad", None)
+    assert K._blas_requested("wgrad", None)
     monkeypatch.setenv("DNN_BLAS", "fwd=1,wgrad=0")
-    assert K._blas("fwd", None) and not K._blas("wgrad", {"blas": 1}) and not K._blas("dgrad", None)
+    assert K._blas_requested("fwd", None) and not K._blas_requested("wgrad", {"blas": 1}) and not K._blas_requested("dgrad", None)
 
 
 def test_reference_tail_waves_match_kernel_forms():
