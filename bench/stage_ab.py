@@ -67,15 +67,17 @@ def case_wgrad(R, M, N, splits, variants):
 
 
 T256, T128 = (256, 256), (128, 128)
+BIG = [(T256, 2), (T256, 5), (T256, 12), (T256, 13), (T256, 14), ((256, 128), 12)]
 CASES = {
-    "f0": lambda: case_fwd(65536, 832, 512, [(T256, 2), (T256, 5), ((256, 128), 5)]),
-    "f1": lambda: case_fwd(65536, 512, 256, [(T256, 2), (T256, 5), ((256, 128), 5)]),
-    "d1": lambda: case_dgrad(65536, 256, 512, [(T256, 2), (T256, 5), ((256, 128), 5)]),
-    "w0": lambda: case_wgrad(65536, 512, 832, 18, [(T128, 2), (T128, 3), (T128, 5)]),
-    "w1": lambda: case_wgrad(65536, 256, 512, 16, [(T128, 2), (T128, 3), (T128, 5)]),
-    "m8f": lambda: case_fwd(65536, 1024, 1024, [(T256, 2), (T256, 5), (T256, 8)]),
-    "m8d": lambda: case_dgrad(65536, 1024, 1024, [(T256, 2), (T256, 5)]),
-    "wide": lambda: case_fwd(16384, 8192, 8192, [(T256, 2), (T256, 5), (T256, 8)]),
+    "f0": lambda: case_fwd(65536, 832, 512, BIG),
+    "f1": lambda: case_fwd(65536, 512, 256, BIG),
+    "d1": lambda: case_dgrad(65536, 256, 512, BIG),
+    "w0": lambda: case_wgrad(65536, 512, 832, 18, [(T128, 2), (T128, 12), (T128, 14),
+                                                    (T256, 2), (T256, 12)]),
+    "w1": lambda: case_wgrad(65536, 256, 512, 64, [(T128, 2), (T128, 12), (T128, 14)]),
+    "m8f": lambda: case_fwd(65536, 1024, 1024, BIG),
+    "m8d": lambda: case_dgrad(65536, 1024, 1024, BIG),
+    "wide": lambda: case_fwd(16384, 8192, 8192, [(T256, 2), (T256, 12), (T256, 13)]),
 }
 
 

@@ -849,14 +849,17 @@ class Stage:
                 self.wgrad_algo != "streamk" and self.device.type == "cuda" and
                 switches.get("DNN_FUSE_FIN_SGD") == "1")
 
-    def _record_fin_sgd(self) -> None:
-        """Record the whole-stage gradient reduction with the SGD update fused in (segment
-        FINO; lr from device memory like record_update)."""
+    def _record_fin_sgd(self, a: int = 0, b: Optional[int] = None) -> None:
+        """Record the gradient reduction of local layers [a, b) (default: all) with the SGD
+        update fused in (segment FINO, or FINO{a}-{b-1} for a layer range: SGD only, so the
+        step counter needs no advance; lr from device memory like record_update)."""
         p = self.params
         p._device_scalars()
         o = p.optim
+        L = len(self.geoms)
+        b = L if b is None else b
         wt_fused = switches.get("DNN_FIN_WT") == "1" and p.shadow is not None
-        jobs = self._jobs(tuple(range(len(self.geoms))), with_wt=wt_fused)
+        jobs = self._jobs(tuple(range(a, b)), with_wt=wt_fused)
         # layers whose W^T comes out of the update launch itself (no transpose launch after it)
         skip = frozenset(i for i in self._wt_by_update_layers()) if wt_fused else frozenset()
         if o.name == "sgd":
@@ -864,8 +867,10 @@ class Stage:
                                             mom=p.state[0] if p.state else None,
                                             shadow=p.shadow, lr=o.lr, momentum=o.momentum,
                                             weight_decay=o.weight_decay, lr_dev=p.lr_dev))
-            p.refresh_t(step=True, skip=skip)
+            p.refresh_t(a, b, step=True, skip=skip)
             return
+        if (a, b) != (0, L):
+            raise ValueError("layer-range fused updates are SGD only")
         ops.reduce_multi(jobs, sgd=dict(grad=p.grad, master=p.master, mom=p.state[0],
                                         v=p.state[1], shadow=p.shadow, lr=o.lr,
                                         weight_decay=o.weight_decay, lr_dev=p.lr_dev,
@@ -1024,6 +1029,13 @@ class Stage:
             if self.fused_fin_sgd_ok():
                 prog.mark("FINO")
                 self._record_fin_sgd()
+                if self.params.optim.name == "sgd" and L > 1:
+                    # per-layer-range forms: the overlap plan updates the small layers on the
+                    # side stream while the big layer's wgrad still runs (DNN_SPLIT_FINO)
+                    for a in range(L):
+                        for b in range(a, L):
+                            prog.mark(f"FINO{a}-{b}")
+                            self._record_fin_sgd(a, b + 1)
             prog.mark("O")
             self.params.record_update()
             for a in range(L if not (self.params.sharded or self.params.fused_layers) else 0):

@@ -419,10 +419,21 @@ class PipelineExecutor:
                 plan += [(st, f"B0.L{i}", 0), (None, "@fork", 0), (st, f"W{i}", 1)]
             else:
                 plan += [(st, f"W{i}", 1), (st, f"B0.L{i}", 0), (None, "@fork", 0)]
-        if plan[-1][1] == "@fork":
+        split = (switches.get("DNN_SPLIT_FINO") == "1" and L > 1 and
+                 f"FINO1-{L - 1}" in segs and "FINO0-0" in segs and 0 not in fused)
+        if plan[-1][1] == "@fork" and not split:
             plan = plan[:-1]
         if switches.get("DNN_FORK_ELIDE") in ("1", "2"):
             plan = self._elide_forks(st, plan, rewait=switches.get("DNN_FORK_ELIDE") == "2")
+        if split:
+            # the side stream reduces + updates layers 1..L-1 (their wgrads are done; the fork
+            # above orders it after the last dgrad, the last reader of their W^T) while the
+            # main stream runs W0; then only layer 0's reduction + update is left at the end
+            if plan[-1][1] != "@fork":
+                plan.append((None, "@fork", 0))
+            plan += [(st, f"FINO1-{L - 1}", 1), (st, "W0", 0), (st, "FINO0-0", 0),
+                     (None, "@join", 0)]
+            return plan
         plan += [(st, "W0", 0), (None, "@join", 0)]
         plan.append((st, "FINO", 0) if "FINO" in segs else (st, "FIN", 0))
         if "FINO" not in segs:

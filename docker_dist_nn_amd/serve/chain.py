@@ -379,12 +379,23 @@ def main(argv: Optional[list[str]] = None) -> int:
     logging.basicConfig(level=logging.INFO, format="%(asctime)s - %(levelname)s - %(message)s")
     plan = json.load(open(a.plan))
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    # a request crosses threads at every hop (ingress worker -> sender -> ... -> receiver ->
+    # worker): with the default 5 ms GIL switch interval a hand-off can wait a whole interval
+    import sys
+
+    sys.setswitchinterval(1e-4)
+    torch.set_num_threads(max(1, min(4, (os.cpu_count() or 8) // max(1, world))))
     use_gpu = plan.get("device", "auto") != "cpu" and torch.cuda.is_available()
     if use_gpu:
-        local = int(os.environ.get("LOCAL_RANK", rank))
+        # DNN_FORCE_DEVICE / DNN_DIST_BACKEND=gloo: every stage on one GPU, hops through host
+        # memory (one-GPU rehearsals of the rank chain; RCCL needs one GPU per rank)
+        local = int(switches.get("DNN_FORCE_DEVICE") or os.environ.get("LOCAL_RANK", rank))
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+        if switches.get("DNN_DIST_BACKEND") == "gloo":
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
     else:
         device = torch.device("cpu")
         dist.init_process_group("gloo", rank=rank, world_size=world)

@@ -3,7 +3,8 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/r3_abt; mkdir -p $O
 cd $R
-B=${1:-profiles/r3_tune/table_asym.json}
+B=${1:-bench/tables/table_asym.json}
+test -f $B || { echo "missing table $B"; exit 1; }
 for i in 1 2 3 4; do
   for t in cur new; do
     if [ $t = new ]; then export DNN_TUNED_TABLE=$B; else unset DNN_TUNED_TABLE; fi

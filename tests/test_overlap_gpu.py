@@ -21,9 +21,12 @@ def test_overlap_plan_bitwise(dev, monkeypatch, model, rows):
     xb[:, :784] = torch.from_numpy(x).to(torch.bfloat16)
     xb, yb = xb.to(dev), torch.from_numpy(y).to(dev)
     res = []
-    for flag in ("0", "1", "2", "3", "4", "1e1", "1e2"):  # 1eK: plan 1 with DNN_FORK_ELIDE=K
+    # 1eK: plan 1 with DNN_FORK_ELIDE=K; 1s: plan 1 with DNN_SPLIT_FINO (layers 1.. reduced and
+    # updated on the side stream during W0)
+    for flag in ("0", "1", "2", "3", "4", "1e1", "1e2", "1s"):
         monkeypatch.setenv("DNN_BW_OVERLAP", flag[0])
-        monkeypatch.setenv("DNN_FORK_ELIDE", flag[2:] or "0")
+        monkeypatch.setenv("DNN_FORK_ELIDE", flag[2:] if flag[1:2] == "e" else "0")
+        monkeypatch.setenv("DNN_SPLIT_FINO", "1" if flag == "1s" else "0")
         tr = Trainer(spec, micro_batch=rows, num_micro=1,
                      optim=OptimConfig(lr=0.1, momentum=0.9), device=dev)
         losses = []
