@@ -50,15 +50,15 @@ __device__ __forceinline__ void gemm_tile_wg(const GemmParams& p, int tiles_n, i
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int m0 = tm * BM, n0 = tn * BN;
-  int kbase, nk;
+  int kbase, nk;  // nk in k-steps of C::BK (split ranges stay in 64-deep units)
   if (p.k_total > 0) {  // uneven split-K: split s takes k-steps [s*KS/S, (s+1)*KS/S)
     const int KS = p.k_total >> 6, S = nwg / (tiles_n * tiles_m);
     const int a = (int)((long)split * KS / S), b = (int)((long)(split + 1) * KS / S);
     kbase = a * 64;
-    nk = b - a;
+    nk = (b - a) * (64 / C::BK);
   } else {
     kbase = split * p.K;
-    nk = p.K >> 6;
+    nk = p.K / C::BK;
   }
 
   f32x4_t acc[C::FM][C::FN];
@@ -213,6 +213,24 @@ static gemm_fn pick4(int ns, int la, int lb, int f32) {
                    : pick_layout<Cfg<BM, BN, 2, 2, 4>>(la, lb, f32);
 }
 
+// Stage codes 12 / 13 / 14: 32-deep k-steps (Cfg BK = 32) with 2 / 3 / 4 ring stages -- e.g. a
+// 64-KiB 256x256 ring, so two workgroups share a CU. Instantiated for the tiles where that
+// changes the residency: 256x256, 256x128, 128x128.
+static gemm_fn pick_bk32(int bm, int bn, int ns, int la, int lb, int f32) {
+  if (bm == 256 && bn == 256) {
+    if (ns == 12) return pick_layout<Cfg<256, 256, 4, 2, 2, 2, 32>>(la, lb, f32);
+    if (ns == 13) return pick_layout<Cfg<256, 256, 4, 2, 3, 3, 32>>(la, lb, f32);
+    if (ns == 14) return pick_layout<Cfg<256, 256, 4, 2, 4, 4, 32>>(la, lb, f32);
+  } else if (bm == 256 && bn == 128) {
+    if (ns == 12) return pick_layout<Cfg<256, 128, 4, 2, 2, 2, 32>>(la, lb, f32);
+    if (ns == 13) return pick_layout<Cfg<256, 128, 4, 2, 3, 3, 32>>(la, lb, f32);
+  } else if (bm == 128 && bn == 128) {
+    if (ns == 12) return pick_layout<Cfg<128, 128, 2, 2, 2, 2, 32>>(la, lb, f32);
+    if (ns == 14) return pick_layout<Cfg<128, 128, 2, 2, 4, 4, 32>>(la, lb, f32);
+  }
+  return nullptr;
+}
+
 bool gemm_tile_supported(int bm, int bn) {
   const bool small = (bm == 64 || bm == 128) && (bn == 64 || bn == 128);
   const bool big = (bm == 256 && (bn == 64 || bn == 128 || bn == 256)) || (bm == 128 && bn == 256);
@@ -226,7 +244,7 @@ const char* gemm_error_string(int code) {
     case 0: return "ok";
     case -1: return "unsupported tile (64|128 x 64|128, 256 x 64|128|256, 128 x 256)";
     case -2: return "M and N must be positive multiples of 8 (edge tiles are partial)";
-    case -3: return "per-split K must be a positive multiple of 64";
+    case -3: return "per-split K must be a positive multiple of 64 (32 for the 32-deep k-step codes 12-14)";
     case -4: return "leading dimensions must be multiples of 8 elements (16-byte rows)";
     case -5: return "pointers must be 16-byte aligned";
     case -6: return "bad layout code";
@@ -236,7 +254,7 @@ const char* gemm_error_string(int code) {
     case -10: return "colsum needs bf16 output and ld_colsum >= N";
     case -11: return "fused cross-entropy needs bf16 output, N == bn <= 128, a bias and 0 < n_cls <= N";
     case -13: return "relu bit masks need bf16 output, act = relu, ld_mask >= N/8, no aux/xent, one-tile form";
-    case -12: return "pipeline stages must be 2..4 or 5 = A3/B2 ring (8-wave tiles: 2, 3, 5; 256x256: 2, 5 or 8 = ping-pong; 5: one-tile form, no fused xent)";
+    case -12: return "pipeline stages must be 2..4, 5 = A3/B2 ring, 12..14 = 32-deep k-steps with 2..4 stages (256x256: 12-14, 256x128: 12-13, 128x128: 12, 14) (8-wave tiles: 2, 3, 5; 256x256: 2, 5 or 8 = ping-pong; 5, 12-14: one-tile form, no fused xent)";
     case -14: return "transposed output ct needs bf16 output (or the fused update), no xent, one split, one-tile form, ld_ct >= M, 16-byte alignment";
     case -15: return "fused SGD epilogue needs f32 output, one split, no accumulate/bias/xent, a device lr, 16-byte aligned buffers, N % 8 == 0, one-tile form";
     default: return "unknown gemm error";
@@ -249,14 +267,15 @@ int default_stages(int bm, int bn) {
   return 2;
 }
 
-int gemm_check(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, int splits) {
+int gemm_check(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, int splits,
+               int kq) {
   if (!gemm_tile_supported(bm, bn)) return -1;
   // partial edge tiles: M and N need only be multiples of 8 (16-byte rows / chunks)
   if (p.M <= 0 || p.N <= 0 || p.M % 8 || p.N % 8) return -2;
   if (splits < 1) return -3;
-  if (p.k_total > 0) {
+  if (p.k_total > 0) {  // uneven split-K ranges are cut in 64-deep units
     if (p.k_total % 64 || splits > p.k_total / 64) return -3;
-  } else if (p.K <= 0 || p.K % 64) {
+  } else if (p.K <= 0 || p.K % kq) {  // kq: the kernel's k-step (64, or 32 for codes 12-14)
     return -3;
   }
   const long ktot = p.k_total > 0 ? (long)p.k_total : (long)p.K * splits;
@@ -290,7 +309,8 @@ int gemm_check(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn,
 
 int gemm_bf16(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, int splits,
               hipStream_t stream, int stages, int persist) {
-  const int rc = gemm_check(p, la, lb, out_f32, bm, bn, splits);
+  const int rc = gemm_check(p, la, lb, out_f32, bm, bn, splits,
+                            stages >= 12 && stages <= 14 ? 32 : 64);
   if (rc) return rc;
   if ((p.mask_out || p.mask_in) && persist) return -13;
   if (p.ct && persist) return -14;
@@ -309,6 +329,17 @@ int gemm_bf16(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, 
   }
   const int nt = gemm_tile_threads(bm, bn);
   const int ns = stages ? stages : default_stages(bm, bn);
+  if (ns >= 12 && ns <= 14) {  // 32-deep k-steps (one-tile form, no fused xent)
+    if (persist || p.xent_labels) return -12;
+    gemm_fn f = pick_bk32(bm, bn, ns, la, lb, out_f32);
+    if (!f) return -12;
+    const int tiles_n = (p.N + bn - 1) / bn, tiles_m = (p.M + bm - 1) / bm;
+    const int nwg = tiles_n * tiles_m * splits;
+    GemmParams q = p;
+    if (q.group_m <= 0) q.group_m = tiles_n >= 8 ? 4 : 1;
+    hipLaunchKernelGGL(f, dim3(nwg), dim3(nt), 0, stream, q, tiles_n, tiles_m, nwg);
+    return hipGetLastError() == hipSuccess ? 0 : -9;
+  }
   // 8-wave tiles: NS = 3 where three stages fit (not 256x256); 5 = asymmetric A3/B2 ring
   if (ns < 2 || ns > 5 || (nt == 512 && (ns == 4 || (ns == 3 && bm == 256 && bn == 256))))
     return -12;

@@ -86,7 +86,7 @@ int gemm_bf16_group(const GemmParams* ps, const int* splits, int n, int layout_a
                     int out_f32, int bm, int bn, int stages, hipStream_t stream);
 // The argument checks of gemm_bf16 (0 or its error code).
 int gemm_check(const GemmParams& p, int layout_a, int layout_b, int out_f32, int bm, int bn,
-               int splits);
+               int splits, int kq = 64);
 int gemm_bf16(const GemmParams& p, int layout_a, int layout_b, int out_f32, int bm, int bn,
               int splits, hipStream_t stream, int stages = 0, int persist = 0);
 // stages == 8 with 256x256 tiles: the ping-pong, half-tile-streamed main loop (gemm_pp.hip).

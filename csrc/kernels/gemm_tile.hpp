@@ -9,9 +9,15 @@
 namespace dnn {
 
 // ---- LDS image swizzles -------------------------------------------------------------------
-// KMAJ image: [rows = BM or BN][64 k] bf16, 128-B rows of 8 16-B chunks; chunk' = c ^ ((r>>1)&7).
-// The 16 rows a ds_read_b128 lane group touches then cover all 16 slots of the 256-B bank row.
-__device__ __forceinline__ int k_swz(int r) { return (r >> 1) & 7; }
+// KMAJ image: [rows = BM or BN][BK k] bf16. BK = 64: 128-B rows of 8 16-B chunks, chunk' =
+// c ^ ((r>>1)&7); BK = 32: 64-B rows of 4 chunks, chunk' = c ^ ((r>>2)&3). Either way the 16
+// rows a ds_read_b128 lane group touches cover all 16 slots of the 256-B bank row.
+template <int BK = 64>
+__device__ __forceinline__ int k_swz(int r) {
+  static_assert(BK == 64 || BK == 32, "k-step depth");
+  if constexpr (BK == 64) return (r >> 1) & 7;
+  return (r >> 2) & 3;
+}
 
 // MNMAJ image: [64 k-rows][T cols] bf16 (T*2-byte rows). A transposed read by one 32-lane half
 // touches 8 k-rows x 32 B; the XOR (always even, so 32-B column pairs stay together) spreads the
@@ -41,18 +47,24 @@ struct cmax {
 // streamed activation panel (HBM), B the weights (L2-resident after the first tiles), and what
 // limits those GEMMs is HBM bytes in flight per CU (profiles/r3_pmc: waves parked in vmcnt
 // waits 47-63 % of their cycles), not LDS. Only that asymmetric pair is implemented.
-template <int BM_, int BN_, int WM_, int WN_, int NS_, int NSB_ = NS_>
+//
+// BK_ (default 64): contraction depth of one k-step / LDS stage. BK = 32 halves every stage, so a
+// 2-stage 256x256 ring is 64 KiB and TWO such workgroups share a CU: one's prologue / epilogue
+// runs beside the other's main loop, and 4 MFMA-issuing waves per SIMD instead of 2 hide the
+// load latency -- at the price of a barrier per 32 k instead of per 64.
+template <int BM_, int BN_, int WM_, int WN_, int NS_, int NSB_ = NS_, int BK_ = 64>
 struct Cfg {
-  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, NS = NS_, NSB = NSB_;
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, NS = NS_, NSB = NSB_, BK = BK_;
   static_assert(NSB == NS || (NS == 3 && NSB == 2), "asymmetric ring: A 3 deep, B 2 deep only");
+  static_assert(BK == 64 || BK == 32, "k-step depth 64 or 32");
   static constexpr bool ASYM = NSB != NS;
   static constexpr int NW = WM * WN, NT = 64 * NW;
   static constexpr int SM = BM / WM, SN = BN / WN, FM = SM / 16, FN = SN / 16;
-  static constexpr int A_BYTES = BM * 128, B_BYTES = BN * 128, STAGE = A_BYTES + B_BYTES;
+  static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   // asymmetric ring layout: [NS A slots][NSB B slots]
   static constexpr int RING = ASYM ? NS * A_BYTES + NSB * B_BYTES : NS * STAGE;
   // LDS-DMA instructions one wave issues per stage (A + B): the vmcnt unit of the pipeline
-  static constexpr int PER_STAGE = (BM + BN) / (8 * NW);
+  static constexpr int PER_STAGE = (BM + BN) * BK / (512 * NW);
   // epilogue: fp32 staging of EPI_ROWS rows at a time (whole tile when it fits)
   static constexpr int CS_LD = BN + 4;
   static constexpr int EPI_ROWS = (NW == 4 && BM <= 128) ? BM : SM;
@@ -61,29 +73,31 @@ struct Cfg {
   static constexpr int RED_BYTES = NT * 32;  // colsum partial staging
   static constexpr int SMEM = cmax<cmax<RING, CS_BYTES + 64>::v, RED_BYTES>::v;
   // per-wave LDS-DMA instructions of one A / one B tile (vmcnt units of the asymmetric ring)
-  static constexpr int PER_A = BM / (8 * NW), PER_B = BN / (8 * NW);
+  static constexpr int PER_A = BM * BK / (512 * NW), PER_B = BN * BK / (512 * NW);
   static_assert(FM >= 1 && FN >= 1 && SM % 16 == 0 && SN % 16 == 0, "wave sub-tile");
-  static_assert(BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "LDS-DMA pieces per wave");
+  static_assert((BM * BK) % (512 * NW) == 0 && (BN * BK) % (512 * NW) == 0,
+                "LDS-DMA pieces per wave");
   static_assert(NT % (BN / 8) == 0 && (EPI_ROWS * (BN / 8)) % NT == 0, "epilogue mapping");
   static_assert(SMEM <= 160 * 1024, "LDS budget");
 };
 
-// Stage one operand tile (T entries of the M/N dim x 64 of K) into LDS with LDS-DMA.
-// Tile bytes = T*128 = T/8 KiB pieces; each of the NW waves issues T/(8*NW) of them.
+// Stage one operand tile (T entries of the M/N dim x BK of K) into LDS with LDS-DMA.
+// Tile bytes = T*BK*2 = T*BK/512 KiB pieces; each of the NW waves issues T*BK/(512*NW) of them.
 // Rows / columns at or past `mn_lim` (a partial edge tile) are clamped onto the last valid
 // row / 8-column chunk: the loads stay in bounds, and the outputs they feed are never stored.
-template <int L, int T, int NW>
+template <int L, int T, int NW, int BK = 64>
 __device__ __forceinline__ void stage_tile(const u16* __restrict__ g, long ld, int mn0, int k0,
                                            char LDS_AS* dst, int wave, int lane, int mn_lim) {
-  constexpr int NI = T / (8 * NW);
+  constexpr int NI = T * BK / (512 * NW);
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
     const int piece = i * NW + wave;
     const int chunk = piece * 64 + lane;
     const u16* src;
     if constexpr (L == KMAJ) {
-      const int r = chunk >> 3, ph = chunk & 7;
-      const int c = ph ^ k_swz(r);
+      constexpr int CPR = BK / 8;  // 16-B chunks per row
+      const int r = chunk / CPR, ph = chunk % CPR;
+      const int c = ph ^ k_swz<BK>(r);
       src = g + (long)min(mn0 + r, mn_lim - 1) * ld + k0 + c * 8;
     } else {
       constexpr int CPR = T / 8;
@@ -98,12 +112,12 @@ __device__ __forceinline__ void stage_tile(const u16* __restrict__ g, long ld, i
 // Fragment of v_mfma_f32_16x16x32_bf16 for 16-wide block `blk` of the tile and k-step s (32 k):
 // lane l holds X[idx = l&15][k = 8*(l>>4) + j], j = 0..7 (guide §3 operand maps). The same form
 // serves A (idx = row m) and B (idx = column n).
-template <int L, int T>
+template <int L, int T, int BK = 64>
 __device__ __forceinline__ bf16x8_t load_frag(const char LDS_AS* tile, int blk, int s, int lane) {
   if constexpr (L == KMAJ) {
     const int r = blk * 16 + (lane & 15);
     const int c = 4 * s + (lane >> 4);
-    return *(const bf16x8_t LDS_AS*)(tile + r * 128 + ((c ^ k_swz(r)) << 4));
+    return *(const bf16x8_t LDS_AS*)(tile + r * (BK * 2) + ((c ^ k_swz<BK>(r)) << 4));
   } else {
     constexpr int RB = T * 2;
     const int i = lane & 15, g = lane >> 4, q = i >> 2, p = i & 3;
@@ -171,12 +185,12 @@ __device__ __forceinline__ void mma_kstep(const char LDS_AS* sa, const char LDS_
                                           int lane) {
   constexpr int FM = C::FM, FN = C::FN;
 #pragma unroll
-  for (int s = 0; s < 2; ++s) {
+  for (int s = 0; s < C::BK / 32; ++s) {
     bf16x8_t a[FM], b[FN];
 #pragma unroll
-    for (int i = 0; i < FM; ++i) a[i] = load_frag<LA, C::BM>(sa, wm * FM + i, s, lane);
+    for (int i = 0; i < FM; ++i) a[i] = load_frag<LA, C::BM, C::BK>(sa, wm * FM + i, s, lane);
 #pragma unroll
-    for (int j = 0; j < FN; ++j) b[j] = load_frag<LB, C::BN>(sb, wn * FN + j, s, lane);
+    for (int j = 0; j < FN; ++j) b[j] = load_frag<LB, C::BN, C::BK>(sb, wn * FN + j, s, lane);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -199,12 +213,12 @@ __device__ __forceinline__ void mma_tile_asym(const GemmParams& p, int m0, int n
   constexpr int A_BYTES = C::A_BYTES, B_BYTES = C::B_BYTES;
   char LDS_AS* ring_b = lds + 3 * A_BYTES;
   auto stage_a = [&](int k) {
-    stage_tile<LA, C::BM, C::NW>(p.A, p.lda, m0, kbase + k * 64, lds + (k % 3) * A_BYTES, wave,
-                                 lane, p.M);
+    stage_tile<LA, C::BM, C::NW, C::BK>(p.A, p.lda, m0, kbase + k * C::BK,
+                                        lds + (k % 3) * A_BYTES, wave, lane, p.M);
   };
   auto stage_b = [&](int k) {
-    stage_tile<LB, C::BN, C::NW>(p.B, p.ldb, n0, kbase + k * 64, ring_b + (k & 1) * B_BYTES,
-                                 wave, lane, p.N);
+    stage_tile<LB, C::BN, C::NW, C::BK>(p.B, p.ldb, n0, kbase + k * C::BK,
+                                        ring_b + (k & 1) * B_BYTES, wave, lane, p.N);
   };
   stage_a(0);
   stage_b(0);
@@ -239,10 +253,10 @@ __device__ __forceinline__ void mma_tile(const GemmParams& p, int m0, int n0, in
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s) {
     if (s < nk) {
-      stage_tile<LA, C::BM, C::NW>(p.A, p.lda, m0, kbase + s * 64, lds + s * STAGE, wave, lane,
-                                   p.M);
-      stage_tile<LB, C::BN, C::NW>(p.B, p.ldb, n0, kbase + s * 64, lds + s * STAGE + A_BYTES,
-                                   wave, lane, p.N);
+      stage_tile<LA, C::BM, C::NW, C::BK>(p.A, p.lda, m0, kbase + s * C::BK, lds + s * STAGE,
+                                          wave, lane, p.M);
+      stage_tile<LB, C::BN, C::NW, C::BK>(p.B, p.ldb, n0, kbase + s * C::BK,
+                                          lds + s * STAGE + A_BYTES, wave, lane, p.N);
     }
   }
   int rd = 0, wr = NS - 1;  // ring slots of tile kt and of tile kt + NS - 1
@@ -251,28 +265,14 @@ __device__ __forceinline__ void mma_tile(const GemmParams& p, int m0, int n0, in
     lds_barrier();
     if (kt + NS - 1 < nk) {
       char LDS_AS* nxt = lds + wr * STAGE;
-      const int k0 = kbase + (kt + NS - 1) * 64;
-      stage_tile<LA, C::BM, C::NW>(p.A, p.lda, m0, k0, nxt, wave, lane, p.M);
-      stage_tile<LB, C::BN, C::NW>(p.B, p.ldb, n0, k0, nxt + A_BYTES, wave, lane, p.N);
+      const int k0 = kbase + (kt + NS - 1) * C::BK;
+      stage_tile<LA, C::BM, C::NW, C::BK>(p.A, p.lda, m0, k0, nxt, wave, lane, p.M);
+      stage_tile<LB, C::BN, C::NW, C::BK>(p.B, p.ldb, n0, k0, nxt + A_BYTES, wave, lane, p.N);
     }
-    const char LDS_AS* sa = lds + rd * STAGE;
-    const char LDS_AS* sb = sa + A_BYTES;
     // (Reading both 32-deep halves' fragments up front behind a sched_barrier was measured:
     // +8 % on 128x128 big GEMMs, -35 % on 256x256 dgrad whose 40 transposed reads exceed what
     // lgkmcnt can count -- the compiler's own interleaving is kept.)
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8_t a[FM], b[FN];
-#pragma unroll
-      for (int i = 0; i < FM; ++i) a[i] = load_frag<LA, C::BM>(sa, wm * FM + i, s, lane);
-#pragma unroll
-      for (int j = 0; j < FN; ++j) b[j] = load_frag<LB, C::BN>(sb, wn * FN + j, s, lane);
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-    }
+    mma_kstep<C, LA, LB>(lds + rd * STAGE, lds + rd * STAGE + A_BYTES, acc, wm, wn, lane);
     rd = rd + 1 == NS ? 0 : rd + 1;
     wr = wr + 1 == NS ? 0 : wr + 1;
   }
