@@ -20,59 +20,9 @@
 // Reference parity: replaces the per-stage NumPy `np.dot(x, W) + b` + activation of
 // /root/reference/src/grpc_node.py:75-97 (forward) and adds the backward the reference only had
 // centrally (/root/reference/scripts/generate_mnist_pytorch.py:41-52).
-#include "gemm_tile.hpp"
+#include "gemm_kernel.hpp"
 
 namespace dnn {
-
-// One output tile (workgroup `bid` of a launch of nwg = tiles * splits workgroups).
-template <class C, int LA, int LB, bool OUT_F32>
-__device__ __forceinline__ void gemm_tile_wg(const GemmParams& p, int tiles_n, int tiles_m,
-                                             int nwg, int bid, char LDS_AS* lds) {
-  constexpr int BM = C::BM, BN = C::BN;
-
-  // XCD-aware bijective remap: hardware deals block b to XCD group b%8; give each group a
-  // contiguous run of logical tiles. Within a split, tiles are walked in groups of
-  // group_m row-tiles (column-major inside a group), so the ~32 workgroups an XCD holds at
-  // once cover e.g. 4 row x 8 column tiles: 12 operand k-slices shared through its L2
-  // instead of 33 for a 1 x 32 strip (guide §5.5 T1 + grouped raster order).
-  const int wgid = xcd_remap(bid, nwg);
-  const int per_split = tiles_n * tiles_m;
-  const int split = wgid / per_split;
-  const int t = wgid - split * per_split;
-  const int gm_full = p.group_m > 1 ? p.group_m : 1;
-  const int per_group = gm_full * tiles_n;
-  const int grp = t / per_group, first_m = grp * gm_full;
-  const int gm = min(tiles_m - first_m, gm_full);
-  const int tin = t - grp * per_group;
-  const int tm = first_m + tin % gm;
-  const int tn = tin / gm;
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int m0 = tm * BM, n0 = tn * BN;
-  int kbase, nk;  // nk in k-steps of C::BK (split ranges stay in 64-deep units)
-  if (p.k_total > 0) {  // uneven split-K: split s takes k-steps [s*KS/S, (s+1)*KS/S)
-    const int KS = p.k_total >> 6, S = nwg / (tiles_n * tiles_m);
-    const int a = (int)((long)split * KS / S), b = (int)((long)(split + 1) * KS / S);
-    kbase = a * 64;
-    nk = (b - a) * (64 / C::BK);
-  } else {
-    kbase = split * p.K;
-    nk = p.K / C::BK;
-  }
-
-  f32x4_t acc[C::FM][C::FN];
-  mma_tile<C, LA, LB>(p, m0, n0, kbase, nk, lds, acc, wave, lane);
-
-  epilogue_staged<C, OUT_F32>(p, acc, lds, m0, n0, tm, split, wave, lane);
-}
-
-template <class C, int LA, int LB, bool OUT_F32>
-__global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(GemmParams p, int tiles_n, int tiles_m,
-                                                          int nwg) {
-  __shared__ __attribute__((aligned(16))) char smem[C::SMEM];
-  gemm_tile_wg<C, LA, LB, OUT_F32>(p, tiles_n, tiles_m, nwg, blockIdx.x, (char LDS_AS*)smem);
-}
 
 // Grouped launch: up to GEMM_GROUP_MAX independent problems with one tile configuration (e.g.
 // every layer's weight gradient of a step) in ONE launch; problem j owns the workgroups
@@ -191,18 +141,6 @@ int gemm_bf16_streamk(const GemmParams& p, int layout_a, int layout_b, int bm, i
   return hipGetLastError() == hipSuccess ? 0 : -9;
 }
 
-typedef void (*gemm_fn)(GemmParams, int, int, int);
-
-template <class C>
-static gemm_fn pick_layout(int la, int lb, int f32) {
-#define DNN_G(LA, LB, F) gemm_bf16_kernel<C, LA, LB, F>
-  if (la == KMAJ && lb == KMAJ) return f32 ? DNN_G(KMAJ, KMAJ, true) : DNN_G(KMAJ, KMAJ, false);
-  if (la == KMAJ && lb == MNMAJ) return f32 ? DNN_G(KMAJ, MNMAJ, true) : DNN_G(KMAJ, MNMAJ, false);
-  if (la == MNMAJ && lb == KMAJ) return f32 ? DNN_G(MNMAJ, KMAJ, true) : DNN_G(MNMAJ, KMAJ, false);
-  return f32 ? DNN_G(MNMAJ, MNMAJ, true) : DNN_G(MNMAJ, MNMAJ, false);
-#undef DNN_G
-}
-
 // 4-wave tiles: any NS in 2..4, or 5 = the asymmetric ring (A 3 deep, B 2 deep); 8-wave tiles:
 // NS = 2, 3 where it fits, or 5 (256x256: 3 x 32 KiB A + 2 x 32 KiB B = all 160 KiB of LDS)
 template <int BM, int BN>
@@ -254,7 +192,7 @@ const char* gemm_error_string(int code) {
     case -10: return "colsum needs bf16 output and ld_colsum >= N";
     case -11: return "fused cross-entropy needs bf16 output, N == bn <= 128, a bias and 0 < n_cls <= N";
     case -13: return "relu bit masks need bf16 output, act = relu, ld_mask >= N/8, no aux/xent, one-tile form";
-    case -12: return "pipeline stages must be 2..4, 5 = A3/B2 ring, 12..14 = 32-deep k-steps with 2..4 stages (256x256: 12-14, 256x128: 12-13, 128x128: 12, 14) (8-wave tiles: 2, 3, 5; 256x256: 2, 5 or 8 = ping-pong; 5, 12-14: one-tile form, no fused xent)";
+    case -12: return "pipeline stages must be 2..4, 5 = A3/B2 ring, 6 / 7 = register-prefetched 2 / 3-deep ring (256x256: 6; 256x128, 128x128, 128x64, 64x64: 6, 7), 12..14 = 32-deep k-steps with 2..4 stages (256x256: 12-14, 256x128: 12-13, 128x128: 12, 14) (8-wave tiles: 2, 3, 5; 256x256: 2, 5 or 8 = ping-pong; 5, 12-14: one-tile form, no fused xent)";
     case -14: return "transposed output ct needs bf16 output (or the fused update), no xent, one split, one-tile form, ld_ct >= M, 16-byte alignment";
     case -15: return "fused SGD epilogue needs f32 output, one split, no accumulate/bias/xent, a device lr, 16-byte aligned buffers, N % 8 == 0, one-tile form";
     default: return "unknown gemm error";
@@ -339,6 +277,12 @@ int gemm_bf16(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, 
     if (q.group_m <= 0) q.group_m = tiles_n >= 8 ? 4 : 1;
     hipLaunchKernelGGL(f, dim3(nwg), dim3(nt), 0, stream, q, tiles_n, tiles_m, nwg);
     return hipGetLastError() == hipSuccess ? 0 : -9;
+  }
+  if (ns == 6 || ns == 7) {  // register-prefetched main loop (one-tile form, no fused xent)
+    if (persist || p.xent_labels) return -12;
+    GemmParams q = p;
+    if (q.group_m <= 0) q.group_m = ((p.N + bn - 1) / bn) >= 8 ? 4 : 1;
+    return gemm_rp_launch(q, la, lb, out_f32, bm, bn, splits, ns, stream);
   }
   // 8-wave tiles: NS = 3 where three stages fit (not 256x256); 5 = asymmetric A3/B2 ring
   if (ns < 2 || ns > 5 || (nt == 512 && (ns == 4 || (ns == 3 && bm == 256 && bn == 256))))

@@ -92,6 +92,9 @@ int gemm_bf16(const GemmParams& p, int layout_a, int layout_b, int out_f32, int 
 // stages == 8 with 256x256 tiles: the ping-pong, half-tile-streamed main loop (gemm_pp.hip).
 int gemm_pp_launch(const GemmParams& q, int la, int lb, int out_f32, int splits,
                    hipStream_t stream);
+// stages == 6 / 7: the register-prefetched main loop with a 2- / 3-deep ring (gemm_rp.hip).
+int gemm_rp_launch(const GemmParams& q, int la, int lb, int out_f32, int bm, int bn, int splits,
+                   int ns, hipStream_t stream);
 int gemm_persist_launch(const GemmParams& q, int la, int lb, int out_f32, int bm, int bn,
                         int splits, int ns, int persist, hipStream_t stream);
 int default_stages(int bm, int bn);

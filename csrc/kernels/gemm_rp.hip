@@ -1,0 +1,32 @@
+// Register-prefetched main-loop variants of the one-tile GEMM (stage codes 6 / 7; Cfg RP,
+// mma_tile_rp in gemm_tile.hpp), in a translation unit of their own so the build compiles
+// them in parallel with gemm.hip.
+#include "gemm_kernel.hpp"
+
+namespace dnn {
+
+// Stage codes 6 / 7: the register-prefetched main loop (Cfg RP, mma_tile_rp) with a 2- / 3-deep
+// ring; 3 deep only where three 64-deep stages fit (not 256x256).
+static gemm_fn pick_rp(int bm, int bn, int ns, int la, int lb, int f32) {
+#define DNN_RP(BM, BN, WM, WN, NS) pick_layout<Cfg<BM, BN, WM, WN, NS, NS, 64, 1>>(la, lb, f32)
+  if (bm == 256 && bn == 256) return ns == 6 ? DNN_RP(256, 256, 4, 2, 2) : nullptr;
+  if (bm == 256 && bn == 128) return ns == 6 ? DNN_RP(256, 128, 4, 2, 2) : DNN_RP(256, 128, 4, 2, 3);
+  if (bm == 128 && bn == 128) return ns == 6 ? DNN_RP(128, 128, 2, 2, 2) : DNN_RP(128, 128, 2, 2, 3);
+  if (bm == 128 && bn == 64) return ns == 6 ? DNN_RP(128, 64, 2, 2, 2) : DNN_RP(128, 64, 2, 2, 3);
+  if (bm == 64 && bn == 64) return ns == 6 ? DNN_RP(64, 64, 2, 2, 2) : DNN_RP(64, 64, 2, 2, 3);
+#undef DNN_RP
+  return nullptr;
+}
+
+int gemm_rp_launch(const GemmParams& q, int la, int lb, int out_f32, int bm, int bn, int splits,
+                   int ns, hipStream_t stream) {
+  gemm_fn f = pick_rp(bm, bn, ns, la, lb, out_f32);
+  if (!f) return -12;
+  const int tiles_n = (q.N + bn - 1) / bn, tiles_m = (q.M + bm - 1) / bm;
+  const int nwg = tiles_n * tiles_m * splits;
+  hipLaunchKernelGGL(f, dim3(nwg), dim3(gemm_tile_threads(bm, bn)), 0, stream, q, tiles_n,
+                     tiles_m, nwg);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
+}  // namespace dnn

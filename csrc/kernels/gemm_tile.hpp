@@ -52,9 +52,15 @@ struct cmax {
 // 2-stage 256x256 ring is 64 KiB and TWO such workgroups share a CU: one's prologue / epilogue
 // runs beside the other's main loop, and 4 MFMA-issuing waves per SIMD instead of 2 hide the
 // load latency -- at the price of a barrier per 32 k instead of per 64.
-template <int BM_, int BN_, int WM_, int WN_, int NS_, int NSB_ = NS_, int BK_ = 64>
+//
+// RP_ (default 0): register-prefetched k-step (mma_tile_rp): fragments of the next 32-deep half
+// are read while the MFMAs of the current one run, and the ring barrier sits between the two
+// halves of a k-step instead of in front of a fragment read that every wave then waits for.
+template <int BM_, int BN_, int WM_, int WN_, int NS_, int NSB_ = NS_, int BK_ = 64, int RP_ = 0>
 struct Cfg {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, NS = NS_, NSB = NSB_, BK = BK_;
+  static constexpr bool RP = RP_ != 0;
+  static_assert(!RP || (BK == 64 && NSB == NS && NS <= 3), "register prefetch: BK 64, NS 2..3");
   static_assert(NSB == NS || (NS == 3 && NSB == 2), "asymmetric ring: A 3 deep, B 2 deep only");
   static_assert(BK == 64 || BK == 32, "k-step depth 64 or 32");
   static constexpr bool ASYM = NSB != NS;
@@ -108,6 +114,43 @@ __device__ __forceinline__ void stage_tile(const u16* __restrict__ g, long ld, i
     __builtin_amdgcn_global_load_lds((const void*)src, (void LDS_AS*)(dst + piece * 1024), 16, 0, 0);
   }
 }
+
+// stage_tile with the LDS-DMA issued from inline asm. The compiler's wait-count pass tracks
+// LDS-DMA it emits itself and, finding no alias information, puts an s_waitcnt vmcnt(0) in
+// front of every later ds_read_b64_tr_b16 -- i.e. each k-step of an MN-major operand waited
+// for the tile just issued for the NEXT k-step. Issued from asm, the loads are invisible to that
+// pass; the pipeline's own counted vmcnt waits (wait_stage) already order them.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"  // M0 in the clobber list (see below)
+template <int L, int T, int NW, int BK = 64>
+__device__ __forceinline__ void stage_tile_asm(const u16* __restrict__ g, long ld, int mn0, int k0,
+                                               char LDS_AS* dst, int wave, int lane, int mn_lim) {
+  constexpr int NI = T * BK / (512 * NW);
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int piece = i * NW + wave;
+    const int chunk = piece * 64 + lane;
+    const u16* src;
+    if constexpr (L == KMAJ) {
+      constexpr int CPR = BK / 8;
+      const int r = chunk / CPR, ph = chunk % CPR;
+      const int c = ph ^ k_swz<BK>(r);
+      src = g + (long)min(mn0 + r, mn_lim - 1) * ld + k0 + c * 8;
+    } else {
+      constexpr int CPR = T / 8;
+      const int r = chunk / CPR, ph = chunk % CPR;
+      const int c = ph ^ mn_swz<T>(r);
+      src = g + (long)(k0 + r) * ld + min(mn0 + c * 8, mn_lim - 8);
+    }
+    const unsigned m0v =
+        __builtin_amdgcn_readfirstlane((unsigned)(size_t)(dst + piece * 1024));
+    // M0 is written inside the asm and listed as clobbered; kernels that use this form issue
+    // all of their LDS-DMA from it (the compiler keeps nothing else in M0 there).
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off"
+                 :: "v"(src), "s"(m0v) : "memory", "m0");
+  }
+}
+#pragma clang diagnostic pop
 
 // Fragment of v_mfma_f32_16x16x32_bf16 for 16-wide block `blk` of the tile and k-step s (32 k):
 // lane l holds X[idx = l&15][k = 8*(l>>4) + j], j = 0..7 (guide §3 operand maps). The same form
@@ -235,6 +278,104 @@ __device__ __forceinline__ void mma_tile_asym(const GemmParams& p, int m0, int n
   __syncthreads();
 }
 
+// Register-prefetched ring (Cfg RP): per 64-deep k-step kt, with the k 0..31 fragments of tile
+// kt already in registers:
+//   read k 32..63 fragments of kt | MFMAs on k 0..31
+//   -> own loads of tile kt+1 landed, lds_barrier (every wave's reads of tile kt are done and
+//      everyone's tile kt+1 landed) -> LDS-DMA tile kt+NS into tile kt's slot
+//   read k 0..31 fragments of kt+1 | MFMAs on k 32..63 of kt
+// so every fragment read overlaps MFMAs of the same wave, and the barrier is followed by MFMAs
+// that do not wait on LDS. NS tiles are staged up front (tile kt+NS reuses tile kt's slot).
+template <class C, int LA, int LB>
+__device__ __forceinline__ void read_half(const char LDS_AS* sa, const char LDS_AS* sb,
+                                          bf16x8_t (&a)[C::FM], bf16x8_t (&b)[C::FN], int wm,
+                                          int wn, int s, int lane) {
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i) a[i] = load_frag<LA, C::BM>(sa, wm * C::FM + i, s, lane);
+#pragma unroll
+  for (int j = 0; j < C::FN; ++j) b[j] = load_frag<LB, C::BN>(sb, wn * C::FN + j, s, lane);
+}
+
+template <class C>
+__device__ __forceinline__ void mfma_half(const bf16x8_t (&a)[C::FM], const bf16x8_t (&b)[C::FN],
+                                          f32x4_t (&acc)[C::FM][C::FN]) {
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j)
+      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+}
+
+template <class C, int LA, int LB>
+__device__ __forceinline__ void mma_tile_rp(const GemmParams& p, int m0, int n0, int kbase,
+                                            int nk, char LDS_AS* lds,
+                                            f32x4_t (&acc)[C::FM][C::FN], int wm, int wn,
+                                            int wave, int lane) {
+  constexpr int NS = C::NS, STAGE = C::STAGE, A_BYTES = C::A_BYTES;
+  auto stage = [&](int k, int slot) {
+    char LDS_AS* dst = lds + slot * STAGE;
+    stage_tile_asm<LA, C::BM, C::NW>(p.A, p.lda, m0, kbase + k * 64, dst, wave, lane, p.M);
+    stage_tile_asm<LB, C::BN, C::NW>(p.B, p.ldb, n0, kbase + k * 64, dst + A_BYTES, wave, lane,
+                                     p.N);
+  };
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+    if (s < nk) stage(s, s);
+  wait_stage<NS + 1, C::PER_STAGE>(min(nk - 1, NS - 1));
+  lds_barrier();
+  bf16x8_t a0[C::FM], b0[C::FN], a1[C::FM], b1[C::FN];
+  read_half<C, LA, LB>(lds, lds + A_BYTES, a0, b0, wm, wn, 0, lane);
+  // Wait counts the compiler's wait-count pass can see (a builtin, unlike inline asm): with no
+  // LDS read pending at the loop head / after the barrier, it lets the MFMAs on registers that
+  // have landed issue while the next half's reads are in flight. The loop body is branch-free
+  // up to the staging issue (the last k-step is peeled), so no control-flow merge forces a
+  // conservative lgkmcnt(0) in front of an MFMA.
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // vmcnt(63) expcnt(7) lgkmcnt(0)
+  // Instruction interleave of both halves (sched_group_barrier masks: 0x8 MFMA, 0x100 DS read):
+  // each fragment read is followed by NM / NR MFMAs, the rest of the MFMAs come last.
+  constexpr int NR = (C::FM + C::FN) * (LA == KMAJ ? 1 : 2) / 2 +
+                     (C::FM + C::FN) * (LB == KMAJ ? 1 : 2) / 2;  // DS reads per half
+  constexpr int NM = C::FM * C::FN;                                // MFMAs per half
+  int rd = 0;  // slot of tile kt
+  for (int kt = 0; kt + 1 < nk; ++kt) {
+    const char LDS_AS* cur = lds + rd * STAGE;
+    read_half<C, LA, LB>(cur, cur + A_BYTES, a1, b1, wm, wn, 1, lane);
+    mfma_half<C>(a0, b0, acc);
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x8, NM / NR > 0 ? NM / NR : 1, 0);
+    }
+    if constexpr (NM > NR * (NM / NR)) __builtin_amdgcn_sched_group_barrier(0x8, NM - NR * (NM / NR), 0);
+    __builtin_amdgcn_sched_barrier(0);
+    wait_stage<NS, C::PER_STAGE>(NS - 2);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    asm volatile("s_barrier" ::: "memory");
+    // Tile kt+NS into tile kt's slot; past the end the last tile is restaged instead (an L2
+    // hit into a slot nobody reads again), so the loop body has no branch and every k-step
+    // leaves the same number of stages in flight.
+    stage(min(kt + NS, nk - 1), rd);
+    rd = rd + 1 == NS ? 0 : rd + 1;
+    const char LDS_AS* nxt = lds + rd * STAGE;
+    read_half<C, LA, LB>(nxt, nxt + A_BYTES, a0, b0, wm, wn, 0, lane);
+    mfma_half<C>(a1, b1, acc);
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x8, NM / NR > 0 ? NM / NR : 1, 0);
+    }
+    if constexpr (NM > NR * (NM / NR)) __builtin_amdgcn_sched_group_barrier(0x8, NM - NR * (NM / NR), 0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+  }
+  wait_vmcnt<0>();  // the restaged tail tiles (nothing reads them; the epilogue reuses LDS)
+  const char LDS_AS* cur = lds + rd * STAGE;
+  read_half<C, LA, LB>(cur, cur + A_BYTES, a1, b1, wm, wn, 1, lane);
+  mfma_half<C>(a0, b0, acc);
+  mfma_half<C>(a1, b1, acc);
+  __syncthreads();
+}
+
 template <class C, int LA, int LB>
 __device__ __forceinline__ void mma_tile(const GemmParams& p, int m0, int n0, int kbase, int nk,
                                          char LDS_AS* lds, f32x4_t (&acc)[C::FM][C::FN],
@@ -247,6 +388,10 @@ __device__ __forceinline__ void mma_tile(const GemmParams& p, int m0, int n0, in
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   if constexpr (C::ASYM) {
     mma_tile_asym<C, LA, LB>(p, m0, n0, kbase, nk, lds, acc, wm, wn, wave, lane);
+    return;
+  }
+  if constexpr (C::RP) {
+    mma_tile_rp<C, LA, LB>(p, m0, n0, kbase, nk, lds, acc, wm, wn, wave, lane);
     return;
   }
 

@@ -505,11 +505,56 @@ def test_bk32_ksteps_bitwise(dev, la, lb):
         assert torch.equal(s2, sn), (bm, bn, code)
 
 
+RP = [((256, 256), 6), ((256, 128), 6), ((256, 128), 7), ((128, 128), 6), ((128, 128), 7),
+      ((128, 64), 6), ((128, 64), 7), ((64, 64), 6), ((64, 64), 7)]
+
+
+@pytest.mark.parametrize("la,lb", LAYOUTS)
+def test_register_prefetch_bitwise(dev, la, lb):
+    """Register-prefetched main loop (stage codes 6 / 7: the next half's fragments are read
+    under the current half's MFMAs, LDS-DMA issued from asm, past-the-end restaging) keeps the
+    MFMA order of the 2-stage kernel: bit-identical for nk = 1, 2, 3, 5, 13, partial edge tiles
+    and uneven split-K."""
+    gen = torch.Generator().manual_seed(43 + 4 * la + 2 * lb)
+    for (bm, bn), code in RP:
+        for K in (64, 128, 192, 320, 832):
+            M, N = 320, 264  # partial edge tiles in both dimensions
+            a = _storage(la, M, K, gen, dev, False)
+            b = _storage(lb, N, K, gen, dev, False)
+            bias = torch.randn(N, generator=gen).to(dev)
+            c2 = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            cn = torch.empty_like(c2)
+            for c, st in ((c2, 2), (cn, code)):
+                ops.gemm(a, b, c, layout_a=la, layout_b=lb, M=M, N=N, K=K, bias=bias,
+                         act="relu", tiles=(bm, bn), stages=st)
+            assert torch.equal(c2, cn), (bm, bn, code, K)
+        R, S = 64 * 23, 5
+        a = _storage(la, bm, R, gen, dev, False)
+        b = _storage(lb, bn, R, gen, dev, False)
+        s2 = torch.empty(S, bm, bn, device=dev)
+        sn = torch.empty_like(s2)
+        for c, st in ((s2, 2), (sn, code)):
+            ops.gemm(a, b, c, layout_a=la, layout_b=lb, M=bm, N=bn, K=R, k_total=R, splits=S,
+                     tiles=(bm, bn), stages=st)
+        assert torch.equal(s2, sn), (bm, bn, code)
+    # and against fp32 once (the 2-stage kernel itself is pinned by the tests above)
+    M, N, K = 256, 256, 832
+    a = _storage(la, M, K, gen, dev, False)
+    b = _storage(lb, N, K, gen, dev, False)
+    c = torch.empty(M, N, device=dev)
+    ops.gemm(a, b, c, layout_a=la, layout_b=lb, M=M, N=N, K=K, tiles=(256, 256), stages=6)
+    ref = _logical(a, la, M, K) @ _logical(b, lb, N, K).t()
+    torch.testing.assert_close(c, ref, rtol=1e-3, atol=1e-3)
+
+
 def test_pipeline_depth_rejects_bad_stages(dev):
     a = torch.zeros(128, 64, device=dev, dtype=torch.bfloat16)
     c = torch.zeros(128, 128, device=dev)
     with pytest.raises(ValueError, match="stages"):
-        ops.gemm(a, a, c, layout_a=KMAJ, layout_b=KMAJ, M=128, N=128, K=64, stages=6)
+        ops.gemm(a, a, c, layout_a=KMAJ, layout_b=KMAJ, M=128, N=128, K=64, stages=11)
+    with pytest.raises(ValueError, match="stages"):  # no 3-deep 256x256 ring
+        ops.gemm(a, a, c, layout_a=KMAJ, layout_b=KMAJ, M=128, N=128, K=64, stages=7,
+                 tiles=(256, 256))
 
 
 
