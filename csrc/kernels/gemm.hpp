@@ -65,6 +65,10 @@ struct GemmParams {
   uint16_t* upd_shadow;
   const float* upd_lr;
   float upd_mu, upd_wd;
+  // optional per-workgroup phase timestamps (one-tile kernels; bench/probes/gemm_timeline.py):
+  // timeline[4 * blockIdx.x + i] = s_memrealtime (100 MHz) at kernel entry (i = 0), after the
+  // ring prologue (1), after the main loop (2) and at the end of the epilogue (3).
+  unsigned long long* timeline;
 };
 
 // Returns 0 on success, a negative code when a shape/alignment precondition fails

@@ -42,10 +42,13 @@ __device__ __forceinline__ void gemm_tile_wg(const GemmParams& p, int tiles_n, i
     nk = p.K / C::BK;
   }
 
+  tl_mark(p, 0);
   f32x4_t acc[C::FM][C::FN];
   mma_tile<C, LA, LB>(p, m0, n0, kbase, nk, lds, acc, wave, lane);
+  tl_mark(p, 2);
 
   epilogue_staged<C, OUT_F32>(p, acc, lds, m0, n0, tm, split, wave, lane);
+  tl_mark(p, 3);
 }
 
 template <class C, int LA, int LB, bool OUT_F32>

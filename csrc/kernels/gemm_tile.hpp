@@ -178,6 +178,12 @@ __device__ __forceinline__ bf16x8_t load_frag(const char LDS_AS* tile, int blk, 
   }
 }
 
+// Phase timestamp of the workgroup (GemmParams::timeline); thread 0 stores it.
+__device__ __forceinline__ void tl_mark(const GemmParams& p, int slot) {
+  if (p.timeline && threadIdx.x == 0)
+    p.timeline[4 * blockIdx.x + slot] = __builtin_amdgcn_s_memrealtime();
+}
+
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
@@ -323,6 +329,7 @@ __device__ __forceinline__ void mma_tile_rp(const GemmParams& p, int m0, int n0,
     if (s < nk) stage(s, s);
   wait_stage<NS + 1, C::PER_STAGE>(min(nk - 1, NS - 1));
   lds_barrier();
+  tl_mark(p, 1);
   bf16x8_t a0[C::FM], b0[C::FN], a1[C::FM], b1[C::FN];
   read_half<C, LA, LB>(lds, lds + A_BYTES, a0, b0, wm, wn, 0, lane);
   // Wait counts the compiler's wait-count pass can see (a builtin, unlike inline asm): with no
@@ -408,6 +415,7 @@ __device__ __forceinline__ void mma_tile(const GemmParams& p, int m0, int n0, in
   for (int kt = 0; kt < nk; ++kt) {
     wait_stage<NS, C::PER_STAGE>(min(nk - 1 - kt, NS - 2));
     lds_barrier();
+    if (kt == 0) tl_mark(p, 1);
     if (kt + NS - 1 < nk) {
       char LDS_AS* nxt = lds + wr * STAGE;
       const int k0 = kbase + (kt + NS - 1) * C::BK;

@@ -252,8 +252,11 @@ def wgrad_config(M: int, N: int, K_total: int, max_splits: int = 48) -> tuple[in
 def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=None, aux=None,
          act=0, accumulate: bool = False, splits: int = 1, tiles: tuple[int, int] | None = None,
          colsum=None, k_total: int = 0, stages: int = 0, group_m: int = 0, persist: int = 0,
-         mask_out=None, mask_in=None, ct=None, upd=None):
+         mask_out=None, mask_in=None, ct=None, upd=None, timeline=None):
     """C (+)= epilogue(A.B). See csrc/kernels/gemm.hpp for the layout/epilogue contract.
+
+    ``timeline`` (int64 GPU tensor, >= 4 per workgroup; one-tile kernels): per-workgroup phase
+    timestamps for bench/probes/gemm_timeline.py (GemmParams::timeline).
 
     ``persist`` != 0 runs the persistent-workgroup form with the register-direct epilogue
     (csrc/kernels/gemm_persist.hip): -1 = one resident round, > 0 = workgroup count.
@@ -353,7 +356,8 @@ def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=
                            upd_master=_p(upd["master"]), upd_mom=_p(upd.get("mom")),
                            upd_shadow=_p(upd.get("shadow")), upd_lr=_p(upd["lr_dev"]),
                            upd_mu=float(upd.get("momentum", 0.0)),
-                           upd_wd=float(upd.get("weight_decay", 0.0)))))
+                           upd_wd=float(upd.get("weight_decay", 0.0)))),
+                       timeline=_p(timeline))
     return c
 
 
