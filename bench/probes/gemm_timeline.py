@@ -29,6 +29,13 @@ def fwd(M, K, N):
                                          bias=b, act="relu", tiles=tile, stages=st, timeline=tl)
 
 
+def fwd32(M, K, N):
+    x, w = rnd(M, K, scale=0.1), rnd(N, K, scale=0.05)
+    y = torch.empty(M, N, device=dev)
+    return lambda tile, st, tl: ops.gemm(x, w, y, layout_a=KMAJ, layout_b=KMAJ, M=M, N=N, K=K,
+                                         tiles=tile, stages=st, timeline=tl)
+
+
 def wgrad(R, M, N, splits):
     dz, x = rnd(R, M), rnd(R, N)
     out = torch.empty(splits, M, N, device=dev)
@@ -38,6 +45,8 @@ def wgrad(R, M, N, splits):
 
 
 CASES = {"f0": lambda: fwd(65536, 832, 512), "f1": lambda: fwd(65536, 512, 256),
+         "f0s": lambda: fwd(8192, 832, 512), "f0m": lambda: fwd(32768, 832, 512),
+         "f0f32": lambda: fwd32(65536, 832, 512), "f0sf32": lambda: fwd32(8192, 832, 512),
          "w0": lambda: wgrad(65536, 512, 832, 18), "m8f": lambda: fwd(65536, 1024, 1024)}
 
 

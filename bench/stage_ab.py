@@ -4,7 +4,7 @@ median / min us over rounds, and checks every variant's output bitwise against t
 
 Variants are (tile, stages): stages 2 = the 2-deep ring, 3 = 3-deep, 5 = asymmetric ring
 (A 3 deep, B 2 deep: csrc/kernels/gemm_tile.hpp mma_tile_asym), 6 / 7 = register-prefetched
-2- / 3-deep ring (mma_tile_rp), 8 = ping-pong (256x256), 12-14 = 32-deep k-steps.
+2- / 3-deep ring (mma_tile_rp), 9 / 10 = the same with the register-direct epilogue, 8 = ping-pong (256x256), 12-14 = 32-deep k-steps.
 
 Usage: python bench/stage_ab.py [--rounds 7] [--cases f0,d1,w0,...]"""
 from __future__ import annotations
@@ -68,20 +68,20 @@ def case_wgrad(R, M, N, splits, variants):
 
 
 T256, T128, T12864 = (256, 256), (128, 128), (128, 64)
-BIG = [(T256, 2), (T256, 6), (T256, 5)]
-WG = [(T128, 2), (T128, 6), (T128, 7), (T12864, 2), (T12864, 6)]
+BIG = [(T256, 2), (T256, 6), (T256, 9)]
+WG = [(T128, 2), (T128, 6), (T128, 9), (T12864, 6), (T12864, 9)]
 CASES = {
     "f0": lambda: case_fwd(65536, 832, 512, BIG),
     "f1": lambda: case_fwd(65536, 512, 256, BIG),
     "d1": lambda: case_dgrad(65536, 256, 512, BIG),
     "w0": lambda: case_wgrad(65536, 512, 832, 18, WG),
     "w1": lambda: case_wgrad(65536, 256, 512, 64, WG),
-    "w2": lambda: case_wgrad(65536, 128, 256, 64, [((64, 64), 2), ((64, 64), 6), ((64, 64), 7),
-                                                    (T12864, 2), (T12864, 6)]),
+    "w2": lambda: case_wgrad(65536, 128, 256, 64, [((64, 64), 2), ((64, 64), 6), ((64, 64), 9),
+                                                    (T12864, 6), (T12864, 9)]),
     "m8f": lambda: case_fwd(65536, 1024, 1024, BIG),
     "m8d": lambda: case_dgrad(65536, 1024, 1024, BIG),
-    "m8w": lambda: case_wgrad(65536, 1024, 1024, 8, [(T128, 2), (T128, 6), (T128, 7)]),
-    "wide": lambda: case_fwd(16384, 8192, 8192, [(T256, 2), (T256, 6)]),
+    "m8w": lambda: case_wgrad(65536, 1024, 1024, 8, [(T128, 2), (T128, 6), (T128, 9)]),
+    "wide": lambda: case_fwd(16384, 8192, 8192, [(T256, 2), (T256, 6), (T256, 9)]),
 }
 
 

@@ -47,7 +47,12 @@ __device__ __forceinline__ void gemm_tile_wg(const GemmParams& p, int tiles_n, i
   mma_tile<C, LA, LB>(p, m0, n0, kbase, nk, lds, acc, wave, lane);
   tl_mark(p, 2);
 
-  epilogue_staged<C, OUT_F32>(p, acc, lds, m0, n0, tm, split, wave, lane);
+  if constexpr (C::DIRECT) {  // register-direct stores (colsum partials in ring slot 0)
+    epilogue_direct<C::FM, C::FN, BN, C::SN, C::WM, C::NS, C::STAGE, OUT_F32>(
+        p, acc, lds, 1, tm, tn, split, wave / C::WN, wave % C::WN, lane, true);
+  } else {
+    epilogue_staged<C, OUT_F32>(p, acc, lds, m0, n0, tm, split, wave, lane);
+  }
   tl_mark(p, 3);
 }
 

@@ -7,7 +7,21 @@ namespace dnn {
 
 // Stage codes 6 / 7: the register-prefetched main loop (Cfg RP, mma_tile_rp) with a 2- / 3-deep
 // ring; 3 deep only where three 64-deep stages fit (not 256x256).
-static gemm_fn pick_rp(int bm, int bn, int ns, int la, int lb, int f32) {
+// Codes 9 / 10: the same loop with swapped MFMA operands and the register-direct epilogue
+// (RP_ = 2): bias / activation / aux derivative / colsum / split-K f32, no ReLU bit masks,
+// transposed copy, fused update or cross-entropy.
+static gemm_fn pick_rp(int bm, int bn, int code, int la, int lb, int f32) {
+  const int ns = code == 6 || code == 9 ? 6 : 7;
+  if (code == 9 || code == 10) {
+#define DNN_RP(BM, BN, WM, WN, NS) pick_layout<Cfg<BM, BN, WM, WN, NS, NS, 64, 2>>(la, lb, f32)
+    if (bm == 256 && bn == 256) return ns == 6 ? DNN_RP(256, 256, 4, 2, 2) : nullptr;
+    if (bm == 256 && bn == 128) return ns == 6 ? DNN_RP(256, 128, 4, 2, 2) : DNN_RP(256, 128, 4, 2, 3);
+    if (bm == 128 && bn == 128) return ns == 6 ? DNN_RP(128, 128, 2, 2, 2) : DNN_RP(128, 128, 2, 2, 3);
+    if (bm == 128 && bn == 64) return ns == 6 ? DNN_RP(128, 64, 2, 2, 2) : DNN_RP(128, 64, 2, 2, 3);
+    if (bm == 64 && bn == 64) return ns == 6 ? DNN_RP(64, 64, 2, 2, 2) : DNN_RP(64, 64, 2, 2, 3);
+#undef DNN_RP
+    return nullptr;
+  }
 #define DNN_RP(BM, BN, WM, WN, NS) pick_layout<Cfg<BM, BN, WM, WN, NS, NS, 64, 1>>(la, lb, f32)
   if (bm == 256 && bn == 256) return ns == 6 ? DNN_RP(256, 256, 4, 2, 2) : nullptr;
   if (bm == 256 && bn == 128) return ns == 6 ? DNN_RP(256, 128, 4, 2, 2) : DNN_RP(256, 128, 4, 2, 3);

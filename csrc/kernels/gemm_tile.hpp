@@ -56,10 +56,14 @@ struct cmax {
 // RP_ (default 0): register-prefetched k-step (mma_tile_rp): fragments of the next 32-deep half
 // are read while the MFMAs of the current one run, and the ring barrier sits between the two
 // halves of a k-step instead of in front of a fragment read that every wave then waits for.
+// RP_ = 2 also swaps the MFMA operands (a lane's accumulator fragment = 4 consecutive output
+// columns of one row) so the tile is stored by the register-direct epilogue (epilogue_direct)
+// instead of being staged through LDS: measured 11 us of a 256x256 bf16 tile's ~32 us was the
+// staged epilogue (bench/probes/gemm_timeline.py), latency-bound even on an idle chip.
 template <int BM_, int BN_, int WM_, int WN_, int NS_, int NSB_ = NS_, int BK_ = 64, int RP_ = 0>
 struct Cfg {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, NS = NS_, NSB = NSB_, BK = BK_;
-  static constexpr bool RP = RP_ != 0;
+  static constexpr bool RP = RP_ != 0, DIRECT = RP_ == 2;
   static_assert(!RP || (BK == 64 && NSB == NS && NS <= 3), "register prefetch: BK 64, NS 2..3");
   static_assert(NSB == NS || (NS == 3 && NSB == 2), "asymmetric ring: A 3 deep, B 2 deep only");
   static_assert(BK == 64 || BK == 32, "k-step depth 64 or 32");
@@ -308,8 +312,12 @@ __device__ __forceinline__ void mfma_half(const bf16x8_t (&a)[C::FM], const bf16
 #pragma unroll
   for (int i = 0; i < C::FM; ++i)
 #pragma unroll
-    for (int j = 0; j < C::FN; ++j)
-      acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    for (int j = 0; j < C::FN; ++j) {
+      if constexpr (C::DIRECT)  // swapped: the fragment is C^T's (epilogue_direct layout)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0);
+      else
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
 }
 
 template <class C, int LA, int LB>

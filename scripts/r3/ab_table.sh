@@ -1,7 +1,7 @@
 # Alternating whole-step A/B of two tuned tables (current vs $1), bench.py default form,
 # 4 rounds x {headline, mlp8, wide}. -> gpurun_out/r3_abt/
 set -o pipefail
-R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/r3_abt; mkdir -p $O
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/r3_abt_${2:-x}; mkdir -p $O
 cd $R
 B=${1:-bench/tables/table_asym.json}
 test -f $B || { echo "missing table $B"; exit 1; }

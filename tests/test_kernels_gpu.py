@@ -506,7 +506,8 @@ def test_bk32_ksteps_bitwise(dev, la, lb):
 
 
 RP = [((256, 256), 6), ((256, 128), 6), ((256, 128), 7), ((128, 128), 6), ((128, 128), 7),
-      ((128, 64), 6), ((128, 64), 7), ((64, 64), 6), ((64, 64), 7)]
+      ((128, 64), 6), ((128, 64), 7), ((64, 64), 6), ((64, 64), 7),
+      ((256, 256), 9), ((256, 128), 10), ((128, 128), 9), ((128, 64), 10), ((64, 64), 9)]
 
 
 @pytest.mark.parametrize("la,lb", LAYOUTS)
@@ -537,6 +538,25 @@ def test_register_prefetch_bitwise(dev, la, lb):
             ops.gemm(a, b, c, layout_a=la, layout_b=lb, M=bm, N=bn, K=R, k_total=R, splits=S,
                      tiles=(bm, bn), stages=st)
         assert torch.equal(s2, sn), (bm, bn, code)
+    # register-direct epilogue (codes 9 / 10): ReLU dgrad from the activation + colsum
+    for (bm, bn), code in RP:
+        if code < 9:
+            continue
+        M, N, K = 320, 264, 192
+        a = _storage(la, M, K, gen, dev, False)
+        b = _storage(lb, N, K, gen, dev, False)
+        aux = torch.randn(M, N, generator=gen).to(torch.bfloat16).to(dev)
+        outs, sums = [], []
+        for st in (2, code):
+            c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            cs = torch.empty(-(-M // bm), N, device=dev)
+            ops.gemm(a, b, c, layout_a=la, layout_b=lb, M=M, N=N, K=K, aux=aux, act="relu",
+                     tiles=(bm, bn), stages=st, colsum=cs)
+            outs.append(c)
+            sums.append(cs)
+        assert torch.equal(outs[0], outs[1]), (bm, bn, code)
+        # column sums: same values, summed in another order (per-wave butterflies + wave rows)
+        torch.testing.assert_close(sums[0], sums[1], rtol=1e-5, atol=1e-3)
     # and against fp32 once (the 2-stage kernel itself is pinned by the tests above)
     M, N, K = 256, 256, 832
     a = _storage(la, M, K, gen, dev, False)
