@@ -821,14 +821,21 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&a
       // instruction) instead of 8-byte ones. Column sums of the stored values are taken in the
       // same layout; per column they add the same rows in the same order (the swap keeps a
       // lane's row), so the result is bitwise that of the generic path.
-      auto relu_body = [&]() {
-      uint4 yv[FN / 2][FM];
+      // from_mask: the derivative comes from the forward's 1-bit ReLU mask (mask_in: one byte
+      // per row and 8-column chunk -- exactly the chunk a lane stores) instead of the activation
+      auto relu_body = [&](auto from_mask) {
+      constexpr bool MASK = decltype(from_mask)::value;
+      [[maybe_unused]] uint4 yv[MASK ? 1 : FN / 2][FM];
+      [[maybe_unused]] unsigned mv[MASK ? FN / 2 : 1][FM];
 #pragma unroll
       for (int jj = 0; jj < FN / 2; ++jj) {
-        const u16* ya = p.aux + min(scol0 + 32 * jj, p.N - 8);
+        const int c = min(scol0 + 32 * jj, p.N - 8);
 #pragma unroll
-        for (int i = 0; i < FM; ++i)
-          yv[jj][i] = *(const uint4*)(ya + min(row0 + 16 * i, p.M - 1) * p.ld_aux);
+        for (int i = 0; i < FM; ++i) {
+          const long r = min(row0 + 16 * i, p.M - 1);
+          if constexpr (MASK) mv[jj][i] = p.mask_in[r * p.ld_mask + (c >> 3)];
+          else yv[jj][i] = *(const uint4*)(p.aux + r * p.ld_aux + c);
+        }
       }
 #pragma unroll
       for (int j = 0; j < FN; j += 2) {
@@ -850,14 +857,22 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&a
           const auto s0 = __builtin_amdgcn_permlane16_swap(x0, z0, false, false);
           const auto s1 = __builtin_amdgcn_permlane16_swap(x1, z1, false, false);
           unsigned w[4] = {s0[0], s1[0], s0[1], s1[1]};
-          const uint4 y = yv[j / 2][i];
-          const unsigned ys[4] = {y.x, y.y, y.z, y.w};
+          if constexpr (MASK) {
+            const unsigned m = mv[j / 2][i];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {  // keep a bf16 where its activation is > 0
-            const unsigned lo = ys[q] & 0xffffu, hi = ys[q] >> 16;
-            const unsigned keep = ((lo & 0x8000u) == 0u && lo != 0u ? 0x0000ffffu : 0u) |
-                                  ((hi & 0x8000u) == 0u && hi != 0u ? 0xffff0000u : 0u);
-            w[q] &= keep;
+            for (int q = 0; q < 4; ++q)  // bit e of the byte = column e of the chunk
+              w[q] &= ((m >> (2 * q)) & 1u ? 0x0000ffffu : 0u) |
+                      ((m >> (2 * q + 1)) & 1u ? 0xffff0000u : 0u);
+          } else {
+            const uint4 y = yv[j / 2][i];
+            const unsigned ys[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {  // keep a bf16 where its activation is > 0
+              const unsigned lo = ys[q] & 0xffffu, hi = ys[q] >> 16;
+              const unsigned keep = ((lo & 0x8000u) == 0u && lo != 0u ? 0x0000ffffu : 0u) |
+                                    ((hi & 0x8000u) == 0u && hi != 0u ? 0xffff0000u : 0u);
+              w[q] &= keep;
+            }
           }
           if (want_sum && row < p.M) {
 #pragma unroll
@@ -961,8 +976,20 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&a
           const auto s0 = __builtin_amdgcn_permlane16_swap(x0, z0, false, false);
           const auto s1 = __builtin_amdgcn_permlane16_swap(x1, z1, false, false);
           const int scol = scol0 + 16 * j;
-          if (row < p.M && scol < p.N)
+          if (row < p.M && scol < p.N) {
             *(uint4*)((u16*)p.C + (long)row * p.ldc + scol) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+            if (!AUX && p.mask_out) {  // forward ReLU mask: bit e = stored bf16 of column e > 0
+              const unsigned w[4] = {s0[0], s1[0], s0[1], s1[1]};
+              unsigned bits = 0;
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                const unsigned lo = w[q] & 0xffffu, hi = w[q] >> 16;
+                bits |= ((lo & 0x8000u) == 0u && lo != 0u ? 1u : 0u) << (2 * q);
+                bits |= ((hi & 0x8000u) == 0u && hi != 0u ? 1u : 0u) << (2 * q + 1);
+              }
+              p.mask_out[(long)row * p.ld_mask + (scol >> 3)] = (unsigned char)bits;
+            }
+          }
         }
         if (want_sum) {  // this pair's column sums over the wave's rows -> LDS [wm][col]
           f32x4_t r0, r1;
@@ -979,7 +1006,8 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&a
         }
       }
       };
-      if (p.aux && p.act == ACT_RELU) relu_body();
+      if (p.aux && p.act == ACT_RELU) relu_body(std::false_type{});
+      else if (p.mask_in) relu_body(std::true_type{});
       else if (p.aux) body(std::true_type{});
       else body(std::false_type{});
       if (want_sum) {

@@ -297,9 +297,8 @@ def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=
                                   t.shape[1] < N or t.stride(0) != (c if c.dim() == 2
                                                                     else c[0]).stride(0)):
                 raise ValueError(f"fused update: {k} must be [M][N] with C's row stride")
-    if stages in (9, 10) and (mask_out is not None or mask_in is not None or ct is not None or
-                              upd is not None):
-        stages -= 3  # the register-direct epilogue has none of these: same loop, staged epilogue
+    if stages in (9, 10) and (ct is not None or upd is not None):
+        stages -= 3  # the register-direct epilogue has neither: same loop, staged epilogue
     if not a.is_cuda:
         ref.gemm(a, b, c, layout_a=layout_a, layout_b=layout_b, M=M, N=N, K=K, bias=bias,
                  aux=aux, act=act, accumulate=accumulate, splits=splits, colsum=colsum,

@@ -1,7 +1,7 @@
 # Round-3 baseline on today's box: default bench (driver form), the three BASELINE steps, and a
 # kernel trace of the headline step. -> gpurun_out/r3_base/
 set -o pipefail
-R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/r3_base; mkdir -p $O
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/${OUT:-r3_base}; mkdir -p $O
 cd $R
 timeout -k 10 300 python bench.py > $O/bench_default.json 2> $O/bench_default.err || { tail -20 $O/bench_default.err; exit 1; }
 tail -1 $O/bench_default.json | cut -c1-200

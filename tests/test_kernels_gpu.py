@@ -557,6 +557,28 @@ def test_register_prefetch_bitwise(dev, la, lb):
         assert torch.equal(outs[0], outs[1]), (bm, bn, code)
         # column sums: same values, summed in another order (per-wave butterflies + wave rows)
         torch.testing.assert_close(sums[0], sums[1], rtol=1e-5, atol=1e-3)
+    # 1-bit ReLU masks through the register-direct epilogue: the forward writes the mask of
+    # its stored output, a dgrad applies one instead of reading the activation
+    for (bm, bn), code in RP:
+        if code < 9:
+            continue
+        M, N, K = 320, 264, 192
+        a = _storage(la, M, K, gen, dev, False)
+        b = _storage(lb, N, K, gen, dev, False)
+        bias = torch.randn(N, generator=gen).to(dev)
+        res = []
+        for st in (2, code):
+            c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            m = torch.full((M, 40), 0xAA, device=dev, dtype=torch.uint8)
+            ops.gemm(a, b, c, layout_a=la, layout_b=lb, M=M, N=N, K=K, bias=bias, act="relu",
+                     tiles=(bm, bn), stages=st, mask_out=m)
+            d = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            ops.gemm(a, b, d, layout_a=la, layout_b=lb, M=M, N=N, K=K, act="relu",
+                     tiles=(bm, bn), stages=st, mask_in=m)
+            res.append((c, m, d))
+        (c2, m2, d2), (cn, mn, dn) = res
+        assert torch.equal(c2, cn) and torch.equal(m2, mn) and torch.equal(d2, dn), (bm, bn, code)
+        assert torch.equal(mn[:, 33:], torch.full_like(mn[:, 33:], 0xAA))  # past N/8 untouched
     # and against fp32 once (the 2-stage kernel itself is pinned by the tests above)
     M, N, K = 256, 256, 832
     a = _storage(la, M, K, gen, dev, False)
