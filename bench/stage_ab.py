@@ -68,8 +68,8 @@ def case_wgrad(R, M, N, splits, variants):
 
 
 T256, T128, T12864 = (256, 256), (128, 128), (128, 64)
-BIG = [(T256, 2), (T256, 6), (T256, 9)]
-WG = [(T128, 2), (T128, 6), (T128, 9), (T12864, 6), (T12864, 9)]
+BIG = [(T256, 2), (T256, 9), (T256, 11)]
+WG = [(T128, 2), (T128, 9), (T128, 11)]
 CASES = {
     "f0": lambda: case_fwd(65536, 832, 512, BIG),
     "f1": lambda: case_fwd(65536, 512, 256, BIG),
@@ -80,8 +80,8 @@ CASES = {
                                                     (T12864, 6), (T12864, 9)]),
     "m8f": lambda: case_fwd(65536, 1024, 1024, BIG),
     "m8d": lambda: case_dgrad(65536, 1024, 1024, BIG),
-    "m8w": lambda: case_wgrad(65536, 1024, 1024, 8, [(T128, 2), (T128, 6), (T128, 9)]),
-    "wide": lambda: case_fwd(16384, 8192, 8192, [(T256, 2), (T256, 6), (T256, 9)]),
+    "m8w": lambda: case_wgrad(65536, 1024, 1024, 8, [(T128, 2), (T128, 9), (T128, 11)]),
+    "wide": lambda: case_fwd(16384, 8192, 8192, [(T256, 2), (T256, 9), (T256, 11)]),
 }
 
 

@@ -45,7 +45,9 @@ struct GemmParams {
   int* correct;
   // raster order: row-tiles per group (<= 0: launcher default, 1 = row-major tiles)
   int group_m;
-  // 1-bit ReLU masks, [M][ld_mask] bytes, bit e of byte c = column 8c + e (bf16 output only):
+  // 1-bit ReLU masks, ceil(M/16) x ld_mask x 16 bytes, row-block-major (gemm_tile.hpp
+  // mask_index: byte of row r, chunk c at ((r/16) * ld_mask + c) * 16 + r % 16); bit e of the
+  // byte of chunk c = column 8c + e (bf16 output only):
   // mask_out (forward, act = relu): bit = stored bf16 output > 0; mask_in (dgrad, act = relu,
   // replaces aux): the derivative reads 1 bit per element instead of the 16-bit activation.
   unsigned char* mask_out;

@@ -7,10 +7,20 @@ namespace dnn {
 
 // Stage codes 6 / 7: the register-prefetched main loop (Cfg RP, mma_tile_rp) with a 2- / 3-deep
 // ring; 3 deep only where three 64-deep stages fit (not 256x256).
+// Code 11: register-direct epilogue over the asymmetric ring (A 3 deep, B 2 deep: two k-steps
+// for the streamed A panel to land), 256x256 / 256x128 / 128x128.
 // Codes 9 / 10: the same loop with swapped MFMA operands and the register-direct epilogue
 // (RP_ = 2): bias / activation / aux derivative / colsum / split-K f32, no ReLU bit masks,
 // transposed copy, fused update or cross-entropy.
 static gemm_fn pick_rp(int bm, int bn, int code, int la, int lb, int f32) {
+  if (code == 11) {  // asymmetric A3/B2 ring, register-direct epilogue
+#define DNN_RPA(BM, BN, WM, WN) pick_layout<Cfg<BM, BN, WM, WN, 3, 2, 64, 2>>(la, lb, f32)
+    if (bm == 256 && bn == 256) return DNN_RPA(256, 256, 4, 2);
+    if (bm == 256 && bn == 128) return DNN_RPA(256, 128, 4, 2);
+    if (bm == 128 && bn == 128) return DNN_RPA(128, 128, 2, 2);
+#undef DNN_RPA
+    return nullptr;
+  }
   const int ns = code == 6 || code == 9 ? 6 : 7;
   if (code == 9 || code == 10) {
 #define DNN_RP(BM, BN, WM, WN, NS) pick_layout<Cfg<BM, BN, WM, WN, NS, NS, 64, 2>>(la, lb, f32)

@@ -63,8 +63,12 @@ struct cmax {
 template <int BM_, int BN_, int WM_, int WN_, int NS_, int NSB_ = NS_, int BK_ = 64, int RP_ = 0>
 struct Cfg {
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, NS = NS_, NSB = NSB_, BK = BK_;
-  static constexpr bool RP = RP_ != 0, DIRECT = RP_ == 2;
-  static_assert(!RP || (BK == 64 && NSB == NS && NS <= 3), "register prefetch: BK 64, NS 2..3");
+  // RP_ bits 0-1: 1 = staged epilogue, 2 = register-direct; bits 2+: fragment-read placement
+  // in each half (0 = one read per NM/NR MFMAs, 1 = two reads per MFMA up front, 2 = all reads
+  // first)
+  static constexpr bool RP = RP_ != 0, DIRECT = (RP_ & 3) == 2;
+  static constexpr int RP_PATTERN = RP_ >> 2;
+  static_assert(!RP || (BK == 64 && NS <= 3), "register prefetch: BK 64, NS 2..3 (or A3/B2)");
   static_assert(NSB == NS || (NS == 3 && NSB == 2), "asymmetric ring: A 3 deep, B 2 deep only");
   static_assert(BK == 64 || BK == 32, "k-step depth 64 or 32");
   static constexpr bool ASYM = NSB != NS;
@@ -180,6 +184,14 @@ __device__ __forceinline__ bf16x8_t load_frag(const char LDS_AS* tile, int blk, 
     f.hi = hi;
     return f;
   }
+}
+
+// Byte of the 1-bit ReLU mask for row `row`, 8-column chunk `c` (GemmParams::mask_out/in):
+// row-block-major, [M/16][ld_mask][16], so the 16 rows x 4 consecutive chunks a wave stores in
+// the register-direct epilogue are 64 contiguous bytes (row-major bytes scattered one store
+// over 16 rows).
+__device__ __forceinline__ long mask_index(long row, long c, long ld) {
+  return (((row >> 4) * ld + c) << 4) + (row & 15);
 }
 
 // Phase timestamp of the workgroup (GemmParams::timeline); thread 0 stores it.
@@ -320,74 +332,118 @@ __device__ __forceinline__ void mfma_half(const bf16x8_t (&a)[C::FM], const bf16
     }
 }
 
+// Placement of a half's NR fragment reads among its NM MFMAs (sched_group_barrier masks:
+// 0x8 MFMA, 0x100 DS read), closed by a sched_barrier so nothing crosses into the wait /
+// barrier that follows.
+template <int PATTERN, int NR, int NM>
+__device__ __forceinline__ void rp_interleave() {
+  if constexpr (PATTERN == 0) {  // one read, then NM / NR MFMAs; the rest of the MFMAs last
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x8, NM / NR > 0 ? NM / NR : 1, 0);
+    }
+    if constexpr (NM > NR * (NM / NR))
+      __builtin_amdgcn_sched_group_barrier(0x8, NM - NR * (NM / NR), 0);
+  } else if constexpr (PATTERN == 1) {  // two reads per MFMA until the reads are out
+    static_assert(NR % 2 == 0, "reads come in pairs");
+#pragma unroll
+    for (int i = 0; i < NR / 2; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+    }
+    if constexpr (NM > NR / 2) __builtin_amdgcn_sched_group_barrier(0x8, NM - NR / 2, 0);
+  } else {  // every read first
+    __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+    __builtin_amdgcn_sched_group_barrier(0x8, NM, 0);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 template <class C, int LA, int LB>
 __device__ __forceinline__ void mma_tile_rp(const GemmParams& p, int m0, int n0, int kbase,
                                             int nk, char LDS_AS* lds,
                                             f32x4_t (&acc)[C::FM][C::FN], int wm, int wn,
                                             int wave, int lane) {
-  constexpr int NS = C::NS, STAGE = C::STAGE, A_BYTES = C::A_BYTES;
-  auto stage = [&](int k, int slot) {
-    char LDS_AS* dst = lds + slot * STAGE;
-    stage_tile_asm<LA, C::BM, C::NW>(p.A, p.lda, m0, kbase + k * 64, dst, wave, lane, p.M);
-    stage_tile_asm<LB, C::BN, C::NW>(p.B, p.ldb, n0, kbase + k * 64, dst + A_BYTES, wave, lane,
+  // Ring slots: symmetric = NS x [A | B] stages; asymmetric (C::ASYM) = 3 A slots then 2 B
+  // slots, so the A operand (the streamed activation panel, HBM) gets two k-steps to land
+  // and the B operand (weights, L2-resident) one.
+  constexpr int NA = C::NS, NB = C::NSB, A_BYTES = C::A_BYTES, B_BYTES = C::B_BYTES;
+  auto a_at = [&](int slot) -> char LDS_AS* {
+    return C::ASYM ? lds + slot * A_BYTES : lds + slot * C::STAGE;
+  };
+  auto b_at = [&](int slot) -> char LDS_AS* {
+    return C::ASYM ? lds + NA * A_BYTES + slot * B_BYTES : lds + slot * C::STAGE + A_BYTES;
+  };
+  auto st_a = [&](int k, int slot) {
+    stage_tile_asm<LA, C::BM, C::NW>(p.A, p.lda, m0, kbase + k * 64, a_at(slot), wave, lane,
+                                     p.M);
+  };
+  auto st_b = [&](int k, int slot) {
+    stage_tile_asm<LB, C::BN, C::NW>(p.B, p.ldb, n0, kbase + k * 64, b_at(slot), wave, lane,
                                      p.N);
   };
+  // Prologue: every slot staged (tiles past the end clamp to the last one: same load counts
+  // whatever nk is), then tile 0 landed.
+  if constexpr (C::ASYM) {  // issue order A0 B0 A1 B1 A2
+    st_a(0, 0);
+    st_b(0, 0);
+    st_a(min(1, nk - 1), 1);
+    st_b(min(1, nk - 1), 1);
+    st_a(min(2, nk - 1), 2);
+    wait_vmcnt<2 * C::PER_A + C::PER_B>();
+  } else {
 #pragma unroll
-  for (int s = 0; s < NS; ++s)
-    if (s < nk) stage(s, s);
-  wait_stage<NS + 1, C::PER_STAGE>(min(nk - 1, NS - 1));
+    for (int s = 0; s < NA; ++s) {
+      st_a(min(s, nk - 1), s);
+      st_b(min(s, nk - 1), s);
+    }
+    wait_vmcnt<(NA - 1) * C::PER_STAGE>();
+  }
   lds_barrier();
   tl_mark(p, 1);
   bf16x8_t a0[C::FM], b0[C::FN], a1[C::FM], b1[C::FN];
-  read_half<C, LA, LB>(lds, lds + A_BYTES, a0, b0, wm, wn, 0, lane);
+  read_half<C, LA, LB>(a_at(0), b_at(0), a0, b0, wm, wn, 0, lane);
   // Wait counts the compiler's wait-count pass can see (a builtin, unlike inline asm): with no
   // LDS read pending at the loop head / after the barrier, it lets the MFMAs on registers that
   // have landed issue while the next half's reads are in flight. The loop body is branch-free
-  // up to the staging issue (the last k-step is peeled), so no control-flow merge forces a
-  // conservative lgkmcnt(0) in front of an MFMA.
+  // (the last k-step is peeled), so no control-flow merge forces a conservative lgkmcnt(0) in
+  // front of an MFMA.
   __builtin_amdgcn_s_waitcnt(0xC07F);  // vmcnt(63) expcnt(7) lgkmcnt(0)
   // Instruction interleave of both halves (sched_group_barrier masks: 0x8 MFMA, 0x100 DS read):
   // each fragment read is followed by NM / NR MFMAs, the rest of the MFMAs come last.
   constexpr int NR = (C::FM + C::FN) * (LA == KMAJ ? 1 : 2) / 2 +
                      (C::FM + C::FN) * (LB == KMAJ ? 1 : 2) / 2;  // DS reads per half
   constexpr int NM = C::FM * C::FN;                                // MFMAs per half
-  int rd = 0;  // slot of tile kt
+  int ra = 0, rb = 0;  // A / B slots of tile kt
   for (int kt = 0; kt + 1 < nk; ++kt) {
-    const char LDS_AS* cur = lds + rd * STAGE;
-    read_half<C, LA, LB>(cur, cur + A_BYTES, a1, b1, wm, wn, 1, lane);
+    read_half<C, LA, LB>(a_at(ra), b_at(rb), a1, b1, wm, wn, 1, lane);
     mfma_half<C>(a0, b0, acc);
-#pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x8, NM / NR > 0 ? NM / NR : 1, 0);
-    }
-    if constexpr (NM > NR * (NM / NR)) __builtin_amdgcn_sched_group_barrier(0x8, NM - NR * (NM / NR), 0);
-    __builtin_amdgcn_sched_barrier(0);
-    wait_stage<NS, C::PER_STAGE>(NS - 2);
+    rp_interleave<C::RP_PATTERN, NR, NM>();
+    // own loads of tile kt+1 landed: asymmetric -- only A(kt+2) was issued after B(kt+1);
+    // symmetric -- tiles kt+2 .. kt+NS-1 may stay in flight
+    if constexpr (C::ASYM) wait_vmcnt<C::PER_A>();
+    else wait_vmcnt<(NA - 2) * C::PER_STAGE>();
     __builtin_amdgcn_s_waitcnt(0xC07F);
     asm volatile("s_barrier" ::: "memory");
-    // Tile kt+NS into tile kt's slot; past the end the last tile is restaged instead (an L2
-    // hit into a slot nobody reads again), so the loop body has no branch and every k-step
-    // leaves the same number of stages in flight.
-    stage(min(kt + NS, nk - 1), rd);
-    rd = rd + 1 == NS ? 0 : rd + 1;
-    const char LDS_AS* nxt = lds + rd * STAGE;
-    read_half<C, LA, LB>(nxt, nxt + A_BYTES, a0, b0, wm, wn, 0, lane);
+    // Tile kt's slots are free: B(kt+NB) and A(kt+NA) into them; past the end the last tile is
+    // restaged instead (an L2 hit into a slot nobody reads again), so the loop body has no
+    // branch and every k-step leaves the same loads in flight.
+    st_b(min(kt + NB, nk - 1), rb);
+    st_a(min(kt + NA, nk - 1), ra);
+    ra = ra + 1 == NA ? 0 : ra + 1;
+    rb = rb + 1 == NB ? 0 : rb + 1;
+    read_half<C, LA, LB>(a_at(ra), b_at(rb), a0, b0, wm, wn, 0, lane);
     mfma_half<C>(a1, b1, acc);
-#pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x8, NM / NR > 0 ? NM / NR : 1, 0);
-    }
-    if constexpr (NM > NR * (NM / NR)) __builtin_amdgcn_sched_group_barrier(0x8, NM - NR * (NM / NR), 0);
-    __builtin_amdgcn_sched_barrier(0);
+    rp_interleave<C::RP_PATTERN, NR, NM>();
     __builtin_amdgcn_s_waitcnt(0xC07F);
   }
-  wait_vmcnt<0>();  // the restaged tail tiles (nothing reads them; the epilogue reuses LDS)
-  const char LDS_AS* cur = lds + rd * STAGE;
-  read_half<C, LA, LB>(cur, cur + A_BYTES, a1, b1, wm, wn, 1, lane);
+  read_half<C, LA, LB>(a_at(ra), b_at(rb), a1, b1, wm, wn, 1, lane);
   mfma_half<C>(a0, b0, acc);
   mfma_half<C>(a1, b1, acc);
+  // the restaged tail tiles (nothing reads them) land before the epilogue reuses LDS; waited
+  // here, after the last k-step, not in front of it
+  wait_vmcnt<0>();
   __syncthreads();
 }
 
@@ -401,12 +457,12 @@ __device__ __forceinline__ void mma_tile(const GemmParams& p, int m0, int n0, in
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  if constexpr (C::ASYM) {
-    mma_tile_asym<C, LA, LB>(p, m0, n0, kbase, nk, lds, acc, wm, wn, wave, lane);
-    return;
-  }
   if constexpr (C::RP) {
     mma_tile_rp<C, LA, LB>(p, m0, n0, kbase, nk, lds, acc, wm, wn, wave, lane);
+    return;
+  }
+  if constexpr (C::ASYM) {
+    mma_tile_asym<C, LA, LB>(p, m0, n0, kbase, nk, lds, acc, wm, wn, wave, lane);
     return;
   }
 
@@ -606,7 +662,7 @@ __device__ __forceinline__ void epilogue_staged(const GemmParams& p,
 #pragma unroll
         for (int it = 0; it < ITER; ++it)
           if (col_ok && gm0 + it * RSTEP < p.M)
-            mk[it] = p.mask_in[(gm0 + it * RSTEP) * p.ld_mask + (gn >> 3)];
+            mk[it] = p.mask_in[mask_index(gm0 + it * RSTEP, gn >> 3, p.ld_mask)];
       }
     }
 #pragma unroll
@@ -674,7 +730,7 @@ __device__ __forceinline__ void epilogue_staged(const GemmParams& p,
         }
         *(bf16x8_t*)((u16*)p.C + gm * p.ldc + gn) = o;
         ov[it] = o;
-        if (p.mask_out) p.mask_out[gm * p.ld_mask + (gn >> 3)] = (unsigned char)bits;
+        if (p.mask_out) p.mask_out[mask_index(gm, gn >> 3, p.ld_mask)] = (unsigned char)bits;
       }
     }
     {
@@ -833,7 +889,7 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&a
 #pragma unroll
         for (int i = 0; i < FM; ++i) {
           const long r = min(row0 + 16 * i, p.M - 1);
-          if constexpr (MASK) mv[jj][i] = p.mask_in[r * p.ld_mask + (c >> 3)];
+          if constexpr (MASK) mv[jj][i] = p.mask_in[mask_index(r, c >> 3, p.ld_mask)];
           else yv[jj][i] = *(const uint4*)(p.aux + r * p.ld_aux + c);
         }
       }
@@ -987,7 +1043,7 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&a
                 bits |= ((lo & 0x8000u) == 0u && lo != 0u ? 1u : 0u) << (2 * q);
                 bits |= ((hi & 0x8000u) == 0u && hi != 0u ? 1u : 0u) << (2 * q + 1);
               }
-              p.mask_out[(long)row * p.ld_mask + (scol >> 3)] = (unsigned char)bits;
+              p.mask_out[mask_index(row, scol >> 3, p.ld_mask)] = (unsigned char)bits;
             }
           }
         }

@@ -482,8 +482,7 @@ class Stage:
         if dev.type == "cuda" and switches.get("DNN_DGRAD_WT") == "1":
             L = len(self.geoms)
             for i in range(L):
-                if (i > 0 or not self.first) and not (self.tail and i >= L - 2) and \
-                        not (i > 0 and self.relu_mask[i - 1] is not None):
+                if (i > 0 or not self.first) and not (self.tail and i >= L - 2):
                     self.params.enable_wt(i)
         if self.tail:
             self.xent_per_micro = ops.tail_blocks(self.mb)

@@ -278,10 +278,11 @@ def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=
             raise ValueError(f"colsum must be fp32 [{-(-M // tiles[0])}][>={N}] row-major")
     if (mask_out is not None or mask_in is not None) and not a.is_cuda:
         raise ValueError("relu bit masks are a GPU-path format (CPU uses aux)")
-    for m in (mask_out, mask_in):
-        if m is not None and (m.dtype != torch.uint8 or m.dim() != 2 or m.stride(1) != 1 or
-                              m.shape[0] < M or m.shape[1] < -(-N // 8)):
-            raise ValueError(f"relu mask must be uint8 [{M}][>={-(-N // 8)}] row-major")
+    for m in (mask_out, mask_in):  # row-block-major bytes (see relu_mask_bits)
+        if m is not None and (m.dtype != torch.uint8 or m.dim() != 2 or not m.is_contiguous() or
+                              M % 16 or m.shape[0] < M or m.shape[1] < -(-N // 8)):
+            raise ValueError(f"relu mask must be a contiguous uint8 [{M}][>={-(-N // 8)}] "
+                             "tensor and M a multiple of 16")
     if ct is not None and (ct.dtype != torch.bfloat16 or ct.dim() != 2 or ct.stride(1) != 1 or
                            ct.shape[0] < N or ct.shape[1] < M or (out_f32 and upd is None)):
         raise ValueError(f"ct must be a bf16 [>={N}][>={M}] row-major transposed output")
@@ -297,8 +298,8 @@ def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=
                                   t.shape[1] < N or t.stride(0) != (c if c.dim() == 2
                                                                     else c[0]).stride(0)):
                 raise ValueError(f"fused update: {k} must be [M][N] with C's row stride")
-    if stages in (9, 10) and (ct is not None or upd is not None):
-        stages -= 3  # the register-direct epilogue has neither: same loop, staged epilogue
+    if stages in (9, 10, 11) and (ct is not None or upd is not None):
+        stages = 6  # the register-direct epilogue has neither: RP loop, staged epilogue
     if not a.is_cuda:
         ref.gemm(a, b, c, layout_a=layout_a, layout_b=layout_b, M=M, N=N, K=K, bias=bias,
                  aux=aux, act=act, accumulate=accumulate, splits=splits, colsum=colsum,
@@ -387,6 +388,16 @@ def gemv(x, w, bias, y, act="relu"):
     native().gemv_bf16(_p(x), x.stride(0), _p(w), w.stride(0), _p(bias), _p(y), y.stride(0),
                        M, N, K, _act(act), int(y.dtype == torch.float32), _stream(x))
     return y
+
+
+def relu_mask_bits(mask: torch.Tensor, M: int, N: int) -> torch.Tensor:
+    """Unpack a GEMM-written ReLU mask (uint8 [M][ld], row-block-major: the byte of row r,
+    8-column chunk c is at flat index ((r // 16) * ld + c) * 16 + r % 16) into bool [M][N]."""
+    ld = mask.shape[1]
+    blocks = mask.reshape(-1)[:M * ld].view(M // 16, ld, 16).transpose(1, 2).reshape(M, ld)
+    bits = (blocks[:, :(N + 7) // 8].to(torch.int32).unsqueeze(-1) >>
+            torch.arange(8, device=mask.device, dtype=torch.int32)) & 1
+    return bits.reshape(M, -1)[:, :N].bool()
 
 
 def linear_fwd(x, w, bias, y, act="relu", mask=None, yt=None):
@@ -559,11 +570,12 @@ def linear_dgrad(dz, w, dx, y_prev=None, act_prev="linear", colsum=None, mask_pr
         elif colsum is not None:
             colsum_partial(dx, colsum, n_part)
         return dx
-    if wt is not None and dz.is_cuda and mask_prev is None:
+    if wt is not None and dz.is_cuda:
         return gemm(dz, wt, dx, layout_a=KMAJ, layout_b=KMAJ, M=M, N=K, K=N, aux=y_prev,
                     act=act_prev, tiles=dgrad_tiles(M, K, N), colsum=colsum,
                     stages=STAGES["dgrad"] or (t or {}).get("stages", 0),
-                    persist=0 if dxt is not None else _persist("dgrad", t), ct=dxt)
+                    persist=0 if (dxt is not None or mask_prev is not None)
+                    else _persist("dgrad", t), mask_in=mask_prev, ct=dxt)
     return gemm(dz, w, dx, layout_a=KMAJ, layout_b=MNMAJ, M=M, N=K, K=N, aux=y_prev,
                 act=act_prev, tiles=dgrad_tiles(M, K, N), colsum=colsum,
                 stages=STAGES["dgrad"] or (t or {}).get("stages", 0),

@@ -507,7 +507,8 @@ def test_bk32_ksteps_bitwise(dev, la, lb):
 
 RP = [((256, 256), 6), ((256, 128), 6), ((256, 128), 7), ((128, 128), 6), ((128, 128), 7),
       ((128, 64), 6), ((128, 64), 7), ((64, 64), 6), ((64, 64), 7),
-      ((256, 256), 9), ((256, 128), 10), ((128, 128), 9), ((128, 64), 10), ((64, 64), 9)]
+      ((256, 256), 9), ((256, 128), 10), ((128, 128), 9), ((128, 64), 10), ((64, 64), 9),
+      ((256, 256), 11), ((256, 128), 11), ((128, 128), 11)]
 
 
 @pytest.mark.parametrize("la,lb", LAYOUTS)
@@ -578,7 +579,9 @@ def test_register_prefetch_bitwise(dev, la, lb):
             res.append((c, m, d))
         (c2, m2, d2), (cn, mn, dn) = res
         assert torch.equal(c2, cn) and torch.equal(m2, mn) and torch.equal(d2, dn), (bm, bn, code)
-        assert torch.equal(mn[:, 33:], torch.full_like(mn[:, 33:], 0xAA))  # past N/8 untouched
+        blocked = mn.view(-1).view(M // 16, 40, 16)  # row-block-major mask bytes
+        assert torch.all(blocked[:, 33:, :] == 0xAA)  # chunks past N/8 untouched
+        assert torch.equal(ops.relu_mask_bits(mn, M, N), cn > 0)
     # and against fp32 once (the 2-stage kernel itself is pinned by the tests above)
     M, N, K = 256, 256, 832
     a = _storage(la, M, K, gen, dev, False)

@@ -23,10 +23,10 @@ def test_mask_roundtrip_bitwise(dev, tile, stages):
     mask = torch.full((M, N // 8 + 3), 0xAA, device=dev, dtype=torch.uint8)
     ops.gemm(x, w, y, layout_a=KMAJ, layout_b=KMAJ, M=M, N=N, K=K, bias=b, act="relu",
              tiles=tile, stages=stages, mask_out=mask)
-    bits = (y > 0).view(M, N // 8, 8).to(torch.int32)
-    want = (bits << torch.arange(8, device=dev, dtype=torch.int32)).sum(-1).to(torch.uint8)
-    assert torch.equal(mask[:, :N // 8], want)
-    assert torch.all(mask[:, N // 8:] == 0xAA)  # nothing written past N/8
+    assert torch.equal(ops.relu_mask_bits(mask, M, N), y > 0)
+    ld = mask.shape[1]  # row-block-major: [M/16][ld][16]; chunks past N/8 never written
+    blocked = mask.view(-1).view(M // 16, ld, 16)
+    assert torch.all(blocked[:, N // 8:, :] == 0xAA)
     # dgrad: dz[M][R2] . w2[R2][N] with the relu derivative of y (aux) vs its mask
     R2 = 192
     dz = torch.randn(M, R2, generator=gen).to(torch.bfloat16).to(dev)
