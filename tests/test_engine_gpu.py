@@ -148,7 +148,8 @@ def test_native_and_graph_optimizers_with_lr_schedule(dev, optim):
     applies the update (fused_layers): they must see this step's rate on every path."""
     import dataclasses
 
-    spec = MLPSpec.parse("784-256-128-10")
+    # SGD: a 1024-wide first layer, whose 1024-row weight gradient is ONE split (fused update)
+    spec = MLPSpec.parse("784-1024-128-10" if optim.name == "sgd" else "784-256-128-10")
     x, y = _batch(1024, dev)
     lrs = [optim.lr * f for f in (1.0, 0.5, 0.25, 0.5, 1.0)]
     results = []
