@@ -31,16 +31,17 @@ import os
 import sys
 import time
 
-# Multi-rank steps run up to four busy streams per rank (compute, forward hops, backward hops,
-# DP buckets; parallel/native_step.py) next to torch's RCCL streams. HIP multiplexes streams
+# Multi-rank steps run several busy streams per rank: the IPC plan 4 + its relay duties
+# (~7 at pp4dp2 with 2 relays), the RCCL fallback plan built next to it for the first-step
+# verification 6 (parallel/native_step.py), torch's and RCCL's own. HIP multiplexes streams
 # onto GPU_MAX_HW_QUEUES hardware queues (default 4) in order, so two streams sharing a queue
-# would serialise a spinning RCCL receive in one direction with a send in the other. Give
-# every stream its own queue (set before the HIP runtime initialises; <= 32 by pool policy).
-# The box exports GPU_MAX_HW_QUEUES=4 (HIP's default), so raise it rather than setdefault;
-# one-GPU rehearsals (DNN_FORCE_DEVICE: many ranks share one GPU) keep what the caller set.
+# would serialise a spinning wait in one direction with the work that releases it. Give every
+# stream its own queue (set before the HIP runtime initialises; <= 32 by pool policy). The box
+# exports GPU_MAX_HW_QUEUES=4 (HIP's default), so raise it rather than setdefault; one-GPU
+# rehearsals (DNN_FORCE_DEVICE: many ranks share one GPU) keep what the caller set.
 if int(os.environ.get("WORLD_SIZE", "1")) > 1 and not os.environ.get("DNN_FORCE_DEVICE"):
-    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 16:
-        os.environ["GPU_MAX_HW_QUEUES"] = "16"
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 24:
+        os.environ["GPU_MAX_HW_QUEUES"] = "24"
 
 import torch  # noqa: E402
 
@@ -97,7 +98,11 @@ def parse_args(argv=None):
 
 
 def _plan(a, spec, n, world, text):
-    relays = int(switches.get("DNN_IPC_RELAYS")) if switches.get("DNN_PIPE") == "ipc" else 0
+    # the relayed IPC transport the trainer picks first on an RCCL job (engine/trainer.py
+    # _pick_pipe); a run that falls back to RCCL reports it in "transport"
+    kr = switches.get("DNN_IPC_RELAYS")
+    relays = (min(2, max(0, n - 2)) if kr == "auto" else int(kr)) \
+        if switches.get("DNN_PIPE") in ("auto", "ipc") and n > 1 else 0
     planner = Planner.calibrated(spec, relays=relays,
                                  dp_grad_bytes=2.0 if a.dp_reduce == "shard" else 4.0)
     loopback = world == 1
@@ -222,7 +227,8 @@ def measure(a, spec, n, world, dev, text):
         "parallelism": plan.parallelism + ("-loopback" if world == 1 and plan.pp > 1 else ""),
         "layer_distribution": plan.distribution, "micro_batch": mb, "num_micro": nm,
         "schedule": sched if plan.pp > 1 else "none",
-        "transport": tr.transport, "native_step": tr.native_step is not None or world == 1,
+        "transport": tr.transport, "transport_reason": tr.transport_reason,
+        "native_step": tr.native_step is not None or world == 1,
         "rccl_plan": tr.native_step.mode if tr.native_step is not None else None,
         "native_fallback": tr.native_fallback,
         "boundary": tr.boundary, "dp_reduce": tr.dp_reduce if plan.dp > 1 else None,
@@ -266,6 +272,7 @@ def measure_tp(a, spec, n, world, dev):
             "parallelism": f"tp{tp}", "layer_distribution": [len(spec.layers)],
             "micro_batch": a.batch, "num_micro": 1, "schedule": "none",
             "transport": "rccl" if torch.distributed.get_backend() == "nccl" else "gloo",
+            "transport_reason": "tensor parallel collectives",
             "native_step": False, "rccl_plan": None, "boundary": "bf16", "dp_reduce": None,
             "hip_graph": False,
             "graph_copies": 0, "loss": m.loss(), "planner_predicted": None,
@@ -321,7 +328,8 @@ def main(argv=None):
             "global_batch": m["global_batch"],
             "seq_len": None,
             **{k: m[k] for k in ("parallelism", "layer_distribution", "micro_batch", "num_micro",
-                                 "schedule", "transport", "native_step", "rccl_plan",
+                                 "schedule", "transport", "transport_reason", "native_step",
+                                 "rccl_plan",
                                  "boundary", "dp_reduce", "hip_graph", "graph_copies")},
             "optimizer": a.optimizer,
         },

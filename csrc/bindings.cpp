@@ -973,6 +973,14 @@ PYBIND11_MODULE(_native, m) {
       py::arg("handle"), py::arg("offset"));
   m.def("ipc_close_all", &dnn::ipc_close_all);
   m.def(
+      "alloc_uncached",
+      [](size_t bytes) { return reinterpret_cast<uintptr_t>(dnn::alloc_uncached(bytes)); },
+      py::arg("bytes"), "zeroed device memory the L2 does not cache (xGMI receive buffers)");
+  m.def(
+      "free_device", [](uintptr_t p) { dnn::free_device(reinterpret_cast<void*>(p)); },
+      py::arg("ptr"));
+  m.def("can_access_peer", &dnn::can_access_peer, py::arg("dev"), py::arg("peer"));
+  m.def(
       "copy_async",
       [](uintptr_t dst, uintptr_t src, size_t n, uintptr_t s) {
         dnn::copy_async(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), n,

@@ -47,6 +47,23 @@ void* ipc_import(const std::string& handle, uint64_t offset) {
   return static_cast<char*>(base) + offset;
 }
 
+void* alloc_uncached(size_t bytes) {
+  void* p = nullptr;
+  ck(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached), "hipExtMallocWithFlags");
+  ck(hipMemset(p, 0, bytes), "hipMemset");
+  return p;
+}
+
+void free_device(void* p) {
+  if (p) (void)hipFree(p);
+}
+
+bool can_access_peer(int dev, int peer) {
+  int ok = 0;
+  if (dev == peer) return true;
+  return hipDeviceCanAccessPeer(&ok, dev, peer) == hipSuccess && ok != 0;
+}
+
 void ipc_close_all() {
   std::lock_guard<std::mutex> g(mu);
   for (auto& kv : opened) (void)hipIpcCloseMemHandle(kv.second);

@@ -22,6 +22,13 @@ namespace dnn {
 std::pair<std::string, uint64_t> ipc_export(void* ptr);
 void* ipc_import(const std::string& handle, uint64_t offset);
 void ipc_close_all();
+// Device memory the L2 does not cache (hipDeviceMallocUncached), zeroed: the receive buffers
+// of xGMI peer writes. A peer's stores land in this GPU's HBM without touching its L2s (one
+// per XCD, not coherent with each other or with the peer), so a cached copy of the previous
+// step's rows could otherwise be read back stale.
+void* alloc_uncached(size_t bytes);
+void free_device(void* p);
+bool can_access_peer(int dev, int peer);
 void copy_async(void* dst, const void* src, size_t n, hipStream_t s);
 void signal_u32(hipStream_t s, void* flag, uint32_t v);
 void wait_geq_u32(hipStream_t s, void* flag, uint32_t v);

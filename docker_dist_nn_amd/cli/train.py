@@ -22,8 +22,8 @@ import numpy as np
 
 if int(os.environ.get("WORLD_SIZE", "1")) > 1 and not os.environ.get("DNN_FORCE_DEVICE"):
     # one hardware queue per stream (see bench.py); the box exports 4, so raise it
-    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 16:
-        os.environ["GPU_MAX_HW_QUEUES"] = "16"
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 24:  # see bench.py
+        os.environ["GPU_MAX_HW_QUEUES"] = "24"
 
 import torch  # noqa: E402
 

@@ -106,6 +106,9 @@ class Trainer:
         if boundary not in ("bf16", "fp8"):
             raise ValueError(f"boundary must be bf16 | fp8, got {boundary!r}")
         self.boundary = boundary if (mesh is not None and pp > 1) else "bf16"
+        self._ipc_verify = None  # set by _pick_pipe while the first IPC step is unverified
+        self._fallback_step = None
+        self.transport_reason = "loopback (one process)"
         if mesh is None:
             if boundary == "fp8" and pp > 1:
                 raise ValueError("the fp8 boundary is a multi-rank hop format (loopback stages "
@@ -126,11 +129,7 @@ class Trainer:
                 if switches.get("DNN_PIPE") == "ipc":
                     raise ValueError("the fp8 boundary runs on the message transport (rccl/gloo)")
                 st.enable_fp8_boundary(mesh.prev_rank is not None, mesh.next_rank is not None)
-            # DNN_PIPE=ipc: xGMI peer writes into IPC-mapped buffers instead of RCCL P2P
-            use_ipc = (switches.get("DNN_PIPE") == "ipc" and
-                       self.device.type == "cuda" and mesh.pp > 1)
-            self.pipe = (IpcPipe(mesh, st, relays=int(switches.get("DNN_IPC_RELAYS")))
-                         if use_ipc else DistPipe(mesh, st))
+            self.pipe = self._pick_pipe(mesh, st, boundary)
             ids = [mesh.stage]
             sync = (GradSync(mesh.dp_group, mesh.dp, shard=self.dp_reduce == "shard")
                     if mesh.dp > 1 or self.dp_reduce == "shard" else None)
@@ -171,6 +170,9 @@ class Trainer:
                     self.native_step = NativeStep(self.executor, mesh, self.transport,
                                                   ipc=self.pipe if self.transport == "ipc"
                                                   else None)
+                    if self._ipc_verify is not None and mesh.backend == "nccl":
+                        # the verified IPC step's fallback: the RCCL plan, built up front
+                        self._fallback_step = NativeStep(self.executor, mesh, "rccl")
                 except Exception as e:  # agreed on below: every rank falls back together
                     err = e
             # A rank running the native step and one running the Python executor would post
@@ -195,10 +197,150 @@ class Trainer:
                     f"DNN_IPC_RELAYS={self.pipe.k} needs the native multi-rank step on every "
                     f"rank, which is unavailable ({self.native_fallback or why}); run with "
                     f"DNN_IPC_RELAYS=0 or fix the native step")
+        if self._ipc_verify is not None and self.native_step is None:
+            # the IPC step cannot be verified without the native step: message transport
+            self._use_fallback_pipe("IPC needs the native multi-rank step "
+                                    f"({self.native_fallback or 'unsupported plan'})")
         self._graph = None
         self._stream = None
         self.graph_nodes = 0
         self.steps_done = 0
+
+    # ---- pipeline transport --------------------------------------------------------------
+    def _pick_pipe(self, mesh, st, boundary):
+        """The hop transport of this rank (all ranks decide alike).
+
+        DNN_PIPE=rccl: RCCL P2P (DistPipe). DNN_PIPE=ipc: xGMI peer writes into IPC-mapped,
+        L2-uncached receive buffers with ``DNN_IPC_RELAYS`` relay stripes per hop (IpcPipe).
+        DNN_PIPE=auto (default): IPC with relays (the planner's link model: a hop then draws
+        on k + 1 xGMI links) on a real multi-GPU RCCL job, when every GPU can map its peers --
+        VERIFIED on the first step: that step runs on both transports from the same state and
+        the weights must agree bit for bit on every rank (``_verify_first_step``), else the job
+        stays on RCCL. The chosen transport and the reason are in ``transport_reason``."""
+        self._ipc_verify = None  # (ipc pipe, fallback pipe) while the first step is pending
+        self._fallback_step = None
+        mode = switches.get("DNN_PIPE")
+        if mode not in ("auto", "ipc", "rccl"):
+            raise ValueError(f"DNN_PIPE must be auto | ipc | rccl, got {mode!r}")
+        if mode == "rccl" or self.device.type != "cuda" or mesh.pp < 2:
+            self.transport_reason = ("DNN_PIPE=rccl" if mode == "rccl" else
+                                     "no pipeline hops" if mesh.pp < 2 else "CPU ranks")
+            return DistPipe(mesh, st)
+        if boundary == "fp8":
+            if mode == "ipc":
+                raise ValueError("the fp8 boundary runs on the message transport (rccl/gloo)")
+            self.transport_reason = "fp8 boundary (message transport)"
+            return DistPipe(mesh, st)
+        if mode == "auto" and mesh.backend != "nccl":
+            self.transport_reason = f"{mesh.backend} ranks (auto picks IPC on RCCL jobs)"
+            return DistPipe(mesh, st)
+        if mode == "auto" and not self._peers_mappable(mesh):
+            self.transport_reason = "a GPU pair of the plan has no peer access"
+            return DistPipe(mesh, st)
+        kr = switches.get("DNN_IPC_RELAYS")
+        world = mesh.pp * mesh.dp
+        k = min(2, max(0, world - 2)) if kr == "auto" else int(kr)
+        verify = switches.get("DNN_IPC_VERIFY")
+        verify = mode == "auto" if verify == "auto" else verify == "1"
+        try:
+            ipc = IpcPipe(mesh, st, relays=k)
+        except RuntimeError as e:  # raised on every rank together (comm.IpcPipe)
+            if mode == "ipc":
+                raise
+            self.transport_reason = f"IPC set-up failed: {e}"[:300]
+            return DistPipe(mesh, st)
+        self.transport_reason = (f"ipc, {k} relays per hop" +
+                                 (" (verification pending: first step)" if verify else ""))
+        if verify:
+            self._ipc_verify = (ipc, DistPipe(mesh, st))
+        return ipc
+
+    def _peers_mappable(self, mesh) -> bool:
+        """Every rank can map every other rank's GPU (one rank per GPU on one node; a relay can
+        be any rank), agreed over the world."""
+        import torch.distributed as dist
+
+        from ..parallel.comm import _cpu_group
+
+        n = native()
+        ndev = torch.cuda.device_count()
+        me = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        devs = [None] * dist.get_world_size()
+        dist.all_gather_object(devs, me, group=_cpu_group())
+        ok = all(n.can_access_peer(me, d) for d in devs if d is not None and d < ndev) and \
+            len(set(devs)) == len(devs)  # ranks sharing a GPU: not a multi-GPU job
+        t = torch.tensor([0 if ok else 1], dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=_cpu_group())
+        return int(t.item()) == 0
+
+    def _use_fallback_pipe(self, why: str) -> None:
+        ipc, fb = self._ipc_verify
+        self._ipc_verify = None
+        self.pipe = fb
+        self.executor.pipe = fb
+        self.transport = "rccl" if self.mesh.backend == "nccl" else self.mesh.backend
+        self.native_step = self._fallback_step
+        self.executor.native_step = self._fallback_step
+        self._fallback_step = None
+        self.transport_reason = f"{self.transport} (IPC not used: {why})"[:300]
+
+    def _state_tensors(self) -> list:
+        out = []
+        for st in self.stages:
+            p = st.params
+            out += [p.master, p.shadow, *p.state, *p.wt.values()]
+            for name in ("lr_dev", "step_dev"):
+                t = getattr(p, name, None)
+                if isinstance(t, torch.Tensor):
+                    out.append(t)
+        return out
+
+    def _verify_first_step(self) -> None:
+        """Run the first step on the IPC plan, then from the same state on the fallback
+        transport; keep IPC only if every rank's weights agree bit for bit (the two move the
+        same bytes) and no flag wait timed out. The fallback's step is the one kept."""
+        import sys
+
+        import torch.distributed as dist
+
+        from ..parallel.comm import _cpu_group
+
+        state = self._state_tensors()
+        snap = [t.clone() for t in state]
+        counts = [st.params.step_count for st in self.stages]
+        self.executor.run_step()  # IPC
+        torch.cuda.synchronize(self.device)
+        ipc_state = [t.clone() for t in state]
+        timeouts = self.native_step.comm_error() if self.native_step is not None else 0
+        if str(self.mesh.rank) in switches.get("DNN_FAULT_IPC_VERIFY").split(","):
+            ipc_state[0].view(-1)[0] += 1.0  # injected corruption (tests the fallback branch)
+        for t, v in zip(state, snap):
+            t.copy_(v)
+        for st, c in zip(self.stages, counts):
+            st.params.step_count = c
+        ipc_ns, ipc_pipe = self.native_step, self.pipe
+        fb = self._ipc_verify[1]
+        self.executor.native_step = self._fallback_step
+        self.executor.pipe = fb
+        self.executor.run_step()  # fallback transport, same state and batch
+        torch.cuda.synchronize(self.device)
+        same = timeouts == 0 and all(torch.equal(a, b) for a, b in zip(ipc_state, state))
+        t = torch.tensor([0 if same else 1], dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=_cpu_group())
+        if int(t.item()) == 0:
+            self.executor.native_step = ipc_ns
+            self.executor.pipe = ipc_pipe
+            self._ipc_verify = None
+            self._fallback_step = None
+            self.transport_reason = self.transport_reason.replace(
+                "(verification pending: first step)",
+                "(first step verified bitwise against the fallback transport)")
+        else:
+            self._use_fallback_pipe("the first step's weights differed from the fallback "
+                                    "transport's on a rank" if timeouts == 0 else
+                                    "a flag wait timed out in the first step")
+            print(f"[trainer] rank {self.mesh.rank}: {self.transport_reason}", file=sys.stderr,
+                  flush=True)
 
     # -------------------------------------------------------------------------------------
     @property
@@ -251,6 +393,8 @@ class Trainer:
             cur.wait_stream(self._stream)
             for st in self.stages:  # the captured update advanced the device step counter
                 st.params.step_count += 1
+        elif self._ipc_verify is not None:
+            self._verify_first_step()
         else:
             self.executor.run_step()
         self.steps_done += 1

@@ -199,6 +199,21 @@ def relay_parts(r0: int, r1: int, k: int) -> list[int]:
     return [r0 + (n * p // (k + 1)) // 8 * 8 for p in range(k + 1)] + [r1]
 
 
+def _cpu_group():
+    """A gloo group over the world for small host-side agreements (works whatever the default
+    backend is)."""
+    import torch.distributed as dist
+
+    global _CPU_GROUP
+    if _CPU_GROUP is None:
+        _CPU_GROUP = dist.new_group(backend="gloo") if dist.get_backend() != "gloo" \
+            else dist.group.WORLD
+    return _CPU_GROUP
+
+
+_CPU_GROUP = None
+
+
 class IpcPipe:
     """Pipeline hops as direct writes into IPC-mapped peer buffers (one stage per rank).
 
@@ -224,7 +239,7 @@ class IpcPipe:
     stripe flags. The consumer's end-of-step ack also covers the relay slots (it follows the
     relay copies it waited for). Flag block: [f[j][p], b[j][p], ack_f, ack_b, relay[d][j]]."""
 
-    def __init__(self, mesh: Mesh, stage, relays: int = 0):
+    def __init__(self, mesh: Mesh, stage, relays: int = 0, uncached: bool = True):
         import torch.distributed as dist
 
         from ..utils.native import native
@@ -238,58 +253,106 @@ class IpcPipe:
         self.nm = nm
         self.k = k = int(relays)
         me = mesh.rank
+        world = dist.get_world_size()
         assign = relay_assignment(mesh.pp, mesh.dp, k) if k else {}
         # my relay duties, in table order: (src, dst, direction, stripe index)
         self.duties = [(h[0], h[1], h[2], rl.index(me) + 1) for h, rl in assign.items()
                        if me in rl]
         self.ackf = 2 * nm * (k + 1)
         self.ackb = self.ackf + 1
-        self.flags = torch.zeros(self.ackf + 2 + len(self.duties) * nm, dtype=torch.int32,
-                                 device=stage.device)
-        # destination rows have the source's width: my output == the consumer's input, my
-        # dx_send == the producer's grad_out
-        self.row_bytes_f = stage.output.stride(0) * stage.output.element_size()
-        self.row_bytes_b = (stage.dx_send.stride(0) * stage.dx_send.element_size()
-                            if stage.dx_send is not None else 0)
-        self.part_max = max(b - a for a, b in zip(relay_parts(0, stage.mb, k),
-                                                  relay_parts(0, stage.mb, k)[1:]))
-        everyone_rb = [None] * dist.get_world_size()
+        # Every rank takes part in every collective below even when its local part failed
+        # (it sends an error marker instead), and all ranks raise together: one rank raising
+        # between two collectives would leave the others blocked in the second one.
+        err = None
+        mine = {}
+        try:
+            self.flags = torch.zeros(self.ackf + 2 + len(self.duties) * nm, dtype=torch.int32,
+                                     device=stage.device)
+            if uncached:  # the buffers peers write into (see utils/devmem.py)
+                self._uncached_recv(stage)
+            # destination rows have the source's width: my output == the consumer's input, my
+            # dx_send == the producer's grad_out
+            self.row_bytes_f = stage.output.stride(0) * stage.output.element_size()
+            self.row_bytes_b = (stage.dx_send.stride(0) * stage.dx_send.element_size()
+                                if stage.dx_send is not None else 0)
+            self.part_max = max(b - a for a, b in zip(relay_parts(0, stage.mb, k),
+                                                      relay_parts(0, stage.mb, k)[1:]))
+        except Exception as e:  # noqa: BLE001 -- agreed on below
+            err = e
+            self.row_bytes_f = self.row_bytes_b = 0
+        everyone_rb = [None] * world
         dist.all_gather_object(everyone_rb, (self.row_bytes_f, self.row_bytes_b))
         # a relay slot holds one stripe of one micro-batch of the hop's rows
         self.relay_bufs = []
-        for src, dst, d, _p in self.duties:
-            rb = everyone_rb[src][0] if d == "f" else everyone_rb[src][1]
-            self.relay_bufs.append((torch.zeros(nm * self.part_max * rb, dtype=torch.uint8,
-                                                device=stage.device), rb))
-        torch.cuda.synchronize(stage.device)
-        mine = {"x_in": self.n.ipc_export(stage.x_in.data_ptr()),
-                "grad_out": self.n.ipc_export(stage.grad_out.data_ptr()),
-                "flags": self.n.ipc_export(self.flags.data_ptr()),
-                "relay": [self.n.ipc_export(b.data_ptr()) for b, _ in self.relay_bufs]}
-        everyone = [None] * dist.get_world_size()
+        if err is None:
+            try:
+                for src, dst, d, _p in self.duties:
+                    rb = everyone_rb[src][0] if d == "f" else everyone_rb[src][1]
+                    shape = (nm * self.part_max * rb,)
+                    buf = (self._uc(shape, torch.uint8) if uncached else
+                           torch.zeros(shape, dtype=torch.uint8, device=stage.device))
+                    self.relay_bufs.append((buf, rb))
+                torch.cuda.synchronize(stage.device)
+                mine = {"x_in": self.n.ipc_export(stage.x_in.data_ptr()),
+                        "grad_out": self.n.ipc_export(stage.grad_out.data_ptr()),
+                        "flags": self.n.ipc_export(self.flags.data_ptr()),
+                        "relay": [self.n.ipc_export(b.data_ptr()) for b, _ in self.relay_bufs]}
+            except Exception as e:  # noqa: BLE001
+                err = e
+        if err is not None:
+            mine = {"error": repr(err)}
+        everyone = [None] * world
         dist.all_gather_object(everyone, mine)
+        bad = [(r, e["error"]) for r, e in enumerate(everyone) if "error" in e]
+        if bad:
+            raise RuntimeError(f"IPC transport unavailable: {bad}")
         self.seq = 0
-        self.prev = self._peer(everyone, mesh.prev_rank)
-        self.next = self._peer(everyone, mesh.next_rank)
-        imp = lambda r, key: self.n.ipc_import(*everyone[r][key])  # noqa: E731
+        try:
+            self.prev = self._peer(everyone, mesh.prev_rank)
+            self.next = self._peer(everyone, mesh.next_rank)
+            imp = lambda r, key: self.n.ipc_import(*everyone[r][key])  # noqa: E731
 
-        def duty_index(r, hop):
-            ds = [h for h, rl in assign.items() if r in rl]
-            return ds.index(hop)
+            def duty_index(r, hop):
+                ds = [h for h, rl in assign.items() if r in rl]
+                return ds.index(hop)
 
-        # my hops' relays: where stripe p >= 1 goes
-        self.relay_out = {"f": [], "b": []}
-        for d, peer in (("f", mesh.next_rank), ("b", mesh.prev_rank)):
-            if peer is None:
-                continue
-            for r in assign.get((me, peer, d), []):
-                di = duty_index(r, (me, peer, d))
-                self.relay_out[d].append({
-                    "buf": self.n.ipc_import(*everyone[r]["relay"][di]),
-                    "flags": imp(r, "flags"), "d": di})
-        # my duties' consumers: where my relay slots go
-        self.relay_dst = [{"buf": imp(dst, "x_in" if d == "f" else "grad_out"),
-                           "flags": imp(dst, "flags")} for _s, dst, d, _p in self.duties]
+            # my hops' relays: where stripe p >= 1 goes
+            self.relay_out = {"f": [], "b": []}
+            for d, peer in (("f", mesh.next_rank), ("b", mesh.prev_rank)):
+                if peer is None:
+                    continue
+                for r in assign.get((me, peer, d), []):
+                    di = duty_index(r, (me, peer, d))
+                    self.relay_out[d].append({
+                        "buf": self.n.ipc_import(*everyone[r]["relay"][di]),
+                        "flags": imp(r, "flags"), "d": di})
+            # my duties' consumers: where my relay slots go
+            self.relay_dst = [{"buf": imp(dst, "x_in" if d == "f" else "grad_out"),
+                               "flags": imp(dst, "flags")} for _s, dst, d, _p in self.duties]
+        except Exception as e:  # noqa: BLE001
+            err = e
+        failed = torch.tensor([1 if err is not None else 0], dtype=torch.int32)
+        dist.all_reduce(failed, op=dist.ReduceOp.MAX, group=_cpu_group())
+        if int(failed.item()):
+            raise RuntimeError(f"IPC transport unavailable (peer mapping failed on a rank; "
+                               f"here: {err!r})")
+
+    def _uc(self, shape, dtype):
+        from ..utils.devmem import uncached_zeros
+
+        return uncached_zeros(shape, dtype, self.stage.device)
+
+    def _uncached_recv(self, st) -> None:
+        """Re-home this stage's receive buffers (x_in of a non-first stage, grad_out = dz[-1] of
+        a non-last stage) in L2-uncached memory. Before any launch is recorded (the recorded
+        programs then bind the new addresses)."""
+        if st._prog is not None:
+            raise RuntimeError("receive buffers must be re-homed before compile_native")
+        if self.mesh.prev_rank is not None:
+            st.x_buf = self._uc(tuple(st.x_buf.shape), st.x_buf.dtype)
+            st.x_in = st.x_buf
+        if self.mesh.next_rank is not None:
+            st.dz[-1] = self._uc(tuple(st.dz[-1].shape), st.dz[-1].dtype)
 
     def fidx(self, j: int, p: int = 0) -> int:
         return j * (self.k + 1) + p

@@ -67,9 +67,16 @@ SWITCHES: dict[str, tuple[str, str]] = {
                       "kernel) | auto (streams when GPU_MAX_HW_QUEUES >= 6)"),
     "DNN_FIRST_STEP_TIMEOUT": ("60", "bench.py: seconds the first multi-rank step may take "
                                "before the plan trace is printed and the run exits"),
-    "DNN_PIPE": ("rccl", "pipeline transport: rccl | ipc (xGMI peer copies + stream flags)"),
-    "DNN_IPC_RELAYS": ("0", "ipc transport: stripe every hop over the direct link + this many "
-                            "relay ranks (two-link paths; native step only)"),
+    "DNN_PIPE": ("auto", "pipeline transport: auto (IPC with relays on RCCL jobs when every "
+                         "GPU maps its peers, first step verified against RCCL) | rccl | ipc "
+                         "(xGMI peer copies + stream flags)"),
+    "DNN_IPC_RELAYS": ("auto", "ipc transport: stripe every hop over the direct link + this "
+                               "many relay ranks (two-link paths; native step only); auto = "
+                               "min(2, world - 2)"),
+    "DNN_IPC_VERIFY": ("auto", "verify the first IPC step bitwise against the fallback "
+                               "transport: auto (with DNN_PIPE=auto) | 1 | 0"),
+    "DNN_FAULT_IPC_VERIFY": ("", "ranks whose IPC verification step is corrupted (tests the "
+                                 "fallback)"),
     "DNN_SERVE_REPLAY": ("graph", "serving engine replay: graph | native | eager"),
     "DNN_SYNC_DEBUG": ("0", "synchronise + check after every kernel (race / fault hunting)"),
     "DNN_AUTOBUILD": ("1", "build the native extension on import if it is missing"),

@@ -462,3 +462,61 @@ def test_rccl_plan_interpreted_bitwise_equals_python(dev, pp, world, mode, bound
                 assert np.array_equal(a, b), (wb, k)
         assert np.array_equal(np.load(os.path.join(d, "py_loss.npy")),
                               np.load(os.path.join(d, "plan_loss.npy")))
+
+
+def _verify_worker(rank, world, port, pipe, fault, relays, steps, out_dir, tag):
+    # one GPU, `world` processes: IPC hops between processes sharing cuda:0, gloo collectives;
+    # the first IPC step is verified against the message transport (Python executor over gloo)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DNN_PIPE=pipe,
+                      DNN_IPC_VERIFY="1", DNN_FAULT_IPC_VERIFY=fault,
+                      DNN_IPC_RELAYS=str(relays), GPU_MAX_HW_QUEUES="8")
+    import torch.distributed as dist
+
+    from docker_dist_nn_amd import MLPSpec
+    from docker_dist_nn_amd.engine import OptimConfig, Trainer
+    from docker_dist_nn_amd.parallel.groups import build_mesh
+
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mesh = build_mesh(world, 1)
+    tr = Trainer(MLPSpec.parse(SPEC), micro_batch=256, num_micro=4, mesh=mesh, device=dev,
+                 schedule="1f1b", optim=OptimConfig(name="sgd", lr=0.05, momentum=0.9))
+    xt, yt = _batch(1024)
+    for _ in range(steps):
+        tr.set_batch(xt.to(dev) if tr.first else None, yt.to(dev) if tr.last else None)
+        tr.step()
+    torch.cuda.synchronize()
+    for k, (w, _b) in tr.local_weights().items():
+        np.save(os.path.join(out_dir, f"{tag}_w{k}.npy"), w)
+    with open(os.path.join(out_dir, f"{tag}_transport_r{rank}.txt"), "w") as f:
+        f.write(f"{tr.transport}\n{tr.transport_reason}\n")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,relays", [(2, 0), (4, 2)])
+def test_ipc_first_step_verification_and_fallback(dev, world, relays):
+    """The verified IPC transport (engine/trainer.py _verify_first_step): the first step runs
+    on the IPC plan and, from the same state, on the fallback transport; with agreeing weights
+    the job stays on IPC, with a corrupted IPC result on ONE rank every rank falls back. Either
+    way training equals a message-transport-only run bit for bit, and every rank records the
+    same transport and reason."""
+    steps = 3
+    with tempfile.TemporaryDirectory() as d:
+        for tag, pipe, fault in (("ref", "rccl", ""), ("ok", "ipc", ""),
+                                 ("fault", "ipc", "1")):
+            mp.start_processes(_verify_worker,
+                               args=(world, _free_port(), pipe, fault, relays, steps, d, tag),
+                               nprocs=world, join=True, start_method="spawn")
+        for k in range(4):
+            ref = np.load(os.path.join(d, f"ref_w{k}.npy"))
+            for tag in ("ok", "fault"):
+                assert np.array_equal(ref, np.load(os.path.join(d, f"{tag}_w{k}.npy"))), (tag, k)
+        for tag, want in (("ok", "ipc"), ("fault", "gloo")):
+            got = {open(os.path.join(d, f"{tag}_transport_r{r}.txt")).read()
+                   for r in range(world)}
+            assert len(got) == 1, got
+            transport, reason = got.pop().split("\n")[:2]
+            assert transport == want, (tag, transport, reason)
+            assert ("verified" in reason) if tag == "ok" else ("differed" in reason), reason
