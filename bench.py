@@ -80,9 +80,11 @@ def parse_args(argv=None):
     ap.add_argument("--micro", type=int, default=0, help="micro-batch rows (0 = planner)")
     ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--optimizer", default="sgd", choices=["sgd", "adam", "adamw"])
-    ap.add_argument("--graph", action="store_true",
-                    help="replay the step as a HIP graph (1 GPU, or N > 1 with the native step); "
-                         "eager is as fast at large batch")
+    ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
+                    help="replay the step as a HIP graph (1 GPU, or N > 1 with the native step). "
+                         "auto: N > 1 on the IPC transport, kept only if its timed steps beat "
+                         "eager ones (the host enqueue of a rank's plan is ~3 us per op eager, "
+                         "~0.4 us per node replayed: profiles/r3_host); eager otherwise")
     ap.add_argument("--graph-copies", type=int, default=2,
                     help="alternate between this many instantiations of the step graph")
     ap.add_argument("--boundary", default="bf16", choices=["bf16", "fp8"],
@@ -179,7 +181,7 @@ def measure(a, spec, n, world, dev, text):
 
     # --graph: the step as a HIP graph (one GPU, or a native multi-rank step: opt-in, the
     # plan's flag waits are kernels so the whole rank step -- hops included -- is captured)
-    use_graph = a.graph and (world == 1 or tr.native_step is not None)
+    use_graph = a.graph == "on" and (world == 1 or tr.native_step is not None)
     step_i = 0
 
     def one_step():
@@ -191,22 +193,49 @@ def measure(a, spec, n, world, dev, text):
 
     if world > 1:  # the first multi-rank step is bounded: a hang prints the plan and exits
         first_step_guard(tr, one_step, dev, float(switches.get("DNN_FIRST_STEP_TIMEOUT")))
-    if use_graph:
-        xb, yb = data.batch(0)
-        tr.set_batch(xb if tr.first else None, yb if tr.last else None)
-        tr.capture(copies=a.graph_copies)
-    for _ in range(a.warmup):
-        one_step()
-
     def barrier():
         if world > 1:
             torch.distributed.barrier()
         torch.cuda.synchronize(dev)
 
+    def timed(k):  # seconds for k steps, max over ranks (every rank gets the same value)
+        barrier()
+        t = time.perf_counter()
+        for _ in range(k):
+            one_step()
+        barrier()
+        t = torch.tensor([time.perf_counter() - t], device=dev, dtype=torch.float64)
+        if world > 1:
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        return float(t.item())
+
+    graph_trial = None
+    if use_graph:
+        xb, yb = data.batch(0)
+        tr.set_batch(xb if tr.first else None, yb if tr.last else None)
+        tr.capture(copies=a.graph_copies)
+    elif a.graph == "auto" and world > 1 and tr.transport == "ipc" and \
+            tr.native_step is not None:
+        # the relayed IPC plan is hundreds of ops per rank: replayed as a graph when that
+        # measures faster (RCCL plans stay eager: capturing RCCL calls is not validated here)
+        eager_s = timed(3)
+        xb, yb = data.batch(0)
+        tr.set_batch(xb if tr.first else None, yb if tr.last else None)
+        tr.capture(copies=a.graph_copies)
+        graph_s = timed(3)
+        use_graph = graph_s < 0.98 * eager_s
+        graph_trial = {"eager_ms": round(eager_s / 3 * 1e3, 4),
+                       "graph_ms": round(graph_s / 3 * 1e3, 4), "kept": use_graph}
+        if not use_graph:
+            tr.release_graph()
+    for _ in range(a.warmup):
+        one_step()
+
     barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         one_step()
+    host_s = time.perf_counter() - t0  # enqueue time of the K steps (no sync inside)
     tr.flush()  # the last step's deferred DP update belongs to the timed region
     barrier()
     elapsed = time.perf_counter() - t0
@@ -233,6 +262,7 @@ def measure(a, spec, n, world, dev, text):
         "native_fallback": tr.native_fallback,
         "boundary": tr.boundary, "dp_reduce": tr.dp_reduce if plan.dp > 1 else None,
         "hip_graph": use_graph, "graph_copies": a.graph_copies if use_graph else 0,
+        "graph_trial": graph_trial, "host_ms_per_step": round(host_s / a.steps * 1e3, 4),
         "loss": loss, "planner_predicted": round(plan.samples_per_s, 1),
     }
     del tr, data
@@ -337,6 +367,8 @@ def main(argv=None):
         "model_tflops": round(spec.flops_per_sample_train() * m["value"] / 1e12, 1),
         "last_loss": None if m["loss"] is None else round(m["loss"], 5),
         "planner_predicted": m["planner_predicted"],
+        "host_ms_per_step": m.get("host_ms_per_step"),
+        "graph_trial": m.get("graph_trial"),
         "dp_only": dp_only,
         "native_fallback": m["native_fallback"],  # why the Python executor ran, if it did
         "switches": switches.active(),  # non-default DNN_* switches of this run
