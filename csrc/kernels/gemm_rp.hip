@@ -48,8 +48,8 @@ int gemm_rp_launch(const GemmParams& q, int la, int lb, int out_f32, int bm, int
   if (!f) return -12;
   const int tiles_n = (q.N + bn - 1) / bn, tiles_m = (q.M + bm - 1) / bm;
   const int nwg = tiles_n * tiles_m * splits;
-  hipLaunchKernelGGL(f, dim3(nwg), dim3(gemm_tile_threads(bm, bn)), 0, stream, q, tiles_n,
-                     tiles_m, nwg);
+  const int nt = gemm_tile_threads(bm, bn);
+  hipLaunchKernelGGL(f, dim3(nwg), dim3(nt), 0, stream, q, tiles_n, tiles_m, nwg);
   return hipGetLastError() == hipSuccess ? 0 : -9;
 }
 
