@@ -68,6 +68,7 @@ def case_wgrad(R, M, N, splits, variants):
 
 
 T256, T128, T12864 = (256, 256), (128, 128), (128, 64)
+TS = [(T256, 9), ((256, 128), 9), ((256, 128), 11), (T128, 9), (T128, 11), (T12864, 9)]
 BIG = [(T256, 2), (T256, 9), (T256, 11)]
 WG = [(T128, 2), (T128, 9), (T128, 11)]
 CASES = {
@@ -82,6 +83,10 @@ CASES = {
     "m8d": lambda: case_dgrad(65536, 1024, 1024, BIG),
     "m8w": lambda: case_wgrad(65536, 1024, 1024, 8, [(T128, 9), (T128, 11)]),
     "wide": lambda: case_fwd(16384, 8192, 8192, [(T256, 2), (T256, 9), (T256, 11)]),
+    # tile sweep of the register-direct form on the headline's thin GEMMs
+    "f0t": lambda: case_fwd(65536, 832, 512, TS),
+    "f1t": lambda: case_fwd(65536, 512, 256, TS),
+    "d1t": lambda: case_dgrad(65536, 256, 512, TS),
 }
 
 
