@@ -148,6 +148,7 @@ class PipelineExecutor:
         # concurrent wgrad streams in native single-process plans (DNN_WGRAD_STREAMS)
         self.wgrad_streams = int(switches.get("DNN_WGRAD_STREAMS"))
         self._side = None
+        self._main_hp = None  # DNN_MAIN_PRIORITY=1: the overlap plan's main stream
         # deferred data-parallel update (DNN_DP_DEFER=0 disables): see dp_split
         self.defer = (grad_sync is not None and grad_sync.world > 1 and
                       not grad_sync.shard and switches.get("DNN_DP_DEFER") != "0")
@@ -537,10 +538,22 @@ class PipelineExecutor:
                 # its workgroups are dispatched ahead of the main stream's pending ones
                 self._side = torch.cuda.Stream(
                     dev, priority=-1 if switches.get("DNN_SIDE_PRIORITY") == "1" else 0)
+            cur = torch.cuda.current_stream(dev)
+            main = cur
+            if self._side is not None and switches.get("DNN_MAIN_PRIORITY") == "1":
+                # the critical path (forward, dgrads, the first layer's wgrad) on a
+                # high-priority stream: when its kernels and the side stream's wgrads are both
+                # pending, its workgroups are dispatched first and the wgrads fill in
+                if self._main_hp is None:
+                    self._main_hp = torch.cuda.Stream(dev, priority=-1)
+                main = self._main_hp
+                main.wait_stream(cur)
             native().run_plan([(st._prog if st is not None else None, seg, si)
                                for st, seg, si in plan],
-                              torch.cuda.current_stream(dev).cuda_stream,
+                              main.cuda_stream,
                               self._side.cuda_stream if self._side is not None else 0)
+            if main is not cur:
+                cur.wait_stream(main)
             for st in self.stages:
                 st.params.step_count += 1
             self.pipe.end_step()

@@ -54,6 +54,8 @@ SWITCHES: dict[str, tuple[str, str]] = {
     "DNN_FWD_TAIL": ("0", "fuse the forward of the layer before the classifier tail into the "
                           "tail launch (mlp_fwd_tail_kernel; ReLU, 256-wide, 256-row tiles); "
                           "headline 0.375 vs 0.372 ms (71 us = the two kernels' sum), opt-in"),
+    "DNN_MAIN_PRIORITY": ("0", "overlap plans: run the main (critical-path) stream at high "
+                               "priority so side-stream wgrads only fill in"),
     "DNN_SIDE_PRIORITY": ("0", "overlap plans: create the side stream at high priority "
                                "(measured no effect: 0.374 vs 0.373 ms)"),
     "DNN_FORK_ELIDE": ("0", "overlap plans: drop a side-stream fork when the main stream "
