@@ -36,6 +36,13 @@
 #include "gemm_tile.hpp"
 #include "mlp_tail.hpp"
 
+// Probe builds only (bench/probes/tail_probe.py compiles this file into a separate library with
+// -DDNN_TAIL_PROBE=bits to time the kernel with parts removed; results are then wrong): 1 = no
+// bias-gradient column sums, 2 = no global stores of H3 / DZ4 / DZ3 / DZ2, 4 = no softmax.
+#ifndef DNN_TAIL_PROBE
+#define DNN_TAIL_PROBE 0
+#endif
+
 namespace dnn {
 namespace tail {
 
@@ -73,6 +80,7 @@ __device__ __forceinline__ void st8(char LDS_AS* p, uint2 v) {
 // 0 / 1 / 2 / 3 holds columns 0..7 of j / 0..7 of j+1 / 8..15 of j / 8..15 of j+1 (the
 // register-direct epilogue of gemm_tile.hpp). `row` points at column 0 of the output row.
 __device__ __forceinline__ void st16_pair(u16* row, int j, int q, uint2 a, uint2 b) {
+  if constexpr (DNN_TAIL_PROBE & 2) return;
   const auto s0 = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
   const auto s1 = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
   *(uint4*)(row + 16 * j + 16 * (q & 1) + 8 * (q >> 1)) =
@@ -83,6 +91,7 @@ __device__ __forceinline__ void st16_pair(u16* row, int j, int q, uint2 a, uint2
 // (the four butterflies run step-major so consecutive DPP adds are independent: a DPP read of a
 // VGPR written by the previous VALU instruction costs wait states)
 __device__ __forceinline__ void acc4(float LDS_AS* rw, uint2 v) {
+  if constexpr (DNN_TAIL_PROBE & 1) return;
   float x[4] = {lo_bf(v.x), hi_bf(v.x), lo_bf(v.y), hi_bf(v.y)};
 #pragma unroll
   for (int e = 0; e < 4; ++e) x[e] += dpp_f<0xB1>(x[e]);
@@ -224,41 +233,46 @@ __device__ __forceinline__ void tail_body(const TailParams& p, char LDS_AS* lds,
     float lv[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) lv[e] = a4[e] + b4r[e];
-    float vals[tail::MAX_CLS];
-#pragma unroll
-    for (int c = 0; c < tail::MAX_CLS; ++c) vals[c] = __shfl(lv[c & 3], i16 + 16 * (c >> 2), 64);
-    float mx = -INFINITY;
-    int amax = 0;
-#pragma unroll
-    for (int c = 0; c < tail::MAX_CLS; ++c)
-      if (c < nc && vals[c] > mx) {
-        mx = vals[c];
-        amax = c;
-      }
-    float se = 0.f;
-#pragma unroll
-    for (int c = 0; c < tail::MAX_CLS; ++c)
-      if (c < nc) se += __expf(vals[c] - mx);
-    const float inv = 1.f / se;
     float dz[4] = {0.f, 0.f, 0.f, 0.f};
-    if (label >= 0) {
-      float vl = 0.f;
+    if constexpr (DNN_TAIL_PROBE & 4) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dz[e] = lv[e] * p.scale;
+    } else {
+      float vals[tail::MAX_CLS];
+#pragma unroll
+      for (int c = 0; c < tail::MAX_CLS; ++c) vals[c] = __shfl(lv[c & 3], i16 + 16 * (c >> 2), 64);
+      float mx = -INFINITY;
+      int amax = 0;
 #pragma unroll
       for (int c = 0; c < tail::MAX_CLS; ++c)
-        if (c == label) vl = vals[c];
-      if (q == 0) {
-        loss_a += -(vl - mx - __logf(se));
-        corr_a += amax == label;
-      }
+        if (c < nc && vals[c] > mx) {
+          mx = vals[c];
+          amax = c;
+        }
+      float se = 0.f;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int c = 4 * q + e;
-        if (c < nc) dz[e] = (__expf(lv[e] - mx) * inv - (c == label ? 1.f : 0.f)) * p.scale;
+      for (int c = 0; c < tail::MAX_CLS; ++c)
+        if (c < nc) se += __expf(vals[c] - mx);
+      const float inv = 1.f / se;
+      if (label >= 0) {
+        float vl = 0.f;
+#pragma unroll
+        for (int c = 0; c < tail::MAX_CLS; ++c)
+          if (c == label) vl = vals[c];
+        if (q == 0) {
+          loss_a += -(vl - mx - __logf(se));
+          corr_a += amax == label;
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = 4 * q + e;
+          if (c < nc) dz[e] = (__expf(lv[e] - mx) * inv - (c == label ? 1.f : 0.f)) * p.scale;
+        }
       }
     }
     const uint2 d4 = make_uint2(pack_bf16x2(dz[0], dz[1]), pack_bf16x2(dz[2], dz[3]));
     tail::st16_pair(p.DZ4 + row * p.lddz4, 0, q, d4, make_uint2(0u, 0u));  // columns 0..31
-    for (int c = 2 * tail::MAX_CLS + 8 * q; c < p.N4; c += 32)
+    for (int c = 2 * tail::MAX_CLS + 8 * q; c < p.N4 && !(DNN_TAIL_PROBE & 2); c += 32)
       *(uint4*)(p.DZ4 + row * p.lddz4 + c) = make_uint4(0u, 0u, 0u, 0u);
     tail::acc4(rw + K3 + N3 + 4 * q, d4);
 
