@@ -46,34 +46,32 @@
 namespace dnn {
 namespace tail {
 
-// Waves per workgroup: 8 (two per SIMD, <= 256 registers each) for the branch-free ReLU form;
-// the generic-activation form needs more registers and runs 4 (one per SIMD, <= 512).
+// Waves per workgroup of the standalone launch: 16 (four per SIMD, <= 128 registers each) for
+// the branch-free ReLU form, so one 16-row block per wave covers 65536 rows in one round and
+// four independent block chains share each SIMD; the generic-activation form needs more
+// registers and runs 4 (one per SIMD). The fused forward + tail launch (mlp_fwd_tail_kernel)
+// runs the body with the 8 waves of its 256x256 GEMM tile.
 template <bool RELU>
-constexpr int waves() { return RELU ? 8 : 4; }
-constexpr int BLOCK_ROWS = 128;  // rows per workgroup iteration that size the grid (8 x 16)
+constexpr int waves() { return RELU ? 16 : 4; }
 constexpr int MAX_CLS = 16;  // classes held by one 16-wide MFMA block
 constexpr int W4_ROWS = 64;  // staged rows of W4 (the dgrad's contraction uses rows 0..31)
 
+// LDS: the two weight images, b3, and one column-sum row per wave. No per-wave scratch: an
+// output that feeds the next product is regrouped into that MFMA's B fragment in registers
+// (frag_from_out), not written to LDS and read back.
 template <int K3, int N3, int NW>
 struct Geo {
   static constexpr int W3_BYTES = N3 * K3 * 2;
   static constexpr int W4_BYTES = W4_ROWS * N3 * 2;
-  static constexpr int SP = (N3 + 8) * 2;  // scratch row pitch (bytes): h3, then dz3
-  static constexpr int S_BYTES = 16 * SP;
-  static constexpr int DP = 80;  // dz4 scratch row pitch: 32 bf16 + 16 B
-  static constexpr int WAVE_BYTES = S_BYTES + 16 * DP;
+  static constexpr int B3_BYTES = N3 * 4;
   static constexpr int RC = K3 + N3 + MAX_CLS + 4;  // per-wave reduction row (floats, 16-B rows)
-  static constexpr int SMEM = W3_BYTES + W4_BYTES + NW * WAVE_BYTES + NW * RC * 4;
+  static constexpr int SMEM = W3_BYTES + W4_BYTES + B3_BYTES + NW * RC * 4;
   static_assert(SMEM <= 160 * 1024, "LDS budget");
   static_assert(K3 / 16 <= 16 && N3 / 16 <= 16, "column-sum lanes");
 };
 
 __device__ __forceinline__ float lo_bf(unsigned x) { return __uint_as_float(x << 16); }
 __device__ __forceinline__ float hi_bf(unsigned x) { return __uint_as_float(x & 0xffff0000u); }
-// 8-byte LDS store / load of a packed bf16 quad (HIP's uint2 has no address-space-3 operators)
-__device__ __forceinline__ void st8(char LDS_AS* p, uint2 v) {
-  *(unsigned long long LDS_AS*)p = ((unsigned long long)v.y << 32) | v.x;
-}
 
 // Global store of two 16-column blocks (j, j + 1) of one row as 16-byte chunks: the lanes of
 // group q hold columns 4 q .. 4 q + 3 of each block; v_permlane16_swap regroups them so group
@@ -85,6 +83,20 @@ __device__ __forceinline__ void st16_pair(u16* row, int j, int q, uint2 a, uint2
   const auto s1 = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
   *(uint4*)(row + 16 * j + 16 * (q & 1) + 8 * (q >> 1)) =
       make_uint4(s0[0], s1[0], s0[1], s1[1]);
+}
+
+// Two output blocks of a 16-row block (a: columns 32 s .. 32 s + 15, b: 32 s + 16 .. 32 s + 31;
+// lane (i, g) holds row i, 4 columns from 4 g) -> the MFMA B fragment of contraction step s
+// (lane (i, g): row i, columns 32 s + 8 g .. 32 s + 8 g + 7). Writing a_g / b_g for the value
+// lane group g holds, a 32-lane swap gives {a0 a1 b0 b1 | a2 a3 b2 b3} and a 16-lane swap of
+// those {a0 a2 b0 b2 | a1 a3 b1 b3}: group g then holds the first and second 4 of its 8
+// columns. Same bf16 values as the LDS write + transposing read it replaces.
+__device__ __forceinline__ bf16x8_t frag_from_out(uint2 a, uint2 b) {
+  const auto x = __builtin_amdgcn_permlane32_swap(a.x, b.x, false, false);
+  const auto y = __builtin_amdgcn_permlane32_swap(a.y, b.y, false, false);
+  const auto xs = __builtin_amdgcn_permlane16_swap(x[0], x[1], false, false);
+  const auto ys = __builtin_amdgcn_permlane16_swap(y[0], y[1], false, false);
+  return __builtin_bit_cast(bf16x8_t, make_uint4(xs[0], ys[0], xs[1], ys[1]));
 }
 
 // rw[0..3] += column sums over the 16 rows (lanes of a DPP row) of the 4 bf16 values in v
@@ -128,52 +140,56 @@ __device__ __forceinline__ bf16x8_t row_frag(const char LDS_AS* img, int blk, in
   return *(const bf16x8_t LDS_AS*)(img + r * (T * 2) + ((c ^ mn_swz<T>(r)) << 4));
 }
 
+// 64 rows [r0, r0 + 64) of a [rows][T] bf16 matrix -> the MNMAJ image layout of gemm_tile.hpp
+// (stage_tile<MNMAJ>), by LDS-DMA in 1-KiB pieces dealt round-robin to the NW waves (any NW:
+// T / 8 pieces need not divide evenly).
+template <int T, int NW>
+__device__ __forceinline__ void stage_rows64(const u16* __restrict__ g, long ld, int r0,
+                                             char LDS_AS* dst, int wave, int lane) {
+  constexpr int CPR = T / 8, PIECES = T / 8;  // 16-B chunks per row; 64 rows x 2T B / 1 KiB
+  for (int piece = wave; piece < PIECES; piece += NW) {  // uniform per wave
+    const int chunk = piece * 64 + lane;
+    const int r = chunk / CPR, ph = chunk % CPR;
+    const u16* src = g + (long)(r0 + r) * ld + (ph ^ mn_swz<T>(r)) * 8;
+    __builtin_amdgcn_global_load_lds((const void*)src, (void LDS_AS*)(dst + piece * 1024), 16, 0,
+                                     0);
+  }
+}
+
 }  // namespace tail
 
-// The whole tail for the 16-row blocks rb = rb_first + wave, + rb_step, ... < rb_end of this
-// workgroup; its bias-gradient / loss partials go to row `wg` of the partial buffers.
-template <int K3, int N3, bool RELU>
+// The whole tail for the 16-row blocks rb = rb_first + wave * wave_stride, + rb_step, ... <
+// rb_end of this workgroup (NW waves); its bias-gradient / loss partials go to row `wg` of the
+// partial buffers.
+template <int K3, int N3, int NW, bool RELU>
 __device__ __forceinline__ void tail_body(const TailParams& p, char LDS_AS* lds, int rb_first,
-                                          int rb_step, int rb_end, long wg) {
+                                          int wave_stride, int rb_step, int rb_end, long wg) {
   using tail::act;
   using tail::dact;
-  constexpr int NW = tail::waves<RELU>();
+  using tail::frag_from_out;
   using G = tail::Geo<K3, N3, NW>;
   using tail::hi_bf;
   using tail::lo_bf;
   constexpr int NK = K3 / 32, NJ = N3 / 16, NS3 = N3 / 32, NKK = K3 / 16;
   char LDS_AS* w3 = lds;
   char LDS_AS* w4 = lds + G::W3_BYTES;
+  float LDS_AS* b3s = (float LDS_AS*)(w4 + G::W4_BYTES);
+  float LDS_AS* red = b3s + N3;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  char LDS_AS* S = w4 + G::W4_BYTES + wave * G::WAVE_BYTES;
-  char LDS_AS* D = S + G::S_BYTES;
-  float LDS_AS* red = (float LDS_AS*)(w4 + G::W4_BYTES + NW * G::WAVE_BYTES);
 
-  // ---- weights -> LDS (64-row pieces of the MNMAJ image, LDS-DMA) --------------------------
+  // ---- weights -> LDS (64-row pieces of the MNMAJ image, LDS-DMA); b3 -> LDS ---------------
 #pragma unroll
   for (int r0 = 0; r0 < N3; r0 += 64)
-    stage_tile<MNMAJ, K3, NW>(p.W3, p.ldw3, 0, r0, w3 + r0 * K3 * 2, wave, lane, K3);
-  stage_tile<MNMAJ, N3, NW>(p.W4, p.ldw4, 0, 0, w4, wave, lane, N3);
+    tail::stage_rows64<K3, NW>(p.W3, p.ldw3, r0, w3 + r0 * K3 * 2, wave, lane);
+  tail::stage_rows64<N3, NW>(p.W4, p.ldw4, 0, w4, wave, lane);
+  for (int c = threadIdx.x; c < N3; c += NW * 64) b3s[c] = p.b3[c];
 
   const int i16 = lane & 15, q = lane >> 4;
   const int nrb = rb_end;
   const int nw = rb_step;
-  int rb = rb_first + wave;
+  int rb = rb_first + wave * wave_stride;
 
-  bf16x8_t xb[NK];
-  if (rb < nrb) {
-    const u16* src = p.X + (long)(rb * 16 + i16) * p.ldx + 8 * q;
-#pragma unroll
-    for (int s = 0; s < NK; ++s) xb[s] = *(const bf16x8_t*)(src + 32 * s);
-  }
-  __syncthreads();  // weights landed (the fence waits for the LDS-DMA loads too)
-
-  // biases in registers for the whole launch: a load inside the loop would queue behind the
-  // block's stores and the next block's prefetch (vmcnt counts in issue order) and stall on all
-  f32x4_t b3r[NJ];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) b3r[j] = *(const f32x4_t*)(p.b3 + 16 * j + 4 * q);
   float b4r[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) b4r[e] = p.b4[4 * q + e];
@@ -186,50 +202,51 @@ __device__ __forceinline__ void tail_body(const TailParams& p, char LDS_AS* lds,
   float loss_a = 0.f;
   int corr_a = 0;
   const int nc = p.n_cls;
+  __syncthreads();  // weights and b3 landed (the fence waits for the LDS-DMA loads too)
 
   for (; rb < nrb; rb += nw) {
+    // The lane index is laundered through an empty asm per block, so the dozens of fragment
+    // and store addresses derived from it are recomputed in the body instead of hoisted out of
+    // the block loop (live across it, they spill a 128-register wave; most waves run the body
+    // once anyway).
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int i16 = ln & 15, q = ln >> 4;
     const long row = (long)rb * 16 + i16;
-    // activation of layer L-3 at this lane's dz2 positions, and the label
-    uint2 hv[NKK];
-#pragma unroll
-    for (int kk = 0; kk < NKK; ++kk) hv[kk] = *(const uint2*)(p.X + row * p.ldx + 16 * kk + 4 * q);
     const int label = p.labels[row];
+    // this block's rows as the forward's B fragments (one block per wave at the headline size:
+    // a prefetch of the next block would only hold 32 registers through the whole body)
+    bf16x8_t xb[NK];
+#pragma unroll
+    for (int s = 0; s < NK; ++s) xb[s] = *(const bf16x8_t*)(p.X + row * p.ldx + 8 * q + 32 * s);
 
     // ---- h3 = act3(X . W3^T + b3) -------------------------------------------------------
-    f32x4_t a3[NJ];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      a3[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s = 0; s < NK; ++s)
-        a3[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tail::row_frag<K3>(w3, j, s, lane), xb[s],
-                                                        a3[j], 0, 0, 0);
-    }
-    if (rb + nw < nrb) {  // next block's rows (xb is dead once the MFMAs above have read it)
-      const u16* src = p.X + (long)((rb + nw) * 16 + i16) * p.ldx + 8 * q;
-#pragma unroll
-      for (int s = 0; s < NK; ++s) xb[s] = *(const bf16x8_t*)(src + 32 * s);
-    }
+    // (one output block at a time, fenced: with all 8 in flight the scheduler hoists their 64
+    // weight-fragment reads and a 128-register wave spills)
     uint2 h3p[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const int col = 16 * j + 4 * q;
+      f32x4_t a3 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < NK; ++s)
+        a3 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tail::row_frag<K3>(w3, j, s, ln), xb[s], a3,
+                                                     0, 0, 0);
+      const f32x4_t b3 = *(const f32x4_t LDS_AS*)(b3s + 16 * j + 4 * q);
       float v[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = act<RELU>(a3[j][e] + b3r[j][e], p.act3);
+      for (int e = 0; e < 4; ++e) v[e] = act<RELU>(a3[e] + b3[e], p.act3);
       h3p[j] = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-      tail::st8(S + i16 * G::SP + col * 2, h3p[j]);
       if (j & 1) tail::st16_pair(p.H3 + row * p.ldh3, j - 1, q, h3p[j - 1], h3p[j]);
+      __builtin_amdgcn_sched_barrier(0);
     }
 
     // ---- logits (classes 0..15) = h3 . W4^T + b4; softmax cross-entropy ------------------
     f32x4_t a4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < NS3; ++s) {
-      const bf16x8_t hb = *(const bf16x8_t LDS_AS*)(S + i16 * G::SP + (32 * s + 8 * q) * 2);
-      a4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tail::row_frag<N3>(w4, 0, s, lane), hb, a4, 0,
-                                                   0, 0);
-    }
+    for (int s = 0; s < NS3; ++s)
+      a4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tail::row_frag<N3>(w4, 0, s, ln),
+                                                   frag_from_out(h3p[2 * s], h3p[2 * s + 1]), a4,
+                                                   0, 0, 0);
     float lv[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) lv[e] = a4[e] + b4r[e];
@@ -277,39 +294,39 @@ __device__ __forceinline__ void tail_body(const TailParams& p, char LDS_AS* lds,
     tail::acc4(rw + K3 + N3 + 4 * q, d4);
 
     // ---- dz3 = (dz4 . W4) * act3'(h3): contraction over classes 0..31 -------------------
-    tail::st8(D + i16 * G::DP + 8 * q, d4);
-    tail::st8(D + i16 * G::DP + 32 + 8 * q, make_uint2(0u, 0u));
-    const bf16x8_t df = *(const bf16x8_t LDS_AS*)(D + i16 * G::DP + 16 * q);
-    uint2 prev = make_uint2(0u, 0u);
+    const bf16x8_t df = frag_from_out(d4, make_uint2(0u, 0u));
+    uint2 o3[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const f32x4_t a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-          load_frag<MNMAJ, N3>(w4, j, 0, lane), df, f32x4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          load_frag<MNMAJ, N3>(w4, j, 0, ln), df, f32x4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
       const float y[4] = {lo_bf(h3p[j].x), hi_bf(h3p[j].x), lo_bf(h3p[j].y), hi_bf(h3p[j].y)};
       float v[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = dact<RELU>(a[e], y[e], p.act3);
-      const uint2 o = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-      const int col = 16 * j + 4 * q;
-      if (j & 1) tail::st16_pair(p.DZ3 + row * p.lddz3, j - 1, q, prev, o);
-      prev = o;
-      tail::st8(S + i16 * G::SP + col * 2, o);
-      tail::acc4(rw + K3 + col, o);
+      o3[j] = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+      if (j & 1) tail::st16_pair(p.DZ3 + row * p.lddz3, j - 1, q, o3[j - 1], o3[j]);
+      tail::acc4(rw + K3 + 16 * j + 4 * q, o3[j]);
+      if (j & 1) __builtin_amdgcn_sched_barrier(0);
     }
 
     // ---- dz2 = (dz3 . W3) * act2'(X) ------------------------------------------------------
     bf16x8_t d3f[NS3];
 #pragma unroll
-    for (int s = 0; s < NS3; ++s)
-      d3f[s] = *(const bf16x8_t LDS_AS*)(S + i16 * G::SP + (32 * s + 8 * q) * 2);
+    for (int s = 0; s < NS3; ++s) d3f[s] = frag_from_out(o3[2 * s], o3[2 * s + 1]);
+    uint2 prev = make_uint2(0u, 0u);
 #pragma unroll
     for (int kk = 0; kk < NKK; ++kk) {
       f32x4_t a = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < NS3; ++s)
-        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(load_frag<MNMAJ, K3>(w3, kk, s, lane), d3f[s],
+        a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(load_frag<MNMAJ, K3>(w3, kk, s, ln), d3f[s],
                                                     a, 0, 0, 0);
-      const float y[4] = {lo_bf(hv[kk].x), hi_bf(hv[kk].x), lo_bf(hv[kk].y), hi_bf(hv[kk].y)};
+      // activation of layer L-3 at this lane's dz2 positions, read per output block (held
+      // through the body, these 32 registers would spill a 128-register wave; the other waves
+      // of the SIMD cover the load)
+      const uint2 hv = *(const uint2*)(p.X + row * p.ldx + 16 * kk + 4 * q);
+      const float y[4] = {lo_bf(hv.x), hi_bf(hv.x), lo_bf(hv.y), hi_bf(hv.y)};
       float v[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = dact<RELU>(a[e], y[e], p.act2);
@@ -317,10 +334,11 @@ __device__ __forceinline__ void tail_body(const TailParams& p, char LDS_AS* lds,
       if (kk & 1) tail::st16_pair(p.DZ2 + row * p.lddz2, kk - 1, q, prev, o);
       prev = o;
       tail::acc4(rw + 16 * kk + 4 * q, o);
+      if (kk & 1) __builtin_amdgcn_sched_barrier(0);
     }
   }
 
-  // ---- per-workgroup partials: the 8 waves' column sums / loss / correct, fixed order -------
+  // ---- per-workgroup partials: the NW waves' column sums / loss / correct, fixed order ------
   loss_a = wave_sum(loss_a);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) corr_a += __shfl_xor(corr_a, o, 64);
@@ -350,8 +368,10 @@ template <int K3, int N3, bool RELU>
 __global__ __launch_bounds__(64 * tail::waves<RELU>()) void mlp_tail_kernel(TailParams p) {
   constexpr int NW = tail::waves<RELU>();
   __shared__ __attribute__((aligned(16))) char smem[tail::Geo<K3, N3, NW>::SMEM];
-  tail_body<K3, N3, RELU>(p, (char LDS_AS*)smem, blockIdx.x * NW, gridDim.x * NW, p.M >> 4,
-                          blockIdx.x);
+  // block rb -> workgroup rb % grid, wave (rb / grid) % NW: a launch of fewer blocks than
+  // waves still spreads them over every workgroup (CU)
+  tail_body<K3, N3, NW, RELU>(p, (char LDS_AS*)smem, blockIdx.x, gridDim.x, gridDim.x * NW,
+                              p.M >> 4, blockIdx.x);
 }
 
 // Forward of the layer BEFORE the tail fused in front of it (ReLU everywhere): workgroup t
@@ -362,8 +382,9 @@ __global__ __launch_bounds__(64 * tail::waves<RELU>()) void mlp_tail_kernel(Tail
 template <int K3, int N3>
 __global__ __launch_bounds__(512) void mlp_fwd_tail_kernel(GemmParams g, TailParams p) {
   using C = Cfg<256, 256, 4, 2, 2>;
-  static_assert(C::NT == 64 * tail::waves<true>() && K3 == C::BN, "one tile = the tail input");
-  constexpr int SM = cmax<C::SMEM, tail::Geo<K3, N3, 8>::SMEM>::v;
+  constexpr int NW = C::NW;
+  static_assert(K3 == C::BN, "one tile = the tail input");
+  constexpr int SM = cmax<C::SMEM, tail::Geo<K3, N3, NW>::SMEM>::v;
   __shared__ __attribute__((aligned(16))) char smem[SM];
   char LDS_AS* lds = (char LDS_AS*)smem;
   const int lane = threadIdx.x & 63;
@@ -376,8 +397,7 @@ __global__ __launch_bounds__(512) void mlp_fwd_tail_kernel(GemmParams g, TailPar
   // before, so no stale L1 lines) are visible to every wave, and the LDS is free for the
   // tail's weight images. (An agent-scope __threadfence() writes back L2 per workgroup.)
   __syncthreads();
-  tail_body<K3, N3, true>(p, lds, tm * (C::BM / 16), tail::waves<true>(),
-                          (tm + 1) * (C::BM / 16), tm);
+  tail_body<K3, N3, NW, true>(p, lds, tm * (C::BM / 16), 1, NW, (tm + 1) * (C::BM / 16), tm);
 }
 
 int mlp_tail_blocks(int M) {
@@ -389,7 +409,8 @@ int mlp_tail_blocks(int M) {
         cus <= 0)
       cus = 256;
   }
-  const int blocks = (M + tail::BLOCK_ROWS - 1) / tail::BLOCK_ROWS;
+  // one workgroup per 16-row block up to one per CU (blocks are dealt round-robin)
+  const int blocks = (M + 15) / 16;
   return blocks < cus ? (blocks > 0 ? blocks : 1) : cus;
 }
 

@@ -167,18 +167,19 @@ def pack_bf16(src, out):
     out[:rows, :cols] = src.to(out.dtype)
 
 
-TAIL_BLOCK_ROWS = 128  # rows per workgroup iteration that size the mlp_tail grid
+TAIL_BLOCK_ROWS = 16  # rows per 16-row block; the mlp_tail grid is one workgroup per block,
+# at most one per CU, blocks dealt round-robin
 
 
 def tail_waves(act3: int, act2: int) -> int:
-    """Waves per workgroup of csrc/kernels/mlp_tail.hip (16 rows each): 8 for ReLU/ReLU."""
-    return 8 if act3 == _RELU and act2 == _RELU else 4
+    """Waves per workgroup of csrc/kernels/mlp_tail.hip (16 rows each): 16 for ReLU/ReLU."""
+    return 16 if act3 == _RELU and act2 == _RELU else 4
 
 
 def mlp_tail(x, w3, b3, w4, b4, labels, h3, dz4, dz3, dz2, n_cls, scale, act3, act2,
              loss_part, correct, cs4, cs3, cs2, n_blocks):
     """Unfused reference of the fused classifier tail. Partials follow the kernel's row
-    assignment: 16-row block rb belongs to workgroup (rb // waves) % n_blocks."""
+    assignment: 16-row block rb belongs to workgroup rb % n_blocks."""
     rows, k3 = x.shape
     n3, n4 = w3.shape[0], w4.shape[0]
     gemm(x, w3, h3, layout_a=KMAJ, layout_b=KMAJ, M=rows, N=n3, K=k3, bias=b3, act=act3)
@@ -194,7 +195,7 @@ def mlp_tail(x, w3, b3, w4, b4, labels, h3, dz4, dz3, dz2, n_cls, scale, act3, a
     softmax_xent(logits, labels, dz4, n_cls, scale)
     gemm(dz4, w4, dz3, layout_a=KMAJ, layout_b=MNMAJ, M=rows, N=n3, K=n4, aux=h3, act=act3)
     gemm(dz3, w3, dz2, layout_a=KMAJ, layout_b=MNMAJ, M=rows, N=k3, K=n3, aux=x, act=act2)
-    owner = (torch.arange(rows) // 16 // tail_waves(act3, act2)) % n_blocks
+    owner = (torch.arange(rows) // 16) % n_blocks
     for t, src, cols in ((cs4, dz4, n4), (cs3, dz3, n3), (cs2, dz2, k3)):
         part = torch.zeros(n_blocks, cols)
         part.index_add_(0, owner, src[:rows, :cols].float())
