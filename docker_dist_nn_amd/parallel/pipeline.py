@@ -420,7 +420,10 @@ class PipelineExecutor:
                 plan += [(st, f"B0.L{i}", 0), (None, "@fork", 0), (st, f"W{i}", 1)]
             else:
                 plan += [(st, f"W{i}", 1), (st, f"B0.L{i}", 0), (None, "@fork", 0)]
-        split = (switches.get("DNN_SPLIT_FINO") == "1" and L > 1 and
+        # auto: on unless a layer updates in its wgrad epilogue (the wide model: there the
+        # side-stream update of layers 1.. competes with the fused W1; profiles/r3b_fino)
+        sf = switches.get("DNN_SPLIT_FINO")
+        split = ((sf == "1" or (sf == "auto" and not fused)) and L > 1 and
                  f"FINO1-{L - 1}" in segs and "FINO0-0" in segs and 0 not in fused)
         if plan[-1][1] == "@fork" and not split:
             plan = plan[:-1]

@@ -44,8 +44,10 @@ SWITCHES: dict[str, tuple[str, str]] = {
                             "on the side (headline 0.377 vs 0.372 ms, rejected); 3 = those under "
                             "W0 (0.386 ms, rejected); 4 = one fork, W1..W3 on the side (0.407 ms, "
                             "rejected); 0 = off"),
-    "DNN_SPLIT_FINO": ("0", "overlap plans: reduce + update layers 1..L-1 on the side stream "
-                       "during W0, only layer 0's after it (SGD)"),
+    "DNN_SPLIT_FINO": ("auto", "overlap plans: reduce + update layers 1..L-1 on the side "
+                       "stream during W0, only layer 0's after it (SGD); auto = when no layer "
+                       "updates in its wgrad epilogue (mlp8 2.918 -> 2.889 ms, headline "
+                       "0.350 -> 0.346, wide excluded: 6.04 -> 6.21)"),
     "DNN_FIN_WT": ("1", "the fused reduce + SGD/Adam launch (FINO) also writes the W^T "
                         "shadows of the layers it updates (no transpose launch per step)"),
     "DNN_FAULT_NATIVE_STEP": ("", "fault injection (tests): comma-separated ranks whose "
