@@ -288,9 +288,10 @@ __device__ __forceinline__ void tail_body(const TailParams& p, char LDS_AS* lds,
       }
     }
     const uint2 d4 = make_uint2(pack_bf16x2(dz[0], dz[1]), pack_bf16x2(dz[2], dz[3]));
-    tail::st16_pair(p.DZ4 + row * p.lddz4, 0, q, d4, make_uint2(0u, 0u));  // columns 0..31
-    for (int c = 2 * tail::MAX_CLS + 8 * q; c < p.N4 && !(DNN_TAIL_PROBE & 2); c += 32)
-      *(uint4*)(p.DZ4 + row * p.lddz4 + c) = make_uint4(0u, 0u, 0u, 0u);
+    // the 16 class columns only (8 bytes per lane, 32 contiguous per row): the padding columns
+    // are constant zero, left as the caller zeroed them (mlp_tail.hpp), 48 of 64 columns of
+    // writes less per row
+    if constexpr (!(DNN_TAIL_PROBE & 2)) *(uint2*)(p.DZ4 + row * p.lddz4 + 4 * q) = d4;
     tail::acc4(rw + K3 + N3 + 4 * q, d4);
 
     // ---- dz3 = (dz4 . W4) * act3'(h3): contraction over classes 0..31 -------------------

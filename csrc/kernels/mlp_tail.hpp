@@ -28,7 +28,8 @@ struct TailParams {
   const int* labels;   // [M], < 0 = padding row
   uint16_t* H3;        // [M][N3]
   long ldh3;
-  uint16_t* DZ4;       // [M][N4]
+  uint16_t* DZ4;       // [M][N4]: columns 0..15 written; 16..N4-1 must already be zero (never
+                       // written: the caller zero-initialises the buffer once)
   long lddz4;
   uint16_t* DZ3;       // [M][N3]
   long lddz3;

@@ -768,7 +768,8 @@ def mlp_tail(x, w3, b3, w4, b4, labels, h3, dz4, dz3, dz2, n_cls, scale, act3="r
              act2="relu", loss_part=None, correct=None, cs4=None, cs3=None, cs2=None):
     """The last two layers of a narrow classifier, forward AND backward, in one launch:
     h3 = act3(x.w3^T + b3); dz4 = (softmax(h3.w4^T + b4) - onehot) * scale;
-    dz3 = (dz4.w4) * act3'(h3); dz2 = (dz3.w3) * act2'(x); bias-gradient partials
+    dz3 = (dz4.w4) * act3'(h3); dz2 = (dz3.w3) * act2'(x) (GPU: dz4 columns >= 16 are not
+    written -- they stay the zeros the caller allocated); bias-gradient partials
     cs4/cs3/cs2 [tail_blocks(rows)][cols] and per-block loss / correct counts.
     CPU: the unfused kernels' reference path (same contract, partials per 64-row block)."""
     rows, k3 = x.shape

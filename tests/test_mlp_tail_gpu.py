@@ -31,7 +31,7 @@ def _run_tail(dev, x, w3, b3, w4, b4, labels, n_cls, scale, act="relu"):
     nb = ops.tail_blocks(rows)
     bf, f32 = torch.bfloat16, torch.float32
     out = dict(h3=torch.full((rows, n3), 7.0, dtype=bf, device=dev),
-               dz4=torch.full((rows, n4), 7.0, dtype=bf, device=dev),
+               dz4=torch.zeros(rows, n4, dtype=bf, device=dev),  # padding stays the caller's
                dz3=torch.full((rows, n3), 7.0, dtype=bf, device=dev),
                dz2=torch.full((rows, k3), 7.0, dtype=bf, device=dev),
                loss=torch.zeros(nb, dtype=f32, device=dev),
@@ -188,7 +188,7 @@ def test_fwd_tail_equals_fwd_then_tail(dev):
         nb = ops.tail_blocks(rows)
         bf, f32 = torch.bfloat16, torch.float32
         out = dict(x=x, h3=torch.full((rows, 128), 7.0, dtype=bf, device=dev),
-                   dz4=torch.full((rows, 64), 7.0, dtype=bf, device=dev),
+                   dz4=torch.zeros(rows, 64, dtype=bf, device=dev),
                    dz3=torch.full((rows, 128), 7.0, dtype=bf, device=dev),
                    dz2=torch.full((rows, 256), 7.0, dtype=bf, device=dev),
                    loss=torch.zeros(nb, dtype=f32, device=dev),
