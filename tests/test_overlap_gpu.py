@@ -40,3 +40,21 @@ def test_overlap_plan_bitwise(dev, monkeypatch, model, rows):
     for r in res[1:]:
         assert res[0][0] == r[0]
         assert torch.equal(res[0][1], r[1])
+
+
+@pytest.mark.parametrize("model,rows,split", [("mnist-fcnn", 8192, True),
+                                              ("784-8192-8192-10", 2048, False)])
+def test_split_fino_auto_plan(dev, monkeypatch, model, rows, split):
+    """DNN_SPLIT_FINO=auto (the default): layers 1.. are reduced and updated on the side stream
+    during W0 unless a layer updates in its wgrad epilogue (the wide model's layer 1)."""
+    from docker_dist_nn_amd import NAMED_MODELS, MLPSpec
+    from docker_dist_nn_amd.engine import OptimConfig, Trainer
+
+    monkeypatch.delenv("DNN_SPLIT_FINO", raising=False)
+    monkeypatch.delenv("DNN_BW_OVERLAP", raising=False)
+    spec = NAMED_MODELS.get(model) or MLPSpec.parse(model)
+    tr = Trainer(spec, micro_batch=rows, num_micro=1, optim=OptimConfig(lr=0.1), device=dev)
+    segs = [(seg, side) for _, seg, side in tr.executor._native_plan()]
+    L = len(spec.layers)
+    assert ((f"FINO1-{L - 1}", 1) in segs and ("FINO0-0", 0) in segs) == split, segs
+    assert (("FINO", 0) in segs) == (not split), segs
