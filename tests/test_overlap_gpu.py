@@ -52,8 +52,15 @@ def test_split_fino_auto_plan(dev, monkeypatch, model, rows, split):
 
     monkeypatch.delenv("DNN_SPLIT_FINO", raising=False)
     monkeypatch.delenv("DNN_BW_OVERLAP", raising=False)
+    from docker_dist_nn_amd.data import synthetic_mnist
+
     spec = NAMED_MODELS.get(model) or MLPSpec.parse(model)
+    x, y = synthetic_mnist(rows, seed=4)
+    xb = torch.zeros(rows, 832, dtype=torch.bfloat16)
+    xb[:, :784] = torch.from_numpy(x).to(torch.bfloat16)
     tr = Trainer(spec, micro_batch=rows, num_micro=1, optim=OptimConfig(lr=0.1), device=dev)
+    tr.set_batch(xb.to(dev), torch.from_numpy(y).to(dev))
+    tr.step()
     segs = [(seg, side) for _, seg, side in tr.executor._native_plan()]
     L = len(spec.layers)
     assert ((f"FINO1-{L - 1}", 1) in segs and ("FINO0-0", 0) in segs) == split, segs
