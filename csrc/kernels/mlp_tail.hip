@@ -7,8 +7,8 @@
 // ~370 us step while their data is ~110 MB (23 us of HBM time). Their weights are 64 + 16 KiB,
 // so they live in LDS for the whole launch and every intermediate stays on chip.
 //
-// Structure (one workgroup per CU; 8 waves for the ReLU form, 4 for other activations; each
-// wave walks 16-row blocks):
+// Structure (one workgroup per CU; 16 waves for the ReLU form, 4 for other activations;
+// 16-row blocks dealt round-robin over the workgroups, one per wave at 65536 rows):
 //   * W3 [N3][K3] and W4 [64][N3] are staged once into LDS with LDS-DMA, in the MNMAJ image
 //     layout of gemm_tile.hpp: the forward reads them row-wise (16-B chunks), the dgrads read
 //     them transposed with ds_read_b64_tr_b16 (load_frag<MNMAJ>), so no transposed copy exists;
@@ -17,9 +17,8 @@
 //     16 j + 4 (lane >> 4) + r), which is the layout of the bias/activation epilogue, of the
 //     ReLU derivative of the next dgrad, and of the softmax (a row's 16 class logits sit in 4
 //     lanes); global stores pair two such blocks into 16-byte chunks (v_permlane16_swap);
-//   * an output that feeds the next product is written to a 16-row per-wave LDS scratch and
-//     read back as the next MFMA's B fragment (same-wave LDS order, no barrier);
-//   * the next block's input rows are loaded while the current block computes;
+//   * an output that feeds the next product becomes the next MFMA's B fragment in registers
+//     (frag_from_out: two lane-group swaps), no LDS round trip;
 //   * bias-gradient column sums: DPP row sums per block, accumulated across the wave's blocks
 //     in the wave's own LDS row, reduced over the waves in fixed order at the end (one partial
 //     per workgroup); softmax and loss follow xent_rows (gemm_tile.hpp) operation for operation.
@@ -48,9 +47,9 @@ namespace tail {
 
 // Waves per workgroup of the standalone launch: 16 (four per SIMD, <= 128 registers each) for
 // the branch-free ReLU form, so one 16-row block per wave covers 65536 rows in one round and
-// four independent block chains share each SIMD; the generic-activation form needs more
-// registers and runs 4 (one per SIMD). The fused forward + tail launch (mlp_fwd_tail_kernel)
-// runs the body with the 8 waves of its 256x256 GEMM tile.
+// four independent block chains share each SIMD; the generic-activation form (runtime
+// activation branches; not on the benchmarked models) runs 4. The fused forward + tail launch
+// (mlp_fwd_tail_kernel) runs the body with the 8 waves of its 256x256 GEMM tile.
 template <bool RELU>
 constexpr int waves() { return RELU ? 16 : 4; }
 constexpr int MAX_CLS = 16;  // classes held by one 16-wide MFMA block
