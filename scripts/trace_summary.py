@@ -19,6 +19,7 @@ def main():
     ap.add_argument("csv")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--end", default="reduce_multi")
+    ap.add_argument("--end-grid", type=int, default=None)
     a = ap.parse_args()
     rows = []
     with open(a.csv) as f:
@@ -27,7 +28,10 @@ def main():
                          int(r["Grid_Size_X"]) // max(1, int(r["Workgroup_Size_X"])),
                          r["VGPR_Count"], r["Accum_VGPR_Count"], r["LDS_Block_Size"]))
     rows.sort()
-    ends = [i for i, r in enumerate(rows) if a.end in r[2]]
+    # --end-grid: with the split reduction (DNN_SPLIT_FINO) a step has two reduce_multi
+    # launches; the main stream's last one (layer 0's) is picked by its grid
+    ends = [i for i, r in enumerate(rows)
+            if a.end in r[2] and (a.end_grid is None or r[3] == a.end_grid)]
     if len(ends) < 2:
         raise SystemExit("fewer than two step ends found")
     n = min(a.steps, len(ends) - 1)
