@@ -7,7 +7,7 @@
 // ~370 us step while their data is ~110 MB (23 us of HBM time). Their weights are 64 + 16 KiB,
 // so they live in LDS for the whole launch and every intermediate stays on chip.
 //
-// Structure (one workgroup per CU; 16 waves for the ReLU form, 4 for other activations;
+// Structure (one workgroup per CU; 16 waves for the ReLU form, 8 for other activations;
 // 16-row blocks dealt round-robin over the workgroups, one per wave at 65536 rows):
 //   * W3 [N3][K3] and W4 [64][N3] are staged once into LDS with LDS-DMA, in the MNMAJ image
 //     layout of gemm_tile.hpp: the forward reads them row-wise (16-B chunks), the dgrads read
@@ -48,10 +48,11 @@ namespace tail {
 // Waves per workgroup of the standalone launch: 16 (four per SIMD, <= 128 registers each) for
 // the branch-free ReLU form, so one 16-row block per wave covers 65536 rows in one round and
 // four independent block chains share each SIMD; the generic-activation form (runtime
-// activation branches; not on the benchmarked models) runs 4. The fused forward + tail launch
-// (mlp_fwd_tail_kernel) runs the body with the 8 waves of its 256x256 GEMM tile.
+// activation branches, <= 128 registers; not on the benchmarked models) runs 8. The fused
+// forward + tail launch (mlp_fwd_tail_kernel) runs the body with the 8 waves of its 256x256
+// GEMM tile.
 template <bool RELU>
-constexpr int waves() { return RELU ? 16 : 4; }
+constexpr int waves() { return RELU ? 16 : 8; }
 constexpr int MAX_CLS = 16;  // classes held by one 16-wide MFMA block
 constexpr int W4_ROWS = 64;  // staged rows of W4 (the dgrad's contraction uses rows 0..31)
 

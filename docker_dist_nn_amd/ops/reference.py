@@ -173,7 +173,7 @@ TAIL_BLOCK_ROWS = 16  # rows per 16-row block; the mlp_tail grid is one workgrou
 
 def tail_waves(act3: int, act2: int) -> int:
     """Waves per workgroup of csrc/kernels/mlp_tail.hip (16 rows each): 16 for ReLU/ReLU."""
-    return 16 if act3 == _RELU and act2 == _RELU else 4
+    return 16 if act3 == _RELU and act2 == _RELU else 8
 
 
 def mlp_tail(x, w3, b3, w4, b4, labels, h3, dz4, dz3, dz2, n_cls, scale, act3, act2,

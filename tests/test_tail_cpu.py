@@ -72,7 +72,7 @@ def test_blas_switch(monkeypatch):
 
 def test_reference_tail_waves_match_kernel_forms():
     assert ref.tail_waves(1, 1) == 16  # branch-free ReLU form: 16 waves
-    assert ref.tail_waves(2, 1) == 4 and ref.tail_waves(0, 0) == 4
+    assert ref.tail_waves(2, 1) == 8 and ref.tail_waves(0, 0) == 8
 
 
 def test_tuner_signatures_include_logits_candidate():
