@@ -324,7 +324,10 @@ class PipelineExecutor:
         if any(st._prog is None or not st._has_w or not st._o_native for st in self.stages):
             return None
         mode = switches.get("DNN_BW_OVERLAP")
-        if mode in ("1", "2", "3", "4") and len(self.stages) == 1:
+        # small steps are host-bound: every fork / join is an event record + wait (~6-8 us of
+        # host time each), more than the overlap can win back on GEMMs of a few thousand rows
+        if mode in ("1", "2", "3", "4") and len(self.stages) == 1 and \
+                self.stages[0].rows >= int(switches.get("DNN_BW_OVERLAP_MIN_ROWS")):
             ov = self._overlap_plan(self.stages[0], mode)
             if ov is not None:
                 self._plan = ov

@@ -44,6 +44,11 @@ SWITCHES: dict[str, tuple[str, str]] = {
                             "on the side (headline 0.377 vs 0.372 ms, rejected); 3 = those under "
                             "W0 (0.386 ms, rejected); 4 = one fork, W1..W3 on the side (0.407 ms, "
                             "rejected); 0 = off"),
+    "DNN_BW_OVERLAP_MIN_ROWS": ("16384", "overlap plans only for steps of at least this many "
+                                         "rows (below, the single-stream plan: no event "
+                                         "packets, the host cost that bounds small steps; "
+                                         "headline model 1024 rows 0.093 -> 0.054 ms, 8192 "
+                                         "even, 16384 0.155 vs 0.166 for the overlap)"),
     "DNN_SPLIT_FINO": ("auto", "overlap plans: reduce + update layers 1..L-1 on the side "
                        "stream during W0, only layer 0's after it (SGD); auto = when no layer "
                        "updates in its wgrad epilogue (mlp8 2.918 -> 2.889 ms, headline "

@@ -16,6 +16,7 @@ def test_overlap_plan_bitwise(dev, monkeypatch, model, rows):
     from docker_dist_nn_amd.engine import OptimConfig, Trainer
 
     spec = NAMED_MODELS.get(model) or MLPSpec.parse(model)
+    monkeypatch.setenv("DNN_BW_OVERLAP_MIN_ROWS", "0")
     x, y = synthetic_mnist(rows, seed=4)
     xb = torch.zeros(rows, 832, dtype=torch.bfloat16)
     xb[:, :784] = torch.from_numpy(x).to(torch.bfloat16)
@@ -52,6 +53,7 @@ def test_split_fino_auto_plan(dev, monkeypatch, model, rows, split):
 
     monkeypatch.delenv("DNN_SPLIT_FINO", raising=False)
     monkeypatch.delenv("DNN_BW_OVERLAP", raising=False)
+    monkeypatch.setenv("DNN_BW_OVERLAP_MIN_ROWS", "0")
     from docker_dist_nn_amd.data import synthetic_mnist
 
     spec = NAMED_MODELS.get(model) or MLPSpec.parse(model)
