@@ -49,7 +49,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from docker_dist_nn_amd import NAMED_MODELS, MLPSpec  # noqa: E402
-from docker_dist_nn_amd import switches  # noqa: E402
+from docker_dist_nn_amd import ladder, switches  # noqa: E402
+from docker_dist_nn_amd.faults import FaultInjector  # noqa: E402
 from docker_dist_nn_amd.data import DeviceDataset, synthetic_mnist  # noqa: E402
 from docker_dist_nn_amd.engine import OptimConfig, Trainer  # noqa: E402
 from docker_dist_nn_amd.parallel.planner import Planner, parse_parallelism  # noqa: E402
@@ -185,16 +186,23 @@ def measure(a, spec, n, world, dev, text):
     # plan's flag waits are kernels so the whole rank step -- hops included -- is captured)
     use_graph = a.graph == "on" and (world == 1 or tr.native_step is not None)
     step_i = 0
+    rank = int(os.environ.get("RANK", "0"))
+    injector = FaultInjector()  # DNN_FAULT (the ladder's tests): stage = global rank
+    beat = ladder.Throttled(5.0)
 
     def one_step():
         nonlocal step_i
+        injector.maybe_inject(rank, step_i)
         xb, yb = data.batch(step_i)
         tr.set_batch(xb if tr.first else None, yb if tr.last else None, zero_copy=True)
         tr.step()
         step_i += 1
+        beat(f"step {step_i}")
 
+    ladder.heartbeat("trainer built")
     if world > 1:  # the first multi-rank step is bounded: a hang prints the plan and exits
         first_step_guard(tr, one_step, dev, float(switches.get("DNN_FIRST_STEP_TIMEOUT")))
+        ladder.heartbeat("first step done")
     def barrier():
         if world > 1:
             torch.distributed.barrier()
@@ -311,11 +319,58 @@ def measure_tp(a, spec, n, world, dev):
             "native_fallback": None}
 
 
+DP_ONLY_KEYS = ("parallelism", "global_batch", "transport", "native_step", "dp_reduce")
+
+
+def supervise(a, argv) -> int:
+    """WORLD_SIZE > 1: this process is the rank's supervisor (ladder.py). It never touches the
+    GPU; every attempt runs ``bench.py`` again as a fresh child per rank (new rendezvous port),
+    climbing the fallback ladder until one attempt succeeds on every rank. Then the
+    data-parallel comparison runs the same way. Rank 0 prints the one JSON line, with every
+    attempt (rung, exit codes, last heartbeat of a stalled child) listed."""
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ["WORLD_SIZE"])
+    base = [sys.executable, "-u", os.path.abspath(__file__),
+            *(sys.argv[1:] if argv is None else argv)]
+    sup = ladder.Supervisor(lambda r: [*base, *r.args, "--no-dp-compare"], rank=rank,
+                            world=world, stall=float(switches.get("DNN_LADDER_STALL")))
+    if a.parallelism.startswith("tp"):
+        rungs = [ladder.Rung("default")]
+    else:
+        rungs = ladder.bench_rungs(world, dp_only=a.parallelism.startswith("dp"))
+    res, rung = sup.climb(rungs)
+    attempts = list(sup.attempts)
+    dp_only = dp_attempts = None
+    if res is not None and not a.no_dp_compare and \
+            not res["config"]["parallelism"].startswith(("dp", "tp")):
+        d, _ = sup.climb(ladder.bench_rungs(world, dp_only=True))
+        dp_attempts = sup.attempts[len(attempts):]
+        dp_only = ({"value": d["value"], "ms_per_step": d["ms_per_step"],
+                    **{k: d["config"].get(k) for k in DP_ONLY_KEYS}} if d is not None else
+                   {"value": None, "error": "every data-parallel rung failed"})
+    if rank == 0:
+        if res is None:
+            out = {"metric": METRIC, "value": None, "unit": "samples/s", "n_gpus": world,
+                   "steps": a.steps, "warmup": a.warmup, "higher_is_better": True,
+                   "error": "every rung of the fallback ladder failed",
+                   "ladder": {"attempts": attempts}}
+        else:
+            out = res
+            out["dp_only"] = dp_only
+            out["ladder"] = {"rung": rung.name, "attempts": attempts,
+                             "dp_attempts": dp_attempts}
+        print(json.dumps(out), flush=True)
+    return 0 if res is not None else 1
+
+
 def main(argv=None):
     a = parse_args(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if a.gpus != world and world > 1:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    if world > 1 and not ladder.is_child() and switches.get("DNN_LADDER") == "1":
+        return supervise(a, argv)
+    ladder.heartbeat("start")
     n = max(a.gpus, world)
     spec = NAMED_MODELS.get(a.model) or MLPSpec.parse(a.model)
 
@@ -328,6 +383,7 @@ def main(argv=None):
         from docker_dist_nn_amd.parallel.groups import init_distributed
 
         init_distributed(switches.get("DNN_DIST_BACKEND"))
+        ladder.heartbeat("rendezvous done")
 
     if a.parallelism.startswith("tp"):
         m = measure_tp(a, spec, n, world, dev)
@@ -376,12 +432,15 @@ def main(argv=None):
         "switches": switches.active(),  # non-default DNN_* switches of this run
     }
     rank = int(os.environ.get("RANK", "0"))
-    if rank == 0:
+    if ladder.is_child():
+        out["ladder_rung"] = os.environ.get(ladder.RUNG_ENV)
+    if rank == 0 and not ladder.write_result(out):
         print(json.dumps(out), flush=True)
     if world > 1:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -947,6 +947,8 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("n_streams", &dnn::StepPlan::n_streams)
       .def("comm_error", &dnn::StepPlan::comm_error)
       .def("flag_timeouts", &dnn::StepPlan::flag_timeouts)
+      .def_property("wait_timeout", &dnn::StepPlan::wait_timeout,
+                    &dnn::StepPlan::set_wait_timeout)
       .def("sync_seq", &dnn::StepPlan::sync_seq)
       .def("clear_ops", &dnn::StepPlan::clear_ops);
   py::class_<dnn::GraphExec>(m, "GraphExec")

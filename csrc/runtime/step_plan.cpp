@@ -61,7 +61,12 @@ const NcclApi& nccl_load(const std::string& path) {
 
 const NcclApi* nccl_api() { return g_loaded ? &g_api : nullptr; }
 
-StepPlan::StepPlan(int n_streams, int n_events) {
+static double default_wait_timeout_s() {
+  const char* e = std::getenv("DNN_FLAG_TIMEOUT");
+  return e ? std::atof(e) : 120.0;
+}
+
+StepPlan::StepPlan(int n_streams, int n_events) : wait_timeout_(default_wait_timeout_s()) {
   if (n_streams < 1 || n_events < 0) throw std::invalid_argument("StepPlan: bad sizes");
   for (int i = 1; i < n_streams; ++i) {
     hipStream_t s;
@@ -98,16 +103,6 @@ uint32_t StepPlan::flag_timeouts() const {
   return e;
 }
 
-static double wait_timeout_s() {
-  static const double t = [] {
-    const char* e = std::getenv("DNN_FLAG_TIMEOUT");
-    // 20 s: far above any hop of a real step, and short enough that a plan stalled on a
-    // flag (e.g. IPC during the first-step verification, engine/trainer.py) reports the
-    // timeout -- and the job falls back -- well inside bench.py's 60 s first-step bound
-    return e ? std::atof(e) : 20.0;
-  }();
-  return t;
-}
 
 StepPlan::~StepPlan() {
   for (auto e : events_) (void)hipEventDestroy(e);
@@ -219,7 +214,7 @@ void StepPlan::run(hipStream_t main) {
         break;
       case WAITV:
         if (p2p_wait_seq(reinterpret_cast<const uint32_t*>(o.a), dev_, (int)o.delta, dev_ + 1,
-                         wait_timeout_s(), s) != 0)
+                         wait_timeout_, s) != 0)
           throw std::runtime_error("p2p_wait_seq failed");
         break;
       case REC:

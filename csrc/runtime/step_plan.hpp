@@ -92,6 +92,11 @@ class StepPlan {
   int n_streams() const { return (int)streams_.size() + 1; }
   // RCCL async-error poll over every communicator the plan uses (0 = healthy).
   int comm_error() const;
+  // Seconds a WAITV spins before it gives up and raises the error word. Steady state: long
+  // (DNN_FLAG_TIMEOUT, default 120 s) -- a wait that gives up lets the plan consume rows that
+  // never arrived. The first-step verification (engine/trainer.py) sets a short one.
+  double wait_timeout() const { return wait_timeout_; }
+  void set_wait_timeout(double s) { wait_timeout_ = s; }
 
  private:
   hipStream_t stream(int i, hipStream_t main) const { return i == 0 ? main : streams_[i - 1]; }
@@ -102,6 +107,7 @@ class StepPlan {
   std::vector<Op> ops_;
   uint32_t seq_ = 0;
   int group_open_ = -1;  // stream of the RCCL group being added, -1 = none
+  double wait_timeout_;
   // [0] = step number read by the SIGNAL / WAITV kernels, [1] = wait-timeout error word
   uint32_t* dev_ = nullptr;
 };

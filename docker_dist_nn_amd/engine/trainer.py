@@ -171,8 +171,11 @@ class Trainer:
                                                   ipc=self.pipe if self.transport == "ipc"
                                                   else None)
                     if self._ipc_verify is not None and mesh.backend == "nccl":
-                        # the verified IPC step's fallback: the RCCL plan, built up front
-                        self._fallback_step = NativeStep(self.executor, mesh, "rccl")
+                        # the verified IPC step's fallback: the RCCL plan, built up front, in
+                        # the `slotted` form -- correct whatever the RCCL kernel residency, so
+                        # the first step needs no co-residency assumption
+                        self._fallback_step = NativeStep(self.executor, mesh, "rccl",
+                                                         mode="slotted")
                 except Exception as e:  # agreed on below: every rank falls back together
                     err = e
             # A rank running the native step and one running the Python executor would post
@@ -190,6 +193,12 @@ class Trainer:
                 self.native_step = None
             if self.native_step is not None:
                 self.executor.native_step = self.native_step
+            elif self._ipc_verify is not None:
+                # DNN_PIPE=auto picked IPC but the native step is unavailable (a schedule it
+                # does not support, hooks, a construction error): the message transport
+                # (this must not raise for auto)
+                self._use_fallback_pipe("IPC needs the native multi-rank step "
+                                        f"({self.native_fallback or why})")
             elif isinstance(self.pipe, IpcPipe) and self.pipe.k:
                 # relayed IPC hops exist only in the native step: name the cause here instead
                 # of failing inside the first Python-executor step
@@ -200,7 +209,7 @@ class Trainer:
         if self._ipc_verify is not None and self.native_step is None:
             # the IPC step cannot be verified without the native step: message transport
             self._use_fallback_pipe("IPC needs the native multi-rank step "
-                                    f"({self.native_fallback or 'unsupported plan'})")
+                                    f"({self.native_fallback or 'native step disabled'})")
         self._graph = None
         self._stream = None
         self.graph_nodes = 0
@@ -237,6 +246,10 @@ class Trainer:
         if mode == "auto" and not self._peers_mappable(mesh):
             self.transport_reason = "a GPU pair of the plan has no peer access"
             return DistPipe(mesh, st)
+        if mode == "auto" and self.schedule in ("1f1b_w", "zb"):
+            self.transport_reason = (f"schedule {self.schedule} (per-micro-batch weight "
+                                     "gradients: no native step, so no IPC)")
+            return DistPipe(mesh, st)
         kr = switches.get("DNN_IPC_RELAYS")
         world = mesh.pp * mesh.dp
         k = min(2, max(0, world - 2)) if kr == "auto" else int(kr)
@@ -248,6 +261,12 @@ class Trainer:
             if mode == "ipc":
                 raise
             self.transport_reason = f"IPC set-up failed: {e}"[:300]
+            return DistPipe(mesh, st)
+        hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+        if mode == "auto" and 4 + len(ipc.duties) > hwq:
+            ipc.close()
+            self.transport_reason = (f"IPC plan needs {4 + len(ipc.duties)} hardware queues, "
+                                     f"GPU_MAX_HW_QUEUES={hwq}")
             return DistPipe(mesh, st)
         self.transport_reason = (f"ipc, {k} relays per hop" +
                                  (" (verification pending: first step)" if verify else ""))
@@ -276,6 +295,7 @@ class Trainer:
     def _use_fallback_pipe(self, why: str) -> None:
         ipc, fb = self._ipc_verify
         self._ipc_verify = None
+        ipc.close()
         self.pipe = fb
         self.executor.pipe = fb
         self.transport = "rccl" if self.mesh.backend == "nccl" else self.mesh.backend
@@ -308,8 +328,18 @@ class Trainer:
         state = self._state_tensors()
         snap = [t.clone() for t in state]
         counts = [st.params.step_count for st in self.stages]
-        self.executor.run_step()  # IPC
-        torch.cuda.synchronize(self.device)
+        # a stalled IPC plan must report well inside bench.py's first-step bound; steady state
+        # keeps the long flag-wait timeout
+        plan = self.native_step.plan if self.native_step is not None else None
+        long_timeout = plan.wait_timeout if plan is not None else None
+        if plan is not None:
+            plan.wait_timeout = float(switches.get("DNN_VERIFY_FLAG_TIMEOUT"))
+        try:
+            self.executor.run_step()  # IPC
+            torch.cuda.synchronize(self.device)
+        finally:
+            if plan is not None:
+                plan.wait_timeout = long_timeout
         ipc_state = [t.clone() for t in state]
         timeouts = self.native_step.comm_error() if self.native_step is not None else 0
         if str(self.mesh.rank) in switches.get("DNN_FAULT_IPC_VERIFY").split(","):
@@ -408,6 +438,13 @@ class Trainer:
         if self.device.type != "cuda" or (self.mesh is not None and self.native_step is None):
             raise RuntimeError("graph capture needs the local GPU path or a native "
                                "multi-rank step (parallel/native_step.py)")
+        if self._ipc_verify is not None:
+            # never capture (and replay) an unverified relayed-IPC plan: the first
+            # step runs the verification, which may switch the transport
+            self.step()
+            if self.mesh is not None and self.native_step is None:
+                raise RuntimeError("graph capture needs a native multi-rank step; the IPC "
+                                   "verification fell back to the Python executor")
         cur = torch.cuda.current_stream(self.device)
         self._stream = torch.cuda.Stream(self.device)
         self._stream.wait_stream(cur)

@@ -1,0 +1,290 @@
+"""Fail-safe multi-rank runs: a ladder of transports / plan forms, each attempt in fresh child
+processes, so that a job produces a result whatever its first choice does.
+
+The reference has no such thing -- a stage that hangs or dies takes its request down, and the
+launcher only logs it (/root/reference/src/run_grpc_fcnn.py:83-155, grpc_node.py:120-140).
+Here the first real run of a cross-GPU plan is also the first execution of several mechanisms
+(relayed xGMI peer writes, per-link RCCL communicators, co-resident RCCL kernels) that a one-GPU
+pool cannot time. A hang or crash in any of them must cost one attempt, not the job.
+
+How it works (``Supervisor``), one supervisor per rank, started by ``torch.distributed.run``:
+
+* the supervisor NEVER touches the GPU (no HIP call: it only imports torch for the c10d
+  ``TCPStore``) and never execs; each attempt is a fresh child process per rank
+  (``subprocess.Popen``, own session), on a fresh rendezvous port chosen by rank 0 and shared
+  through the store;
+* each supervisor watches its child: exit code, and a heartbeat file the child touches at every
+  phase / step (``DNN_LADDER_HEARTBEAT``); a child silent for ``stall`` seconds is killed;
+* every rank's outcome is published under ``attempt/<i>/rc/<rank>``. When ANY rank's child
+  fails, every other supervisor kills its own child (whose peers are gone, so it would only
+  hang) and publishes "killed". An attempt succeeded iff every rank's child exited 0 -- every
+  supervisor reads the same keys, so all agree without another collective;
+* on failure all supervisors move to the next rung together; on success rank 0's child has
+  written its result (``DNN_LADDER_RESULT``) and rank 0 reports it with the list of attempts.
+
+Rungs of the training benchmark (``bench_rungs``), most capable first:
+
+  1. ``default``       -- the configured transport (DNN_PIPE=auto: relayed IPC, its first step
+                          verified against the RCCL ``slotted`` plan);
+  2. ``rccl-slotted``  -- RCCL, one grouped send/recv per logical clock slot (safe with ONE
+                          resident RCCL kernel per rank);
+  3. ``rccl-streams``  -- RCCL, one stream + communicator per link channel;
+  4. ``python``        -- the Python executor over torch.distributed P2P;
+  5. ``dp-native`` / ``dp-python`` -- data parallelism only (no pipeline hops at all).
+"""
+from __future__ import annotations
+
+import json
+import os
+import signal
+import subprocess
+import sys
+import time
+from dataclasses import dataclass, field
+from typing import Callable, Optional, Sequence
+
+HEARTBEAT_ENV = "DNN_LADDER_HEARTBEAT"
+RESULT_ENV = "DNN_LADDER_RESULT"
+RUNG_ENV = "DNN_LADDER_RUNG"
+CHILD_ENV = "DNN_LADDER_CHILD"
+
+
+@dataclass
+class Rung:
+    name: str
+    env: dict = field(default_factory=dict)     # overrides for the child's environment
+    args: list = field(default_factory=list)    # extra command-line arguments (appended)
+
+
+def bench_rungs(n: int, dp_only: bool = False) -> list[Rung]:
+    """The training benchmark's ladder for ``n`` ranks. ``dp_only``: the layout is already
+    data-parallel (no hops), only the executor can fall back."""
+    dp = [Rung("dp-native", {}, ["--parallelism", f"dp{n}"]),
+          Rung("dp-python", {"DNN_NATIVE_DIST": "0"}, ["--parallelism", f"dp{n}"])]
+    if dp_only:
+        return dp
+    return [Rung("default"),
+            Rung("rccl-slotted", {"DNN_PIPE": "rccl", "DNN_RCCL_PLAN": "slotted"}),
+            Rung("rccl-streams", {"DNN_PIPE": "rccl", "DNN_RCCL_PLAN": "streams"}),
+            Rung("python", {"DNN_PIPE": "rccl", "DNN_NATIVE_DIST": "0"}),
+            *dp]
+
+
+# ---- child side ---------------------------------------------------------------------------
+def is_child() -> bool:
+    return os.environ.get(CHILD_ENV) == "1"
+
+
+def heartbeat(phase: str = "") -> None:
+    """Tell the supervisor this child is making progress (no-op outside a ladder)."""
+    path = os.environ.get(HEARTBEAT_ENV)
+    if path:
+        try:
+            with open(path, "w") as f:
+                f.write(f"{time.time():.3f} {phase}\n")
+        except OSError:
+            pass
+
+
+class Throttled:
+    """Per-step heartbeat that writes at most every ``interval`` seconds (a step loop calls it
+    every step; the cost is one clock read)."""
+
+    def __init__(self, interval: float = 5.0):
+        self.interval = interval
+        self.last = 0.0
+        self.on = bool(os.environ.get(HEARTBEAT_ENV))
+
+    def __call__(self, phase: str = "") -> None:
+        if self.on:
+            t = time.monotonic()
+            if t - self.last >= self.interval:
+                self.last = t
+                heartbeat(phase)
+
+
+def write_result(obj: dict) -> bool:
+    """Child rank 0: hand the result to the supervisor. False outside a ladder."""
+    path = os.environ.get(RESULT_ENV)
+    if not path:
+        return False
+    tmp = path + ".tmp"
+    with open(tmp, "w") as f:
+        json.dump(obj, f)
+    os.replace(tmp, path)
+    return True
+
+
+def rung_fault(rung: str, spec: str) -> str:
+    """``DNN_LADDER_FAULT`` = 'rung=fault;rung=fault' (fault in DNN_FAULT syntax): the fault
+    the child of ``rung`` injects (tests of the ladder itself)."""
+    for item in filter(None, (s.strip() for s in spec.split(";"))):
+        name, _, fault = item.partition("=")
+        if name.strip() == rung:
+            return fault.strip()
+    return ""
+
+
+# ---- supervisor side ----------------------------------------------------------------------
+def _store(rank: int, world: int):
+    """The job's c10d store (CPU only). Under torch.distributed.run the elastic agent hosts it
+    on MASTER_PORT; otherwise rank 0 hosts it."""
+    from datetime import timedelta
+
+    import torch.distributed as dist
+
+    host = os.environ.get("MASTER_ADDR", "127.0.0.1")
+    port = int(os.environ["MASTER_PORT"])
+    agent = os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "").lower() in ("1", "true")
+    master = rank == 0 and not agent
+    st = dist.TCPStore(host, port, world if master else None, master,
+                       timeout=timedelta(seconds=600), wait_for_workers=False)
+    run = os.environ.get("TORCHELASTIC_RUN_ID", "")
+    return dist.PrefixStore(f"dnn_ladder/{run}/", st)
+
+
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _kill(p: subprocess.Popen) -> None:
+    try:
+        os.killpg(p.pid, signal.SIGKILL)
+    except (ProcessLookupError, PermissionError):
+        pass
+    try:
+        p.wait(30)
+    except subprocess.TimeoutExpired:
+        pass
+
+
+class Supervisor:
+    """Runs a ladder of attempts on every rank (see the module docstring).
+
+    ``command(rung)`` -> the child's argv. ``stall``: seconds without a heartbeat (or an exit)
+    before a child is killed; ``store``: a c10d store shared by the ranks (default: the job's)."""
+
+    def __init__(self, command: Callable[[Rung], Sequence[str]], *, rank: int, world: int,
+                 stall: float = 180.0, store=None, workdir: Optional[str] = None,
+                 log=None):
+        self.command = command
+        self.rank, self.world = rank, world
+        self.stall = float(stall)
+        self.store = store if store is not None else _store(rank, world)
+        self.workdir = workdir or os.path.join(
+            os.environ.get("TMPDIR", "/tmp"),
+            f"dnn_ladder_{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}")
+        os.makedirs(self.workdir, exist_ok=True)
+        self.log = log or (lambda msg: print(f"[ladder r{rank}] {msg}", file=sys.stderr,
+                                              flush=True))
+        self.attempts: list[dict] = []
+        self._n = 0  # attempts made (store keys are per attempt index)
+
+    def _key(self, i: int, what: str) -> str:
+        return f"attempt/{i}/{what}"
+
+    def _peer_rcs(self, i: int) -> dict:
+        out = {}
+        for r in range(self.world):
+            k = self._key(i, f"rc/{r}")
+            if self.store.check([k]):
+                out[r] = self.store.get(k).decode()
+        return out
+
+    def attempt(self, rung: Rung) -> tuple[bool, Optional[dict]]:
+        """One attempt of ``rung`` on every rank; returns (success, rank 0's result)."""
+        i = self._n
+        self._n += 1
+        if self.rank == 0:
+            self.store.set(self._key(i, "port"), str(_free_port()))
+        port = self.store.get(self._key(i, "port")).decode()
+        hb = os.path.join(self.workdir, f"hb_{i}_{self.rank}")
+        res = os.path.join(self.workdir, f"result_{i}.json")
+        for path in (hb, res):
+            if os.path.exists(path) and (path == hb or self.rank == 0):
+                os.remove(path)
+        env = dict(os.environ)
+        env.update({k: str(v) for k, v in rung.env.items()})
+        env.update({"MASTER_PORT": port, "TORCHELASTIC_USE_AGENT_STORE": "False",
+                    CHILD_ENV: "1", RUNG_ENV: rung.name, HEARTBEAT_ENV: hb})
+        if self.rank == 0:
+            env[RESULT_ENV] = res
+        else:
+            env.pop(RESULT_ENV, None)
+        fault = rung_fault(rung.name, os.environ.get("DNN_LADDER_FAULT", ""))
+        if fault:
+            env["DNN_FAULT"] = fault
+        cmd = list(self.command(rung))
+        heartbeat_t = time.monotonic()
+        with open(hb, "w") as f:
+            f.write("spawn\n")
+        t0 = time.monotonic()
+        p = subprocess.Popen(cmd, env=env, start_new_session=True)
+        mine = None      # this rank's outcome: exit code or "stall" / "killed"
+        tail = ""
+        while True:
+            rc = p.poll()
+            if mine is None and rc is not None:
+                mine = str(rc)
+                self.store.set(self._key(i, f"rc/{self.rank}"), mine)
+            rcs = self._peer_rcs(i)
+            if mine is None:
+                failed = [r for r, v in rcs.items() if v != "0" and r != self.rank]
+                try:
+                    mt = os.path.getmtime(hb)
+                    heartbeat_t = max(heartbeat_t, time.monotonic() - (time.time() - mt))
+                except OSError:
+                    pass
+                stalled = time.monotonic() - heartbeat_t > self.stall
+                if failed or stalled:
+                    _kill(p)
+                    mine = "stall" if stalled and not failed else "killed"
+                    try:
+                        with open(hb) as f:
+                            tail = f.read().strip()[-200:]
+                    except OSError:
+                        pass
+                    self.store.set(self._key(i, f"rc/{self.rank}"), mine)
+                    rcs[self.rank] = mine
+            if mine is not None and len(rcs) == self.world:
+                break
+            time.sleep(0.2)
+        ok = all(v == "0" for v in rcs.values())
+        result = None
+        if ok and self.rank == 0:
+            try:
+                with open(res) as f:
+                    result = json.load(f)
+            except (OSError, ValueError) as e:
+                ok = False
+                rcs[0] = f"no result ({e.__class__.__name__})"
+        if self.rank == 0:  # rank 0's view decides whether its result is usable: share it
+            self.store.set(self._key(i, "ok"), "1" if ok else "0")
+        ok = self.store.get(self._key(i, "ok")).decode() == "1"
+        # every rank has read the outcome before rank 0 (which may host the store) moves on or
+        # exits
+        self.store.add(self._key(i, "read"), 1)
+        if self.rank == 0:
+            while self.store.add(self._key(i, "read"), 0) < self.world:
+                time.sleep(0.05)
+        rec ={"rung": rung.name, "ok": ok, "seconds": round(time.monotonic() - t0, 1),
+               "rc": {str(r): rcs[r] for r in sorted(rcs)}}
+        if tail and not ok:
+            rec["last_heartbeat"] = tail
+        self.attempts.append(rec)
+        self.log(f"attempt {i} rung {rung.name}: {'ok' if ok else 'FAILED'} {rec['rc']}")
+        return ok, result
+
+    def climb(self, rungs: Sequence[Rung]) -> tuple[Optional[dict], Optional[Rung]]:
+        """Try ``rungs`` in order until one succeeds; (rank 0's result or None, the rung)."""
+        for rung in rungs:
+            ok, result = self.attempt(rung)
+            if ok:
+                return result, rung
+        return None, None

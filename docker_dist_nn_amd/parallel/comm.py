@@ -337,6 +337,18 @@ class IpcPipe:
             raise RuntimeError(f"IPC transport unavailable (peer mapping failed on a rank; "
                                f"here: {err!r})")
 
+    def close(self) -> None:
+        """Drop what only this transport uses -- relay slots, the flag block, peer mappings --
+        when the job falls back to another transport (they were pinned for the
+        life of the process). The re-homed receive buffers stay: the stage's recorded programs
+        read them whatever the transport. Uncached memory is freed when its last tensor view
+        dies (utils/devmem.py)."""
+        self.relay_bufs = []
+        self.relay_out = {"f": [], "b": []}
+        self.relay_dst = []
+        self.prev = self.next = None
+        self.flags = None
+
     def _uc(self, shape, dtype):
         from ..utils.devmem import uncached_zeros
 

@@ -76,6 +76,13 @@ SWITCHES: dict[str, tuple[str, str]] = {
                       "kernel) | auto (streams when GPU_MAX_HW_QUEUES >= 6)"),
     "DNN_FIRST_STEP_TIMEOUT": ("60", "bench.py: seconds the first multi-rank step may take "
                                "before the plan trace is printed and the run exits"),
+    "DNN_LADDER": ("1", "bench.py with WORLD_SIZE > 1: a supervisor per rank runs each attempt "
+                        "in fresh child processes and climbs the fallback ladder (ladder.py) "
+                        "on a hang or crash; 0 = measure in this process"),
+    "DNN_LADDER_STALL": ("180", "ladder: seconds a child may go without a heartbeat before "
+                                "it is killed and the next rung runs"),
+    "DNN_LADDER_FAULT": ("", "ladder fault injection (tests): 'rung=stage:S,step:N,kind:K;...' "
+                             "-- the child of that rung gets DNN_FAULT (stage = rank)"),
     "DNN_PIPE": ("auto", "pipeline transport: auto (IPC with relays on RCCL jobs when every "
                          "GPU maps its peers, first step verified against RCCL) | rccl | ipc "
                          "(xGMI peer copies + stream flags)"),
@@ -84,6 +91,9 @@ SWITCHES: dict[str, tuple[str, str]] = {
                                "min(2, world - 2)"),
     "DNN_IPC_VERIFY": ("auto", "verify the first IPC step bitwise against the fallback "
                                "transport: auto (with DNN_PIPE=auto) | 1 | 0"),
+    "DNN_VERIFY_FLAG_TIMEOUT": ("20", "seconds a flag wait of the IPC first-step "
+                                      "verification may spin before the step is declared "
+                                      "stalled (steady state: DNN_FLAG_TIMEOUT, 120 s)"),
     "DNN_FAULT_IPC_VERIFY": ("", "ranks whose IPC verification step is corrupted (tests the "
                                  "fallback)"),
     "DNN_SERVE_REPLAY": ("graph", "serving engine replay: graph | native | eager"),

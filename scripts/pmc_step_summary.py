@@ -1,44 +1,107 @@
-"""Per-kernel derived metrics of the headline step from scripts/gpu_pmc_step.sh output:
+"""Per-DISPATCH derived metrics of one training step from a PMC run (scripts/pmc_step.sh):
 HBM read/write MB (FETCH_SIZE / WRITE_SIZE, KiB units), MFMA busy share of the kernel's GPU
-cycles, LDS bank-conflict share of LDS cycles. Kernels are keyed by name + grid, averaged over
-dispatches. Usage: python scripts/pmc_step_summary.py gpurun_out/pmc_step
+cycles, LDS bank-conflict share of LDS cycles, duration.
+
+Rows are keyed by the kernel's POSITION in the step (dispatch order), not by name + grid: the
+headline step's fwd 784->512 and dgrad 256->512 are the same kernel with the same grid and
+used to be merged into one row. The step period is found as the shortest
+repeating suffix of the dispatch-name sequence; each position is averaged over the last
+``--steps`` periods of every pass. Usage:
+    python scripts/pmc_step_summary.py gpurun_out/pmc_step [--steps 2]
 
 Calibration (MI355X, measured): SQ_VALU_MFMA_BUSY_CYCLES = MFMA instructions x 16 summed over
 all SIMDs; GRBM_GUI_ACTIVE counts GPU cycles summed over the 8 XCDs. MFMA% = busy / (cycles/8 x
-1024 SIMDs) = the kernel's share of the dense bf16 MFMA peak at the clock it ran.
-FETCH_SIZE / WRITE_SIZE are KiB."""
+1024 SIMDs) = the kernel's share of the dense bf16 MFMA peak at the clock it ran."""
+import argparse
 import csv
 import glob
-import sys
+import os
+import re
 from collections import defaultdict
 
-root = sys.argv[1]
-vals = defaultdict(lambda: defaultdict(list))
-dur = defaultdict(list)
-for pas in ("sq", "fetch", "write"):
-    for f in glob.glob(f"{root}/{pas}/**/*counter_collection.csv", recursive=True):
-        with open(f) as fh:
-            for r in csv.DictReader(fh):
-                key = (r["Kernel_Name"][:70], r.get("Grid_Size", r.get("Grid_Size_X", "")))
-                vals[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
-    for f in glob.glob(f"{root}/{pas}/**/*kernel_trace.csv", recursive=True):
-        with open(f) as fh:
-            for r in csv.DictReader(fh):
-                key = (r["Kernel_Name"][:70], r.get("Grid_Size_X", ""))
-                dur[key].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 
-print(f"{'kernel':72s} {'grid':>8s} {'us':>7s} {'rd MB':>7s} {'wr MB':>7s} {'TB/s':>6s} "
-      f"{'MFMA%':>6s} {'LDSc%':>6s}")
-for key, c in sorted(vals.items(), key=lambda kv: kv[0][0]):
-    if not any(t in key[0] for t in ("gemm", "reduce", "sgd", "mlp_tail", "Cijk", "colsum")):
-        continue
-    m = {k: sum(v) / len(v) for k, v in c.items()}
-    us = dur.get(key) or dur.get((key[0], ""), [0.0])
-    us = sorted(us)[len(us) // 2] if us else 0.0
-    rd = m.get("FETCH_SIZE", 0) / 1024
-    wr = m.get("WRITE_SIZE", 0) / 1024
-    bw = (rd + wr) / us if us else 0  # MB/us = TB/s
-    cyc = m.get("GRBM_GUI_ACTIVE", 0) / 8
-    mf = 100 * m.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / max(1.0, cyc * 1024)
-    lc = 100 * m.get("SQ_LDS_BANK_CONFLICT", 0) / max(1, m.get("SQ_LDS_IDX_ACTIVE", 1))
-    print(f"{key[0]:72s} {key[1]:>8s} {us:7.1f} {rd:7.1f} {wr:7.1f} {bw:6.2f} {mf:6.1f} {lc:6.2f}")
+def short(name: str) -> str:
+    name = re.sub(r"\(.*$", "", name)
+    name = name.replace("gemm_bf16_kernel<", "gemm<").replace("dnn::", "")
+    return name[:60]
+
+
+def load_pass(d):
+    """{dispatch id: (name, grid, {counter: value}, us)} of one pass directory."""
+    cnt = defaultdict(dict)
+    meta = {}
+    for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                i = int(r["Dispatch_Id"])
+                cnt[i][r["Counter_Name"]] = cnt[i].get(r["Counter_Name"], 0.0) + \
+                    float(r["Counter_Value"])
+                meta[i] = (r["Kernel_Name"], r.get("Grid_Size", r.get("Grid_Size_X", "")))
+    dur = {}
+    for f in glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                i = int(r["Dispatch_Id"])
+                dur[i] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+                if i not in meta:
+                    meta[i] = (r["Kernel_Name"], r.get("Grid_Size_X", r.get("Grid_Size", "")))
+    return {i: (meta[i][0], meta[i][1], cnt.get(i, {}), dur.get(i, 0.0)) for i in sorted(meta)}
+
+
+def period(names, max_p=200):
+    """Shortest p such that the last 2p names are two copies of one period."""
+    for p in range(1, min(max_p, len(names) // 2) + 1):
+        if names[-p:] == names[-2 * p:-p]:
+            return p
+    return len(names)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("root")
+    ap.add_argument("--steps", type=int, default=2)
+    a = ap.parse_args()
+    acc = defaultdict(lambda: defaultdict(list))
+    names_of = {}
+    p_seen = None
+    for pas in sorted(os.listdir(a.root)):
+        d = os.path.join(a.root, pas)
+        if not os.path.isdir(d):
+            continue
+        disp = load_pass(d)
+        if not disp:
+            continue
+        ids = list(disp)
+        names = [disp[i][0] for i in ids]
+        p = period(names)
+        p_seen = p
+        last = ids[-p * a.steps:]
+        for k, i in enumerate(last):
+            pos = k % p
+            name, grid, c, us = disp[i]
+            names_of[pos] = (name, grid)
+            acc[pos]["us"].append(us)
+            for cn, v in c.items():
+                acc[pos][cn].append(v)
+    print(f"step period: {p_seen} dispatches; averaged over the last {a.steps} steps")
+    print(f"{'#':>3s} {'kernel':60s} {'grid':>8s} {'us':>7s} {'rd MB':>7s} {'wr MB':>7s} "
+          f"{'TB/s':>6s} {'MFMA%':>6s} {'LDSc%':>6s}")
+    tot = 0.0
+    for pos in sorted(acc):
+        m = {k: sum(v) / len(v) for k, v in acc[pos].items() if v}
+        name, grid = names_of[pos]
+        us = sorted(acc[pos]["us"])[len(acc[pos]["us"]) // 2] if acc[pos]["us"] else 0.0
+        tot += us
+        rd = m.get("FETCH_SIZE", 0) / 1024
+        wr = m.get("WRITE_SIZE", 0) / 1024
+        bw = (rd + wr) / us if us else 0  # MB/us = TB/s
+        cyc = m.get("GRBM_GUI_ACTIVE", 0) / 8
+        mf = 100 * m.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / max(1.0, cyc * 1024)
+        lc = 100 * m.get("SQ_LDS_BANK_CONFLICT", 0) / max(1, m.get("SQ_LDS_IDX_ACTIVE", 1))
+        print(f"{pos:3d} {short(name):60s} {grid:>8s} {us:7.1f} {rd:7.1f} {wr:7.1f} {bw:6.2f} "
+              f"{mf:6.1f} {lc:6.2f}")
+    print(f"sum of kernel durations (profiled, serialised): {tot:.1f} us")
+
+
+if __name__ == "__main__":
+    main()

@@ -520,3 +520,25 @@ def test_ipc_first_step_verification_and_fallback(dev, world, relays):
             transport, reason = got.pop().split("\n")[:2]
             assert transport == want, (tag, transport, reason)
             assert ("verified" in reason) if tag == "ok" else ("differed" in reason), reason
+
+
+def test_uncached_buffers_freed_with_their_last_view(dev):
+    """utils/devmem.py: an uncached receive / relay buffer lives as long as any tensor view of
+    it and is freed when the last one dies (they used to be pinned until exit)."""
+    import gc
+
+    from docker_dist_nn_amd.utils.devmem import live_buffers, uncached_zeros
+
+    gc.collect()
+    n0 = live_buffers()
+    t = uncached_zeros((64, 128), torch.bfloat16, dev)
+    v = t[3:5]
+    del t
+    gc.collect()
+    assert live_buffers() == n0 + 1  # the view keeps the allocation
+    v.fill_(1.5)
+    torch.cuda.synchronize(dev)
+    assert float(v.float().sum()) == 1.5 * 2 * 128
+    del v
+    gc.collect()
+    assert live_buffers() == n0

@@ -1,0 +1,126 @@
+"""The fail-safe ladder's supervisors (docker_dist_nn_amd/ladder.py), on CPU.
+
+Two supervisor ranks (under torch.distributed.run, so through the elastic agent's store, and
+with rank 0 hosting the store) run a fake child per attempt: on rung "a" rank 0 hangs without
+heartbeats (killed as stalled; rank 1, alive and beating, is killed because its peer failed),
+on rung "b" rank 1 crashes (rank 0 killed), rung "c" succeeds. Every supervisor must agree on
+every outcome and rank 0 must report rung c's result with all three attempts listed."""
+import json
+import os
+import socket
+import subprocess
+import sys
+import textwrap
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+SCRIPT = textwrap.dedent("""
+    import json, os, sys, time
+    sys.path.insert(0, {root!r})
+    from docker_dist_nn_amd import ladder
+    rank = int(os.environ["RANK"])
+    if ladder.is_child():
+        ladder.heartbeat("start")
+        fault = os.environ.get("DNN_FAULT", "")
+        mine = f"stage:{{rank}}," in fault + ","
+        if fault and mine and "kind:hang" in fault:
+            while True:          # a hang: no heartbeat, never exits
+                time.sleep(1)
+        if fault and mine and "kind:crash" in fault:
+            os._exit(87)
+        if fault:                # a healthy rank of a failing attempt: alive, beating, stuck
+            while True:
+                ladder.heartbeat("waiting for a peer")
+                time.sleep(0.2)
+        ladder.write_result({{"rung": os.environ[ladder.RUNG_ENV],
+                              "port": os.environ["MASTER_PORT"]}})
+        sys.exit(0)
+    world = int(os.environ["WORLD_SIZE"])
+    sup = ladder.Supervisor(lambda r: [sys.executable, __file__], rank=rank, world=world,
+                            stall=3.0)
+    res, rung = sup.climb([ladder.Rung("a"), ladder.Rung("b"), ladder.Rung("c")])
+    print(json.dumps({{"rank": rank, "res": res, "rung": rung.name if rung else None,
+                      "attempts": sup.attempts}}), flush=True)
+""")
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _check(outs):
+    recs = [json.loads(l) for o in outs for l in o.splitlines() if l.startswith("{")]
+    assert sorted(r["rank"] for r in recs) == [0, 1], outs
+    for r in recs:
+        assert r["rung"] == "c"
+        a = r["attempts"]
+        assert [x["rung"] for x in a] == ["a", "b", "c"]
+        assert [x["ok"] for x in a] == [False, False, True]
+        assert a[0]["rc"] == {"0": "stall", "1": "killed"}, a[0]
+        assert a[1]["rc"] == {"0": "killed", "1": "87"}, a[1]
+        assert a[2]["rc"] == {"0": "0", "1": "0"}
+    r0 = next(r for r in recs if r["rank"] == 0)
+    assert r0["res"]["rung"] == "c"
+    ports = {r0["res"]["port"]}
+    assert len(ports) == 1
+
+
+FAULT = "a=stage:0,step:0,kind:hang;b=stage:1,step:0,kind:crash"
+
+
+def _env(tmp_path):
+    env = dict(os.environ)
+    env.update(DNN_LADDER_FAULT=FAULT, TMPDIR=str(tmp_path), PYTHONPATH=ROOT)
+    return env
+
+
+@pytest.mark.timeout(120)
+def test_ladder_supervisors_agree_torchrun(tmp_path):
+    script = tmp_path / "sup.py"
+    script.write_text(SCRIPT.format(root=ROOT))
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+                        "--master-port", str(_port()), str(script)],
+                       env=_env(tmp_path), capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    _check([r.stdout])
+
+
+@pytest.mark.timeout(120)
+def test_ladder_supervisors_agree_own_store(tmp_path):
+    script = tmp_path / "sup.py"
+    script.write_text(SCRIPT.format(root=ROOT))
+    port = _port()
+    procs = []
+    for rank in range(2):
+        env = _env(tmp_path)
+        env.pop("TORCHELASTIC_USE_AGENT_STORE", None)
+        env.update(RANK=str(rank), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(script)], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                                      text=True))
+    outs = []
+    for p in procs:
+        o, e = p.communicate(timeout=110)
+        assert p.returncode == 0, e[-3000:]
+        outs.append(o)
+    _check(outs)
+
+
+def test_rung_fault_parse():
+    from docker_dist_nn_amd.ladder import bench_rungs, rung_fault
+
+    assert rung_fault("b", FAULT) == "stage:1,step:0,kind:crash"
+    assert rung_fault("z", FAULT) == ""
+    names = [r.name for r in bench_rungs(8)]
+    assert names == ["default", "rccl-slotted", "rccl-streams", "python", "dp-native",
+                     "dp-python"]
+    assert [r.name for r in bench_rungs(4, dp_only=True)] == ["dp-native", "dp-python"]
+    assert bench_rungs(4)[-1].args == ["--parallelism", "dp4"]
