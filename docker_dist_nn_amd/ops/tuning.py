@@ -10,7 +10,10 @@ Signatures (the GEMM as the kernel sees it: C[M][N] = sum over K):
   dgrad : M = rows, N = layer input width,  K = layer output width
   wgrad : M = layer output width, N = layer input width, K = rows (split-K contraction)
 ``DNN_TUNED=0`` disables the table (A/B against the rules); ``DNN_TUNED_TABLE`` reads another
-table file (A/B of two tunings).
+table file (A/B of two tunings). Such a file may be an override table --
+``{"base": "default", "override": {signature: entry or null}}`` -- which is the default table
+with those entries replaced (null: removed); experiment tables are kept in that form
+(``scripts/table_diff.py`` converts full copies).
 """
 from __future__ import annotations
 
@@ -19,17 +22,34 @@ import os
 from typing import Optional
 from .. import switches
 
-TABLE_PATH = (switches.get("DNN_TUNED_TABLE") or
-              os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_gfx950.json"))
+DEFAULT_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned_gfx950.json")
+TABLE_PATH = switches.get("DNN_TUNED_TABLE") or DEFAULT_PATH
 _table: Optional[dict] = None
+
+
+def load_table(path: str) -> dict:
+    """Entries of a table file; an override table is applied on top of the default table."""
+    with open(path) as f:
+        doc = json.load(f)
+    if "override" not in doc:
+        return doc.get("entries", {})
+    if doc.get("base", "default") != "default":
+        raise ValueError(f"{path}: override tables apply to the default table only")
+    with open(DEFAULT_PATH) as f:
+        entries = dict(json.load(f).get("entries", {}))
+    for k, v in doc["override"].items():
+        if v is None:
+            entries.pop(k, None)
+        else:
+            entries[k] = v
+    return entries
 
 
 def _load() -> dict:
     global _table
     if _table is None:
         try:
-            with open(TABLE_PATH) as f:
-                _table = json.load(f).get("entries", {})
+            _table = load_table(TABLE_PATH)
         except FileNotFoundError:
             _table = {}
     return _table
