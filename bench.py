@@ -106,7 +106,7 @@ def _plan(a, spec, n, world, text):
     # the relayed IPC transport the trainer picks first on an RCCL job (engine/trainer.py
     # _pick_pipe); a run that falls back to RCCL reports it in "transport"
     kr = switches.get("DNN_IPC_RELAYS")
-    relays = (min(2, max(0, n - 2)) if kr == "auto" else int(kr)) \
+    relays = ("plan" if kr == "auto" else int(kr)) \
         if switches.get("DNN_PIPE") in ("auto", "ipc") and n > 1 else 0
     planner = Planner.calibrated(spec, relays=relays,
                                  dp_grad_bytes=2.0 if a.dp_reduce == "shard" else 4.0)

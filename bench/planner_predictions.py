@@ -1,7 +1,7 @@
 """Planner predictions for every BASELINE config at N = 1, 2, 4, 8 GPUs (weak scaling):
 the pipeline layout bench.py runs (bf16 and fp8 hops) and the data-parallel-only layout.
 
-    python bench/planner_predictions.py > profiles/r2_planner/predictions.jsonl
+    python bench/planner_predictions.py > profiles/r4_planner/predictions.jsonl
 """
 from __future__ import annotations
 
@@ -23,16 +23,20 @@ def main():
         pl = Planner.calibrated(spec)
         p8 = Planner.calibrated(spec, boundary_bytes=FP8_BYTES)
         pr = Planner.calibrated(spec, relays=2)  # DNN_PIPE=ipc DNN_IPC_RELAYS=2
+        pa = Planner.calibrated(spec, relays="plan")  # DNN_IPC_RELAYS=auto: per-hop plan
         for n in (1, 2, 4, 8):
             a = pl.pipeline_layout(spec, n, rows)
             b = p8.evaluate(spec, a.pp, a.dp, rows * a.pp, distribution=a.distribution)
             c = pr.evaluate(spec, a.pp, a.dp, rows * a.pp, distribution=a.distribution)
+            e = pa.pipeline_layout(spec, n, rows)
             d = pl.evaluate(spec, 1, n, rows)
             print(json.dumps({"model": model, "n": n, "layout": a.parallelism,
                               "dist": a.distribution, "nm": a.num_micro,
                               "pipe_bf16_Msps": round(a.samples_per_s / 1e6, 1),
                               "pipe_fp8_Msps": round(b.samples_per_s / 1e6, 1),
                               "pipe_ipc_relay2_Msps": round(c.samples_per_s / 1e6, 1),
+                              "pipe_ipc_planned_Msps": round(e.samples_per_s / 1e6, 1),
+                              "planned_dist": e.distribution,
                               "dp_only_Msps": round(d.samples_per_s / 1e6, 1),
                               "dp_allreduce_ms": d.detail["allreduce_ms"]}))
 

@@ -252,7 +252,11 @@ class Trainer:
             return DistPipe(mesh, st)
         kr = switches.get("DNN_IPC_RELAYS")
         world = mesh.pp * mesh.dp
-        k = min(2, max(0, world - 2)) if kr == "auto" else int(kr)
+        hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+        if kr == "auto":  # per-hop relay counts from the directed-link load model
+            k = self.relay_table(mesh, max_duties=max(0, min(6, hwq - 6)))
+        else:
+            k = int(kr)
         verify = switches.get("DNN_IPC_VERIFY")
         verify = mode == "auto" if verify == "auto" else verify == "1"
         try:
@@ -262,17 +266,35 @@ class Trainer:
                 raise
             self.transport_reason = f"IPC set-up failed: {e}"[:300]
             return DistPipe(mesh, st)
-        hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
         if mode == "auto" and 4 + len(ipc.duties) > hwq:
             ipc.close()
             self.transport_reason = (f"IPC plan needs {4 + len(ipc.duties)} hardware queues, "
                                      f"GPU_MAX_HW_QUEUES={hwq}")
             return DistPipe(mesh, st)
-        self.transport_reason = (f"ipc, {k} relays per hop" +
+        kdesc = (f"{k} relays per hop" if isinstance(k, int) else
+                 "per-hop relays " + "/".join(str(len(v)) for h, v in sorted(k.items())
+                                              if h[2] == "f" and h[0] < mesh.pp))
+        self.transport_reason = (f"ipc, {kdesc}" +
                                  (" (verification pending: first step)" if verify else ""))
         if verify:
             self._ipc_verify = (ipc, DistPipe(mesh, st))
         return ipc
+
+    def relay_table(self, mesh, max_duties: int = 6) -> dict:
+        """comm.relay_plan for this job: per step, every boundary hop moves rows x padded
+        width x 2 bytes each way and every stage's DP group exchanges its bf16 gradient and
+        weights; the same table on every rank (a pure function of the layout)."""
+        from ..models.mlp import round_up
+        from ..parallel.comm import relay_plan
+
+        rows = self.micro_batch * self.num_micro
+        hop_bytes = [rows * round_up(self.spec.layers[p.layer_end - 1].out_dim, 64) * 2
+                     for p in self.plans[:-1]]
+        dp_bytes = [2 * (mesh.dp - 1) / mesh.dp * 2 *
+                    sum(l.params for l in self.spec.layers[p.layer_start:p.layer_end])
+                    for p in self.plans]
+        return relay_plan(mesh.pp, mesh.dp, hop_bytes, dp_bytes=dp_bytes,
+                          max_k=min(6, mesh.pp * mesh.dp - 2), max_duties=max_duties)
 
     def _peers_mappable(self, mesh) -> bool:
         """Every rank can map every other rank's GPU (one rank per GPU on one node; a relay can

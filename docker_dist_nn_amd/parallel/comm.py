@@ -193,6 +193,174 @@ def relay_assignment(pp: int, dp: int, k: int) -> dict:
     return out
 
 
+def relay_plan(pp: int, dp: int, hop_bytes, dp_bytes=None, max_k: int = 6,
+               max_duties: int = 6, relay_eff: float = 0.8) -> dict:
+    """Relay ranks of every directed pipeline hop, chosen PER HOP from a load model of the
+    node's directed xGMI links (each GPU pair has its own link both ways):
+
+    * a hop src -> dst of boundary b moves ``hop_bytes[b]`` per step; with k relays its rows
+      are striped over k + 1 paths -- the direct link and src -> r -> dst for each relay -- so
+      each path carries 1/(k + 1) of the bytes, a relayed path's two links at 1/relay_eff (the
+      relay re-reads the stripe from its HBM and adds a hop of latency);
+    * data-parallel traffic (``dp_bytes[s]`` per step for the stage-s gradient exchange of a
+      ring over the replicas) loads the links between replicas of a stage;
+    * widest hops first (two passes), each hop takes the relay count k <= ``max_k`` that
+      minimises its own transfer time -- the most loaded link on any of its paths, given
+      everything else on the links -- adding relays least-loaded first, each extra relay kept
+      only if it saves >= 2 % (a relay costs a stream on its rank and HBM traffic there); a
+      rank takes at most ``max_duties`` relay duties.
+
+    The wide boundary of a pipeline (e.g. 784-512-... at pp4: 512 columns after stage 0, 4x
+    the 128-column one) thus gets more paths than the narrow ones, instead of the uniform
+    ``relay_assignment`` k. Returns {(src, dst, "f" | "b"): [relay ranks]} -- a pure function
+    of its arguments: every rank computes the same table. Rank = replica * pp + stage."""
+    world = pp * dp
+    hops = []  # (src, dst, direction, bytes)
+    for r in range(dp):
+        for s in range(pp - 1):
+            a, b = r * pp + s, r * pp + s + 1
+            hops += [(a, b, "f", float(hop_bytes[s])), (b, a, "b", float(hop_bytes[s]))]
+    load = {}
+
+    def add(link, v):
+        load[link] = load.get(link, 0.0) + v
+
+    if dp_bytes is not None and dp > 1:
+        for s in range(pp):
+            ring = [r * pp + s for r in range(dp)]
+            for i, a in enumerate(ring):
+                b = ring[(i + 1) % dp]
+                if a != b:
+                    add((a, b), float(dp_bytes[s]))
+    relays = {(h[0], h[1], h[2]): [] for h in hops}
+    duties = [0] * world
+
+    def contribution(h, rl, sign):
+        src, dst, _d, nb = h
+        frac = nb / (len(rl) + 1)
+        add((src, dst), sign * frac)
+        for x in rl:
+            add((src, x), sign * frac / relay_eff)
+            add((x, dst), sign * frac / relay_eff)
+
+    def hop_time(h, rl):  # h's most loaded link once its stripes are on (h not in `load`)
+        src, dst, _d, nb = h
+        frac = nb / (len(rl) + 1)
+        t = load.get((src, dst), 0.0) + frac
+        for x in rl:
+            t = max(t, load.get((src, x), 0.0) + frac / relay_eff,
+                    load.get((x, dst), 0.0) + frac / relay_eff)
+        return t
+
+    for h in hops:
+        contribution(h, [], +1)
+    order = sorted(hops, key=lambda h: (-h[3], h[0], h[1]))
+    for _ in range(2):
+        for h in order:
+            key = (h[0], h[1], h[2])
+            contribution(h, relays[key], -1)
+            for x in relays[key]:
+                duties[x] -= 1
+            best_rl, best_t = [], hop_time(h, [])
+            rl = []
+            while len(rl) < max_k:
+                cands = [x for x in range(world) if x not in (h[0], h[1]) and x not in rl and
+                         duties[x] < max_duties]
+                if not cands:
+                    break
+                x = min(cands, key=lambda x: (max(load.get((h[0], x), 0.0),
+                                                  load.get((x, h[1]), 0.0)), duties[x],
+                                              (x - h[0]) % world))
+                rl = rl + [x]
+                t = hop_time(h, rl)
+                if t < best_t * 0.98:
+                    best_rl, best_t = list(rl), t
+            relays[key] = best_rl
+            for x in best_rl:
+                duties[x] += 1
+            contribution(h, best_rl, +1)
+    return relays
+
+
+def relay_link_loads(pp: int, dp: int, table: dict, hop_bytes, dp_bytes=None,
+                     relay_eff: float = 0.8) -> dict:
+    """Per-hop transfer cost under ``table``: {(src, dst, dir): bytes-equivalent of the most
+    loaded link on any of the hop's paths} (the planner's effective hop bandwidth)."""
+    load = {}
+
+    def add(link, v):
+        load[link] = load.get(link, 0.0) + v
+
+    hops = {}
+    for r in range(dp):
+        for s in range(pp - 1):
+            a, b = r * pp + s, r * pp + s + 1
+            hops[(a, b, "f")] = hops[(b, a, "b")] = float(hop_bytes[s])
+    if dp_bytes is not None and dp > 1:
+        for s in range(pp):
+            ring = [r * pp + s for r in range(dp)]
+            for i, a in enumerate(ring):
+                b = ring[(i + 1) % dp]
+                if a != b:
+                    add((a, b), float(dp_bytes[s]))
+    for (src, dst, d), nb in hops.items():
+        rl = table.get((src, dst, d), [])
+        frac = nb / (len(rl) + 1)
+        add((src, dst), frac)
+        for x in rl:
+            add((src, x), frac / relay_eff)
+            add((x, dst), frac / relay_eff)
+    out = {}
+    for (src, dst, d), nb in hops.items():
+        rl = table.get((src, dst, d), [])
+        links = [(src, dst)] + [l for x in rl for l in ((src, x), (x, dst))]
+        out[(src, dst, d)] = max(load[l] for l in links)
+    return out
+
+
+class RelayLayout:
+    """One rank's view of a relay table (relay_plan / relay_assignment): stripe counts of its
+    own hops, its relay duties, the flag-block indices and the relay slot sizes. The flag block
+    reserves kmax + 1 stripe flags per micro-batch and direction (kmax = the table's largest
+    k), so every rank computes every peer's flag indices without knowing the peer's hops."""
+
+    def __init__(self, table: dict, me: int, prev: Optional[int], nxt: Optional[int], nm: int,
+                 mb: int):
+        self.table = table
+        self.nm, self.mb = nm, mb
+        self.kmax = max((len(v) for v in table.values()), default=0)
+        hk = lambda h: len(table.get(h, []))  # noqa: E731
+        self.k_in = {"f": hk((prev, me, "f")) if prev is not None else 0,
+                     "b": hk((nxt, me, "b")) if nxt is not None else 0}
+        self.k_out = {"f": hk((me, nxt, "f")) if nxt is not None else 0,
+                      "b": hk((me, prev, "b")) if prev is not None else 0}
+        # my duties, in table order: (src, dst, direction, stripe index), their hops' k
+        self.duties = [(h[0], h[1], h[2], rl.index(me) + 1) for h, rl in table.items()
+                       if me in rl]
+        self.duty_k = [hk((d[0], d[1], d[2])) for d in self.duties]
+        self.ackf = 2 * nm * (self.kmax + 1)
+        self.ackb = self.ackf + 1
+        self.n_flags = self.ackf + 2 + len(self.duties) * nm
+
+    def fidx(self, j: int, p: int = 0) -> int:
+        return j * (self.kmax + 1) + p
+
+    def bidx(self, j: int, p: int = 0) -> int:
+        return self.nm * (self.kmax + 1) + j * (self.kmax + 1) + p
+
+    def ridx(self, d: int, j: int) -> int:
+        return self.ackf + 2 + d * self.nm + j
+
+    def part_max(self, k: int) -> int:
+        """Rows of the largest stripe of a micro-batch split k + 1 ways."""
+        b = relay_parts(0, self.mb, k)
+        return max(y - x for x, y in zip(b, b[1:]))
+
+    def duty_index(self, r: int, hop) -> int:
+        """Index of ``hop`` among rank r's duties (the slot it relays that hop into)."""
+        return [h for h, rl in self.table.items() if r in rl].index(hop)
+
+
 def relay_parts(r0: int, r1: int, k: int) -> list[int]:
     """Row bounds of the k + 1 stripes of rows [r0, r1) (stripe 0 = the direct link)."""
     n = r1 - r0
@@ -251,23 +419,30 @@ class IpcPipe:
         self.stage = stage
         nm = stage.nm
         self.nm = nm
-        self.k = k = int(relays)
         me = mesh.rank
         world = dist.get_world_size()
-        assign = relay_assignment(mesh.pp, mesh.dp, k) if k else {}
+        # relays: k (the same count on every hop, relay_assignment) or a per-hop table
+        # (relay_plan); RelayLayout = this rank's stripes, duties and flag indices
+        if isinstance(relays, dict):
+            assign = relays
+        else:
+            k = int(relays)
+            assign = relay_assignment(mesh.pp, mesh.dp, k) if k else {}
+        self.table = assign
+        self.layout = lay = RelayLayout(assign, me, mesh.prev_rank, mesh.next_rank, nm,
+                                        stage.mb)
+        self.k = lay.kmax
+        self.k_in, self.k_out = lay.k_in, lay.k_out
         # my relay duties, in table order: (src, dst, direction, stripe index)
-        self.duties = [(h[0], h[1], h[2], rl.index(me) + 1) for h, rl in assign.items()
-                       if me in rl]
-        self.ackf = 2 * nm * (k + 1)
-        self.ackb = self.ackf + 1
+        self.duties = lay.duties
+        self.ackf, self.ackb = lay.ackf, lay.ackb
         # Every rank takes part in every collective below even when its local part failed
         # (it sends an error marker instead), and all ranks raise together: one rank raising
         # between two collectives would leave the others blocked in the second one.
         err = None
         mine = {}
         try:
-            self.flags = torch.zeros(self.ackf + 2 + len(self.duties) * nm, dtype=torch.int32,
-                                     device=stage.device)
+            self.flags = torch.zeros(lay.n_flags, dtype=torch.int32, device=stage.device)
             if uncached:  # the buffers peers write into (see utils/devmem.py)
                 self._uncached_recv(stage)
             # destination rows have the source's width: my output == the consumer's input, my
@@ -275,8 +450,8 @@ class IpcPipe:
             self.row_bytes_f = stage.output.stride(0) * stage.output.element_size()
             self.row_bytes_b = (stage.dx_send.stride(0) * stage.dx_send.element_size()
                                 if stage.dx_send is not None else 0)
-            self.part_max = max(b - a for a, b in zip(relay_parts(0, stage.mb, k),
-                                                      relay_parts(0, stage.mb, k)[1:]))
+            # rows of a relay slot per micro-batch: the largest stripe of that duty's hop
+            self.duty_part_max = [lay.part_max(k) for k in lay.duty_k]
         except Exception as e:  # noqa: BLE001 -- agreed on below
             err = e
             self.row_bytes_f = self.row_bytes_b = 0
@@ -286,9 +461,9 @@ class IpcPipe:
         self.relay_bufs = []
         if err is None:
             try:
-                for src, dst, d, _p in self.duties:
+                for (src, dst, d, _p), pm in zip(self.duties, self.duty_part_max):
                     rb = everyone_rb[src][0] if d == "f" else everyone_rb[src][1]
-                    shape = (nm * self.part_max * rb,)
+                    shape = (nm * pm * rb,)
                     buf = (self._uc(shape, torch.uint8) if uncached else
                            torch.zeros(shape, dtype=torch.uint8, device=stage.device))
                     self.relay_bufs.append((buf, rb))
@@ -312,20 +487,18 @@ class IpcPipe:
             self.next = self._peer(everyone, mesh.next_rank)
             imp = lambda r, key: self.n.ipc_import(*everyone[r][key])  # noqa: E731
 
-            def duty_index(r, hop):
-                ds = [h for h, rl in assign.items() if r in rl]
-                return ds.index(hop)
-
-            # my hops' relays: where stripe p >= 1 goes
+            # my hops' relays: where stripe p >= 1 goes (the relay's slot holds, per
+            # micro-batch, the largest stripe of this hop)
             self.relay_out = {"f": [], "b": []}
             for d, peer in (("f", mesh.next_rank), ("b", mesh.prev_rank)):
                 if peer is None:
                     continue
+                pm = lay.part_max(self.k_out[d])
                 for r in assign.get((me, peer, d), []):
-                    di = duty_index(r, (me, peer, d))
+                    di = lay.duty_index(r, (me, peer, d))
                     self.relay_out[d].append({
                         "buf": self.n.ipc_import(*everyone[r]["relay"][di]),
-                        "flags": imp(r, "flags"), "d": di})
+                        "flags": imp(r, "flags"), "d": di, "part_max": pm})
             # my duties' consumers: where my relay slots go
             self.relay_dst = [{"buf": imp(dst, "x_in" if d == "f" else "grad_out"),
                                "flags": imp(dst, "flags")} for _s, dst, d, _p in self.duties]
@@ -367,13 +540,13 @@ class IpcPipe:
             st.dz[-1] = self._uc(tuple(st.dz[-1].shape), st.dz[-1].dtype)
 
     def fidx(self, j: int, p: int = 0) -> int:
-        return j * (self.k + 1) + p
+        return self.layout.fidx(j, p)
 
     def bidx(self, j: int, p: int = 0) -> int:
-        return self.nm * (self.k + 1) + j * (self.k + 1) + p
+        return self.layout.bidx(j, p)
 
     def ridx(self, d: int, j: int) -> int:
-        return self.ackf + 2 + d * self.nm + j
+        return self.layout.ridx(d, j)
 
     def _peer(self, everyone, rank):
         if rank is None:

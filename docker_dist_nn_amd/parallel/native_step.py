@@ -226,7 +226,7 @@ class NativeStep:
         """The producer's copies + flags: wait on the compute stream."""
         p = self.ipc
         base = p.flags.data_ptr()
-        for part in range(p.k + 1):  # the direct stripe and every relayed one
+        for part in range(p.k_in[direction] + 1):  # the direct stripe and every relayed one
             idx = p.fidx(j, part) if direction == "f" else p.bidx(j, part)
             self.ops.append(dict(kind=WAITV, stream=MAIN, a=base + 4 * idx, delta=0))
 
@@ -245,8 +245,9 @@ class NativeStep:
         dst_base = peer["x_in"] if direction == "f" else peer["grad_out"]
         row_bytes = p.row_bytes_f if direction == "f" else p.row_bytes_b
         r = st.rows_of(j)
-        bounds = relay_parts(r.start, r.stop, p.k)
-        for part in range(p.k + 1):  # stripe 0 direct, stripe q via relay q - 1
+        k = p.k_out[direction]  # this hop's relays (per hop: comm.relay_plan)
+        bounds = relay_parts(r.start, r.stop, k)
+        for part in range(k + 1):  # stripe 0 direct, stripe q via relay q - 1
             a0, a1 = bounds[part], bounds[part + 1]
             src = ptr + (a0 - r.start) * row_bytes
             if part == 0:
@@ -257,7 +258,7 @@ class NativeStep:
                                      delta=0))
             else:
                 rel = p.relay_out[direction][part - 1]
-                slot = rel["buf"] + j * p.part_max * row_bytes
+                slot = rel["buf"] + j * rel["part_max"] * row_bytes
                 self.ops.append(dict(kind=COPY, stream=s, a=src, b=slot,
                                      count=(a1 - a0) * row_bytes))
                 self.ops.append(dict(kind=SIGNAL, stream=s,
@@ -472,14 +473,15 @@ class NativeStep:
         for d, ((src, dst, direction, part), dst_ptrs) in enumerate(zip(p.duties, p.relay_dst)):
             stream = 4 + d
             buf, rb = p.relay_bufs[d]
+            k, pm = p.layout.duty_k[d], p.duty_part_max[d]
             for j in range(st.nm):
                 r = st.rows_of(j)  # every stage shares the micro-batch row layout
-                bounds = relay_parts(r.start, r.stop, p.k)
+                bounds = relay_parts(r.start, r.stop, k)
                 a0, a1 = bounds[part], bounds[part + 1]
                 self.ops.append(dict(kind=WAITV, stream=stream,
                                      a=p.flags.data_ptr() + 4 * p.ridx(d, j), delta=0))
                 self.ops.append(dict(kind=COPY, stream=stream,
-                                     a=buf.data_ptr() + j * p.part_max * rb,
+                                     a=buf.data_ptr() + j * pm * rb,
                                      b=dst_ptrs["buf"] + a0 * rb, count=(a1 - a0) * rb))
                 idx = p.fidx(j, part) if direction == "f" else p.bidx(j, part)
                 self.ops.append(dict(kind=SIGNAL, stream=stream, a=dst_ptrs["flags"] + 4 * idx,

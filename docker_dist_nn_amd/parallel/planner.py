@@ -68,10 +68,10 @@ def compositions(n: int, k: int):
 
 # Measured one-GPU training steps on MI355X with the round-2 own-kernel table
 # (profiles/r2_own_kernels, profiles/r2_epilogue): widths -> (rows, ms per step).
-MEASURED_STEP_MS = {
-    (784, 512, 256, 128, 10): (65536, 0.373),
-    (784, 1024, 1024, 1024, 1024, 1024, 1024, 1024, 10): (65536, 3.31),
-    (784, 8192, 8192, 10): (16384, 6.27),
+MEASURED_STEP_MS = {  # round 3: driver BENCH_r03 (headline), profiles/r3b_final4 (others)
+    (784, 512, 256, 128, 10): (65536, 0.350),
+    (784, 1024, 1024, 1024, 1024, 1024, 1024, 1024, 10): (65536, 2.88),
+    (784, 8192, 8192, 10): (16384, 5.96),
 }
 
 
@@ -82,7 +82,7 @@ class Planner:
     def __init__(self, tflops: float = 550.0, link_gbps: float = 64.0,
                  hop_latency_us: float = 15.0, allreduce_gbps: float = 150.0,
                  step_overhead_us: float = 20.0, boundary_bytes: float = 2.0,
-                 dp_grad_bytes: float = 2.0, relays: int = 0, relay_eff: float = 0.8):
+                 dp_grad_bytes: float = 2.0, relays=0, relay_eff: float = 0.8):
         self.rate = tflops * 1e12
         self.link = link_gbps * 1e9
         self.lat = hop_latency_us * 1e-6
@@ -90,10 +90,15 @@ class Planner:
         self.ovh = step_overhead_us * 1e-6
         self.bb = boundary_bytes  # bytes per boundary element on the wire (bf16 = 2)
         self.gb = dp_grad_bytes   # bytes per parameter per DP collective (shard bf16 = 2)
-        # relayed IPC hops (parallel/comm.relay_assignment): a hop's rows striped over the
-        # direct link and `relays` two-link paths, each path worth `relay_eff` of a link (the
-        # relay's second copy adds latency and HBM traffic on the relay GPU)
-        self.hop_bw = self.link * (1.0 + relays * relay_eff)
+        # relayed IPC hops: a hop's rows striped over the direct link and k two-link paths,
+        # each path worth `relay_eff` of a link (the relay's second copy adds latency and HBM
+        # traffic on the relay GPU). relays = k (the same on every hop,
+        # comm.relay_assignment) or "plan": per-hop k from the directed-link load model
+        # (comm.relay_plan -- what the IPC transport uses with DNN_IPC_RELAYS=auto), each hop
+        # costing its most loaded link with every other hop and the DP exchange on the links
+        self.relays = relays
+        self.relay_eff = relay_eff
+        self.hop_bw = self.link * (1.0 + (0 if relays == "plan" else relays) * relay_eff)
 
     @classmethod
     def calibrated(cls, spec: MLPSpec, **kw) -> "Planner":
@@ -105,22 +110,53 @@ class Planner:
             kw["tflops"] = sum(layer_train_flops(spec)) * rows / (ms * 1e-3) / 1e12
         return cls(**kw)
 
-    def _stage_costs(self, spec: MLPSpec, dist: list[int], mb: int):
+    def hop_ratios(self, spec: MLPSpec, dist: list[int], dp: int = 1,
+                   rows: int = 65536) -> list[float]:
+        """Per boundary: seconds per byte of that hop relative to one direct link (1.0 = a
+        link of its own; < 1 with relays). With relays == "plan" this is the slowest direction /
+        replica of the boundary under comm.relay_plan's table."""
+        pp = len(dist)
+        widths, g = [], 0
+        for k in dist[:-1]:
+            g += k
+            widths.append(spec.layers[g - 1].out_dim)
+        if self.relays != "plan" or pp < 2:
+            return [self.link / self.hop_bw] * len(widths)
+        from .comm import relay_link_loads, relay_plan
+
+        hb = [rows * w * self.bb for w in widths]
+        dpb, g = [], 0
+        for k in dist:
+            params = sum(l.params for l in spec.layers[g:g + k])
+            g += k
+            dpb.append(2 * (dp - 1) / max(1, dp) * params * self.gb)
+        table = relay_plan(pp, dp, hb, dp_bytes=dpb, max_k=min(6, pp * dp - 2),
+                           relay_eff=self.relay_eff)
+        loads = relay_link_loads(pp, dp, table, hb, dp_bytes=dpb, relay_eff=self.relay_eff)
+        out = [0.0] * len(widths)
+        for (src, dst, d), v in loads.items():
+            b = min(src, dst) % pp  # boundary between stages b and b + 1
+            out[b] = max(out[b], v / hb[b])
+        return out
+
+    def _stage_costs(self, spec: MLPSpec, dist: list[int], mb: int, dp: int = 1):
         fl = layer_train_flops(spec)
+        ratios = self.hop_ratios(spec, dist, dp, mb)
         comp, hops, g = [], [], 0
         for k in dist:
             comp.append(sum(fl[g:g + k]) * mb / self.rate)
             g += k
             if g < len(spec.layers):
-                hops.append(self.lat + mb * spec.layers[g - 1].out_dim * self.bb / self.hop_bw)
+                hops.append(self.lat + mb * spec.layers[g - 1].out_dim * self.bb *
+                            ratios[len(hops)] / self.link)
         return comp, hops
 
-    def best_distribution(self, spec: MLPSpec, pp: int, mb: int) -> list[int]:
+    def best_distribution(self, spec: MLPSpec, pp: int, mb: int, dp: int = 1) -> list[int]:
         """The split minimising the slowest stage / hop per micro-batch; among hop-bound ties
         (equal-width boundaries), the one with the most balanced compute."""
         best, best_k = None, (float("inf"), float("inf"))
         for dist in compositions(len(spec.layers), pp):
-            comp, hops = self._stage_costs(spec, dist, mb)
+            comp, hops = self._stage_costs(spec, dist, mb, dp)
             k = (round(max(comp + hops), 12), max(comp))
             if k < best_k:
                 best, best_k = dist, k
@@ -140,8 +176,9 @@ class Planner:
         mb = micro_batch or (rows_per_replica if pp == 1 else
                              max(64, rows_per_replica // (4 * pp) // 64 * 64))
         M = max(1, rows_per_replica // mb)
-        dist = distribution or (self.best_distribution(spec, pp, mb) if pp > 1 else [len(L)])
-        comp, hops = self._stage_costs(spec, dist, mb)
+        dist = distribution or (self.best_distribution(spec, pp, mb, dp) if pp > 1
+                                else [len(L)])
+        comp, hops = self._stage_costs(spec, dist, mb, dp)
         per_micro = max(comp + hops)
         pipe = (M + pp - 1) * per_micro if pp > 1 else comp[0]
         ar, g = 0.0, 0

@@ -88,7 +88,8 @@ SWITCHES: dict[str, tuple[str, str]] = {
                          "(xGMI peer copies + stream flags)"),
     "DNN_IPC_RELAYS": ("auto", "ipc transport: stripe every hop over the direct link + this "
                                "many relay ranks (two-link paths; native step only); auto = "
-                               "min(2, world - 2)"),
+                               "per-hop counts from the directed-link load model "
+                               "(comm.relay_plan: up to 6 on 8 ranks, wide boundaries first)"),
     "DNN_IPC_VERIFY": ("auto", "verify the first IPC step bitwise against the fallback "
                                "transport: auto (with DNN_PIPE=auto) | 1 | 0"),
     "DNN_VERIFY_FLAG_TIMEOUT": ("20", "seconds a flag wait of the IPC first-step "
@@ -96,6 +97,9 @@ SWITCHES: dict[str, tuple[str, str]] = {
                                       "stalled (steady state: DNN_FLAG_TIMEOUT, 120 s)"),
     "DNN_FAULT_IPC_VERIFY": ("", "ranks whose IPC verification step is corrupted (tests the "
                                  "fallback)"),
+    "DNN_CHAIN_FAST": ("1", "rank chain: serving-size requests (<= 8 rows) take the device-side "
+                            "chain (serve/fastpath.py: IPC slots + flags, no host hop); 0 = "
+                            "the message-passing chain for every request"),
     "DNN_SERVE_REPLAY": ("graph", "serving engine replay: graph | native | eager"),
     "DNN_SYNC_DEBUG": ("0", "synchronise + check after every kernel (race / fault hunting)"),
     "DNN_AUTOBUILD": ("1", "build the native extension on import if it is missing"),

@@ -28,7 +28,8 @@ from docker_dist_nn_amd.engine.stage import OptimConfig, StageParams
 from docker_dist_nn_amd.models.mlp import LayerGeom
 from docker_dist_nn_amd.parallel import native_step as nsmod
 from docker_dist_nn_amd.parallel import plan_sim
-from docker_dist_nn_amd.parallel.comm import IpcPipe, relay_assignment, relay_parts
+from docker_dist_nn_amd.parallel.comm import (IpcPipe, RelayLayout, relay_assignment,
+                                               relay_parts, relay_plan)
 from docker_dist_nn_amd.parallel.pipeline import schedule_ops
 from docker_dist_nn_amd.partition import plan_stages
 
@@ -109,21 +110,19 @@ def build_rccl(rank, pp, dp, nm, mb=256, spec="784-512-256-128-10", dist=None,
 
 
 def build_ipc(rank, pp, dp, nm, mb, k, width, sched):
+    """k: relays per hop (relay_assignment), or a per-hop table (relay_plan)."""
     spec = MLPSpec.parse("-".join([str(width)] * (pp + 1)))
     st, mesh = _stage(rank, pp, dp, nm, mb, spec, [1] * pp, "bf16", "allreduce")
     st._prog = NS(segments=lambda: {"FINO", "W"})
-    assign = relay_assignment(pp, dp, k) if k else {}
-    ipc = NS(k=k, nm=nm, seq=0)
-    ipc.duties = [(h[0], h[1], h[2], rl.index(rank) + 1) for h, rl in assign.items()
-                  if rank in rl]
-    ipc.ackf = 2 * nm * (k + 1)
-    ipc.ackb = ipc.ackf + 1
+    assign = k if isinstance(k, dict) else (relay_assignment(pp, dp, k) if k else {})
+    lay = RelayLayout(assign, rank, mesh.prev_rank, mesh.next_rank, nm, mb)
+    ipc = NS(k=lay.kmax, nm=nm, seq=0, layout=lay, k_in=lay.k_in, k_out=lay.k_out,
+             duties=lay.duties, ackf=lay.ackf, ackb=lay.ackb)
     for f in ("fidx", "bidx", "ridx"):
         setattr(ipc, f, getattr(IpcPipe, f).__get__(ipc))
     ipc.flags = FakeTensor(_addr(rank, "flags"), 1, 1, 4)
     ipc.row_bytes_f = ipc.row_bytes_b = width * 2
-    b = relay_parts(0, mb, k)
-    ipc.part_max = max(y - x for x, y in zip(b, b[1:]))
+    ipc.duty_part_max = [lay.part_max(kk) for kk in lay.duty_k]
     ipc.relay_bufs = [(FakeTensor(_addr(rank, f"relay{d}"), 1, 1, 1), width * 2)
                       for d in range(len(ipc.duties))]
 
@@ -135,17 +134,14 @@ def build_ipc(rank, pp, dp, nm, mb, k, width, sched):
 
     ipc.prev, ipc.next = peer(mesh.prev_rank), peer(mesh.next_rank)
 
-    def duty_index(r, hop):
-        return [h for h, rl in assign.items() if r in rl].index(hop)
-
     ipc.relay_out = {"f": [], "b": []}
     for d, pr in (("f", mesh.next_rank), ("b", mesh.prev_rank)):
         if pr is None:
             continue
         for r in assign.get((rank, pr, d), []):
-            di = duty_index(r, (rank, pr, d))
+            di = lay.duty_index(r, (rank, pr, d))
             ipc.relay_out[d].append({"buf": _addr(r, f"relay{di}"), "flags": _addr(r, "flags"),
-                                     "d": di})
+                                     "d": di, "part_max": lay.part_max(lay.k_out[d])})
     ipc.relay_dst = [{"buf": _addr(dst, "x_in" if d == "f" else "grad_out"),
                       "flags": _addr(dst, "flags")} for _s, dst, d, _p in ipc.duties]
     ex = NS(stages=[st], ops=[schedule_ops(sched, pp, nm, mesh.stage)], kind=sched)
@@ -321,10 +317,22 @@ def test_slotted_groups_match_partner_slots():
 
 
 # ---- IPC transport (xGMI peer copies + flags) ------------------------------------------------
+# the headline model's boundaries (512, 256, 128 columns): the planner's per-hop relay table
+HEAD_HOPS = [512, 256, 128]
+
+
+def _plan_table(pp, dp):
+    return relay_plan(pp, dp, [w * 2 * 65536 for w in (HEAD_HOPS * 3)[:pp - 1]])
+
+
 @pytest.mark.parametrize("pp,dp,k", [(2, 1, 0), (3, 1, 0), (4, 1, 0), (3, 1, 1), (4, 1, 2),
-                                     (4, 2, 0), (4, 2, 2), (8, 1, 2), (2, 4, 2), (4, 2, 6)])
+                                     (4, 2, 0), (4, 2, 2), (8, 1, 2), (2, 4, 2), (4, 2, 4),
+                                     (4, 2, 6), (8, 1, 6), (4, 1, "plan"), (4, 2, "plan"),
+                                     (8, 1, "plan"), (2, 4, "plan")])
 def test_ipc_plans_deadlock_free(pp, dp, k):
     nm = 2 * pp
+    if k == "plan":
+        k = _plan_table(pp, dp)
     builds = {r: build_ipc(r, pp, dp, nm, 64, k, 64, "1f1b") for r in range(pp * dp)}
     for ns in builds.values():
         check_enqueue_order(ns.ops)
@@ -337,10 +345,14 @@ def test_ipc_relay_plans_deadlock_free_per_schedule(sched):
     assert sim(builds, steps=3).makespan > 0
 
 
-def test_relay_stripes_reach_every_row_once():
+@pytest.mark.parametrize("k", [2, 4, 6, "plan"])
+def test_relay_stripes_reach_every_row_once(k):
     """Every consumer row of every micro-batch is written by exactly one COPY (direct or
-    relayed), for every hop of a pp4 x dp2 mesh with 2 relays."""
-    pp, dp, nm, mb, k, width = 4, 2, 4, 64, 2, 64
+    relayed), for every hop of a pp4 x dp2 mesh with k relays per hop, or the planner's
+    per-hop table."""
+    pp, dp, nm, mb, width = 4, 2, 4, 64, 64
+    if k == "plan":
+        k = _plan_table(pp, dp)
     rb = width * 2
     writes = {}
     for r in range(pp * dp):
@@ -353,3 +365,26 @@ def test_relay_stripes_reach_every_row_once():
     assert set(writes.values()) == {1}
     # (pp - 1) boundaries x 2 directions x dp replicas x all rows
     assert len(writes) == (pp - 1) * 2 * dp * nm * mb
+
+
+def test_relay_plan_gives_the_wide_boundary_more_paths():
+    """comm.relay_plan: per-hop relay counts from the directed-link load model. At pp4 x dp2 on
+    the headline model the 512-column boundary gets more relays than the 128-column one, no
+    rank has more duties than allowed, relays never include the hop's own ends, the table is
+    deterministic, and the most loaded link carries far less than the un-relayed wide hop."""
+    from docker_dist_nn_amd.parallel.comm import relay_link_loads
+
+    hb = [w * 2 * 65536 for w in HEAD_HOPS]
+    t = relay_plan(4, 2, hb, max_duties=6)
+    assert t == relay_plan(4, 2, hb, max_duties=6)
+    k = {h: len(v) for h, v in t.items()}
+    assert k[(0, 1, "f")] > k[(2, 3, "f")] and k[(4, 5, "f")] > k[(6, 7, "f")]
+    assert max(k.values()) <= 6
+    duties = {}
+    for (src, dst, _d), rl in t.items():
+        assert src not in rl and dst not in rl and len(set(rl)) == len(rl)
+        for x in rl:
+            duties[x] = duties.get(x, 0) + 1
+    assert max(duties.values()) <= 6
+    loads = relay_link_loads(4, 2, t, hb)
+    assert max(loads.values()) < 0.5 * hb[0]
