@@ -192,7 +192,7 @@ const char* gemm_error_string(int code) {
     case -10: return "colsum needs bf16 output and ld_colsum >= N";
     case -11: return "fused cross-entropy needs bf16 output, N == bn <= 128, a bias and 0 < n_cls <= N";
     case -13: return "relu bit masks need bf16 output, act = relu, ld_mask >= N/8, no aux/xent, one-tile form";
-    case -12: return "pipeline stages must be 2..4, 5 = A3/B2 ring, 6 / 7 = register-prefetched 2 / 3-deep ring (256x256: 6; 256x128, 128x128, 128x64, 64x64: 6, 7), 9 / 10 = the same with the register-direct epilogue (no ct / fused update), 11 = register-direct epilogue on the A3/B2 ring (256x256, 256x128, 128x128), 12..14 = 32-deep k-steps with 2..4 stages (256x256: 12-14, 256x128: 12-13, 128x128: 12, 14) (8-wave tiles: 2, 3, 5; 256x256: 2, 5 or 8 = ping-pong; 5, 12-14: one-tile form, no fused xent)";
+    case -12: return "pipeline stages must be 2..4, 5 = A3/B2 ring, 6 / 7 = register-prefetched 2 / 3-deep ring (256x256: 6; 256x128, 128x128, 128x64, 64x64: 6, 7), 9 / 10 = the same with the register-direct epilogue (no ct / fused update), 11 = register-direct epilogue on the A3/B2 ring (256x256, 256x128, 128x128), 12..14 = 32-deep k-steps with 2..4 stages (256x256: 12-14, 256x128: 12-13, 128x128: 12, 14), 15 / 16 = code 9 with an L2 touch-prefetch 1 / 2 k-steps ahead (256x256, 256x128, 128x128, 64x64), 17 = code 11 with touch distance 1 (256x128, 128x128) (8-wave tiles: 2, 3, 5; 256x256: 2, 5 or 8 = ping-pong; 5, 12-14: one-tile form, no fused xent)";
     case -14: return "transposed output ct needs bf16 output (or the fused update), no xent, one split, one-tile form, ld_ct >= M, 16-byte alignment";
     case -15: return "fused SGD epilogue needs f32 output, one split, no accumulate/bias/xent, a device lr, 16-byte aligned buffers, N % 8 == 0, one-tile form";
     default: return "unknown gemm error";
@@ -278,9 +278,9 @@ int gemm_bf16(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, 
     hipLaunchKernelGGL(f, dim3(nwg), dim3(nt), 0, stream, q, tiles_n, tiles_m, nwg);
     return hipGetLastError() == hipSuccess ? 0 : -9;
   }
-  if (ns == 6 || ns == 7 || (ns >= 9 && ns <= 11)) {  // register-prefetched loop
+  if (ns == 6 || ns == 7 || (ns >= 9 && ns <= 11) || (ns >= 15 && ns <= 17)) {  // RP loop
     if (persist || p.xent_labels) return -12;
-    if (ns >= 9) {  // register-direct epilogue: no transposed copy / fused update
+    if (ns >= 9) {  // register-direct epilogue (9-11, 15-17): no transposed copy / fused update
       if (p.ct) return -14;
       if (p.upd_master) return -15;
     }

@@ -12,7 +12,26 @@ namespace dnn {
 // Codes 9 / 10: the same loop with swapped MFMA operands and the register-direct epilogue
 // (RP_ = 2): bias / activation / aux derivative / colsum / split-K f32, no ReLU bit masks,
 // transposed copy, fused update or cross-entropy.
+// Codes 15 / 16: code 9 (2-deep ring, register-direct epilogue) with the L2 touch-prefetch
+// (Cfg TOUCH, touch_tiles) one / two k-steps beyond the ring; code 17: code 11 (A3/B2 ring)
+// with touch distance 1 (256x128, 128x128).
 static gemm_fn pick_rp(int bm, int bn, int code, int la, int lb, int f32) {
+  if (code == 15 || code == 16 || code == 17) {
+    constexpr int T1 = 2 | (1 << 4), T2 = 2 | (2 << 4);
+#define DNN_RPT(BM, BN, WM, WN, NS, NSB, RPV) pick_layout<Cfg<BM, BN, WM, WN, NS, NSB, 64, RPV>>(la, lb, f32)
+    if (code == 17) {
+      // (256x256 A3/B2 fills all 160 KiB: no room for the touch scratch)
+      if (bm == 256 && bn == 128) return DNN_RPT(256, 128, 4, 2, 3, 2, T1);
+      if (bm == 128 && bn == 128) return DNN_RPT(128, 128, 2, 2, 3, 2, T1);
+      return nullptr;
+    }
+    if (bm == 256 && bn == 256) return code == 15 ? DNN_RPT(256, 256, 4, 2, 2, 2, T1) : DNN_RPT(256, 256, 4, 2, 2, 2, T2);
+    if (bm == 256 && bn == 128) return code == 15 ? DNN_RPT(256, 128, 4, 2, 2, 2, T1) : DNN_RPT(256, 128, 4, 2, 2, 2, T2);
+    if (bm == 128 && bn == 128) return code == 15 ? DNN_RPT(128, 128, 2, 2, 2, 2, T1) : DNN_RPT(128, 128, 2, 2, 2, 2, T2);
+    if (bm == 64 && bn == 64) return code == 15 ? DNN_RPT(64, 64, 2, 2, 2, 2, T1) : DNN_RPT(64, 64, 2, 2, 2, 2, T2);
+#undef DNN_RPT
+    return nullptr;
+  }
   if (code == 11) {  // asymmetric A3/B2 ring, register-direct epilogue
 #define DNN_RPA(BM, BN, WM, WN) pick_layout<Cfg<BM, BN, WM, WN, 3, 2, 64, 2>>(la, lb, f32)
     if (bm == 256 && bn == 256) return DNN_RPA(256, 256, 4, 2);

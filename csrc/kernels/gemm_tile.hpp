@@ -67,7 +67,11 @@ struct Cfg {
   // in each half (0 = one read per NM/NR MFMAs, 1 = two reads per MFMA up front, 2 = all reads
   // first)
   static constexpr bool RP = RP_ != 0, DIRECT = (RP_ & 3) == 2;
-  static constexpr int RP_PATTERN = RP_ >> 2;
+  static constexpr int RP_PATTERN = (RP_ >> 2) & 3;
+  // RP_ bits 4-5: L2 touch-prefetch distance D (0 = off; touch_tiles): every k-step also
+  // touches the streamed operand tiles D k-steps beyond the newest LDS-DMA tile, so HBM
+  // misses are in flight further ahead than the LDS ring can hold
+  static constexpr int TOUCH = (RP_ >> 4) & 3;
   static_assert(!RP || (BK == 64 && NS <= 3), "register prefetch: BK 64, NS 2..3 (or A3/B2)");
   static_assert(NSB == NS || (NS == 3 && NSB == 2), "asymmetric ring: A 3 deep, B 2 deep only");
   static_assert(BK == 64 || BK == 32, "k-step depth 64 or 32");
@@ -85,7 +89,9 @@ struct Cfg {
   static constexpr int CHUNKS = BM / EPI_ROWS, WPC = EPI_ROWS / SM;  // wave-rows per chunk
   static constexpr int CS_BYTES = EPI_ROWS * CS_LD * 4;
   static constexpr int RED_BYTES = NT * 32;  // colsum partial staging
-  static constexpr int SMEM = cmax<cmax<RING, CS_BYTES + 64>::v, RED_BYTES>::v;
+  // touch-prefetch scratch: the 256 B every touch instruction writes (never read)
+  static constexpr int TOUCH_OFF = RING, RING_T = RING + (TOUCH ? 256 : 0);
+  static constexpr int SMEM = cmax<cmax<RING_T, CS_BYTES + 64>::v, RED_BYTES>::v;
   // per-wave LDS-DMA instructions of one A / one B tile (vmcnt units of the asymmetric ring)
   static constexpr int PER_A = BM * BK / (512 * NW), PER_B = BN * BK / (512 * NW);
   static_assert(FM >= 1 && FN >= 1 && SM % 16 == 0 && SN % 16 == 0, "wave sub-tile");
@@ -155,6 +161,52 @@ __device__ __forceinline__ void stage_tile_asm(const u16* __restrict__ g, long l
     // M0 is written inside the asm and listed as clobbered; kernels that use this form issue
     // all of their LDS-DMA from it (the compiler keeps nothing else in M0 there).
     asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off"
+                 :: "v"(src), "s"(m0v) : "memory", "m0");
+  }
+}
+#pragma clang diagnostic pop
+
+// L2 touch-prefetch of the k-step at k0 (Cfg TOUCH): one 4-byte LDS-DMA per 128-byte line of
+// the streamed operand tiles (A always; B when it is MN-major, i.e. an activation of the weight
+// gradient rather than a weight), into a 256-byte LDS scratch nobody reads. The load brings the
+// line into L2 / the Infinity Cache, so the real LDS-DMA of that tile a few k-steps later finds
+// it on-die instead of waiting for HBM: the bytes in flight per CU are no longer bounded by the
+// LDS ring. Every wave issues exactly touch_count<C, LA, LB>() instructions (lanes past the
+// line count repeat a line), which is what the ring's counted vmcnt waits allow for.
+template <int L, int T>
+__device__ __forceinline__ constexpr int touch_lines() {
+  return L == KMAJ ? T : 64 * ((T * 2 + 127) / 128);  // T rows of 128 B | 64 k-rows of T*2 B
+}
+template <class C, int LA, int LB>
+__device__ __forceinline__ constexpr int touch_count() {
+  constexpr int NL = touch_lines<LA, C::BM>() + (LB == MNMAJ ? touch_lines<LB, C::BN>() : 0);
+  return (NL + C::NT - 1) / C::NT;
+}
+
+template <int L, int T>
+__device__ __forceinline__ const u16* touch_addr(const u16* __restrict__ g, long ld, int mn0,
+                                                 int k0, int line, int mn_lim) {
+  if constexpr (L == KMAJ) return g + (long)min(mn0 + line, mn_lim - 1) * ld + k0;
+  constexpr int LPR = (T * 2 + 127) / 128;  // lines per k-row
+  const int r = line / LPR, c = line - r * LPR;
+  return g + (long)(k0 + r) * ld + max(0, min(mn0 + c * 64, mn_lim - 64));
+}
+
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+template <class C, int LA, int LB>
+__device__ __forceinline__ void touch_tiles(const GemmParams& p, int m0, int n0, int k0,
+                                            char LDS_AS* scratch, int wave, int lane) {
+  constexpr int NA = touch_lines<LA, C::BM>();
+  constexpr int NL = NA + (LB == MNMAJ ? touch_lines<LB, C::BN>() : 0);
+  constexpr int TI = touch_count<C, LA, LB>();
+  const unsigned m0v = __builtin_amdgcn_readfirstlane((unsigned)(size_t)scratch);
+#pragma unroll
+  for (int i = 0; i < TI; ++i) {
+    const int line = (i * C::NT + wave * 64 + lane) % NL;
+    const u16* src = line < NA ? touch_addr<LA, C::BM>(p.A, p.lda, m0, k0, line, p.M)
+                               : touch_addr<LB, C::BN>(p.B, p.ldb, n0, k0, line - NA, p.N);
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off"
                  :: "v"(src), "s"(m0v) : "memory", "m0");
   }
 }
@@ -383,6 +435,15 @@ __device__ __forceinline__ void mma_tile_rp(const GemmParams& p, int m0, int n0,
     stage_tile_asm<LB, C::BN, C::NW>(p.B, p.ldb, n0, kbase + k * 64, b_at(slot), wave, lane,
                                      p.N);
   };
+  // L2 touch-prefetch (C::TOUCH = D > 0): tile kt + NA + D is touched right after the DMA of
+  // tile kt + NA; TI instructions per wave younger than that DMA are allowed in the waits
+  constexpr int D = C::TOUCH;
+  constexpr int TI = D ? touch_count<C, LA, LB>() : 0;
+  auto touch = [&](int k) {
+    if constexpr (D > 0)
+      touch_tiles<C, LA, LB>(p, m0, n0, kbase + min(k, nk - 1) * 64, lds + C::TOUCH_OFF, wave,
+                             lane);
+  };
   // Prologue: every slot staged (tiles past the end clamp to the last one: same load counts
   // whatever nk is), then tile 0 landed.
   if constexpr (C::ASYM) {  // issue order A0 B0 A1 B1 A2
@@ -391,14 +452,18 @@ __device__ __forceinline__ void mma_tile_rp(const GemmParams& p, int m0, int n0,
     st_a(min(1, nk - 1), 1);
     st_b(min(1, nk - 1), 1);
     st_a(min(2, nk - 1), 2);
-    wait_vmcnt<2 * C::PER_A + C::PER_B>();
+#pragma unroll
+    for (int d = 0; d < D; ++d) touch(NA + d);
+    wait_vmcnt<2 * C::PER_A + C::PER_B + D * TI>();
   } else {
 #pragma unroll
     for (int s = 0; s < NA; ++s) {
       st_a(min(s, nk - 1), s);
       st_b(min(s, nk - 1), s);
     }
-    wait_vmcnt<(NA - 1) * C::PER_STAGE>();
+#pragma unroll
+    for (int d = 0; d < D; ++d) touch(NA + d);
+    wait_vmcnt<(NA - 1) * C::PER_STAGE + D * TI>();
   }
   lds_barrier();
   tl_mark(p, 1);
@@ -422,8 +487,8 @@ __device__ __forceinline__ void mma_tile_rp(const GemmParams& p, int m0, int n0,
     rp_interleave<C::RP_PATTERN, NR, NM>();
     // own loads of tile kt+1 landed: asymmetric -- only A(kt+2) was issued after B(kt+1);
     // symmetric -- tiles kt+2 .. kt+NS-1 may stay in flight
-    if constexpr (C::ASYM) wait_vmcnt<C::PER_A>();
-    else wait_vmcnt<(NA - 2) * C::PER_STAGE>();
+    if constexpr (C::ASYM) wait_vmcnt<C::PER_A + TI>();
+    else wait_vmcnt<(NA - 2) * C::PER_STAGE + TI>();
     __builtin_amdgcn_s_waitcnt(0xC07F);
     asm volatile("s_barrier" ::: "memory");
     // Tile kt's slots are free: B(kt+NB) and A(kt+NA) into them; past the end the last tile is
@@ -431,6 +496,7 @@ __device__ __forceinline__ void mma_tile_rp(const GemmParams& p, int m0, int n0,
     // branch and every k-step leaves the same loads in flight.
     st_b(min(kt + NB, nk - 1), rb);
     st_a(min(kt + NA, nk - 1), ra);
+    touch(kt + NA + D);
     ra = ra + 1 == NA ? 0 : ra + 1;
     rb = rb + 1 == NB ? 0 : rb + 1;
     read_half<C, LA, LB>(a_at(ra), b_at(rb), a0, b0, wm, wn, 0, lane);

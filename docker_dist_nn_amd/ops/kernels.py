@@ -298,7 +298,7 @@ def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=
                                   t.shape[1] < N or t.stride(0) != (c if c.dim() == 2
                                                                     else c[0]).stride(0)):
                 raise ValueError(f"fused update: {k} must be [M][N] with C's row stride")
-    if stages in (9, 10, 11) and (ct is not None or upd is not None):
+    if stages in (9, 10, 11, 15, 16, 17) and (ct is not None or upd is not None):
         stages = 6  # the register-direct epilogue has neither: RP loop, staged epilogue
     if not a.is_cuda:
         ref.gemm(a, b, c, layout_a=layout_a, layout_b=layout_b, M=M, N=N, K=K, bias=bias,

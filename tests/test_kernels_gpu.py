@@ -508,7 +508,10 @@ def test_bk32_ksteps_bitwise(dev, la, lb):
 RP = [((256, 256), 6), ((256, 128), 6), ((256, 128), 7), ((128, 128), 6), ((128, 128), 7),
       ((128, 64), 6), ((128, 64), 7), ((64, 64), 6), ((64, 64), 7),
       ((256, 256), 9), ((256, 128), 10), ((128, 128), 9), ((128, 64), 10), ((64, 64), 9),
-      ((256, 256), 11), ((256, 128), 11), ((128, 128), 11)]
+      ((256, 256), 11), ((256, 128), 11), ((128, 128), 11),
+      # L2 touch-prefetch variants (codes 15 / 16 / 17): the touches change no arithmetic
+      ((256, 256), 15), ((256, 256), 16), ((128, 128), 15), ((128, 128), 16), ((64, 64), 15),
+      ((256, 128), 17), ((128, 128), 17)]
 
 
 @pytest.mark.parametrize("la,lb", LAYOUTS)
