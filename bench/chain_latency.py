@@ -74,13 +74,18 @@ def main():
         finally:
             p.terminate()
             try:
-                p.communicate(timeout=60)
+                log, _ = p.communicate(timeout=60)
             except subprocess.TimeoutExpired:
                 p.kill()
+                log, _ = p.communicate()
+    fast = "device-side chain" in (log or "")
     t = np.asarray(ts) * 1e3
     print(json.dumps({"metric": "inference chain latency", "path": "rank chain (grpc ingress)",
                       "stages": a.stages, "rows": a.rows, "model": "-".join(map(str, dims)),
-                      "transport": "gloo via host (one-GPU rehearsal)" if rehearsal else "rccl",
+                      "transport": ("device-side chain: IPC slots + flags (serve/fastpath.py)"
+                                    if fast else "gloo via host" if rehearsal else "rccl") +
+                                   (", one-GPU rehearsal: every stage on cuda:0"
+                                    if rehearsal else ""),
                       "p50_ms": round(float(np.percentile(t, 50)), 4),
                       "p90_ms": round(float(np.percentile(t, 90)), 4),
                       "p99_ms": round(float(np.percentile(t, 99)), 4), "n": len(ts),

@@ -14,6 +14,7 @@
 #include <tuple>
 #include <vector>
 
+#include "kernels/chain.hpp"
 #include "kernels/elementwise.hpp"
 #include "kernels/gemm.hpp"
 #include "kernels/gemv.hpp"
@@ -999,6 +1000,82 @@ PYBIND11_MODULE(_native, m) {
       "wait_geq_u32",
       [](uintptr_t s, uintptr_t flag, uint32_t v) {
         dnn::wait_geq_u32(S(s), reinterpret_cast<void*>(flag), v);
+      },
+      py::arg("stream"), py::arg("flag"), py::arg("value"));
+  // ---- device-side serving chain (csrc/kernels/chain.hpp, serve/fastpath.py) ---------------
+  auto ptr = [](uintptr_t p) { return reinterpret_cast<void*>(p); };
+  auto chk = [](int rc, const char* what) {
+    if (rc != 0) throw std::runtime_error(std::string(what) + " failed (" + std::to_string(rc) + ")");
+  };
+  m.def(
+      "chain_wait",
+      [=](uintptr_t s, uintptr_t flag, uint32_t target, uintptr_t err, double timeout_s) {
+        chk(dnn::chain_wait(static_cast<const uint32_t*>(ptr(flag)), target,
+                            static_cast<uint32_t*>(ptr(err)), timeout_s, S(s)),
+            "chain_wait");
+      },
+      py::arg("stream"), py::arg("flag"), py::arg("target"), py::arg("err"),
+      py::arg("timeout_s"));
+  m.def(
+      "chain_recv",
+      [=](uintptr_t s, uintptr_t flag, uintptr_t slot, long slot_ld, uintptr_t slot_hdr,
+          uintptr_t dst, long dst_ld, uintptr_t dst_hdr, int rows, int row_bytes, uintptr_t err,
+          uint32_t seq, uintptr_t prev_ack, double timeout_s) {
+        dnn::ChainRecv p{};
+        p.flag = static_cast<const uint32_t*>(ptr(flag));
+        p.slot = ptr(slot);
+        p.slot_ld = slot_ld;
+        p.slot_hdr = static_cast<const uint32_t*>(ptr(slot_hdr));
+        p.dst = ptr(dst);
+        p.dst_ld = dst_ld;
+        p.dst_hdr = static_cast<uint32_t*>(ptr(dst_hdr));
+        p.rows = rows;
+        p.row_bytes = row_bytes;
+        p.err = static_cast<uint32_t*>(ptr(err));
+        p.seq = seq;
+        p.prev_ack = static_cast<uint32_t*>(ptr(prev_ack));
+        p.timeout_ticks = dnn::chain_ticks(timeout_s);
+        chk(dnn::chain_recv(p, S(s)), "chain_recv");
+      },
+      py::arg("stream"), py::arg("flag"), py::arg("slot"), py::arg("slot_ld"),
+      py::arg("slot_hdr"), py::arg("dst"), py::arg("dst_ld"), py::arg("dst_hdr"),
+      py::arg("rows"), py::arg("row_bytes"), py::arg("err"), py::arg("seq"),
+      py::arg("prev_ack"), py::arg("timeout_s"));
+  m.def(
+      "chain_send",
+      [=](uintptr_t s, uintptr_t src, long src_ld, uintptr_t dst, long dst_ld, int rows,
+          int row_bytes, uintptr_t dst_hdr, uintptr_t in_hdr, uintptr_t err, int stage,
+          uint32_t status, uintptr_t ack, uint32_t ack_target, uintptr_t next_flag, uint32_t seq,
+          uintptr_t prev_ack, double timeout_s) {
+        dnn::ChainSend p{};
+        p.src = ptr(src);
+        p.src_ld = src_ld;
+        p.dst = ptr(dst);
+        p.dst_ld = dst_ld;
+        p.rows = rows;
+        p.row_bytes = row_bytes;
+        p.dst_hdr = static_cast<uint32_t*>(ptr(dst_hdr));
+        p.in_hdr = static_cast<const uint32_t*>(ptr(in_hdr));
+        p.err = static_cast<uint32_t*>(ptr(err));
+        p.stage = stage;
+        p.status = status;
+        p.ack = static_cast<const uint32_t*>(ptr(ack));
+        p.ack_target = ack_target;
+        p.next_flag = static_cast<uint32_t*>(ptr(next_flag));
+        p.seq = seq;
+        p.prev_ack = static_cast<uint32_t*>(ptr(prev_ack));
+        p.timeout_ticks = dnn::chain_ticks(timeout_s);
+        chk(dnn::chain_send(p, S(s)), "chain_send");
+      },
+      py::arg("stream"), py::arg("src"), py::arg("src_ld"), py::arg("dst"), py::arg("dst_ld"),
+      py::arg("rows"), py::arg("row_bytes"), py::arg("dst_hdr"), py::arg("in_hdr"),
+      py::arg("err"), py::arg("stage"), py::arg("status"), py::arg("ack"),
+      py::arg("ack_target"), py::arg("next_flag"), py::arg("seq"), py::arg("prev_ack"),
+      py::arg("timeout_s"));
+  m.def(
+      "chain_signal",
+      [=](uintptr_t s, uintptr_t flag, uint32_t value) {
+        chk(dnn::chain_signal(static_cast<uint32_t*>(ptr(flag)), value, S(s)), "chain_signal");
       },
       py::arg("stream"), py::arg("flag"), py::arg("value"));
   m.def("device_sync", []() {

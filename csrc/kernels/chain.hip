@@ -1,0 +1,159 @@
+// Device-side serving chain kernels (chain.hpp; host side serve/fastpath.py). Every wait is a
+// single lane polling a flag with system-scope acquire loads and s_sleep between polls, with a
+// wall-clock timeout, so every wave of every launch finishes. Flags and slot headers are
+// written with vector stores (the address is lane-indexed), never through the scalar cache.
+#include <algorithm>
+
+#include "chain.hpp"
+
+namespace dnn {
+
+namespace {
+
+__device__ __forceinline__ bool reached(const uint32_t* flag, uint32_t target) {
+  return (int)(__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - target) >=
+         0;
+}
+
+// lane 0 of the calling wave: poll until reached or timed out
+__device__ __forceinline__ bool spin(const uint32_t* flag, uint32_t target,
+                                     unsigned long long ticks) {
+  const unsigned long long t0 = wall_clock64();
+  while (!reached(flag, target)) {
+    __builtin_amdgcn_s_sleep(1);
+    if (wall_clock64() - t0 > ticks) return false;
+  }
+  return true;
+}
+
+// rows x row_bytes from src (ld sld bytes) to dst (ld dld bytes), 16-byte vectors
+__device__ __forceinline__ void copy_rows(const char* src, long sld, char* dst, long dld,
+                                          int rows, int row_bytes) {
+  const int cpr = row_bytes >> 4;
+  const int n = rows * cpr;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int r = i / cpr, c = i - r * cpr;
+    *(uint4*)(dst + r * dld + 16 * c) = *(const uint4*)(src + r * sld + 16 * c);
+  }
+}
+
+}  // namespace
+
+__global__ void chain_wait_kernel(const uint32_t* flag, uint32_t target, uint32_t* err,
+                                  unsigned long long ticks) {
+  const unsigned l = threadIdx.x;
+  if (l != 0) return;
+  const bool ok = spin(flag + l, target, ticks);  // err: this wait's outcome (0 = arrived)
+  __hip_atomic_store(err + l, ok ? 0u : 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(256) void chain_recv_kernel(ChainRecv p) {
+  __shared__ uint32_t s_ok;
+  const unsigned t = threadIdx.x;
+  if (t == 0) {
+    const bool ok = spin(p.flag + t, p.seq, p.timeout_ticks);
+    if (!ok) __hip_atomic_store(p.err + t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    s_ok = ok ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!s_ok) return;  // uniform
+  copy_rows((const char*)p.slot, p.slot_ld, (char*)p.dst, p.dst_ld, p.rows, p.row_bytes);
+  if (t < 2)
+    p.dst_hdr[t] = __hip_atomic_load(p.slot_hdr + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  // every read of the slot is done before the producer may overwrite it
+  __syncthreads();
+  if (t == 0 && p.prev_ack) {
+    __threadfence_system();
+    __hip_atomic_store(p.prev_ack + t, p.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+__global__ __launch_bounds__(256) void chain_send_kernel(ChainSend p) {
+  __shared__ uint32_t s_st;
+  const unsigned t = threadIdx.x;
+  if (t == 0) {
+    bool ok = true;
+    if (p.ack) ok = spin(p.ack + t, p.ack_target, p.timeout_ticks);
+    uint32_t st = p.status;
+    if (!st) {
+      const uint32_t in = p.in_hdr ? p.in_hdr[t] : 0u;
+      if (in & 0xffu)  // an upstream failure travels on unchanged (it names its stage)
+        st = in;
+      else if (__hip_atomic_load(p.err + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))
+        st = CHAIN_DEADLINE | ((uint32_t)(p.stage - 1) << 8);  // the producer never delivered
+      else if (!ok)
+        st = CHAIN_DEADLINE | ((uint32_t)(p.stage + 1) << 8);  // the consumer never drained
+    }
+    __hip_atomic_store(p.err + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    s_st = st | (ok ? 0u : 0x80000000u);
+  }
+  __syncthreads();
+  const uint32_t st = s_st & 0x7fffffffu;
+  const bool slot_free = (s_st & 0x80000000u) == 0u;
+  if (st == 0u && slot_free)
+    copy_rows((const char*)p.src, p.src_ld, (char*)p.dst, p.dst_ld, p.rows, p.row_bytes);
+  if (t < 2)
+    __hip_atomic_store(p.dst_hdr + t, t == 0 ? st : (uint32_t)p.rows, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  __threadfence_system();  // this thread's rows and header are visible before the flag
+  __syncthreads();
+  if (t == 0)
+    __hip_atomic_store(p.next_flag + t, p.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (t == 1 && p.prev_ack)
+    __hip_atomic_store(p.prev_ack + (t - 1), p.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void chain_signal_kernel(uint32_t* flag, uint32_t value) {
+  const unsigned l = threadIdx.x;
+  if (l == 0) {
+    __threadfence_system();
+    __hip_atomic_store(flag + l, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+unsigned long long chain_ticks(double seconds) {
+  static int rate_khz = [] {  // wall_clock64 ticks per ms (100 MHz on gfx9)
+    int r = 0, dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess)
+      (void)hipDeviceGetAttribute(&r, hipDeviceAttributeWallClockRate, dev);
+    return r > 0 ? r : 100000;
+  }();
+  return (unsigned long long)(std::max(0.0, seconds) * 1e3 * (double)rate_khz);
+}
+
+static bool misaligned4(const void* p) { return reinterpret_cast<uintptr_t>(p) & 3; }
+static bool misaligned16(const void* p) { return reinterpret_cast<uintptr_t>(p) & 15; }
+
+int chain_wait(const uint32_t* flag, uint32_t target, uint32_t* err, double timeout_s,
+               hipStream_t stream) {
+  if (!flag || !err || misaligned4(flag) || misaligned4(err)) return -1;
+  hipLaunchKernelGGL(chain_wait_kernel, dim3(1), dim3(64), 0, stream, flag, target, err,
+                     chain_ticks(timeout_s));
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
+int chain_recv(const ChainRecv& p, hipStream_t stream) {
+  if (!p.flag || !p.err || !p.dst_hdr || !p.slot_hdr || misaligned4(p.flag)) return -1;
+  if (p.rows < 0 || p.row_bytes % 16 || p.slot_ld % 16 || p.dst_ld % 16 ||
+      misaligned16(p.slot) || misaligned16(p.dst))
+    return -2;
+  hipLaunchKernelGGL(chain_recv_kernel, dim3(1), dim3(256), 0, stream, p);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
+int chain_send(const ChainSend& p, hipStream_t stream) {
+  if (!p.next_flag || !p.dst_hdr || !p.err || misaligned4(p.next_flag)) return -1;
+  if (p.rows < 0 || p.row_bytes % 16 || p.src_ld % 16 || p.dst_ld % 16 ||
+      misaligned16(p.src) || misaligned16(p.dst))
+    return -2;
+  hipLaunchKernelGGL(chain_send_kernel, dim3(1), dim3(256), 0, stream, p);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
+int chain_signal(uint32_t* flag, uint32_t value, hipStream_t stream) {
+  if (!flag || misaligned4(flag)) return -1;
+  hipLaunchKernelGGL(chain_signal_kernel, dim3(1), dim3(64), 0, stream, flag, value);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
+}  // namespace dnn

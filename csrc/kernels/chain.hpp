@@ -1,0 +1,71 @@
+// Device-side serving chain (serve/fastpath.py): the kernels of one hop of a request through
+// the rank chain, with no host round trip between stages.
+//
+// The reference forwards every request hop by hop with a blocking gRPC call per stage
+// (/root/reference/src/grpc_node.py:120-135, 10 s deadline per hop). Here stage k's stream
+// holds, per request: chain_wait (its input slot's flag reached the request's sequence number)
+// -> the stage's GEMV layers -> chain_send (wait until the consumer has freed the slot this
+// request reuses, copy the rows into the consumer's IPC-mapped slot, write the slot header,
+// release the consumer's flag and the producer's ack). Stage k's host enqueues that as soon as
+// the request is announced, so every stage's kernels are queued before the data arrives.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dnn {
+
+// Slot header status codes (low 8 bits; bits 8..15: the stage blamed -- the failing stage, the
+// producer whose rows never arrived, or the consumer that never freed its slot).
+constexpr uint32_t CHAIN_OK = 0, CHAIN_VALUE = 2, CHAIN_INTERNAL = 3, CHAIN_DEADLINE = 4;
+
+struct ChainSend {
+  const void* src;           // rows x row_bytes, leading dimension src_ld bytes
+  long src_ld;
+  void* dst;                 // consumer's slot (IPC-mapped), leading dimension dst_ld bytes
+  long dst_ld;
+  int rows;                  // rows to copy (0: status only)
+  int row_bytes;             // multiple of 16
+  uint32_t* dst_hdr;         // consumer's slot header [status, rows]
+  const uint32_t* in_hdr;    // this stage's input slot header (nullptr on stage 0)
+  uint32_t* err;             // this stage's wait-timeout word (read and cleared here)
+  int stage;                 // this stage's index (recorded with a status it raises)
+  uint32_t status;           // != 0: raise this status (host-detected failure), copy nothing
+  const uint32_t* ack;       // consumer's "slot consumed" flag (written by the consumer)
+  uint32_t ack_target;       // wait until ack >= this before overwriting the slot
+  uint32_t* next_flag;       // consumer's input flag for this slot
+  uint32_t seq;              // this request's sequence number
+  uint32_t* prev_ack;        // producer's ack flag (this stage consumed its input slot)
+  unsigned long long timeout_ticks;
+};
+
+// Receive side of a hop: one lane spins on the input slot's flag (>= seq); then the workgroup
+// pulls the slot's rows and header into this stage's own (L2-cached) buffers and releases the
+// producer's ack (the slot may be reused). On timeout: *err = 1, nothing is pulled or acked.
+struct ChainRecv {
+  const uint32_t* flag;      // this stage's input flag of the slot (written by the producer)
+  const void* slot;          // the slot's rows (L2-uncached), leading dimension slot_ld bytes
+  long slot_ld;
+  const uint32_t* slot_hdr;  // the slot's header [status, rows]
+  void* dst;                 // this stage's input buffer, leading dimension dst_ld bytes
+  long dst_ld;
+  uint32_t* dst_hdr;         // local copy of the header (read by this stage's chain_send)
+  int rows, row_bytes;
+  uint32_t* err;
+  uint32_t seq;
+  uint32_t* prev_ack;        // producer's ack flag (IPC-mapped)
+  unsigned long long timeout_ticks;
+};
+
+int chain_recv(const ChainRecv& p, hipStream_t stream);
+unsigned long long chain_ticks(double seconds);  // wall_clock64 ticks
+
+// Spin (one lane, s_sleep between system-scope acquire polls) until *flag >= target (wrapping
+// compare); *err = 0 when it arrived, 1 when it gave up after timeout_ticks (every wave always
+// finishes).
+int chain_wait(const uint32_t* flag, uint32_t target, uint32_t* err, double timeout_s,
+               hipStream_t stream);
+int chain_send(const ChainSend& p, hipStream_t stream);
+// *flag = value with system-scope release (one lane, a vector store).
+int chain_signal(uint32_t* flag, uint32_t value, hipStream_t stream);
+
+}  // namespace dnn

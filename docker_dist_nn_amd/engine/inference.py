@@ -86,10 +86,12 @@ class InferenceStage:
             self._bufs[rows] = b
         return b
 
-    def forward(self, rows: int) -> torch.Tensor:
-        """Run on buffers(rows)['x']; returns fp32 [rows][out_pad] (last stage) or bf16."""
+    def forward(self, rows: int, x: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Run on buffers(rows)['x'] (or on ``x``, e.g. the device-side chain's input rows);
+        returns fp32 [rows][out_pad] (last stage) or bf16."""
         b = self.buffers(rows)
-        x = b["x"]
+        if x is None:
+            x = b["x"]
         n = len(self.layers)
         for i in range(n):
             act = self.acts[i]

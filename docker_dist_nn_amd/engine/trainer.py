@@ -467,6 +467,18 @@ class Trainer:
             if self.mesh is not None and self.native_step is None:
                 raise RuntimeError("graph capture needs a native multi-rank step; the IPC "
                                    "verification fell back to the Python executor")
+        ns = self.native_step
+        if ns is not None and ns.mode == "ipc":
+            # the multi-stream IPC plan spins on flags in branches that other branches (and
+            # other ranks) release; a graph executor may order independent branches any way
+            # it likes (the captured relayed step stalled: VERDICT r3 #4). The slotted form is
+            # ONE stream in global clock order, so its graph is a single chain that completes
+            # whatever the executor does (parallel/native_step._build_ipc_slotted).
+            from ..parallel.native_step import NativeStep
+
+            self.native_step = NativeStep(self.executor, self.mesh, "ipc", ipc=self.pipe,
+                                          mode="slotted")
+            self.executor.native_step = self.native_step
         cur = torch.cuda.current_stream(self.device)
         self._stream = torch.cuda.Stream(self.device)
         self._stream.wait_stream(cur)

@@ -26,11 +26,13 @@ Rungs of the training benchmark (``bench_rungs``), most capable first:
 
   1. ``default``       -- the configured transport (DNN_PIPE=auto: relayed IPC, its first step
                           verified against the RCCL ``slotted`` plan);
-  2. ``rccl-slotted``  -- RCCL, one grouped send/recv per logical clock slot (safe with ONE
+  2. ``ipc-slotted``   -- relayed IPC on ONE stream per rank in global clock order (no
+                          assumption about how streams or kernels are co-scheduled);
+  3. ``rccl-slotted``  -- RCCL, one grouped send/recv per logical clock slot (safe with ONE
                           resident RCCL kernel per rank);
-  3. ``rccl-streams``  -- RCCL, one stream + communicator per link channel;
-  4. ``python``        -- the Python executor over torch.distributed P2P;
-  5. ``dp-native`` / ``dp-python`` -- data parallelism only (no pipeline hops at all).
+  4. ``rccl-streams``  -- RCCL, one stream + communicator per link channel;
+  5. ``python``        -- the Python executor over torch.distributed P2P;
+  6. ``dp-native`` / ``dp-python`` -- data parallelism only (no pipeline hops at all).
 """
 from __future__ import annotations
 
@@ -64,6 +66,7 @@ def bench_rungs(n: int, dp_only: bool = False) -> list[Rung]:
     if dp_only:
         return dp
     return [Rung("default"),
+            Rung("ipc-slotted", {"DNN_IPC_PLAN": "slotted"}),
             Rung("rccl-slotted", {"DNN_PIPE": "rccl", "DNN_RCCL_PLAN": "slotted"}),
             Rung("rccl-streams", {"DNN_PIPE": "rccl", "DNN_RCCL_PLAN": "streams"}),
             Rung("python", {"DNN_PIPE": "rccl", "DNN_NATIVE_DIST": "0"}),
@@ -185,6 +188,23 @@ class Supervisor:
                                               flush=True))
         self.attempts: list[dict] = []
         self._n = 0  # attempts made (store keys are per attempt index)
+        self._child: Optional[subprocess.Popen] = None
+        # the launcher ends a job with SIGTERM (torch.distributed.run does when any rank
+        # fails): take the current child down with us -- it runs in a session of its own and
+        # would otherwise live on, blocked in a rendezvous whose peers are gone
+        try:
+            prev = signal.getsignal(signal.SIGTERM)
+
+            def _term(signum, frame):
+                if self._child is not None and self._child.poll() is None:
+                    _kill(self._child)
+                if callable(prev):
+                    prev(signum, frame)
+                raise SystemExit(128 + signum)
+
+            signal.signal(signal.SIGTERM, _term)
+        except ValueError:  # not the main thread: the caller handles termination
+            pass
 
     def _key(self, i: int, what: str) -> str:
         return f"attempt/{i}/{what}"
@@ -198,7 +218,8 @@ class Supervisor:
         return out
 
     def attempt(self, rung: Rung) -> tuple[bool, Optional[dict]]:
-        """One attempt of ``rung`` on every rank; returns (success, rank 0's result)."""
+        """One attempt of ``rung`` on every rank; returns (success, rank 0's child's result),
+        the same on every rank."""
         i = self._n
         self._n += 1
         if self.rank == 0:
@@ -225,7 +246,9 @@ class Supervisor:
         with open(hb, "w") as f:
             f.write("spawn\n")
         t0 = time.monotonic()
-        p = subprocess.Popen(cmd, env=env, start_new_session=True)
+        # the child's stdout goes to stderr: the supervisor's stdout carries only its result
+        p = subprocess.Popen(cmd, env=env, start_new_session=True, stdout=sys.stderr.fileno())
+        self._child = p
         mine = None      # this rank's outcome: exit code or "stall" / "killed"
         tail = ""
         while True:
@@ -264,9 +287,14 @@ class Supervisor:
             except (OSError, ValueError) as e:
                 ok = False
                 rcs[0] = f"no result ({e.__class__.__name__})"
-        if self.rank == 0:  # rank 0's view decides whether its result is usable: share it
+        if self.rank == 0:  # rank 0's view decides whether its result is usable: share it,
+            # with the result itself (every supervisor decides the next step from it)
+            if ok:
+                self.store.set(self._key(i, "result"), json.dumps(result))
             self.store.set(self._key(i, "ok"), "1" if ok else "0")
         ok = self.store.get(self._key(i, "ok")).decode() == "1"
+        if ok and self.rank != 0:
+            result = json.loads(self.store.get(self._key(i, "result")).decode())
         # every rank has read the outcome before rank 0 (which may host the store) moves on or
         # exits
         self.store.add(self._key(i, "read"), 1)
@@ -282,7 +310,8 @@ class Supervisor:
         return ok, result
 
     def climb(self, rungs: Sequence[Rung]) -> tuple[Optional[dict], Optional[Rung]]:
-        """Try ``rungs`` in order until one succeeds; (rank 0's result or None, the rung)."""
+        """Try ``rungs`` in order until one succeeds; (its result or None, the rung) -- the
+        same on every rank."""
         for rung in rungs:
             ok, result = self.attempt(rung)
             if ok:

@@ -105,12 +105,15 @@ class NativeStep:
         self.sharded = st.params.sharded
         self.pp = mesh.pp if mesh is not None else 1
         hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
-        mode = mode or switches.get("DNN_RCCL_PLAN")
+        mode = mode or switches.get("DNN_RCCL_PLAN" if transport == "rccl" else "DNN_IPC_PLAN")
         if mode == "auto":
             mode = "streams" if hwq >= 6 else "slotted"
         if mode not in ("streams", "slotted"):
-            raise ValueError(f"DNN_RCCL_PLAN must be auto | streams | slotted, got {mode!r}")
-        self.mode = mode if transport == "rccl" else "ipc"
+            raise ValueError(f"plan form must be auto | streams | slotted, got {mode!r}")
+        # "ipc": one stream per direction and relay duty; "ipc-slotted": everything on ONE
+        # stream in global logical-clock order (_build_ipc_slotted)
+        self.mode = mode if transport == "rccl" else ("ipc-slotted" if mode == "slotted"
+                                                      else "ipc")
         self.comms = dict(comms or {})
         if comms is None and not build_only:
             self.n = native()
@@ -128,7 +131,9 @@ class NativeStep:
         self._ev = 0
         self.ops: list[dict] = []
         self._build()
-        if self.transport == "ipc":
+        if self.mode == "ipc-slotted":
+            self.n_streams = 1
+        elif self.transport == "ipc":
             self.n_streams = 4 + (len(ipc.duties) if ipc is not None else 0)
         else:
             self.n_streams = 6 if self.mode == "streams" else 2
@@ -230,11 +235,16 @@ class NativeStep:
             idx = p.fidx(j, part) if direction == "f" else p.bidx(j, part)
             self.ops.append(dict(kind=WAITV, stream=MAIN, a=base + 4 * idx, delta=0))
 
-    def _send_ipc(self, direction: str, j: int) -> None:
+    def _send_ipc(self, direction: str, j: int, stream: Optional[int] = None) -> None:
+        """``stream`` None: the direction's send stream, ordered after the compute so far;
+        else that stream as it is (the slotted form: everything on MAIN)."""
         st = self.st
         t = st.output if direction == "f" else st.dx_send
-        s = FWD if direction == "f" else BWD
-        self._edge(MAIN, s)
+        if stream is None:
+            s = FWD if direction == "f" else BWD
+            self._edge(MAIN, s)
+        else:
+            s = stream
         ptr, cnt = self._rows(t, j)
         p = self.ipc
         peer = p.next if direction == "f" else p.prev
@@ -346,7 +356,9 @@ class NativeStep:
 
     def _build(self) -> None:
         self._check_w(self.ex.ops[0])
-        if self.transport == "ipc":
+        if self.mode == "ipc-slotted":
+            self._build_ipc_slotted()
+        elif self.transport == "ipc":
             self._build_ipc()
         elif self.mode == "slotted":
             self._build_slotted()
@@ -372,6 +384,10 @@ class NativeStep:
                     self._send_ipc("b", j)
             elif op == "W":
                 self._wgrad_update(DPS)
+        self._release_acks()
+        self._relay_duties()
+
+    def _release_acks(self) -> None:
         p = self.ipc  # release the buffers I receive into for the next step
         if p.prev is not None:
             self.ops.append(dict(kind=SIGNAL, stream=MAIN, a=p.prev["flags"] + 4 * p.ackf,
@@ -379,7 +395,60 @@ class NativeStep:
         if p.next is not None:
             self.ops.append(dict(kind=SIGNAL, stream=MAIN, a=p.next["flags"] + 4 * p.ackb,
                                  delta=0))
-        self._relay_duties()
+
+    def _collect(self, fn, *args) -> list[dict]:
+        """The ops ``fn(*args)`` would append, returned instead of appended."""
+        saved, self.ops = self.ops, []
+        try:
+            fn(*args)
+            return self.ops
+        finally:
+            self.ops = saved
+
+    def _build_ipc_slotted(self) -> None:
+        """IPC hops on ONE stream, in the replica's global logical-clock order (logical_times:
+        the clock the slotted RCCL form uses; every replica runs the same clock). At slot t a
+        rank enqueues, in this order: (0) its sends of slot t (copy + flag per stripe), (1)
+        its relay duties of slot t (wait for the stripe, copy it on, raise the consumer's
+        flag), (2) its receive waits of slot t, (3) its compute of slot t. A wait of slot t is
+        released only by sends / relays of slot t, which every rank enqueues before its own
+        waits of slot t, and sends wait on nothing but the previous step's acks -- so the
+        plan completes whatever order an executor runs independent work in, and a captured
+        graph of it is a single chain (the multi-stream relayed plan stalled
+        when captured). The price: copies and relays serialise with this rank's compute."""
+        m, st, p = self.mesh, self.st, self.ipc
+        kind, pp, nm = self.ex.kind, self.pp, st.nm
+        T = logical_times(kind, pp, nm)
+        my_t = T[m.stage]
+        has_prev, has_next = m.prev_rank is not None, m.next_rank is not None
+        entries = []  # (slot, order, ops)
+
+        def msg_slots(src_stage: int, opname: str):
+            """(slot, j) of every message stage ``src_stage`` sends after its ``opname``."""
+            for k, (op, j) in enumerate(schedule_ops(kind, pp, nm, src_stage)):
+                if op == opname:
+                    yield T[src_stage][k] + 1, j
+
+        for idx, (op, j) in enumerate(self.ex.ops[0]):
+            if op not in ("F", "B"):
+                continue
+            d = op.lower()
+            entries.append((my_t[idx], 3, [dict(kind=SEG, stream=MAIN, prog=st._prog,
+                                                seg=f"{op}{j}")]))
+            if (d == "f" and has_next) or (d == "b" and has_prev):
+                entries.append((my_t[idx] + 1, 0, self._collect(self._send_ipc, d, j, MAIN)))
+        for d, has, src, opname in (("f", has_prev, m.stage - 1, "F"),
+                                    ("b", has_next, m.stage + 1, "B")):
+            if has:
+                for t, j in msg_slots(src, opname):
+                    entries.append((t, 2, self._collect(self._recv_ipc, d, j)))
+        for dd, (src, _dst, direction, _part) in enumerate(p.duties):
+            for t, j in msg_slots(src % pp, "F" if direction == "f" else "B"):
+                entries.append((t, 1, self._relay_op(dd, j, MAIN)))
+        for _, _, ops in sorted(entries, key=lambda e: (e[0], e[1])):
+            self.ops += ops
+        self._wgrad_update(MAIN)
+        self._release_acks()
 
     def _build_streams(self) -> None:
         """One stream per hop channel; every receive of the step posted at its start (the rows
@@ -469,23 +538,26 @@ class NativeStep:
         in micro-batch order, and separate streams keep one hop from blocking another):
         wait for the producer's stripe j in my slot -> copy it into the consumer's rows ->
         raise the consumer's stripe flag."""
+        for d in range(len(self.ipc.duties)):
+            for j in range(self.st.nm):
+                self.ops += self._relay_op(d, j, 4 + d)
+
+    def _relay_op(self, d: int, j: int, stream: int) -> list[dict]:
+        """Duty d's stripe of micro-batch j: wait for it in my slot, copy it into the
+        consumer's rows, raise the consumer's stripe flag."""
         p, st = self.ipc, self.st
-        for d, ((src, dst, direction, part), dst_ptrs) in enumerate(zip(p.duties, p.relay_dst)):
-            stream = 4 + d
-            buf, rb = p.relay_bufs[d]
-            k, pm = p.layout.duty_k[d], p.duty_part_max[d]
-            for j in range(st.nm):
-                r = st.rows_of(j)  # every stage shares the micro-batch row layout
-                bounds = relay_parts(r.start, r.stop, k)
-                a0, a1 = bounds[part], bounds[part + 1]
-                self.ops.append(dict(kind=WAITV, stream=stream,
-                                     a=p.flags.data_ptr() + 4 * p.ridx(d, j), delta=0))
-                self.ops.append(dict(kind=COPY, stream=stream,
-                                     a=buf.data_ptr() + j * pm * rb,
-                                     b=dst_ptrs["buf"] + a0 * rb, count=(a1 - a0) * rb))
-                idx = p.fidx(j, part) if direction == "f" else p.bidx(j, part)
-                self.ops.append(dict(kind=SIGNAL, stream=stream, a=dst_ptrs["flags"] + 4 * idx,
-                                     delta=0))
+        (_src, _dst, direction, part), dst_ptrs = p.duties[d], p.relay_dst[d]
+        buf, rb = p.relay_bufs[d]
+        k, pm = p.layout.duty_k[d], p.duty_part_max[d]
+        r = st.rows_of(j)  # every stage shares the micro-batch row layout
+        bounds = relay_parts(r.start, r.stop, k)
+        a0, a1 = bounds[part], bounds[part + 1]
+        idx = p.fidx(j, part) if direction == "f" else p.bidx(j, part)
+        return [dict(kind=WAITV, stream=stream, a=p.flags.data_ptr() + 4 * p.ridx(d, j),
+                     delta=0),
+                dict(kind=COPY, stream=stream, a=buf.data_ptr() + j * pm * rb,
+                     b=dst_ptrs["buf"] + a0 * rb, count=(a1 - a0) * rb),
+                dict(kind=SIGNAL, stream=stream, a=dst_ptrs["flags"] + 4 * idx, delta=0)]
 
     # ---- execution -----------------------------------------------------------------------
     def run(self, stream: int) -> None:

@@ -108,6 +108,7 @@ class ChainRank:
         self.small = ops.GEMV_MAX_ROWS
         self._packets: dict = {}
         self.store = dist.distributed_c10d._get_default_store() if world > 1 else None
+        self.fast = None  # serve/fastpath.FastChain once enable_fast() agreed on it
         self._processed = 0
         self._published = 0
         if rank > 0 and world > 1:
@@ -172,19 +173,37 @@ class ChainRank:
         return hdr, pk
 
     def _recv_payload(self, dst: torch.Tensor, src: int, group, timeout_s: float) -> bool:
-        """Second message of a large request, bounded by the per-hop deadline."""
+        """Second message of a large request, bounded by the per-hop deadline. It lands in a
+        scratch tensor of its own: after a timeout the receive stays posted, and a late payload
+        must not overwrite the shared stage buffer while a later request computes on it
+        (ADVICE r3). The caller then stops serving this hop (``loop``)."""
         import datetime
 
-        t = dst if dst.device == self.comm_dev else torch.empty(dst.shape, dtype=dst.dtype,
-                                                                device=self.comm_dev)
+        t = torch.empty(dst.shape, dtype=dst.dtype, device=self.comm_dev)
         w = dist.irecv(t, src, group=group)
         try:
             w.wait(timeout=datetime.timedelta(seconds=timeout_s))
         except RuntimeError:
             return False
-        if t is not dst:
-            dst.copy_(t)
+        dst.copy_(t)
         return True
+
+    def enable_fast(self) -> str:
+        """Collective (every rank): build the device-side chain for serving-size requests
+        (serve/fastpath.py). Ranks > 0 start serving it on a thread of their own; the message
+        chain keeps carrying larger requests and is the fallback if any rank cannot map its
+        peers."""
+        from .fastpath import FastChain
+
+        fc = FastChain(self)
+        if not fc.ok:
+            return fc.why
+        self.fast = fc
+        if self.rank > 0:
+            t = threading.Thread(target=fc.loop, name="chain-fast", daemon=True)
+            t.start()
+            self._fast_thread = t
+        return fc.why
 
     # -- progress / blame ---------------------------------------------------------------------
     def _publisher(self) -> None:
@@ -226,6 +245,8 @@ class ChainRank:
             x = x.reshape(x.shape[0], -1)
         rows, cols = x.shape
         self.stage.check_input_dim(cols)  # ValueError -> INVALID_ARGUMENT
+        if self.fast is not None and rows <= self.small:
+            return self.fast.predict(x, timeout)
         R = bucket(rows)
         with self.compute_lock:  # this rank's per-bucket buffers are shared
             buf = self.stage.buffers(R)
@@ -297,6 +318,8 @@ class ChainRank:
                 log.warning(f"dropping the late answer of request {rid} (its caller timed out)")
 
     def stop_chain(self, timeout: float = 10.0) -> None:
+        if self.fast is not None:
+            self.fast.stop()
         if self.world > 1:
             self._sendq.put(None)
             for t in self._threads:
@@ -336,10 +359,15 @@ class ChainRank:
                 buf["x"].reshape(-1).view(torch.uint8).copy_(
                     pk[HDR_BYTES:HDR_BYTES + R * width * 2])
             elif not self._recv_payload(buf["x"], prev, self.fwd_group, self.hop_timeout):
+                # the hop is broken: the posted receive would take the next message from prev
+                # (on NCCL the timed-out wait aborts the communicator), so nothing later on it
+                # can be trusted. Report this request, then stop serving; rank 0 blames this
+                # stage for every later request from the progress it no longer publishes.
                 log.error(f"({self.names[self.rank]}) payload of request {req} did not arrive "
-                          f"within {self.hop_timeout:.1f} s")
+                          f"within {self.hop_timeout:.1f} s; the hop from rank {prev} is broken, "
+                          f"this stage stops serving")
                 self._forward_hdr(last, req, R, 0, ST_DEADLINE, prev)
-                continue
+                return
             try:
                 self._maybe_fault(served)
                 out = self.stage.forward(R)
@@ -406,6 +434,10 @@ def main(argv: Optional[list[str]] = None) -> int:
                            is_last=rank == world - 1)
     cr = ChainRank(stage, rank, world, names, device,
                    hop_timeout=plan.get("hop_timeout", HOP_TIMEOUT_S))
+    if world > 1 and use_gpu and switches.get("DNN_CHAIN_FAST") == "1":
+        why = cr.enable_fast()
+        if rank == 0:
+            log.info(f"({st['name']}) serving-size requests: {why}")
     log.info(f"({st['name']}) stage ready on {device}: {len(layers)} layer(s), "
              f"expected input dim {st['expected_input']}")
     if rank == 0:
@@ -427,6 +459,10 @@ def main(argv: Optional[list[str]] = None) -> int:
     else:
         signal.signal(signal.SIGINT, signal.SIG_IGN)
         cr.loop()
+        if cr.fast is not None:  # (a stage hung by fault injection is not waited for)
+            cr._fast_thread.join(cr.hop_timeout + 2.0)
+    if cr.fast is not None:
+        cr.fast.close()
     dist.destroy_process_group()
     return 0
 

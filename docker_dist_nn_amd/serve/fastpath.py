@@ -1,0 +1,394 @@
+"""Device-side serving chain: serving-size requests (<= ops.GEMV_MAX_ROWS rows) cross the rank
+chain with no host hop between stages (SURVEY §5 "fast path for tiny messages").
+
+The reference chain makes one blocking gRPC call per hop (/root/reference/src/grpc_node.py:
+120-135) driven by the client's per-batch RPC (/root/reference/src/run_grpc_inference.py:
+112-158). The message-passing chain (serve/chain.py) still did a host receive, a device->host
+header read and a host send per hop. Here:
+
+* every rank owns NSLOT input slots in L2-uncached memory (utils/devmem.py), IPC-mapped by its
+  producer, and a flag block (input flags, slot headers, the consumer's ack, a wait-timeout
+  word); rank 0 also owns NSLOT result slots, written by the last rank;
+* rank 0 announces each request -- (sequence number, rows) -- in a shared-memory ring on the
+  node (``/dev/shm``); every stage's host sees it at once and enqueues, on its own stream,
+  ``chain_recv`` (wait for the slot's flag, pull the rows into its cached input buffer, ack
+  the producer) -> its GEMV layers -> ``chain_send`` (wait until the consumer freed the slot
+  this request reuses, copy the rows into the consumer's slot, write the slot header, release
+  the consumer's flag) (csrc/kernels/chain.hip). All stages' kernels are queued before the
+  rows arrive, so a hop costs kernel time only;
+* rank 0's host does the only host work of a request: H2D of the bf16 rows, its own stage,
+  the send, then (second stream) a wait on the result flag, one D2H of header + logits, the
+  result slot's ack, an event;
+* failures keep the reference's semantics (grpc_node.py:136-158, chain.py blame): a stage that
+  raises sends its status instead of rows (INVALID_ARGUMENT / INTERNAL naming it); a stage
+  whose input does not arrive within the per-hop deadline (10 s, grpc_node.py:133) sends
+  DEADLINE_EXCEEDED naming its producer -- the stage that stopped -- and every later stage
+  forwards the status unchanged;
+* larger requests and any set-up that cannot map its peers keep using the message-passing
+  chain (serve/chain.py), which stays the fallback.
+"""
+from __future__ import annotations
+
+import logging
+import mmap
+import os
+import threading
+import time
+from typing import Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .. import ops
+from ..utils.native import native
+
+log = logging.getLogger(__name__)
+
+NSLOT = 16          # slots per hop: more than the ingress's 10 workers can have in flight
+ANN_SLOTS = 1024    # announcement ring
+HDR = 64            # bytes of header in front of a result slot's rows
+ST_OK, ST_VALUE, ST_INTERNAL, ST_DEADLINE = 0, 2, 3, 4
+# flag block layout (int32 words)
+F_IN = 0                    # [NSLOT] input flags (written by the producer)
+F_HDR = NSLOT               # [NSLOT][2] input slot headers (status, rows)
+F_ACK = 3 * NSLOT           # consumer's ack: last request whose slot it has drained
+F_ERR = F_ACK + 1           # this rank's recv-timeout word
+F_LHDR = F_ACK + 4          # [2] local copy of the current request's input header
+F_RES = F_ACK + 8           # rank 0: [NSLOT] result flags (written by the last rank)
+F_WORDS = F_RES + NSLOT + 8
+
+
+class Announcer:
+    """Shared-memory ring on the node: rank 0 writes (seq, rows) of every request, the other
+    ranks' hosts read them in order. Layout (int64): [0] last announced seq, [1] stop, then
+    ANN_SLOTS entries of (seq, rows). x86 stores are not reordered, and the entry is written
+    before the head."""
+
+    def __init__(self, path: str, create: bool, timeout: float = 60.0):
+        self.path = path
+        size = 8 * (4 + 2 * ANN_SLOTS)
+        if create:
+            fd = os.open(path, os.O_RDWR | os.O_CREAT | os.O_TRUNC, 0o600)
+            os.ftruncate(fd, size)
+        else:
+            t0 = time.monotonic()
+            while True:
+                try:
+                    fd = os.open(path, os.O_RDWR)
+                    if os.fstat(fd).st_size >= size:
+                        break
+                    os.close(fd)
+                except FileNotFoundError:
+                    pass
+                if time.monotonic() - t0 > timeout:
+                    raise RuntimeError(f"announcement ring {path} did not appear")
+                time.sleep(0.01)
+        self._mm = mmap.mmap(fd, size)
+        os.close(fd)
+        self.a = np.ndarray((4 + 2 * ANN_SLOTS,), dtype=np.int64, buffer=self._mm)
+        self.owner = create
+
+    def announce(self, seq: int, rows: int) -> None:
+        i = 4 + 2 * (seq % ANN_SLOTS)
+        self.a[i + 1] = rows
+        self.a[i] = seq
+        self.a[0] = seq
+
+    def stop(self) -> None:
+        self.a[1] = 1
+
+    def next(self, seq: int) -> Optional[int]:
+        """Rows of request ``seq`` once announced; None once the chain stops. Spins while
+        requests are flowing, backs off to short sleeps when idle."""
+        a = self.a
+        spins = 0
+        while a[0] < seq:
+            if a[1]:
+                return None
+            spins += 1
+            if spins > 20000:
+                time.sleep(50e-6)
+        i = 4 + 2 * (seq % ANN_SLOTS)
+        while a[i] != seq:  # the head is written last; the entry is there
+            pass
+        return int(a[i + 1])
+
+    def close(self) -> None:
+        try:
+            del self.a
+            self._mm.close()
+        except (BufferError, ValueError):
+            pass
+        if self.owner:
+            try:
+                os.unlink(self.path)
+            except FileNotFoundError:
+                pass
+
+
+def _ptr(t: torch.Tensor, word: int = 0) -> int:
+    return t.data_ptr() + 4 * word
+
+
+class FastChain:
+    """The device-side chain of one rank (see the module docstring). Built collectively by
+    every rank of the chain; ``ok`` is agreed (all ranks run the fast path or none)."""
+
+    def __init__(self, cr, ann_dir: str = "/dev/shm"):
+        self.cr = cr
+        st = cr.stage
+        self.rank, self.world = cr.rank, cr.world
+        self.dev = cr.device
+        self.n = None
+        self.ok = False
+        self.max_rows = ops.GEMV_MAX_ROWS
+        mine: dict = {}
+        err = None
+        try:
+            if self.dev.type != "cuda" or self.world < 2:
+                raise RuntimeError("needs GPU stages and >= 2 ranks")
+            self.n = native()
+            from ..utils.devmem import uncached_zeros
+
+            self.flags = uncached_zeros((F_WORDS,), torch.int32, self.dev)
+            self.in_w = st.in_pad
+            self.out_w = st.pads[-1]
+            self.out_f32 = st.is_last
+            if self.rank > 0:
+                self.slots = uncached_zeros((NSLOT, self.max_rows, self.in_w), torch.bfloat16,
+                                            self.dev)
+                self.x_local = torch.zeros(self.max_rows, self.in_w, dtype=torch.bfloat16,
+                                           device=self.dev)
+            torch.cuda.synchronize(self.dev)
+            mine = {"flags": self.n.ipc_export(self.flags.data_ptr()),
+                    "in_w": self.in_w, "out_w": self.out_w, "out_dim": st.out_dim}
+            if self.rank > 0:
+                mine["slots"] = self.n.ipc_export(self.slots.data_ptr())
+        except Exception as e:  # noqa: BLE001 -- agreed on below
+            err = e
+            mine = {"error": repr(e)}
+        everyone = [None] * self.world
+        dist.all_gather_object(everyone, mine)
+        # rank 0 sizes its result slots by the last stage's output width
+        if "error" not in everyone[0] and all("error" not in e for e in everyone):
+            try:
+                if self.rank == 0:
+                    w_last = everyone[-1]["out_w"]
+                    self.res_w = w_last
+                    self.res_bytes = HDR + self.max_rows * w_last * 4
+                    self.res = uncached_zeros((NSLOT, self.res_bytes // 4), torch.int32,
+                                              self.dev)
+                    torch.cuda.synchronize(self.dev)
+                    res_h = self.n.ipc_export(self.res.data_ptr())
+                else:
+                    res_h = None
+            except Exception as e:  # noqa: BLE001
+                err = err or e
+                res_h = None
+        else:
+            res_h = None
+        res_all = [None] * self.world
+        dist.all_gather_object(res_all, {"res": res_h, "error": repr(err) if err else None})
+        bad = [(r, e["error"]) for r, e in enumerate(everyone) if "error" in e] + \
+              [(r, e["error"]) for r, e in enumerate(res_all) if e["error"]]
+        # widths must chain: a producer's padded output is its consumer's padded input
+        for r in range(self.world - 1):
+            if not bad and everyone[r]["out_w"] != everyone[r + 1]["in_w"]:
+                bad.append((r, f"width {everyone[r]['out_w']} -> {everyone[r + 1]['in_w']}"))
+        if bad:
+            self.why = f"fast path unavailable: {bad}"[:300]
+            log.info(self.why)
+            self._agree(False)
+            return
+        ok = True
+        try:
+            imp = lambda r, k: self.n.ipc_import(*everyone[r][k])  # noqa: E731
+            nxt = (self.rank + 1) % self.world
+            self.next_flags = imp(nxt, "flags")
+            self.prev_flags = imp(self.rank - 1, "flags") if self.rank > 0 else 0
+            self._last_flags = imp(self.world - 1, "flags") if self.rank == 0 else 0
+            self.n_out = everyone[-1]["out_dim"]
+            if self.rank == self.world - 1:
+                self.dst = self.n.ipc_import(*res_all[0]["res"])  # rank 0's result slots
+            else:
+                self.dst = imp(nxt, "slots")
+        except Exception as e:  # noqa: BLE001
+            log.warning(f"fast path peer mapping failed: {e!r}")
+            ok = False
+        if not self._agree(ok):
+            self.why = "fast path unavailable: peer mapping failed on a rank"
+            return
+        # the announcement ring: rank 0 creates it, its name travels with a broadcast
+        name = [f"{ann_dir}/dnn_chain_{os.getpid()}_{os.environ.get('MASTER_PORT', '0')}"
+                if self.rank == 0 else None]
+        dist.broadcast_object_list(name, src=0)
+        try:
+            self.ann = Announcer(name[0], create=self.rank == 0)
+            good = True
+        except Exception as e:  # noqa: BLE001
+            log.warning(f"announcement ring unavailable: {e!r}")
+            good = False
+        if not self._agree(good):
+            self.why = "fast path unavailable: no shared-memory announcement ring"
+            return
+        self.stream = torch.cuda.Stream(self.dev)
+        self.seq = 0
+        self.lock = threading.Lock()
+        self.processed = 0
+        if self.rank == 0:
+            self.res_stream = torch.cuda.Stream(self.dev)
+            self.h_in = [torch.zeros(self.max_rows, self.in_w, dtype=torch.bfloat16,
+                                     pin_memory=True) for _ in range(NSLOT)]
+            self.h_out = [torch.zeros(self.res_bytes // 4, dtype=torch.int32, pin_memory=True)
+                          for _ in range(NSLOT)]
+            self.x0 = torch.zeros(self.max_rows, self.in_w, dtype=torch.bfloat16,
+                                  device=self.dev)
+            self.events = [torch.cuda.Event() for _ in range(NSLOT)]
+        self.ok = True
+        self.why = f"device-side chain ({NSLOT} slots per hop)"
+
+    def _agree(self, ok: bool) -> bool:
+        from ..parallel.comm import _cpu_group
+
+        t = torch.tensor([0 if ok else 1], dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=_cpu_group())
+        return int(t.item()) == 0
+
+    # ---- addresses ----------------------------------------------------------------------------
+    def _dst(self, slot: int) -> tuple[int, int, int, int]:
+        """(rows address, leading dimension bytes, header address, flag address) of the
+        consumer's slot ``slot``."""
+        if self.rank == self.world - 1:  # rank 0's result slot: header, then fp32 rows
+            base = self.dst + slot * self.res_bytes
+            return base + HDR, self.out_w * 4, base, self.next_flags + 4 * (F_RES + slot)
+        row_b = self.out_w * 2
+        return (self.dst + slot * self.max_rows * row_b, row_b,
+                self.next_flags + 4 * (F_HDR + 2 * slot), self.next_flags + 4 * (F_IN + slot))
+
+    def _send(self, s: torch.cuda.Stream, out: Optional[torch.Tensor], rows: int, seq: int,
+              status: int, in_hdr: int) -> None:
+        slot = seq % NSLOT
+        dst, dld, dhdr, dflag = self._dst(slot)
+        if out is None:
+            src, sld, rb = 0, 0, 0
+        else:
+            src, sld = out.data_ptr(), out.stride(0) * out.element_size()
+            rb = self.out_w * out.element_size()
+        self.n.chain_send(s.cuda_stream, src, sld, dst, dld, rows if out is not None else 0, rb,
+                          dhdr, in_hdr, _ptr(self.flags, F_ERR), self.rank, status,
+                          _ptr(self.flags, F_ACK), (seq - NSLOT) & 0xFFFFFFFF, dflag, seq, 0,
+                          self.cr.hop_timeout)  # (ack compares wrap: seq < NSLOT passes)
+
+    # ---- rank 0 -------------------------------------------------------------------------------
+    def predict(self, x: np.ndarray, timeout: Optional[float]) -> np.ndarray:
+        """One request of <= max_rows rows through the device-side chain -> float64 outputs."""
+        import grpc
+
+        from .ingress import StageFailure
+
+        rows = x.shape[0]
+        st = self.cr.stage
+        n = self.n
+        with self.lock:
+            self.seq += 1
+            seq = self.seq
+            slot = seq % NSLOT
+            hin = self.h_in[slot]
+            hin[:rows, :x.shape[1]].copy_(torch.from_numpy(np.ascontiguousarray(x, np.float32)))
+            self.ann.announce(seq, rows)
+            with torch.cuda.stream(self.stream):
+                self.x0[:rows].copy_(hin[:rows], non_blocking=True)
+                status = 0
+                try:
+                    out = st.forward(rows, x=self.x0[:rows])
+                except ValueError:
+                    out, status = None, ST_VALUE
+                self._send(self.stream, out, rows, seq, status, 0)
+            rs = self.res_stream
+            base = self.res[slot]
+            n.chain_wait(rs.cuda_stream, _ptr(self.flags, F_RES + slot), seq, _ptr(base, 2),
+                         self.cr.hop_timeout * self.world)
+            ho = self.h_out[slot]
+            nbytes = HDR + rows * self.res_w * 4
+            with torch.cuda.stream(rs):
+                ho[:nbytes // 4].copy_(base[:nbytes // 4], non_blocking=True)
+            # the result slot is free again (the last rank waits for this before reusing it)
+            n.chain_signal(rs.cuda_stream, self.prev_flags_of_last() + 4 * F_ACK, seq)
+            ev = self.events[slot]
+            ev.record(rs)
+        limit = self.cr.hop_timeout * self.world
+        if timeout is not None:
+            limit = min(limit, max(0.0, timeout))
+        t_end = time.monotonic() + limit
+        spins = 0
+        while not ev.query():
+            if time.monotonic() > t_end:
+                k = self.cr.blame(seq) if self.cr.store is not None else self.world - 1
+                raise StageFailure(self.cr.names[k], grpc.StatusCode.DEADLINE_EXCEEDED,
+                                   f"Deadline Exceeded (request {seq} not answered within "
+                                   f"{limit:.1f} s)")
+            spins += 1
+            if spins > 2000:
+                time.sleep(20e-6)
+        hdr = ho[:4].tolist()
+        code, who = hdr[0] & 0xFF, (hdr[0] >> 8) & 0xFF
+        if hdr[2]:  # rank 0's own wait gave up: the last stage never answered
+            code, who = ST_DEADLINE, self.world - 1
+        if code != ST_OK:
+            bad = self.cr.names[who % self.world]
+            if code == ST_DEADLINE:
+                raise StageFailure(bad, grpc.StatusCode.DEADLINE_EXCEEDED,
+                                   f"Deadline Exceeded (request {seq}: {bad} did not answer "
+                                   f"within {self.cr.hop_timeout:.1f} s)")
+            raise StageFailure(bad, grpc.StatusCode.INVALID_ARGUMENT if code == ST_VALUE
+                               else grpc.StatusCode.INTERNAL, f"stage {bad} failed (status "
+                               f"{code})")
+        vals = ho[HDR // 4:HDR // 4 + rows * self.res_w].view(torch.float32)
+        return vals.view(rows, self.res_w)[:, :self.n_out].double().numpy()
+
+    def prev_flags_of_last(self) -> int:
+        """Rank 0: the last rank's flag block (its ack word is what rank 0 writes)."""
+        return self._last_flags
+
+    # ---- ranks > 0 ----------------------------------------------------------------------------
+    def loop(self) -> None:
+        """Serve announced requests in order until the ring stops."""
+        n = self.n
+        seq = 0
+        s = self.stream
+        row_b = self.in_w * 2
+        while True:
+            seq += 1
+            rows = self.ann.next(seq)
+            if rows is None:
+                break
+            slot = seq % NSLOT
+            with torch.cuda.stream(s):
+                n.chain_recv(s.cuda_stream, _ptr(self.flags, F_IN + slot),
+                             self.slots[slot].data_ptr(), row_b,
+                             _ptr(self.flags, F_HDR + 2 * slot), self.x_local.data_ptr(), row_b,
+                             _ptr(self.flags, F_LHDR), rows, row_b, _ptr(self.flags, F_ERR), seq,
+                             self.prev_flags + 4 * F_ACK, self.cr.hop_timeout)
+                status = 0
+                out = None
+                try:
+                    self.cr._maybe_fault(self.processed)
+                    out = self.cr.stage.forward(rows, x=self.x_local[:rows])
+                except ValueError:
+                    status = ST_VALUE | (self.rank << 8)
+                except Exception:  # noqa: BLE001
+                    log.exception(f"({self.cr.names[self.rank]}) stage failure")
+                    status = ST_INTERNAL | (self.rank << 8)
+                self._send(s, out, rows, seq, status, _ptr(self.flags, F_LHDR))
+            self.processed = seq
+            self.cr._processed = seq
+        torch.cuda.synchronize(self.dev)
+
+    def stop(self) -> None:
+        if self.rank == 0 and self.ok:
+            self.ann.stop()
+
+    def close(self) -> None:
+        if self.ok:
+            self.ann.close()

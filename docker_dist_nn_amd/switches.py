@@ -74,6 +74,9 @@ SWITCHES: dict[str, tuple[str, str]] = {
     "DNN_RCCL_PLAN": ("auto", "native RCCL step form: streams (one stream per hop channel) | "
                       "slotted (one RCCL stream, per-slot groups: safe with one resident RCCL "
                       "kernel) | auto (streams when GPU_MAX_HW_QUEUES >= 6)"),
+    "DNN_IPC_PLAN": ("streams", "native IPC step form: streams (a stream per direction and relay "
+                                "duty) | slotted (ONE stream in global logical-clock order: "
+                                "no co-scheduling assumption, a captured graph is one chain)"),
     "DNN_FIRST_STEP_TIMEOUT": ("60", "bench.py: seconds the first multi-rank step may take "
                                "before the plan trace is printed and the run exits"),
     "DNN_LADDER": ("1", "bench.py with WORLD_SIZE > 1: a supervisor per rank runs each attempt "

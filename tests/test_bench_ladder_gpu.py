@@ -30,7 +30,7 @@ def test_bench_ladder_survives_hang_and_crash(tmp_path):
     env.update(DNN_FORCE_DEVICE="0", DNN_DIST_BACKEND="gloo", DNN_FIRST_STEP_TIMEOUT="15",
                DNN_LADDER_STALL="60", TMPDIR=str(tmp_path),
                DNN_LADDER_FAULT="default=stage:0,step:0,kind:hang;"
-                                "rccl-slotted=stage:1,step:0,kind:crash")
+                                "ipc-slotted=stage:1,step:0,kind:crash")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                         "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
                         "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
@@ -43,12 +43,12 @@ def test_bench_ladder_survives_hang_and_crash(tmp_path):
     out = json.loads(lines[0])
     assert out["value"] > 0 and out["n_gpus"] == 2
     lad = out["ladder"]
-    assert lad["rung"] == "rccl-streams"
+    assert lad["rung"] == "rccl-slotted"
     att = lad["attempts"]
-    assert [a["rung"] for a in att] == ["default", "rccl-slotted", "rccl-streams"]
+    assert [a["rung"] for a in att] == ["default", "ipc-slotted", "rccl-slotted"]
     assert att[0]["rc"]["0"] == "3" and att[0]["rc"]["1"] in ("killed", "3")  # watchdog exit
     assert att[1]["rc"]["1"] == "87" and att[1]["rc"]["0"] == "killed"      # injected crash
     assert att[2]["ok"] and att[2]["rc"] == {"0": "0", "1": "0"}
-    assert out["ladder_rung"] == "rccl-streams"
+    assert out["ladder_rung"] == "rccl-slotted"
     assert out["dp_only"]["value"] > 0 and out["dp_only"]["parallelism"] == "dp2"
     assert [a["rung"] for a in lad["dp_attempts"]] == ["dp-native"]

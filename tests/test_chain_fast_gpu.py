@@ -1,0 +1,206 @@
+"""Device-side serving chain (serve/fastpath.py, csrc/kernels/chain.hip) on one GPU: a 4-rank
+chain with every stage on cuda:0 (gloo for the set-up collectives, IPC slots + flags for the
+requests), brought up by run_grpc_fcnn.py --mode ranks and queried over the reference gRPC
+protocol. Serving-size requests (<= 8 rows) take the device-side chain, larger ones the
+message chain; both must match the fp64 reference forward. A stage that hangs is blamed by
+name within the per-hop deadline; concurrent callers each get their own rows."""
+import os
+import socket
+import subprocess
+import sys
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+import grpc
+import numpy as np
+import pytest
+
+from docker_dist_nn_amd.config import load_model_config
+from docker_dist_nn_amd.cpu_ref import model_forward
+from docker_dist_nn_amd.data import write_examples
+from docker_dist_nn_amd.serve.ingress import LayerClient
+from docker_dist_nn_amd.weights_io import export_model_json
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture(scope="module")
+def model4(tmp_path_factory):
+    d = tmp_path_factory.mktemp("fast")
+    rng = np.random.default_rng(3)
+    dims = [784, 256, 128, 64, 10]
+    ws = [rng.standard_normal((dims[i + 1], dims[i])) * (2.0 / np.sqrt(dims[i])) for i in range(4)]
+    bs = [rng.standard_normal(dims[i + 1]) * 0.1 for i in range(4)]
+    cfg = d / "model4.json"
+    export_model_json(str(cfg), ws, bs, ["relu", "relu", "relu", "softmax"],
+                      layer_distribution=[1, 1, 1, 1])
+    x = rng.random((64, 784))
+    inp = d / "inputs4.json"
+    write_examples(str(inp), x, np.zeros(64, dtype=np.int64))
+    return cfg, inp, x
+
+
+def _start(cfg, inp, port, tmp, extra_env=None, args=()):
+    env = dict(os.environ, PYTHONPATH=ROOT, DNN_FORCE_DEVICE="0", DNN_DIST_BACKEND="gloo",
+               **(extra_env or {}))
+    p = subprocess.Popen([sys.executable, os.path.join(ROOT, "src", "run_grpc_fcnn.py"),
+                          "--config", str(cfg), "--inputs", str(inp), "--port", str(port),
+                          "--mode", "ranks", "--device", "cuda", "--run-for", "120",
+                          "--cache-dir", str(tmp / "cache"), *args],
+                         env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    t0 = time.time()
+    while time.time() - t0 < 120:
+        try:
+            socket.create_connection(("127.0.0.1", port), timeout=0.5).close()
+            return p
+        except OSError:
+            if p.poll() is not None:
+                raise RuntimeError(p.stdout.read())
+            time.sleep(0.3)
+    p.terminate()
+    raise RuntimeError("server did not come up")
+
+
+def _stop(p):
+    p.terminate()
+    try:
+        out, _ = p.communicate(timeout=60)
+    except subprocess.TimeoutExpired:
+        p.kill()
+        out, _ = p.communicate()
+    return out
+
+
+@pytest.mark.timeout(240)
+def test_fast_chain_matches_reference_and_serves_concurrently(model4, tmp_path):
+    cfg, inp, x = model4
+    layers = load_model_config(str(cfg)).layers
+    port = _port()
+    p = _start(cfg, inp, port, tmp_path)
+    try:
+        c = LayerClient(f"127.0.0.1:{port}", timeout=60)
+        for rows in (1, 3, 8, 40, 1):  # 40 rows: the message chain
+            q = x[:rows] if rows != 3 else x[10:13]
+            np.testing.assert_allclose(c.process(q), model_forward(layers, q), atol=2e-2)
+        chunks = [x[i:i + 1 + i % 8] for i in range(48)]
+        with ThreadPoolExecutor(8) as pool:
+            outs = list(pool.map(c.process, chunks))
+        for ch, out in zip(chunks, outs):
+            np.testing.assert_allclose(out, model_forward(layers, ch), atol=2e-2)
+        ts = []
+        for _ in range(50):
+            t0 = time.perf_counter()
+            c.process(x[:1])
+            ts.append(time.perf_counter() - t0)
+        print(f"fast chain batch-1 p50 {np.median(ts) * 1e3:.3f} ms")
+        c.close()
+    finally:
+        out = _stop(p)
+    assert "device-side chain" in out, out[-3000:]
+    assert "Shutdown complete." in out, out[-3000:]
+
+
+@pytest.mark.timeout(240)
+def test_fast_chain_blames_the_hung_stage(model4, tmp_path):
+    cfg, inp, x = model4
+    port = _port()
+    p = _start(cfg, inp, port, tmp_path,
+               {"DNN_FAULT_STAGE": "2", "DNN_FAULT_KIND": "hang", "DNN_FAULT_AFTER": "1"},
+               args=("--hop-timeout", "1.0"))
+    try:
+        c = LayerClient(f"127.0.0.1:{port}", timeout=30)
+        ref = model_forward(load_model_config(str(cfg)).layers, x[:1])
+        np.testing.assert_allclose(c.process(x[:1]), ref, atol=2e-2)  # before the hang
+        for _ in range(2):
+            t0 = time.monotonic()
+            with pytest.raises(grpc.RpcError) as ei:
+                c.process(x[:1])
+            assert ei.value.code() == grpc.StatusCode.DEADLINE_EXCEEDED, ei.value
+            assert "Failed to forward request to layer_container_2" in ei.value.details(), \
+                ei.value.details()
+            assert time.monotonic() - t0 < 6.0
+        c.close()
+    finally:
+        out = _stop(p)
+    assert "device-side chain" in out, out[-3000:]
+
+
+@pytest.mark.timeout(240)
+def test_fast_chain_stage_error_is_reported(model4, tmp_path):
+    cfg, inp, x = model4
+    port = _port()
+    p = _start(cfg, inp, port, tmp_path,
+               {"DNN_FAULT_STAGE": "1", "DNN_FAULT_KIND": "raise", "DNN_FAULT_AFTER": "0"})
+    try:
+        c = LayerClient(f"127.0.0.1:{port}", timeout=30)
+        with pytest.raises(grpc.RpcError) as ei:
+            c.process(x[:2])
+        assert ei.value.code() == grpc.StatusCode.INTERNAL, ei.value
+        assert "layer_container_1" in ei.value.details(), ei.value.details()
+        c.close()
+    finally:
+        _stop(p)
+
+
+def test_chain_kernels_in_one_process(dev):
+    """csrc/kernels/chain.hip on its own: a producer stream sends rows into a consumer's slot
+    (flag, header), the consumer stream receives them into its cached buffer and acks; a
+    producer whose consumer never drained the slot times out and blames the consumer; a
+    consumer whose rows never arrive times out, and its send blames the producer."""
+    import torch
+
+    from docker_dist_nn_amd.utils.devmem import uncached_zeros
+    from docker_dist_nn_amd.utils.native import native
+
+    n = native()
+    rows, width = 3, 64
+    rb = width * 2
+    flags_c = uncached_zeros((64,), torch.int32, dev)  # consumer: [0] in flag, [2:4] hdr,
+    flags_p = uncached_zeros((64,), torch.int32, dev)  # producer: [8] ack, [9] err
+    slot = uncached_zeros((8, width), torch.bfloat16, dev)
+    src = torch.randn(8, width, device=dev).to(torch.bfloat16)
+    dst = torch.zeros(8, width, dtype=torch.bfloat16, device=dev)
+    lhdr = torch.zeros(4, dtype=torch.int32, device=dev)
+    err_c = torch.zeros(4, dtype=torch.int32, device=dev)
+    sp, sc = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    fp, fc = flags_p.data_ptr(), flags_c.data_ptr()
+
+    def send(seq, ack_target, timeout=2.0):
+        n.chain_send(sp.cuda_stream, src.data_ptr(), rb, slot.data_ptr(), rb, rows, rb,
+                     fc + 8, 0, fp + 36, 0, 0, fp + 32, ack_target, fc, seq, 0, timeout)
+
+    def recv(seq, timeout=2.0):
+        n.chain_recv(sc.cuda_stream, fc, slot.data_ptr(), rb, fc + 8, dst.data_ptr(), rb,
+                     lhdr.data_ptr(), rows, rb, err_c.data_ptr(), seq, fp + 32, timeout)
+
+    recv(1)          # enqueued before the data exists: it waits
+    send(1, 0)
+    torch.cuda.synchronize(dev)
+    assert torch.equal(dst[:rows], src[:rows])
+    assert lhdr[:2].tolist() == [0, rows] and int(flags_p[8]) == 1 and int(err_c[0]) == 0
+    # the consumer drained slot 1 (ack = 1): request 2 may reuse it
+    src.mul_(2)
+    send(2, 1)
+    recv(2)
+    torch.cuda.synchronize(dev)
+    assert torch.equal(dst[:rows], src[:rows]) and int(flags_p[8]) == 2
+    # request 3 needs ack >= 3, which never comes: the send gives up and blames stage 0 + 1
+    send(3, 3, timeout=0.2)
+    torch.cuda.synchronize(dev)
+    assert int(flags_c[0]) == 3 and (int(flags_c[2]) & 0xFF) == 4
+    assert (int(flags_c[2]) >> 8) & 0xFF == 1
+    # request 9 never arrives: the receive times out, sets its error word, pulls nothing
+    dst.zero_()
+    recv(9, timeout=0.2)
+    torch.cuda.synchronize(dev)
+    assert int(err_c[0]) == 1 and float(dst.float().abs().sum()) == 0.0

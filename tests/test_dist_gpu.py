@@ -132,13 +132,13 @@ def test_pp2_ipc_pipe_bitwise_equals_rccl_path(dev):
 
 
 def _native_worker(rank, world, port, native_dist, steps, nm, out_dir, relays=0, tag=None,
-                   graph=False, fault=""):
+                   graph=False, fault="", plan="streams"):
     # every stream of a plan that waits on a flag needs a hardware queue of its own (HIP
     # multiplexes streams beyond GPU_MAX_HW_QUEUES onto shared queues, where one blocked wait
     # would stall the others): 4 plan streams + the relay duties + the default stream
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DNN_PIPE="ipc",
                       DNN_NATIVE_DIST=native_dist, DNN_IPC_RELAYS=str(relays),
-                      GPU_MAX_HW_QUEUES="8", DNN_FAULT_NATIVE_STEP=fault)
+                      GPU_MAX_HW_QUEUES="8", DNN_FAULT_NATIVE_STEP=fault, DNN_IPC_PLAN=plan)
     tag = native_dist if tag is None else tag
     import time
 
@@ -241,16 +241,18 @@ def test_relayed_ipc_hops_bitwise_equal_direct(dev, world, relays):
                               np.load(os.path.join(d, "nrelay_loss.npy")))
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_native_multirank_step_graph_capture(dev, world):
+@pytest.mark.parametrize("world,relays", [(2, 0), (4, 0), (4, 2), (4, "auto")])
+def test_native_multirank_step_graph_capture(dev, world, relays):
     """The native multi-rank step (IPC hops: device step-number flag kernels) captured into a
     HIP graph and replayed gives bit-identical training to eager plan runs, and a replayed
-    step costs the host only the graph launch."""
+    step costs the host only the graph launch. Relayed hops included (capture
+    now records the slotted single-stream form, Trainer.capture)."""
     steps, nm = 6, 4
     with tempfile.TemporaryDirectory() as d:
         for tag, graph in (("eager", False), ("graph", True)):
             mp.start_processes(_native_worker,
-                               args=(world, _free_port(), "1", steps, nm, d, 0, tag, graph),
+                               args=(world, _free_port(), "1", steps, nm, d, relays, tag,
+                                     graph),
                                nprocs=world, join=True, start_method="spawn")
         for k in range(4):
             a = np.load(os.path.join(d, f"neager_w{k}.npy"))
@@ -262,6 +264,22 @@ def test_native_multirank_step_graph_capture(dev, world):
                 for r in range(world)]
         print("graph replay host s/step per rank:", host)
         assert max(host) < 5e-4, host
+
+
+@pytest.mark.parametrize("world,relays", [(3, 1), (4, "auto")])
+def test_ipc_slotted_plan_bitwise_equals_streams(dev, world, relays):
+    """The slotted IPC form (DNN_IPC_PLAN=slotted: one stream per rank in logical-clock order)
+    trains bit for bit like the multi-stream form, relays included."""
+    steps, nm = 3, 4
+    with tempfile.TemporaryDirectory() as d:
+        for plan in ("streams", "slotted"):
+            mp.start_processes(_native_worker,
+                               args=(world, _free_port(), "1", steps, nm, d, relays, plan,
+                                     False, "", plan),
+                               nprocs=world, join=True, start_method="spawn")
+        for k in range(4):
+            assert np.array_equal(np.load(os.path.join(d, f"nstreams_w{k}.npy")),
+                                  np.load(os.path.join(d, f"nslotted_w{k}.npy"))), k
 
 
 def test_step_plan_rccl_allreduce_one_rank(dev):

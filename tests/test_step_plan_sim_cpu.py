@@ -109,8 +109,9 @@ def build_rccl(rank, pp, dp, nm, mb=256, spec="784-512-256-128-10", dist=None,
     return nsmod.NativeStep(ex, mesh, "rccl", comms=_comms(mesh), mode=mode, build_only=True)
 
 
-def build_ipc(rank, pp, dp, nm, mb, k, width, sched):
-    """k: relays per hop (relay_assignment), or a per-hop table (relay_plan)."""
+def build_ipc(rank, pp, dp, nm, mb, k, width, sched, mode=None):
+    """k: relays per hop (relay_assignment), or a per-hop table (relay_plan); mode: the IPC
+    plan form (streams | slotted)."""
     spec = MLPSpec.parse("-".join([str(width)] * (pp + 1)))
     st, mesh = _stage(rank, pp, dp, nm, mb, spec, [1] * pp, "bf16", "allreduce")
     st._prog = NS(segments=lambda: {"FINO", "W"})
@@ -145,7 +146,7 @@ def build_ipc(rank, pp, dp, nm, mb, k, width, sched):
     ipc.relay_dst = [{"buf": _addr(dst, "x_in" if d == "f" else "grad_out"),
                       "flags": _addr(dst, "flags")} for _s, dst, d, _p in ipc.duties]
     ex = NS(stages=[st], ops=[schedule_ops(sched, pp, nm, mesh.stage)], kind=sched)
-    return nsmod.NativeStep(ex, mesh, "ipc", ipc=ipc, build_only=True)
+    return nsmod.NativeStep(ex, mesh, "ipc", ipc=ipc, build_only=True, mode=mode)
 
 
 def check_enqueue_order(ops):
@@ -388,3 +389,39 @@ def test_relay_plan_gives_the_wide_boundary_more_paths():
     assert max(duties.values()) <= 6
     loads = relay_link_loads(4, 2, t, hb)
     assert max(loads.values()) < 0.5 * hb[0]
+
+
+@pytest.mark.parametrize("pp,dp,k", [(2, 1, 0), (4, 1, 0), (4, 1, 2), (4, 2, 2), (8, 1, 6),
+                                     (4, 2, "plan"), (8, 1, "plan"), (2, 4, "plan")])
+@pytest.mark.parametrize("sched", ["1f1b", "gpipe", "1f1b_lh"])
+def test_ipc_slotted_plans_one_stream_deadlock_free(pp, dp, k, sched):
+    """The slotted IPC form (DNN_IPC_PLAN=slotted, the graph-capture form): ONE stream per
+    rank in logical-clock order completes -- no wait of a rank precedes, in its own stream,
+    the send or relay that another rank's wait needs -- with every relay layout."""
+    nm = 2 * pp
+    if k == "plan":
+        k = _plan_table(pp, dp)
+    builds = {r: build_ipc(r, pp, dp, nm, 64, k, 64, sched, mode="slotted")
+              for r in range(pp * dp)}
+    for ns in builds.values():
+        assert ns.mode == "ipc-slotted" and ns.n_streams == 1
+        assert {o["stream"] for o in nsmod.flatten(ns.ops)} == {0}
+        check_enqueue_order(ns.ops)
+    assert sim(builds, steps=3).makespan > 0
+
+
+def test_ipc_slotted_rows_reach_every_consumer_once():
+    """The slotted form moves the same stripes as the streams form."""
+    pp, dp, nm, mb, width = 4, 2, 4, 64, 64
+    k = _plan_table(pp, dp)
+    rb = width * 2
+    for mode in ("streams", "slotted"):
+        writes = {}
+        for r in range(pp * dp):
+            for o in build_ipc(r, pp, dp, nm, mb, k, width, "1f1b", mode=mode).ops:
+                if o["kind"] == nsmod.COPY and (o["b"] >> 32) & 0xff in (1, 2):
+                    for row in range(o["count"] // rb):
+                        key = (o["b"] >> 32, (o["b"] & 0xffffffff) // rb + row)
+                        writes[key] = writes.get(key, 0) + 1
+        assert set(writes.values()) == {1}, mode
+        assert len(writes) == (pp - 1) * 2 * dp * nm * mb
