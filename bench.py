@@ -338,7 +338,7 @@ def supervise(a, argv) -> int:
         rungs = [ladder.Rung("default")]
     else:
         rungs = ladder.bench_rungs(world, dp_only=a.parallelism.startswith("dp"))
-    res, rung = sup.climb(rungs)
+    res, rung = sup.climb(rungs, budget_s=float(switches.get("DNN_LADDER_BUDGET")))
     attempts = list(sup.attempts)
     dp_only = dp_attempts = None
     if res is not None and not a.no_dp_compare and \

@@ -309,10 +309,23 @@ class Supervisor:
         self.log(f"attempt {i} rung {rung.name}: {'ok' if ok else 'FAILED'} {rec['rc']}")
         return ok, result
 
-    def climb(self, rungs: Sequence[Rung]) -> tuple[Optional[dict], Optional[Rung]]:
+    def climb(self, rungs: Sequence[Rung],
+              budget_s: Optional[float] = None) -> tuple[Optional[dict], Optional[Rung]]:
         """Try ``rungs`` in order until one succeeds; (its result or None, the rung) -- the
         same on every rank."""
-        for rung in rungs:
+        t0 = time.monotonic()
+        for k, rung in enumerate(rungs):
+            # past the time budget only the last (most conservative) rung is still tried;
+            # every rank measures the same attempts' outcomes but its own clock, so the skip
+            # decision is rank 0's, shared through the store
+            if budget_s is not None and k < len(rungs) - 1:
+                key = self._key(self._n, "skip")
+                if self.rank == 0:
+                    self.store.set(key, "1" if time.monotonic() - t0 > budget_s else "0")
+                if self.store.get(key).decode() == "1":
+                    self.log(f"time budget {budget_s:.0f} s spent: skipping rung {rung.name}")
+                    self.attempts.append({"rung": rung.name, "ok": False, "skipped": True})
+                    continue
             ok, result = self.attempt(rung)
             if ok:
                 return result, rung

@@ -84,6 +84,8 @@ SWITCHES: dict[str, tuple[str, str]] = {
                         "on a hang or crash; 0 = measure in this process"),
     "DNN_LADDER_STALL": ("180", "ladder: seconds a child may go without a heartbeat before "
                                 "it is killed and the next rung runs"),
+    "DNN_LADDER_BUDGET": ("900", "ladder: seconds of attempts after which only the last, "
+                                 "most conservative rung is still tried"),
     "DNN_LADDER_FAULT": ("", "ladder fault injection (tests): 'rung=stage:S,step:N,kind:K;...' "
                              "-- the child of that rung gets DNN_FAULT (stage = rank)"),
     "DNN_PIPE": ("auto", "pipeline transport: auto (IPC with relays on RCCL jobs when every "
