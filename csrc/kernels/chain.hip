@@ -10,6 +10,9 @@ namespace dnn {
 
 namespace {
 
+bool misaligned4(const void* p) { return reinterpret_cast<uintptr_t>(p) & 3; }
+bool misaligned16(const void* p) { return reinterpret_cast<uintptr_t>(p) & 15; }
+
 __device__ __forceinline__ bool reached(const uint32_t* flag, uint32_t target) {
   return (int)(__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - target) >=
          0;
@@ -111,6 +114,44 @@ __global__ void chain_signal_kernel(uint32_t* flag, uint32_t value) {
   }
 }
 
+__global__ __launch_bounds__(256) void p2p_copy_signal_seq_kernel(
+    const uint4* __restrict__ src, uint4* __restrict__ dst, long n16,
+    const unsigned char* __restrict__ src_t, unsigned char* __restrict__ dst_t, int tail,
+    uint32_t* flag, const uint32_t* seq, int delta, uint32_t* counter) {
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n16; i += (long)gridDim.x * 256)
+    dst[i] = src[i];
+  if (blockIdx.x == 0 && (int)threadIdx.x < tail) dst_t[threadIdx.x] = src_t[threadIdx.x];
+  __threadfence_system();  // this thread's part is visible before the workgroup counts in
+  __syncthreads();
+  const unsigned t = threadIdx.x;
+  if (t == 0) {
+    const uint32_t prev = __hip_atomic_fetch_add(counter + t, 1u, __ATOMIC_ACQ_REL,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1) {  // the last workgroup: every part has landed
+      __hip_atomic_store(counter + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t v = __hip_atomic_load(seq + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __threadfence_system();
+      __hip_atomic_store(flag + t, v + (uint32_t)delta, __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+int p2p_copy_signal_seq(void* dst, const void* src, size_t bytes, uint32_t* flag,
+                        const uint32_t* seq, int delta, uint32_t* counter, hipStream_t stream) {
+  if ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15) return -1;
+  if (!flag || !seq || !counter || misaligned4(flag) || misaligned4(counter)) return -1;
+  const long n16 = (long)(bytes / 16);
+  const int tail = (int)(bytes % 16);
+  const int grid = (int)std::min<long>(std::max<long>(1, (n16 + 255) / 256), 2048);
+  hipLaunchKernelGGL(p2p_copy_signal_seq_kernel, dim3(grid), dim3(256), 0, stream,
+                     reinterpret_cast<const uint4*>(src), reinterpret_cast<uint4*>(dst), n16,
+                     reinterpret_cast<const unsigned char*>(src) + n16 * 16,
+                     reinterpret_cast<unsigned char*>(dst) + n16 * 16, tail, flag, seq, delta,
+                     counter);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
 unsigned long long chain_ticks(double seconds) {
   static int rate_khz = [] {  // wall_clock64 ticks per ms (100 MHz on gfx9)
     int r = 0, dev = 0;
@@ -121,8 +162,6 @@ unsigned long long chain_ticks(double seconds) {
   return (unsigned long long)(std::max(0.0, seconds) * 1e3 * (double)rate_khz);
 }
 
-static bool misaligned4(const void* p) { return reinterpret_cast<uintptr_t>(p) & 3; }
-static bool misaligned16(const void* p) { return reinterpret_cast<uintptr_t>(p) & 15; }
 
 int chain_wait(const uint32_t* flag, uint32_t target, uint32_t* err, double timeout_s,
                hipStream_t stream) {

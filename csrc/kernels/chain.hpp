@@ -68,4 +68,12 @@ int chain_send(const ChainSend& p, hipStream_t stream);
 // *flag = value with system-scope release (one lane, a vector store).
 int chain_signal(uint32_t* flag, uint32_t value, hipStream_t stream);
 
+// Training step plans (runtime/step_plan.cpp COPYSIG): a peer copy followed by its flag in ONE
+// launch. Every workgroup copies its share, fences, and bumps `counter`; the last one to
+// arrive resets the counter and stores *flag = *seq + delta (system-scope release), so the
+// flag is raised only after every workgroup's rows are visible. `counter` starts at 0 and is
+// left at 0.
+int p2p_copy_signal_seq(void* dst, const void* src, size_t bytes, uint32_t* flag,
+                        const uint32_t* seq, int delta, uint32_t* counter, hipStream_t stream);
+
 }  // namespace dnn

@@ -1,5 +1,6 @@
 #include "runtime/step_plan.hpp"
 #include "runtime/p2p.hpp"
+#include "kernels/chain.hpp"
 #include "kernels/elementwise.hpp"
 
 #include <dlfcn.h>
@@ -110,6 +111,7 @@ StepPlan::~StepPlan() {
   if (fork_) (void)hipEventDestroy(fork_);
   for (auto s : streams_) (void)hipStreamDestroy(s);
   if (dev_) (void)hipFree(dev_);
+  if (counters_) (void)hipFree(counters_);
 }
 
 void StepPlan::add(const Op& op) {
@@ -136,6 +138,26 @@ void StepPlan::add(const Op& op) {
   } else if (group_open_ >= 0 && (!(op.kind == SEND || op.kind == RECV) ||
                                   op.stream != group_open_)) {
     throw std::invalid_argument("StepPlan op: only SEND / RECV of the group's stream in a group");
+  }
+  if (op.kind == COPYSIG) throw std::invalid_argument("StepPlan op: COPYSIG is internal");
+  // a flag that follows its copy on the same stream rides in the copy's launch
+  static const bool merge = [] {
+    const char* e = std::getenv("DNN_PLAN_COPYSIG");
+    return !(e && e[0] == '0');
+  }();
+  if (merge && op.kind == SIGNAL && !ops_.empty() && ops_.back().kind == COPY &&
+      ops_.back().stream == op.stream && n_counters_ < MAX_COUNTERS) {
+    if (!counters_) {
+      ck(hipMalloc(&counters_, MAX_COUNTERS * sizeof(uint32_t)), "hipMalloc");
+      ck(hipMemset(counters_, 0, MAX_COUNTERS * sizeof(uint32_t)), "hipMemset");
+      ck(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    }
+    Op& c = ops_.back();
+    c.kind = COPYSIG;
+    c.flag = op.a;
+    c.delta = op.delta;
+    c.counter = n_counters_++;
+    return;
   }
   ops_.push_back(op);
 }
@@ -207,6 +229,12 @@ void StepPlan::run(hipStream_t main) {
         break;
       case COPY:  // kernels, not hipMemcpyAsync / hipStreamWriteValue32 (runtime/p2p.cpp)
         copy_async(reinterpret_cast<void*>(o.b), reinterpret_cast<const void*>(o.a), o.count, s);
+        break;
+      case COPYSIG:
+        if (p2p_copy_signal_seq(reinterpret_cast<void*>(o.b), reinterpret_cast<const void*>(o.a),
+                                o.count, reinterpret_cast<uint32_t*>(o.flag), dev_,
+                                (int)o.delta, counters_ + o.counter, s) != 0)
+          throw std::runtime_error("p2p_copy_signal_seq failed");
         break;
       case SIGNAL:  // flag = device step number + delta (kernels: capturable, non-blocking)
         if (p2p_signal_seq(reinterpret_cast<uint32_t*>(o.a), dev_, (int)o.delta, s) != 0)

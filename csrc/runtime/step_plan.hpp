@@ -53,8 +53,10 @@ const NcclApi* nccl_api();  // nullptr until nccl_load succeeded
 
 class StepPlan {
  public:
+  // COPYSIG is never added from outside: add() merges a SIGNAL that directly follows a COPY
+  // on the same stream into the COPY (one kernel: kernels/chain.hpp p2p_copy_signal_seq)
   enum Kind { SEG = 0, SEND, RECV, ALLREDUCE, REDUCE_SCATTER, ALL_GATHER, COPY, SIGNAL, WAITV,
-              REC, WAIT, GSTART, GEND };
+              REC, WAIT, GSTART, GEND, COPYSIG };
   struct Op {
     Kind kind;
     int stream = 0;
@@ -66,6 +68,8 @@ class StepPlan {
     int dtype = 0, peer = 0;
     int64_t delta = 0;      // SIGNAL / WAITV value = seq + delta
     int event = 0, src = 0; // REC: event id on `stream`; WAIT: `stream` waits event id
+    uint64_t flag = 0;      // COPYSIG: the merged SIGNAL's flag (value = seq + delta)
+    int counter = -1;       // COPYSIG: its arrival counter slot
   };
 
   explicit StepPlan(int n_streams, int n_events);
@@ -77,6 +81,7 @@ class StepPlan {
   void clear_ops() {
     ops_.clear();
     group_open_ = -1;
+    n_counters_ = 0;  // (the counters are back at 0 after every completed run)
   }
   // One step on `main`; advances the sequence number first (seq() = 1 in the first step).
   void run(hipStream_t main);
@@ -110,6 +115,11 @@ class StepPlan {
   double wait_timeout_;
   // [0] = step number read by the SIGNAL / WAITV kernels, [1] = wait-timeout error word
   uint32_t* dev_ = nullptr;
+  // COPYSIG arrival counters (one per merged op, zero between runs); merging can be turned
+  // off with DNN_PLAN_COPYSIG=0
+  uint32_t* counters_ = nullptr;
+  int n_counters_ = 0;
+  static constexpr int MAX_COUNTERS = 4096;
 };
 
 }  // namespace dnn
