@@ -111,7 +111,8 @@ class Announcer:
                 time.sleep(50e-6)
         i = 4 + 2 * (seq % ANN_SLOTS)
         while a[i] != seq:  # the head is written last; the entry is there
-            pass
+            if a[i] > seq:  # lapped: rank 0 ran a whole ring ahead of this stage
+                raise RuntimeError(f"announcement ring overrun at request {seq}")
         return int(a[i + 1])
 
     def close(self) -> None:
