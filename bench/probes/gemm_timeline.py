@@ -44,7 +44,18 @@ def wgrad(R, M, N, splits):
                                          timeline=tl)
 
 
+def dgrad(M, K, N):
+    """dX = dZ . W with the W^T shadow (both K-major), ReLU derivative from the stored
+    activation (the headline's dgrad 256 -> 512)."""
+    dz, wt, h = rnd(M, K, scale=0.1), rnd(N, K, scale=0.05), rnd(M, N)
+    y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    return lambda tile, st, tl: ops.gemm(dz, wt, y, layout_a=KMAJ, layout_b=KMAJ, M=M, N=N,
+                                         K=K, aux=h, act="relu", tiles=tile, stages=st,
+                                         timeline=tl)
+
+
 CASES = {"f0": lambda: fwd(65536, 832, 512), "f1": lambda: fwd(65536, 512, 256),
+         "d1": lambda: dgrad(65536, 256, 512), "d1s": lambda: dgrad(8192, 256, 512),
          "f0s": lambda: fwd(8192, 832, 512), "f0m": lambda: fwd(32768, 832, 512),
          "f0f32": lambda: fwd32(65536, 832, 512), "f0sf32": lambda: fwd32(8192, 832, 512),
          "w0": lambda: wgrad(65536, 512, 832, 18), "m8f": lambda: fwd(65536, 1024, 1024)}
@@ -84,5 +95,7 @@ for name in a.cases.split(","):
             "prologue_us_med": round(float(q(pro.tolist(), .5)), 2),
             "loop_us_med": round(float(q(loop.tolist(), .5)), 2),
             "epilogue_us_med": round(float(q(epi.tolist(), .5)), 2),
+            "epilogue_us_p10_p90": [round(float(q(epi.tolist(), f)), 2) for f in (.1, .9)],
+            "loop_us_p10_p90": [round(float(q(loop.tolist(), f)), 2) for f in (.1, .9)],
             "wg_total_us_med": round(float(q((d[:, 3] - d[:, 0]).tolist(), .5)), 2)}),
             flush=True)
