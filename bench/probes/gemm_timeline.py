@@ -70,7 +70,11 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--cases", default="f0,f1,w0,m8f")
 ap.add_argument("--variants", default="256x256:2,256x256:6")
 ap.add_argument("--wvariants", default="128x128:2,128x128:6")
+ap.add_argument("--cold", action="store_true",
+                help="evict the Infinity Cache (write 1 GiB) before the timed run: operands "
+                     "come from HBM, as inside the training step")
 a = ap.parse_args()
+flush = torch.empty(1 << 29, dtype=torch.bfloat16, device=dev) if a.cold else None
 tl = torch.zeros(4 * 65536, dtype=torch.int64, device=dev)
 for name in a.cases.split(","):
     run = CASES[name]()
@@ -80,6 +84,8 @@ for name in a.cases.split(","):
         for _ in range(3):
             run(tile, int(st), None)
         tl.zero_()
+        if flush is not None:
+            flush.fill_(1.0)
         torch.cuda.synchronize()
         run(tile, int(st), tl)
         torch.cuda.synchronize()
@@ -89,7 +95,7 @@ for name in a.cases.split(","):
         start, pro, loop, epi = (d[:, 0] - t0), (d[:, 1] - d[:, 0]), (d[:, 2] - d[:, 1]), \
             (d[:, 3] - d[:, 2])
         print(json.dumps({
-            "case": name, "tile": list(tile), "stages": int(st), "wgs": int(d.shape[0]),
+            "case": name, "cold": bool(a.cold), "tile": list(tile), "stages": int(st), "wgs": int(d.shape[0]),
             "span_us": round(float(d[:, 3].max() - t0), 2),
             "start_us_p10_p50_p90": [round(float(q(start.tolist(), f)), 2) for f in (.1, .5, .9)],
             "prologue_us_med": round(float(q(pro.tolist(), .5)), 2),
