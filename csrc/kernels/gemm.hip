@@ -191,7 +191,7 @@ const char* gemm_error_string(int code) {
     case -9: return "hip launch failed";
     case -10: return "colsum needs bf16 output and ld_colsum >= N";
     case -11: return "fused cross-entropy needs bf16 output, N == bn <= 128, a bias and 0 < n_cls <= N";
-    case -13: return "relu bit masks need bf16 output, act = relu, ld_mask >= N/8, no aux/xent, one-tile form";
+    case -13: return "relu bit masks need bf16 output, act = relu, ld_mask >= N/8 (or < 0: fragment order, stage codes 9-11 / 15-17), no aux/xent, one-tile form";
     case -12: return "pipeline stages must be 2..4, 5 = A3/B2 ring, 6 / 7 = register-prefetched 2 / 3-deep ring (256x256: 6; 256x128, 128x128, 128x64, 64x64: 6, 7), 9 / 10 = the same with the register-direct epilogue (no ct / fused update), 11 = register-direct epilogue on the A3/B2 ring (256x256, 256x128, 128x128), 12..14 = 32-deep k-steps with 2..4 stages (256x256: 12-14, 256x128: 12-13, 128x128: 12, 14), 15 / 16 = code 9 with an L2 touch-prefetch 1 / 2 k-steps ahead (256x256, 256x128, 128x128, 64x64), 17 = code 11 with touch distance 1 (256x128, 128x128) (8-wave tiles: 2, 3, 5; 256x256: 2, 5 or 8 = ping-pong; 5, 12-14: one-tile form, no fused xent)";
     case -14: return "transposed output ct needs bf16 output (or the fused update), no xent, one split, one-tile form, ld_ct >= M, 16-byte alignment";
     case -15: return "fused SGD epilogue needs f32 output, one split, no accumulate/bias/xent, a device lr, 16-byte aligned buffers, N % 8 == 0, one-tile form";
@@ -240,7 +240,7 @@ int gemm_check(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn,
     return -15;
   if ((p.mask_out || p.mask_in) &&
       (out_f32 || p.act != ACT_RELU || (p.mask_in && p.aux) || (p.mask_out && p.mask_in) ||
-       p.xent_labels || p.ld_mask < (p.N + 7) / 8))
+       p.xent_labels || (p.ld_mask >= 0 && p.ld_mask < (p.N + 7) / 8)))
     return -13;
   return 0;
 }
@@ -251,6 +251,9 @@ int gemm_bf16(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, 
                             stages >= 12 && stages <= 14 ? 32 : 64);
   if (rc) return rc;
   if ((p.mask_out || p.mask_in) && persist) return -13;
+  // fragment-order masks (ld_mask < 0) exist only in the register-direct epilogue
+  const bool direct = stages == 9 || stages == 10 || stages == 11 || (stages >= 15 && stages <= 17);
+  if ((p.mask_out || p.mask_in) && p.ld_mask < 0 && !direct) return -13;
   if (p.ct && persist) return -14;
   if (p.upd_master && persist) return -15;
 
@@ -340,6 +343,7 @@ int gemm_bf16_group(const GemmParams* ps, const int* splits, int n, int la, int 
     // the one-problem validation (shapes, alignment, layouts, epilogue combinations)
     const int rc = gemm_check(ps[j], la, lb, out_f32, bm, bn, splits[j]);
     if (rc) return rc;
+    if ((ps[j].mask_out || ps[j].mask_in) && ps[j].ld_mask < 0) return -13;
     g.p[j] = ps[j];
     g.tiles_n[j] = (ps[j].N + bn - 1) / bn;
     g.tiles_m[j] = (ps[j].M + bm - 1) / bm;

@@ -50,6 +50,8 @@ struct GemmParams {
   // byte of chunk c = column 8c + e (bf16 output only):
   // mask_out (forward, act = relu): bit = stored bf16 output > 0; mask_in (dgrad, act = relu,
   // replaces aux): the derivative reads 1 bit per element instead of the 16-bit activation.
+  // ld_mask < 0: FRAGMENT order instead (gemm_tile.hpp frag_mask_offset; register-direct
+  // epilogue only, forward and dgrad on the same tile / wave layout).
   unsigned char* mask_out;
   const unsigned char* mask_in;
   long ld_mask;

@@ -10,7 +10,8 @@ namespace dnn {
 // Code 11: register-direct epilogue over the asymmetric ring (A 3 deep, B 2 deep: two k-steps
 // for the streamed A panel to land), 256x256 / 256x128 / 128x128.
 // Codes 9 / 10: the same loop with swapped MFMA operands and the register-direct epilogue
-// (RP_ = 2): bias / activation / aux derivative / colsum / split-K f32, no ReLU bit masks,
+// (RP_ = 2): bias / activation / aux derivative / colsum / split-K f32, ReLU bit masks (both
+// layouts, fragment order only here), no
 // transposed copy, fused update or cross-entropy.
 // Codes 15 / 16: code 9 (2-deep ring, register-direct epilogue) with the L2 touch-prefetch
 // (Cfg TOUCH, touch_tiles) one / two k-steps beyond the ring; code 17: code 11 (A3/B2 ring)

@@ -246,6 +246,39 @@ __device__ __forceinline__ long mask_index(long row, long c, long ld) {
   return (((row >> 4) * ld + c) << 4) + (row & 15);
 }
 
+// Fragment-order ReLU masks (GemmParams::ld_mask < 0; register-direct epilogue only). The
+// NB = FM * FN / 2 mask bytes one lane stores (forward) or reads (dgrad) -- byte jj * FM + i =
+// row 16 i of the lane, the 8-column chunk it holds of fragment pair jj after the 16-lane swap
+// -- are contiguous, lane-major within a wave and wave-major within a tile: one NB-byte access
+// per lane moves a wave's whole mask, where the row-block-major layout takes NB one-byte
+// accesses of 64 bytes per wave. Forward and dgrad must run the same tile / wave layout
+// (ops.FragMask pins it). Buffer: tiles_m * tiles_n * BM * BN / 8 bytes.
+template <int FM, int FN, int BN, int SN, int WM>
+__device__ __forceinline__ long frag_mask_offset(const GemmParams& p, int tm, int tn, int wm,
+                                                 int wn, int lane) {
+  constexpr int WN = BN / SN, NB = FM * FN / 2;
+  const long tiles_n = (p.N + BN - 1) / BN;
+  return ((((long)tm * tiles_n + tn) * (WM * WN) + wm * WN + wn) * 64 + lane) * NB;
+}
+template <int NB>
+__device__ __forceinline__ void frag_mask_store(unsigned char* dst, const unsigned* w) {
+  if constexpr (NB == 16) *(uint4*)dst = make_uint4(w[0], w[1], w[2], w[3]);
+  else if constexpr (NB == 8) *(uint2*)dst = make_uint2(w[0], w[1]);
+  else *(unsigned*)dst = w[0];
+}
+template <int NB>
+__device__ __forceinline__ void frag_mask_load(const unsigned char* src, unsigned* w) {
+  if constexpr (NB == 16) {
+    const uint4 v = *(const uint4*)src;
+    w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+  } else if constexpr (NB == 8) {
+    const uint2 v = *(const uint2*)src;
+    w[0] = v.x; w[1] = v.y;
+  } else {
+    w[0] = *(const unsigned*)src;
+  }
+}
+
 // Phase timestamp of the workgroup (GemmParams::timeline); thread 0 stores it.
 __device__ __forceinline__ void tl_mark(const GemmParams& p, int slot) {
   if (p.timeline && threadIdx.x == 0)
@@ -945,18 +978,35 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&a
       // lane's row), so the result is bitwise that of the generic path.
       // from_mask: the derivative comes from the forward's 1-bit ReLU mask (mask_in: one byte
       // per row and 8-column chunk -- exactly the chunk a lane stores) instead of the activation
+      constexpr int NB = FM * FN / 2;  // fragment-order mask bytes per lane
+      const bool frag = p.ld_mask < 0;  // uniform
       auto relu_body = [&](auto from_mask) {
       constexpr bool MASK = decltype(from_mask)::value;
       [[maybe_unused]] uint4 yv[MASK ? 1 : FN / 2][FM];
       [[maybe_unused]] unsigned mv[MASK ? FN / 2 : 1][FM];
+      [[maybe_unused]] unsigned fw[MASK && NB >= 4 ? NB / 4 : 1];
+      if constexpr (MASK && NB >= 4 && NB <= 16) {
+        if (frag)
+          frag_mask_load<NB>(p.mask_in + frag_mask_offset<FM, FN, BN, SN, WM>(p, tm, tn, wm, wn,
+                                                                             lane), fw);
+      }
 #pragma unroll
       for (int jj = 0; jj < FN / 2; ++jj) {
         const int c = min(scol0 + 32 * jj, p.N - 8);
 #pragma unroll
         for (int i = 0; i < FM; ++i) {
           const long r = min(row0 + 16 * i, p.M - 1);
-          if constexpr (MASK) mv[jj][i] = p.mask_in[mask_index(r, c >> 3, p.ld_mask)];
-          else yv[jj][i] = *(const uint4*)(p.aux + r * p.ld_aux + c);
+          if constexpr (MASK) {
+            if constexpr (NB >= 4 && NB <= 16) {
+              const int b = jj * FM + i;
+              mv[jj][i] = frag ? (fw[b >> 2] >> (8 * (b & 3))) & 0xffu
+                               : p.mask_in[mask_index(r, c >> 3, p.ld_mask)];
+            } else {
+              mv[jj][i] = p.mask_in[mask_index(r, c >> 3, p.ld_mask)];
+            }
+          } else {
+            yv[jj][i] = *(const uint4*)(p.aux + r * p.ld_aux + c);
+          }
         }
       }
 #pragma unroll
@@ -1023,6 +1073,7 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&a
       };
       auto body = [&](auto has_aux) {
       constexpr bool AUX = decltype(has_aux)::value;
+      [[maybe_unused]] unsigned fw[NB >= 4 ? NB / 4 : 1] = {};  // fragment-order mask_out
       [[maybe_unused]] f32x4_t bv[AUX ? 1 : FN];
       [[maybe_unused]] uint2 yv[AUX ? FN : 1][FM];
 #pragma unroll
@@ -1109,7 +1160,13 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&a
                 bits |= ((lo & 0x8000u) == 0u && lo != 0u ? 1u : 0u) << (2 * q);
                 bits |= ((hi & 0x8000u) == 0u && hi != 0u ? 1u : 0u) << (2 * q + 1);
               }
-              p.mask_out[mask_index(row, scol >> 3, p.ld_mask)] = (unsigned char)bits;
+              if constexpr (NB >= 4 && NB <= 16) {
+                const int b = (j / 2) * FM + i;
+                if (frag) fw[b >> 2] |= bits << (8 * (b & 3));
+                else p.mask_out[mask_index(row, scol >> 3, p.ld_mask)] = (unsigned char)bits;
+              } else {
+                p.mask_out[mask_index(row, scol >> 3, p.ld_mask)] = (unsigned char)bits;
+              }
             }
           }
         }
@@ -1126,6 +1183,11 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&a
             *(f32x4_t LDS_AS*)(d + 16) = r1;
           }
         }
+      }
+      if constexpr (!AUX && NB >= 4 && NB <= 16) {
+        if (frag && p.mask_out)  // the whole tile's bits, one NB-byte store per lane
+          frag_mask_store<NB>(p.mask_out + frag_mask_offset<FM, FN, BN, SN, WM>(p, tm, tn, wm,
+                                                                               wn, lane), fw);
       }
       };
       if (p.aux && p.act == ACT_RELU) relu_body(std::false_type{});

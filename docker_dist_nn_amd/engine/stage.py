@@ -445,11 +445,22 @@ class Stage:
         # the byte-granular mask stores/loads cost more than the activation bytes saved):
         # the dgrad epilogue then reads N/8 bytes per row instead of the bf16 activation (the
         # activation itself is still kept: it is the next layer's wgrad operand)
-        use_mask = dev.type == "cuda" and switches.get("DNN_RELU_MASK") == "1"
-        self.relu_mask = [torch.zeros(R, g.np_ // 8, dtype=torch.uint8, device=dev)
-                          if use_mask and i < len(self.geoms) - 1 and
-                          g.spec.activation == "relu" else None
-                          for i, g in enumerate(self.geoms)]
+        # DNN_RELU_MASK=2: fragment-order masks (ops.FragMask: one 16-byte access per lane), only
+        # where a GEMM dgrad of this stage consumes them and it runs the forward's tile shape
+        self.tail = self._tail_ok()
+        mask_mode = switches.get("DNN_RELU_MASK") if dev.type == "cuda" else "0"
+        L = len(self.geoms)
+        self.relu_mask = []
+        for i, g in enumerate(self.geoms):
+            m = None
+            if mask_mode == "1" and i < L - 1 and g.spec.activation == "relu":
+                m = torch.zeros(R, g.np_ // 8, dtype=torch.uint8, device=dev)
+            elif mask_mode == "2" and i < L - 1 and g.spec.activation == "relu" and \
+                    not (self.tail and i + 1 >= L - 2):
+                tiles = ops.frag_mask_tiles(self.mb, g.np_, g.kp, self.geoms[i + 1].np_)
+                if tiles is not None:
+                    m = ops.FragMask.alloc(R, g.np_, tiles, dev)
+            self.relu_mask.append(m)
         self.dz = [torch.zeros(R, g.np_, dtype=bf, device=dev) for g in self.geoms]
         self.dx_send = None if self.first else torch.zeros(R, g0.kp, dtype=bf, device=dev)
         self.labels = torch.full((R,), -1, dtype=torch.int32, device=dev) if self.last else None
@@ -457,7 +468,6 @@ class Stage:
         # Narrow classifier tail (csrc/kernels/mlp_tail.hip): the forward of the last two
         # layers, the softmax CE and both of their dgrads run as ONE kernel inside the last
         # layer's forward; the second-to-last layer's forward and both dgrads are then no-ops.
-        self.tail = self._tail_ok()
         # K-major weight gradients (ops.linear_wgrad dzt / xt): for big hidden layers whose dZ
         # and input activation come from this stage's own one-tile GEMMs, those GEMMs also write
         # the transposed copies in their epilogues (+1 write of each, -20 % wgrad time)

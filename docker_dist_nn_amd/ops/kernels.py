@@ -278,7 +278,16 @@ def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=
             raise ValueError(f"colsum must be fp32 [{-(-M // tiles[0])}][>={N}] row-major")
     if (mask_out is not None or mask_in is not None) and not a.is_cuda:
         raise ValueError("relu bit masks are a GPU-path format (CPU uses aux)")
-    for m in (mask_out, mask_in):  # row-block-major bytes (see relu_mask_bits)
+    frag = isinstance(mask_out, FragMask) or isinstance(mask_in, FragMask)
+    for m in (mask_out, mask_in):
+        if isinstance(m, FragMask):
+            if tiles is None or tuple(tiles) != m.tiles or stages not in DIRECT_STAGES or \
+                    m.m < M or m.n < N or m.buf.numel() < FragMask.nbytes(M, N, m.tiles):
+                raise ValueError(f"fragment mask of tile {m.tiles} [{m.m}][{m.n}] used by a "
+                                 f"{tiles} GEMM (stage code {stages}) of [{M}][{N}]")
+        elif m is not None and frag:
+            raise ValueError("mask_out and mask_in must share one layout")
+    for m in () if frag else (mask_out, mask_in):  # row-block-major bytes (relu_mask_bits)
         if m is not None and (m.dtype != torch.uint8 or m.dim() != 2 or not m.is_contiguous() or
                               M % 16 or m.shape[0] < M or m.shape[1] < -(-N // 8)):
             raise ValueError(f"relu mask must be a contiguous uint8 [{M}][>={-(-N // 8)}] "
@@ -351,8 +360,10 @@ def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=
                        splits, _stream(a), _p(colsum),
                        colsum.stride(0) if colsum is not None else 0, k_total=int(k_total),
                        stages=int(stages), group_m=int(group_m), persist=int(persist),
-                       mask_out=_p(mask_out), mask_in=_p(mask_in),
-                       ld_mask=(mask_out if mask_out is not None else mask_in).stride(0)
+                       mask_out=_p(mask_out.buf if frag and mask_out is not None else mask_out),
+                       mask_in=_p(mask_in.buf if frag and mask_in is not None else mask_in),
+                       ld_mask=-1 if frag else
+                       (mask_out if mask_out is not None else mask_in).stride(0)
                        if (mask_out is not None or mask_in is not None) else 0,
                        ct=_p(ct), ld_ct=ct.stride(0) if ct is not None else 0,
                        **({} if upd is None else dict(
@@ -388,6 +399,85 @@ def gemv(x, w, bias, y, act="relu"):
     native().gemv_bf16(_p(x), x.stride(0), _p(w), w.stride(0), _p(bias), _p(y), y.stride(0),
                        M, N, K, _act(act), int(y.dtype == torch.float32), _stream(x))
     return y
+
+
+# wave grid (WM, WN) of the register-direct tiles that take fragment-order masks (NB >= 4 bytes
+# per lane; gemm_rp.hip pick_rp)
+FRAG_WAVES = {(256, 256): (4, 2), (256, 128): (4, 2), (128, 128): (2, 2), (128, 64): (2, 2)}
+DIRECT_STAGES = (9, 10, 11, 15, 16, 17)
+
+
+class FragMask:
+    """1-bit ReLU mask in FRAGMENT order (GemmParams::ld_mask < 0, gemm_tile.hpp
+    frag_mask_offset): the bits a lane of the register-direct epilogue stores or reads are
+    contiguous, so one 4/8/16-byte access per lane moves them, instead of the row-block-major
+    layout's one-byte accesses (the reason DNN_RELU_MASK=1 measured slower than reading the
+    activation). Tied to one tile shape: the forward that writes it and the dgrad that reads it
+    must both run ``tiles`` with a register-direct stage code. Tiles are row-major in the
+    buffer, so the rows of a micro-batch starting on a tile boundary are one byte range
+    (``mask[r]`` with r a slice of rows)."""
+
+    def __init__(self, buf: torch.Tensor, tiles: tuple[int, int], m: int, n: int):
+        self.buf, self.tiles, self.m, self.n = buf, tuple(tiles), m, n
+
+    @staticmethod
+    def nbytes(M: int, N: int, tiles) -> int:
+        bm, bn = tiles
+        return -(-M // bm) * -(-N // bn) * bm * bn // 8
+
+    @classmethod
+    def alloc(cls, M: int, N: int, tiles, device) -> "FragMask":
+        if tuple(tiles) not in FRAG_WAVES:
+            raise ValueError(f"no fragment-order mask for tile {tuple(tiles)}")
+        return cls(torch.zeros(cls.nbytes(M, N, tiles), dtype=torch.uint8, device=device),
+                   tiles, M, N)
+
+    def __getitem__(self, r: slice) -> "FragMask":
+        bm, bn = self.tiles
+        start, stop, step = r.indices(self.m)
+        if step != 1 or start % bm:
+            raise ValueError(f"fragment mask rows must start on a {bm}-row tile boundary")
+        per_row_tile = -(-self.n // bn) * bm * bn // 8
+        return FragMask(self.buf[start // bm * per_row_tile:], self.tiles, stop - start, self.n)
+
+    def bits(self) -> torch.Tensor:
+        """Unpack into bool [m][n] (tests)."""
+        bm, bn = self.tiles
+        wm_n, wn_n = FRAG_WAVES[self.tiles]
+        fm, sn = bm // wm_n // 16, bn // wn_n
+        fn = sn // 16
+        nb = fm * fn // 2
+        tm_n, tn_n = -(-self.m // bm), -(-self.n // bn)
+        dev = self.buf.device
+        raw = self.buf[:tm_n * tn_n * bm * bn // 8].view(tm_n, tn_n, wm_n, wn_n, 64, fn // 2, fm)
+        ar = lambda k: torch.arange(k, device=dev)  # noqa: E731
+        tm, tn, wm, wn, lane, jj, i, e = torch.meshgrid(
+            ar(tm_n), ar(tn_n), ar(wm_n), ar(wn_n), ar(64), ar(fn // 2), ar(fm), ar(8),
+            indexing="ij")
+        row = tm * bm + wm * 16 * fm + (lane & 15) + 16 * i
+        col = tn * bn + wn * sn + 16 * ((lane >> 4) & 1) + 8 * (lane >> 5) + 32 * jj + e
+        bit = (raw.unsqueeze(-1).to(torch.int32) >> ar(8).to(torch.int32)) & 1
+        out = torch.zeros(tm_n * bm, tn_n * bn, dtype=torch.bool, device=dev)
+        out[row.reshape(-1), col.reshape(-1)] = bit.reshape(-1).bool()
+        assert nb == fm * fn // 2
+        return out[:self.m, :self.n]
+
+
+def frag_mask_tiles(M: int, N: int, K: int, N_next: int) -> tuple[int, int] | None:
+    """Tile of a fragment-order mask between the forward [M][N] (contraction K) of a ReLU layer
+    and the dgrad that produces its dZ from the next layer's [M][N_next] gradient, or None when
+    those two GEMMs do not both run one register-direct tile shape (linear_fwd / linear_dgrad
+    pick their tiles and stage codes from the tuned table)."""
+    tf = tuning.lookup("fwd", M, N, K)
+    tiles = tuple(tf["tile"]) if tf else pick_tiles(M, N)
+    td = tuning.lookup("dgrad", M, N, N_next)
+    sf = STAGES["fwd"] or (tf or {}).get("stages", 0)
+    sd = STAGES["dgrad"] or (td or {}).get("stages", 0)
+    if M <= GEMV_MAX_ROWS or tiles != dgrad_tiles(M, N, N_next) or tiles not in FRAG_WAVES or \
+            sf not in DIRECT_STAGES or sd not in DIRECT_STAGES or M % tiles[0] or \
+            _blas("fwd", tf) or _blas("dgrad", td):
+        return None
+    return tiles
 
 
 def relu_mask_bits(mask: torch.Tensor, M: int, N: int) -> torch.Tensor:

@@ -585,6 +585,26 @@ def test_register_prefetch_bitwise(dev, la, lb):
         blocked = mn.view(-1).view(M // 16, 40, 16)  # row-block-major mask bytes
         assert torch.all(blocked[:, 33:, :] == 0xAA)  # chunks past N/8 untouched
         assert torch.equal(ops.relu_mask_bits(mn, M, N), cn > 0)
+        # fragment-order masks (ld_mask < 0): same outputs, one wide access per lane
+        if (bm, bn) in ops.kernels.FRAG_WAVES:
+            fm = ops.FragMask.alloc(M, N, (bm, bn), dev)
+            cf = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            ops.gemm(a, b, cf, layout_a=la, layout_b=lb, M=M, N=N, K=K, bias=bias, act="relu",
+                     tiles=(bm, bn), stages=code, mask_out=fm)
+            df = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            ops.gemm(a, b, df, layout_a=la, layout_b=lb, M=M, N=N, K=K, act="relu",
+                     tiles=(bm, bn), stages=code, mask_in=fm)
+            assert torch.equal(cf, cn) and torch.equal(df, dn), ("frag", bm, bn, code)
+            assert torch.equal(fm.bits(), cn > 0), ("frag bits", bm, bn, code)
+            if la == KMAJ:  # rows from a tile boundary on: a byte range of the same buffer
+                sub = fm[slice(bm, M)]
+                ds = torch.empty(M - bm, N, device=dev, dtype=torch.bfloat16)
+                ops.gemm(a[bm:], b, ds, layout_a=la, layout_b=lb, M=M - bm, N=N, K=K,
+                         act="relu", tiles=(bm, bn), stages=code, mask_in=sub)
+                assert torch.equal(ds, dn[bm:]), ("frag rows", bm, bn, code)
+            with pytest.raises(ValueError, match="fragment mask"):
+                ops.gemm(a, b, df, layout_a=la, layout_b=lb, M=M, N=N, K=K, act="relu",
+                         tiles=(bm, bn), stages=2, mask_in=fm)
     # and against fp32 once (the 2-stage kernel itself is pinned by the tests above)
     M, N, K = 256, 256, 832
     a = _storage(la, M, K, gen, dev, False)

@@ -79,3 +79,38 @@ def test_engine_mask_path_bitwise_equals_activation_path(dev, monkeypatch):
         res.append((losses, tr.stages[0].params.master.clone()))
     assert res[0][0] == res[1][0]
     assert torch.equal(res[0][1], res[1][1])
+
+
+def test_engine_fragment_mask_bitwise_equals_activation_path(dev, monkeypatch):
+    """DNN_RELU_MASK=2 on the headline shape (65536 rows: the tuned table runs the 784->512
+    forward and the 256->512 dgrad as the same 256x256 register-direct tile, so the
+    fragment-order mask applies): the same losses and weights as reading the activation."""
+    from docker_dist_nn_amd import NAMED_MODELS
+    from docker_dist_nn_amd.data import synthetic_mnist
+    from docker_dist_nn_amd.engine import OptimConfig, Trainer
+
+    R = 65536
+    x, y = synthetic_mnist(R, seed=3)
+    xb = torch.zeros(R, 832, dtype=torch.bfloat16)
+    xb[:, :784] = torch.from_numpy(x).to(torch.bfloat16)
+    xb, yb = xb.to(dev), torch.from_numpy(y).to(dev)
+    res = []
+    for flag in ("0", "2"):
+        monkeypatch.setenv("DNN_RELU_MASK", flag)
+        tr = Trainer(NAMED_MODELS["mnist-fcnn"], micro_batch=R, num_micro=1,
+                     optim=OptimConfig(lr=0.1), device=dev)
+        m = tr.stages[0].relu_mask
+        if flag == "2":
+            assert isinstance(m[0], ops.FragMask) and m[0].tiles == (256, 256)
+            assert all(v is None for v in m[1:])  # the tail's own dgrads read activations
+        else:
+            assert all(v is None for v in m)
+        losses = []
+        for _ in range(3):
+            tr.set_batch(xb, yb)
+            tr.step()
+            losses.append(tr.loss())
+        res.append((losses, tr.stages[0].params.master.clone()))
+        del tr
+    assert res[0][0] == res[1][0]
+    assert torch.equal(res[0][1], res[1][1])
