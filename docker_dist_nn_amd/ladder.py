@@ -61,15 +61,18 @@ class Rung:
 def bench_rungs(n: int, dp_only: bool = False) -> list[Rung]:
     """The training benchmark's ladder for ``n`` ranks. ``dp_only``: the layout is already
     data-parallel (no hops), only the executor can fall back."""
-    dp = [Rung("dp-native", {}, ["--parallelism", f"dp{n}"]),
-          Rung("dp-python", {"DNN_NATIVE_DIST": "0"}, ["--parallelism", f"dp{n}"])]
+    # every rung after the first replays eagerly: a failed first attempt may have been the
+    # graph replay itself (bench --graph auto)
+    eager = ["--graph", "off"]
+    dp = [Rung("dp-native", {}, ["--parallelism", f"dp{n}", *eager]),
+          Rung("dp-python", {"DNN_NATIVE_DIST": "0"}, ["--parallelism", f"dp{n}", *eager])]
     if dp_only:
         return dp
     return [Rung("default"),
-            Rung("ipc-slotted", {"DNN_IPC_PLAN": "slotted"}),
-            Rung("rccl-slotted", {"DNN_PIPE": "rccl", "DNN_RCCL_PLAN": "slotted"}),
-            Rung("rccl-streams", {"DNN_PIPE": "rccl", "DNN_RCCL_PLAN": "streams"}),
-            Rung("python", {"DNN_PIPE": "rccl", "DNN_NATIVE_DIST": "0"}),
+            Rung("ipc-slotted", {"DNN_IPC_PLAN": "slotted"}, eager),
+            Rung("rccl-slotted", {"DNN_PIPE": "rccl", "DNN_RCCL_PLAN": "slotted"}, eager),
+            Rung("rccl-streams", {"DNN_PIPE": "rccl", "DNN_RCCL_PLAN": "streams"}, eager),
+            Rung("python", {"DNN_PIPE": "rccl", "DNN_NATIVE_DIST": "0"}, eager),
             *dp]
 
 

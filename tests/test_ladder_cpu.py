@@ -121,4 +121,5 @@ def test_rung_fault_parse():
     assert names == ["default", "ipc-slotted", "rccl-slotted", "rccl-streams", "python",
                      "dp-native", "dp-python"]
     assert [r.name for r in bench_rungs(4, dp_only=True)] == ["dp-native", "dp-python"]
-    assert bench_rungs(4)[-1].args == ["--parallelism", "dp4"]
+    assert bench_rungs(4)[-1].args == ["--parallelism", "dp4", "--graph", "off"]
+    assert bench_rungs(4)[0].args == [] and bench_rungs(4)[1].args == ["--graph", "off"]
