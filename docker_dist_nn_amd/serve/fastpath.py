@@ -40,7 +40,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from .. import ops
+from .. import ops, switches
 from ..utils.native import native
 
 log = logging.getLogger(__name__)
@@ -234,6 +234,7 @@ class FastChain:
             self.why = "fast path unavailable: no shared-memory announcement ring"
             return
         self.stream = torch.cuda.Stream(self.dev)
+        self.trace = switches.get("DNN_CHAIN_TRACE") == "1"
         self.seq = 0
         self.lock = threading.Lock()
         self.processed = 0
@@ -298,6 +299,8 @@ class FastChain:
             hin = self.h_in[slot]
             hin[:rows, :x.shape[1]].copy_(torch.from_numpy(np.ascontiguousarray(x, np.float32)))
             self.ann.announce(seq, rows)
+            if self.trace:
+                self._trace(seq, f"announced rows={rows}")
             with torch.cuda.stream(self.stream):
                 self.x0[:rows].copy_(hin[:rows], non_blocking=True)
                 status = 0
@@ -333,6 +336,8 @@ class FastChain:
             if spins > 2000:
                 time.sleep(20e-6)
         hdr = ho[:4].tolist()
+        if self.trace:
+            self._trace(seq, f"result hdr {hdr}")
         code, who = hdr[0] & 0xFF, (hdr[0] >> 8) & 0xFF
         if hdr[2]:  # rank 0's own wait gave up: the last stage never answered
             code, who = ST_DEADLINE, self.world - 1
@@ -347,6 +352,13 @@ class FastChain:
                                f"{code})")
         vals = ho[HDR // 4:HDR // 4 + rows * self.res_w].view(torch.float32)
         return vals.view(rows, self.res_w)[:, :self.n_out].double().numpy()
+
+    def _trace(self, seq: int, what: str) -> None:
+        f = self.flags.tolist()
+        log.warning(f"[chain-fast r{self.rank} {time.monotonic():.4f}] seq {seq}: {what}; "
+                    f"in={f[F_IN:F_IN + NSLOT]} hdr={f[F_HDR:F_HDR + 2 * NSLOT]} "
+                    f"ack={f[F_ACK]} err={f[F_ERR]} lhdr={f[F_LHDR:F_LHDR + 2]}"
+                    + (f" res={f[F_RES:F_RES + NSLOT]}" if self.rank == 0 else ""))
 
     def prev_flags_of_last(self) -> int:
         """Rank 0: the last rank's flag block (its ack word is what rank 0 writes)."""
@@ -382,6 +394,10 @@ class FastChain:
                     log.exception(f"({self.cr.names[self.rank]}) stage failure")
                     status = ST_INTERNAL | (self.rank << 8)
                 self._send(s, out, rows, seq, status, _ptr(self.flags, F_LHDR))
+            if self.trace:
+                self._trace(seq, f"enqueued rows={rows} status={status}")
+                s.synchronize()
+                self._trace(seq, "done")
             self.processed = seq
             self.cr._processed = seq
         torch.cuda.synchronize(self.dev)

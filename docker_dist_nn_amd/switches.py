@@ -104,6 +104,8 @@ SWITCHES: dict[str, tuple[str, str]] = {
                                       "stalled (steady state: DNN_FLAG_TIMEOUT, 120 s)"),
     "DNN_FAULT_IPC_VERIFY": ("", "ranks whose IPC verification step is corrupted (tests the "
                                  "fallback)"),
+    "DNN_CHAIN_TRACE": ("0", "device-side chain: 1 = every rank logs each request's steps and, "
+                             "after synchronising, its flag words (diagnosis; serialises)"),
     "DNN_CHAIN_FAST": ("1", "rank chain: serving-size requests (<= 8 rows) take the device-side "
                             "chain (serve/fastpath.py: IPC slots + flags, no host hop); 0 = "
                             "the message-passing chain for every request"),

@@ -87,6 +87,7 @@ def test_fast_chain_matches_reference_and_serves_concurrently(model4, tmp_path):
     layers = load_model_config(str(cfg)).layers
     port = _port()
     p = _start(cfg, inp, port, tmp_path)
+    ok = False
     try:
         c = LayerClient(f"127.0.0.1:{port}", timeout=60)
         for rows in (1, 3, 8, 40, 1):  # 40 rows: the message chain
@@ -104,8 +105,11 @@ def test_fast_chain_matches_reference_and_serves_concurrently(model4, tmp_path):
             ts.append(time.perf_counter() - t0)
         print(f"fast chain batch-1 p50 {np.median(ts) * 1e3:.3f} ms")
         c.close()
+        ok = True
     finally:
         out = _stop(p)
+        if not ok:  # the servers' side of a failure
+            print(out[-12000:])
     assert "device-side chain" in out, out[-3000:]
     assert "Shutdown complete." in out, out[-3000:]
 
