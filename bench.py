@@ -81,13 +81,14 @@ def parse_args(argv=None):
     ap.add_argument("--micro", type=int, default=0, help="micro-batch rows (0 = planner)")
     ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--optimizer", default="sgd", choices=["sgd", "adam", "adamw"])
-    ap.add_argument("--graph", default="off", choices=["auto", "on", "off"],
+    ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
                     help="replay the step as a HIP graph (1 GPU, or N > 1 with the native step). "
-                         "auto: N > 1 on the IPC transport, kept only if its timed steps beat "
-                         "eager ones (the host enqueue of a rank's plan is ~3 us per op eager, "
-                         "~0.4 us per node replayed: profiles/r3_host). Not the default: a "
-                         "captured relayed-IPC plan hung in a 4-rank one-GPU rehearsal "
-                         "(profiles/r3_ipc/README.md)")
+                         "auto (default): N > 1 on the IPC transport, kept only if its timed "
+                         "steps beat eager ones (the host enqueue of a rank's plan is ~3 us per "
+                         "op eager, ~0.4 us per node replayed: profiles/r3_host). The captured "
+                         "plan is the slotted single-stream form, deadlock-free whatever order "
+                         "the graph executor picks (profiles/r4_multirank); the ladder's later "
+                         "rungs run with --graph off")
     ap.add_argument("--graph-copies", type=int, default=2,
                     help="alternate between this many instantiations of the step graph")
     ap.add_argument("--boundary", default="bf16", choices=["bf16", "fp8"],
