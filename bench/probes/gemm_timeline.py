@@ -29,6 +29,35 @@ def fwd(M, K, N):
                                          bias=b, act="relu", tiles=tile, stages=st, timeline=tl)
 
 
+def fwd_mask(M, K, N):
+    """fwd with the fragment-order ReLU mask written too (DNN_RELU_MASK=2)."""
+    x, w, b = rnd(M, K, scale=0.1), rnd(N, K, scale=0.05), torch.randn(N, device=dev)
+    y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    masks = {}
+
+    def run(tile, st, tl):
+        m = masks.setdefault(tile, ops.FragMask.alloc(M, N, tile, dev))
+        return ops.gemm(x, w, y, layout_a=KMAJ, layout_b=KMAJ, M=M, N=N, K=K, bias=b,
+                        act="relu", tiles=tile, stages=st, timeline=tl, mask_out=m)
+    return run
+
+
+def dgrad_mask(M, K, N):
+    """dgrad with the ReLU derivative from a fragment-order mask instead of the activation."""
+    dz, wt = rnd(M, K, scale=0.1), rnd(N, K, scale=0.05)
+    y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    masks = {}
+
+    def run(tile, st, tl):
+        m = masks.get(tile)
+        if m is None:
+            m = masks[tile] = ops.FragMask.alloc(M, N, tile, dev)
+            m.buf.random_(0, 256)
+        return ops.gemm(dz, wt, y, layout_a=KMAJ, layout_b=KMAJ, M=M, N=N, K=K, act="relu",
+                        tiles=tile, stages=st, timeline=tl, mask_in=m)
+    return run
+
+
 def fwd32(M, K, N):
     x, w = rnd(M, K, scale=0.1), rnd(N, K, scale=0.05)
     y = torch.empty(M, N, device=dev)
@@ -56,6 +85,7 @@ def dgrad(M, K, N):
 
 CASES = {"f0": lambda: fwd(65536, 832, 512), "f1": lambda: fwd(65536, 512, 256),
          "d1": lambda: dgrad(65536, 256, 512), "d1s": lambda: dgrad(8192, 256, 512),
+         "f0k": lambda: fwd_mask(65536, 832, 512), "d1k": lambda: dgrad_mask(65536, 256, 512),
          "f0s": lambda: fwd(8192, 832, 512), "f0m": lambda: fwd(32768, 832, 512),
          "f0f32": lambda: fwd32(65536, 832, 512), "f0sf32": lambda: fwd32(8192, 832, 512),
          "w0": lambda: wgrad(65536, 512, 832, 18), "m8f": lambda: fwd(65536, 1024, 1024)}
