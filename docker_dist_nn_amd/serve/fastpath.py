@@ -171,13 +171,14 @@ class FastChain:
             mine = {"error": repr(e)}
         everyone = [None] * self.world
         dist.all_gather_object(everyone, mine)
-        # rank 0 sizes its result slots by the last stage's output width
+        # rank 0 sizes its result slots by the last stage's output width (the last rank
+        # addresses them with the same stride)
         if "error" not in everyone[0] and all("error" not in e for e in everyone):
             try:
+                w_last = everyone[-1]["out_w"]
+                self.res_w = w_last
+                self.res_bytes = HDR + self.max_rows * w_last * 4
                 if self.rank == 0:
-                    w_last = everyone[-1]["out_w"]
-                    self.res_w = w_last
-                    self.res_bytes = HDR + self.max_rows * w_last * 4
                     self.res = uncached_zeros((NSLOT, self.res_bytes // 4), torch.int32,
                                               self.dev)
                     torch.cuda.synchronize(self.dev)
