@@ -48,12 +48,15 @@ def load_pass(d):
     return {i: (meta[i][0], meta[i][1], cnt.get(i, {}), dur.get(i, 0.0)) for i in sorted(meta)}
 
 
-def period(names, max_p=200):
-    """Shortest p such that the last 2p names are two copies of one period."""
-    for p in range(1, min(max_p, len(names) // 2) + 1):
-        if names[-p:] == names[-2 * p:-p]:
-            return p
-    return len(names)
+def period(names, max_p=200, max_tail=8):
+    """(p, t): the shortest p such that, after dropping the last t dispatches (end-of-run work
+    such as the final loss read-back), the last 2p names are two copies of one period."""
+    for p in range(2, min(max_p, len(names) // 2) + 1):
+        for t in range(0, max_tail + 1):
+            body = names[:len(names) - t]
+            if len(body) >= 2 * p and body[-p:] == body[-2 * p:-p]:
+                return p, t
+    return len(names), 0
 
 
 def main():
@@ -73,8 +76,9 @@ def main():
             continue
         ids = list(disp)
         names = [disp[i][0] for i in ids]
-        p = period(names)
+        p, t = period(names)
         p_seen = p
+        ids = ids[:len(ids) - t]
         last = ids[-p * a.steps:]
         for k, i in enumerate(last):
             pos = k % p
