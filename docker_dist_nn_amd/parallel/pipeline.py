@@ -326,7 +326,7 @@ class PipelineExecutor:
         mode = switches.get("DNN_BW_OVERLAP")
         # small steps are host-bound: every fork / join is an event record + wait (~6-8 us of
         # host time each), more than the overlap can win back on GEMMs of a few thousand rows
-        if mode in ("1", "2", "3", "4") and len(self.stages) == 1 and \
+        if mode in ("1", "2", "3", "4", "5") and len(self.stages) == 1 and \
                 self.stages[0].rows >= int(switches.get("DNN_BW_OVERLAP_MIN_ROWS")):
             ov = self._overlap_plan(self.stages[0], mode)
             if ov is not None:
@@ -417,17 +417,33 @@ class PipelineExecutor:
             if "FINO" not in segs:
                 plan.append((st, "O", 0))
             return plan
+        # auto: on unless a layer updates in its wgrad epilogue (the wide model: there the
+        # side-stream update of layers 1.. competes with the fused W1; profiles/r3b_fino)
+        sf = switches.get("DNN_SPLIT_FINO")
+        split = ((sf == "1" or (sf == "auto" and not fused)) and L > 1 and
+                 f"FINO1-{L - 1}" in segs and "FINO0-0" in segs and 0 not in fused)
+        if mode == "5" and L >= 3 and not fused:
+            # one fork: the small wgrads (L-1 .. 2) on the side under the dgrads; W1 on the
+            # main stream right after the last dgrad, then W0 -- so W1 and W0 never share the
+            # chip whatever the dgrads cost (with the fragment-mask dgrad the default plan lets
+            # W0 start before W1: profiles/r4_timeline)
+            plan = [(st, "F0", 0), (None, "@fork", 0)]
+            plan += [(st, f"W{i}", 1) for i in range(L - 1, 1, -1)]
+            plan += [(st, f"B0.L{i}", 0) for i in range(L - 1, 0, -1)] + [(st, "W1", 0)]
+            if split:
+                return plan + [(None, "@fork", 0), (st, f"FINO1-{L - 1}", 1), (st, "W0", 0),
+                               (st, "FINO0-0", 0), (None, "@join", 0)]
+            plan += [(st, "W0", 0), (None, "@join", 0)]
+            plan.append((st, "FINO", 0) if "FINO" in segs else (st, "FIN", 0))
+            if "FINO" not in segs:
+                plan.append((st, "O", 0))
+            return plan
         plan = [(st, "F0", 0), (None, "@fork", 0)]
         for i in range(L - 1, 0, -1):
             if i in fused:  # dgrad_i reads the old W_i^T: the updating wgrad_i starts after it
                 plan += [(st, f"B0.L{i}", 0), (None, "@fork", 0), (st, f"W{i}", 1)]
             else:
                 plan += [(st, f"W{i}", 1), (st, f"B0.L{i}", 0), (None, "@fork", 0)]
-        # auto: on unless a layer updates in its wgrad epilogue (the wide model: there the
-        # side-stream update of layers 1.. competes with the fused W1; profiles/r3b_fino)
-        sf = switches.get("DNN_SPLIT_FINO")
-        split = ((sf == "1" or (sf == "auto" and not fused)) and L > 1 and
-                 f"FINO1-{L - 1}" in segs and "FINO0-0" in segs and 0 not in fused)
         if plan[-1][1] == "@fork" and not split:
             plan = plan[:-1]
         if switches.get("DNN_FORK_ELIDE") in ("1", "2"):
