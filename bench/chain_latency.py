@@ -46,7 +46,12 @@ def main():
     rehearsal = n_gpu < a.stages
     env = dict(os.environ, PYTHONPATH=ROOT)
     if rehearsal:
+        # every stage on cuda:0: 8 processes x the default 4 hardware queues each oversubscribe
+        # the GPU's queue slots, and the scheduler's queue rotation put ~13 ms outliers into
+        # the p99 (profiles/r4_chain: 13.7 ms at 4 queues, 0.75 ms at 2); one real GPU per
+        # stage has no such sharing
         env.update(DNN_FORCE_DEVICE="0", DNN_DIST_BACKEND="gloo")
+        env.setdefault("GPU_MAX_HW_QUEUES", "2")
     with tempfile.TemporaryDirectory() as d:
         cfg = os.path.join(d, "model.json")
         export_model_json(cfg, ws, bs, ["relu"] * (a.stages - 1) + ["softmax"],
@@ -86,6 +91,7 @@ def main():
                                     if fast else "gloo via host" if rehearsal else "rccl") +
                                    (", one-GPU rehearsal: every stage on cuda:0"
                                     if rehearsal else ""),
+                      "gpu_max_hw_queues": env.get("GPU_MAX_HW_QUEUES"),
                       "p50_ms": round(float(np.percentile(t, 50)), 4),
                       "p90_ms": round(float(np.percentile(t, 90)), 4),
                       "p99_ms": round(float(np.percentile(t, 99)), 4), "n": len(ts),

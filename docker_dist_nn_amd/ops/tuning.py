@@ -51,6 +51,8 @@ def _load() -> dict:
         try:
             _table = load_table(TABLE_PATH)
         except FileNotFoundError:
+            if TABLE_PATH != DEFAULT_PATH:  # an explicitly requested table must exist
+                raise
             _table = {}
     return _table
 
