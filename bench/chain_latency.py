@@ -84,6 +84,11 @@ def main():
                 p.kill()
                 log, _ = p.communicate()
     fast = "device-side chain" in (log or "")
+    import re
+    m = re.search(r"predict latency over (\d+) requests: p50 ([\d.]+) ms p90 ([\d.]+) ms "
+                  r"p99 ([\d.]+) ms", log or "")
+    inner = ({"requests": int(m.group(1)), "p50_ms": float(m.group(2)),
+              "p90_ms": float(m.group(3)), "p99_ms": float(m.group(4))} if m else None)
     t = np.asarray(ts) * 1e3
     print(json.dumps({"metric": "inference chain latency", "path": "rank chain (grpc ingress)",
                       "stages": a.stages, "rows": a.rows, "model": "-".join(map(str, dims)),
@@ -92,6 +97,9 @@ def main():
                                    (", one-GPU rehearsal: every stage on cuda:0"
                                     if rehearsal else ""),
                       "gpu_max_hw_queues": env.get("GPU_MAX_HW_QUEUES"),
+                      # rank 0's predict() alone (request in -> logits out, no gRPC): the
+                      # device-side chain's own latency, warm-up requests included
+                      "chain_only": inner,
                       "p50_ms": round(float(np.percentile(t, 50)), 4),
                       "p90_ms": round(float(np.percentile(t, 90)), 4),
                       "p99_ms": round(float(np.percentile(t, 99)), 4), "n": len(ts),

@@ -29,6 +29,7 @@ header read and a host send per hop. Here:
 """
 from __future__ import annotations
 
+import collections
 import logging
 import mmap
 import os
@@ -236,6 +237,7 @@ class FastChain:
             return
         self.stream = torch.cuda.Stream(self.dev)
         self.trace = switches.get("DNN_CHAIN_TRACE") == "1"
+        self.lat: collections.deque = collections.deque(maxlen=100000)  # rank 0: seconds
         self.seq = 0
         self.lock = threading.Lock()
         self.processed = 0
@@ -290,6 +292,7 @@ class FastChain:
 
         from .ingress import StageFailure
 
+        t_in = time.perf_counter()
         rows = x.shape[0]
         st = self.cr.stage
         n = self.n
@@ -352,7 +355,19 @@ class FastChain:
                                else grpc.StatusCode.INTERNAL, f"stage {bad} failed (status "
                                f"{code})")
         vals = ho[HDR // 4:HDR // 4 + rows * self.res_w].view(torch.float32)
-        return vals.view(rows, self.res_w)[:, :self.n_out].double().numpy()
+        out = vals.view(rows, self.res_w)[:, :self.n_out].double().numpy()
+        self.lat.append(time.perf_counter() - t_in)
+        return out
+
+    def latency_summary(self) -> str:
+        """Rank 0: percentiles of predict() itself -- request in to logits out, the whole
+        device-side chain without the gRPC ingress around it."""
+        t = np.asarray(self.lat, dtype=np.float64) * 1e3
+        if t.size == 0:
+            return "device-side chain: no requests"
+        p = np.percentile(t, [50, 90, 99])
+        return (f"device-side chain predict latency over {t.size} requests: p50 {p[0]:.4f} ms "
+                f"p90 {p[1]:.4f} ms p99 {p[2]:.4f} ms")
 
     def _trace(self, seq: int, what: str) -> None:
         f = self.flags.tolist()
@@ -406,6 +421,7 @@ class FastChain:
     def stop(self) -> None:
         if self.rank == 0 and self.ok:
             self.ann.stop()
+            log.info(self.latency_summary())
 
     def close(self) -> None:
         if self.ok:
