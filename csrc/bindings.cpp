@@ -1073,6 +1073,46 @@ PYBIND11_MODULE(_native, m) {
       py::arg("ack_target"), py::arg("next_flag"), py::arg("seq"), py::arg("prev_ack"),
       py::arg("timeout_s"));
   m.def(
+      "chain_gemv_send",
+      [=](uintptr_t s, uintptr_t x, long ldx, uintptr_t w, long ldw, uintptr_t bias, int act,
+          int rows, int N, int K, int out_f32, uintptr_t dst, long dst_ld, uintptr_t dst_hdr,
+          uintptr_t in_hdr, uintptr_t err, int stage, uint32_t status, uintptr_t ack,
+          uint32_t ack_target, uintptr_t next_flag, uint32_t seq, uintptr_t prev_ack,
+          uintptr_t counter, double timeout_s) {
+        dnn::ChainGemvSend p{};
+        p.x = static_cast<const uint16_t*>(ptr(x));
+        p.ldx = ldx;
+        p.w = static_cast<const uint16_t*>(ptr(w));
+        p.ldw = ldw;
+        p.bias = static_cast<const float*>(ptr(bias));
+        p.act = act;
+        p.rows = rows;
+        p.N = N;
+        p.K = K;
+        p.out_f32 = out_f32;
+        p.dst = ptr(dst);
+        p.dst_ld = dst_ld;
+        p.dst_hdr = static_cast<uint32_t*>(ptr(dst_hdr));
+        p.in_hdr = static_cast<const uint32_t*>(ptr(in_hdr));
+        p.err = static_cast<uint32_t*>(ptr(err));
+        p.stage = stage;
+        p.status = status;
+        p.ack = static_cast<const uint32_t*>(ptr(ack));
+        p.ack_target = ack_target;
+        p.next_flag = static_cast<uint32_t*>(ptr(next_flag));
+        p.seq = seq;
+        p.prev_ack = static_cast<uint32_t*>(ptr(prev_ack));
+        p.counter = static_cast<uint32_t*>(ptr(counter));
+        p.timeout_ticks = dnn::chain_ticks(timeout_s);
+        chk(dnn::chain_gemv_send(p, S(s)), "chain_gemv_send");
+      },
+      py::arg("stream"), py::arg("x"), py::arg("ldx"), py::arg("w"), py::arg("ldw"),
+      py::arg("bias"), py::arg("act"), py::arg("rows"), py::arg("N"), py::arg("K"),
+      py::arg("out_f32"), py::arg("dst"), py::arg("dst_ld"), py::arg("dst_hdr"),
+      py::arg("in_hdr"), py::arg("err"), py::arg("stage"), py::arg("status"), py::arg("ack"),
+      py::arg("ack_target"), py::arg("next_flag"), py::arg("seq"), py::arg("prev_ack"),
+      py::arg("counter"), py::arg("timeout_s"));
+  m.def(
       "chain_signal",
       [=](uintptr_t s, uintptr_t flag, uint32_t value) {
         chk(dnn::chain_signal(static_cast<uint32_t*>(ptr(flag)), value, S(s)), "chain_signal");

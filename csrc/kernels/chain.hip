@@ -5,6 +5,8 @@
 #include <algorithm>
 
 #include "chain.hpp"
+#include "common.hpp"
+#include "gemv.hpp"
 
 namespace dnn {
 
@@ -106,6 +108,103 @@ __global__ __launch_bounds__(256) void chain_send_kernel(ChainSend p) {
     __hip_atomic_store(p.prev_ack + (t - 1), p.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// The status a hop sends on (chain_send's rule): an upstream failure travels on unchanged,
+// a missed input blames the producer, an ack timeout the consumer.
+__device__ __forceinline__ uint32_t hop_status(uint32_t status, const uint32_t* in_hdr,
+                                               const uint32_t* err, int stage, bool ack_ok,
+                                               unsigned t) {
+  if (status) return status;
+  const uint32_t in = in_hdr ? in_hdr[t] : 0u;
+  if (in & 0xffu) return in;
+  if (__hip_atomic_load(err + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))
+    return CHAIN_DEADLINE | ((uint32_t)(stage - 1) << 8);
+  if (!ack_ok) return CHAIN_DEADLINE | ((uint32_t)(stage + 1) << 8);
+  return 0u;
+}
+
+constexpr int CG_WAVES = 4;  // output neurons (waves) per 256-thread workgroup, as gemv.hip
+
+template <int M, bool OUT_F32>
+__global__ __launch_bounds__(256) void chain_gemv_send_kernel(ChainGemvSend p) {
+  __shared__ uint32_t s_go;
+  const unsigned t = threadIdx.x;
+  const int lane = t & 63;
+  if (t == 0) {
+    const bool ok = p.ack ? spin(p.ack + t, p.ack_target, p.timeout_ticks) : true;
+    if (!ok)  // a consumer that never freed the slot: remembered for the last workgroup
+      __hip_atomic_fetch_or(p.counter + 1 + t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_go = hop_status(p.status, p.in_hdr, p.err, p.stage, ok, t) == 0u ? 1u : 0u;
+  }
+  __syncthreads();
+  const int n = blockIdx.x * CG_WAVES + (int)(t >> 6);
+  if (s_go && n < p.N) {  // (no early return: every thread reaches the barrier below)
+    const uint16_t* wr = p.w + (long)n * p.ldw;
+    float acc[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) acc[m] = 0.f;
+    constexpr int U = 4;
+    for (int k0 = 0; k0 < p.K; k0 += 512 * U) {
+      bf16x8_t wv[U], xv[U][M];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = k0 + u * 512 + lane * 8;
+        if (k < p.K) {
+          wv[u] = *(const bf16x8_t*)(wr + k);
+#pragma unroll
+          for (int m = 0; m < M; ++m)
+            xv[u][m] = m < p.rows ? *(const bf16x8_t*)(p.x + m * p.ldx + k) : bf16x8_t{};
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = k0 + u * 512 + lane * 8;
+        if (k < p.K) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float we = bf2f((u16)wv[u][e]);
+#pragma unroll
+            for (int m = 0; m < M; ++m) acc[m] += we * bf2f((u16)xv[u][m][e]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < M; ++m) acc[m] = wave_sum(acc[m]);
+    if (lane < p.rows) {
+      float v = 0.f;
+#pragma unroll
+      for (int m = 0; m < M; ++m)
+        if (m == lane) v = acc[m];
+      v = act_fwd(v + (p.bias ? p.bias[n] : 0.f), p.act);
+      if constexpr (OUT_F32)
+        ((float*)p.dst)[(long)lane * p.dst_ld + n] = v;
+      else
+        ((u16*)p.dst)[(long)lane * p.dst_ld + n] = f2bf(v);
+    }
+  }
+  __threadfence_system();  // this thread's rows are visible before the workgroup counts in
+  __syncthreads();
+  if (t == 0) {
+    const uint32_t prev = __hip_atomic_fetch_add(p.counter + t, 1u, __ATOMIC_ACQ_REL,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1) {  // the last workgroup: every row has landed
+      const uint32_t fail = __hip_atomic_load(p.counter + 1 + t, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t st = hop_status(p.status, p.in_hdr, p.err, p.stage, fail == 0u, t);
+      __hip_atomic_store(p.counter + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p.counter + 1 + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(p.err + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(p.dst_hdr + t, st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(p.dst_hdr + 1 + t, (uint32_t)p.rows, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+      __threadfence_system();
+      __hip_atomic_store(p.next_flag + t, p.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (p.prev_ack)
+        __hip_atomic_store(p.prev_ack + t, p.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 __global__ void chain_signal_kernel(uint32_t* flag, uint32_t value) {
   const unsigned l = threadIdx.x;
   if (l == 0) {
@@ -186,6 +285,31 @@ int chain_send(const ChainSend& p, hipStream_t stream) {
       misaligned16(p.src) || misaligned16(p.dst))
     return -2;
   hipLaunchKernelGGL(chain_send_kernel, dim3(1), dim3(256), 0, stream, p);
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
+int chain_gemv_send(const ChainGemvSend& p, hipStream_t stream) {
+  if (!p.next_flag || !p.dst_hdr || !p.err || !p.counter || !p.dst || !p.x || !p.w ||
+      misaligned4(p.next_flag) || misaligned4(p.counter))
+    return -1;
+  if (p.rows < 1 || p.rows > GEMV_MAX_ROWS || p.N < 1 || p.K < 8 || p.K % 8 || p.ldx < p.K ||
+      p.ldw < p.K || p.ldx % 8 || p.ldw % 8 || p.dst_ld < p.N || misaligned16(p.x) ||
+      misaligned16(p.w))
+    return -2;
+  const dim3 grid((p.N + CG_WAVES - 1) / CG_WAVES), block(256);
+#define DNN_CG(MM)                                                                           \
+  if (p.out_f32)                                                                             \
+    hipLaunchKernelGGL((chain_gemv_send_kernel<MM, true>), grid, block, 0, stream, p);       \
+  else                                                                                       \
+    hipLaunchKernelGGL((chain_gemv_send_kernel<MM, false>), grid, block, 0, stream, p);
+  switch (p.rows) {
+    case 1: DNN_CG(1) break;
+    case 2: DNN_CG(2) break;
+    case 3:
+    case 4: DNN_CG(4) break;
+    default: DNN_CG(8) break;
+  }
+#undef DNN_CG
   return hipGetLastError() == hipSuccess ? 0 : -9;
 }
 

@@ -68,6 +68,39 @@ int chain_send(const ChainSend& p, hipStream_t stream);
 // *flag = value with system-scope release (one lane, a vector store).
 int chain_signal(uint32_t* flag, uint32_t value, hipStream_t stream);
 
+// A stage's LAST serving layer fused with the send of its hop: the GEMV of gemv.hip (one wave
+// per output neuron, bias + activation) writes its rows straight into the consumer's
+// IPC-mapped slot instead of a local buffer, and the last workgroup to finish (a counter, as
+// in p2p_copy_signal_seq) writes the slot header and releases the consumer's flag -- one
+// launch and no row copy instead of gemv + chain_send. Status / blame as chain_send: an
+// upstream failure or a missed input travels on, a consumer that never freed the slot
+// (ack timeout in any workgroup) is blamed, and then no workgroup writes rows.
+struct ChainGemvSend {
+  const uint16_t* x;         // [rows][ldx] bf16 input rows (this stage's, L2-cached)
+  long ldx;
+  const uint16_t* w;         // [N][ldw] bf16 weights (nn.Linear layout)
+  long ldw;
+  const float* bias;         // [N] or nullptr
+  int act;                   // Act code (forward activation)
+  int rows, N, K;            // rows <= GEMV_MAX_ROWS; K % 8 == 0
+  int out_f32;               // the slot holds fp32 (else bf16) rows
+  void* dst;                 // consumer's slot, leading dimension dst_ld ELEMENTS
+  long dst_ld;
+  uint32_t* dst_hdr;
+  const uint32_t* in_hdr;
+  uint32_t* err;
+  int stage;
+  uint32_t status;
+  const uint32_t* ack;
+  uint32_t ack_target;
+  uint32_t* next_flag;
+  uint32_t seq;
+  uint32_t* prev_ack;
+  uint32_t* counter;         // [2] zero-initialised, left zeroed: arrivals, ack failures
+  unsigned long long timeout_ticks;
+};
+int chain_gemv_send(const ChainGemvSend& p, hipStream_t stream);
+
 // Training step plans (runtime/step_plan.cpp COPYSIG): a peer copy followed by its flag in ONE
 // launch. Every workgroup copies its share, fences, and bumps `counter`; the last one to
 // arrive resets the counter and stores *flag = *seq + delta (system-scope release), so the

@@ -86,14 +86,16 @@ class InferenceStage:
             self._bufs[rows] = b
         return b
 
-    def forward(self, rows: int, x: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def forward(self, rows: int, x: Optional[torch.Tensor] = None,
+                upto: Optional[int] = None) -> torch.Tensor:
         """Run on buffers(rows)['x'] (or on ``x``, e.g. the device-side chain's input rows);
-        returns fp32 [rows][out_pad] (last stage) or bf16."""
+        returns fp32 [rows][out_pad] (last stage) or bf16. ``upto``: only layers [0, upto)
+        (the device-side chain runs the last one fused with its send)."""
         b = self.buffers(rows)
         if x is None:
             x = b["x"]
         n = len(self.layers)
-        for i in range(n):
+        for i in range(n if upto is None else upto):
             act = self.acts[i]
             last = i == n - 1
             h, f = b["h"][i], b["f32"][i]

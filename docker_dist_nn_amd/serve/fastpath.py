@@ -236,6 +236,11 @@ class FastChain:
             self.why = "fast path unavailable: no shared-memory announcement ring"
             return
         self.stream = torch.cuda.Stream(self.dev)
+        # the stage's last layer fused with the send of its hop (chain_gemv_send): not for a
+        # softmax output (a row-wise second pass)
+        self.fused = (switches.get("DNN_CHAIN_FUSED") == "1" and
+                      st.acts[-1] != "softmax")
+        self.counter = torch.zeros(4, dtype=torch.int32, device=self.dev)
         self.trace = switches.get("DNN_CHAIN_TRACE") == "1"
         self.lat: collections.deque = collections.deque(maxlen=100000)  # rank 0: seconds
         self.seq = 0
@@ -251,7 +256,8 @@ class FastChain:
                                   device=self.dev)
             self.events = [torch.cuda.Event() for _ in range(NSLOT)]
         self.ok = True
-        self.why = f"device-side chain ({NSLOT} slots per hop)"
+        self.why = (f"device-side chain ({NSLOT} slots per hop"
+                    + (", last layer fused with the send" if self.fused else "") + ")")
 
     def _agree(self, ok: bool) -> bool:
         from ..parallel.comm import _cpu_group
@@ -285,6 +291,25 @@ class FastChain:
                           _ptr(self.flags, F_ACK), (seq - NSLOT) & 0xFFFFFFFF, dflag, seq, 0,
                           self.cr.hop_timeout)  # (ack compares wrap: seq < NSLOT passes)
 
+    def _gemv_send(self, s: torch.cuda.Stream, x: torch.Tensor, rows: int, seq: int,
+                   in_hdr: int) -> None:
+        """The stage's layers up to the last, then the last one fused with the hop's send:
+        its rows go straight into the consumer's slot (csrc/kernels/chain.hip)."""
+        st = self.cr.stage
+        L = len(st.layers)
+        if L > 1:
+            x = st.forward(rows, x=x, upto=L - 1)
+        w, b = st.w[-1], st.b[-1]
+        slot = seq % NSLOT
+        dst, dld, dhdr, dflag = self._dst(slot)
+        f32 = self.rank == self.world - 1  # the last rank fills rank 0's fp32 result slots
+        self.n.chain_gemv_send(s.cuda_stream, x.data_ptr(), x.stride(0), w.data_ptr(),
+                               w.stride(0), b.data_ptr(), ops.kernels._act(st.acts[-1]), rows,
+                               w.shape[0], x.shape[1], int(f32), dst, dld // (4 if f32 else 2),
+                               dhdr, in_hdr, _ptr(self.flags, F_ERR), self.rank, 0,
+                               _ptr(self.flags, F_ACK), (seq - NSLOT) & 0xFFFFFFFF, dflag, seq,
+                               0, self.counter.data_ptr(), self.cr.hop_timeout)
+
     # ---- rank 0 -------------------------------------------------------------------------------
     def predict(self, x: np.ndarray, timeout: Optional[float]) -> np.ndarray:
         """One request of <= max_rows rows through the device-side chain -> float64 outputs."""
@@ -307,12 +332,17 @@ class FastChain:
                 self._trace(seq, f"announced rows={rows}")
             with torch.cuda.stream(self.stream):
                 self.x0[:rows].copy_(hin[:rows], non_blocking=True)
-                status = 0
+                status, out, sent = 0, None, False
                 try:
-                    out = st.forward(rows, x=self.x0[:rows])
+                    if self.fused:
+                        self._gemv_send(self.stream, self.x0[:rows], rows, seq, 0)
+                        sent = True
+                    else:
+                        out = st.forward(rows, x=self.x0[:rows])
                 except ValueError:
                     out, status = None, ST_VALUE
-                self._send(self.stream, out, rows, seq, status, 0)
+                if not sent:
+                    self._send(self.stream, out, rows, seq, status, 0)
             rs = self.res_stream
             base = self.res[slot]
             n.chain_wait(rs.cuda_stream, _ptr(self.flags, F_RES + slot), seq, _ptr(base, 2),
@@ -399,17 +429,22 @@ class FastChain:
                              _ptr(self.flags, F_HDR + 2 * slot), self.x_local.data_ptr(), row_b,
                              _ptr(self.flags, F_LHDR), rows, row_b, _ptr(self.flags, F_ERR), seq,
                              self.prev_flags + 4 * F_ACK, self.cr.hop_timeout)
-                status = 0
-                out = None
+                status, out, sent = 0, None, False
                 try:
                     self.cr._maybe_fault(self.processed)
-                    out = self.cr.stage.forward(rows, x=self.x_local[:rows])
+                    if self.fused:
+                        self._gemv_send(s, self.x_local[:rows], rows, seq,
+                                        _ptr(self.flags, F_LHDR))
+                        sent = True
+                    else:
+                        out = self.cr.stage.forward(rows, x=self.x_local[:rows])
                 except ValueError:
                     status = ST_VALUE | (self.rank << 8)
                 except Exception:  # noqa: BLE001
                     log.exception(f"({self.cr.names[self.rank]}) stage failure")
                     status = ST_INTERNAL | (self.rank << 8)
-                self._send(s, out, rows, seq, status, _ptr(self.flags, F_LHDR))
+                if not sent:
+                    self._send(s, out, rows, seq, status, _ptr(self.flags, F_LHDR))
             if self.trace:
                 self._trace(seq, f"enqueued rows={rows} status={status}")
                 s.synchronize()

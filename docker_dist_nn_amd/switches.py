@@ -105,6 +105,9 @@ SWITCHES: dict[str, tuple[str, str]] = {
                                       "stalled (steady state: DNN_FLAG_TIMEOUT, 120 s)"),
     "DNN_FAULT_IPC_VERIFY": ("", "ranks whose IPC verification step is corrupted (tests the "
                                  "fallback)"),
+    "DNN_CHAIN_FUSED": ("1", "device-side chain: a stage's last (non-softmax) layer runs fused "
+                             "with the hop's send (chain_gemv_send: rows straight into the "
+                             "consumer's slot); 0 = gemv + chain_send"),
     "DNN_CHAIN_TRACE": ("0", "device-side chain: 1 = every rank logs each request's steps and, "
                              "after synchronising, its flag words (diagnosis; serialises)"),
     "DNN_CHAIN_FAST": ("1", "rank chain: serving-size requests (<= 8 rows) take the device-side "

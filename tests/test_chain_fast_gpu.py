@@ -208,3 +208,49 @@ def test_chain_kernels_in_one_process(dev):
     recv(9, timeout=0.2)
     torch.cuda.synchronize(dev)
     assert int(err_c[0]) == 1 and float(dst.float().abs().sum()) == 0.0
+
+
+@pytest.mark.parametrize("rows", [1, 3, 8])
+def test_chain_gemv_send_in_one_process(dev, rows):
+    """chain_gemv_send (a stage's last layer fused with its send): the rows it writes into the
+    consumer's slot equal ops.gemv's bit for bit, the header / flag / counter protocol matches
+    chain_send's, and a consumer that never acks is blamed with no rows written."""
+    import torch
+
+    from docker_dist_nn_amd import ops
+    from docker_dist_nn_amd.utils.devmem import uncached_zeros
+    from docker_dist_nn_amd.utils.native import native
+
+    n = native()
+    K, N = 832, 1024
+    g = torch.Generator().manual_seed(rows)
+    x = (torch.randn(8, K, generator=g) * 0.5).to(torch.bfloat16).to(dev)
+    w = (torch.randn(N, K, generator=g) * 0.05).to(torch.bfloat16).to(dev)
+    b = torch.randn(N, generator=g).to(dev)
+    ref = torch.empty(rows, N, dtype=torch.bfloat16, device=dev)
+    ops.gemv(x[:rows], w, b, ref, act="relu")
+    flags_c = uncached_zeros((64,), torch.int32, dev)  # consumer: [0] flag, [2:4] header
+    flags_p = uncached_zeros((64,), torch.int32, dev)  # producer: [8] ack, [9] err
+    slot = uncached_zeros((8, N), torch.bfloat16, dev)
+    counter = torch.zeros(4, dtype=torch.int32, device=dev)
+    s = torch.cuda.Stream(dev)
+    fp, fc = flags_p.data_ptr(), flags_c.data_ptr()
+
+    def send(seq, ack_target, timeout=2.0):
+        n.chain_gemv_send(s.cuda_stream, x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0),
+                          b.data_ptr(), 1, rows, N, K, 0, slot.data_ptr(), N, fc + 8, 0,
+                          fp + 36, 0, 0, fp + 32, ack_target, fc, seq, 0, counter.data_ptr(),
+                          timeout)
+
+    send(1, 0)
+    torch.cuda.synchronize(dev)
+    assert torch.equal(slot[:rows], ref)
+    assert int(flags_c[0]) == 1 and flags_c[2:4].tolist() == [0, rows]
+    assert counter.tolist() == [0, 0, 0, 0]
+    # the consumer never drained the slot (ack stays 0 < 2): blamed (stage 0 + 1), no rows
+    slot.zero_()
+    send(2, 2, timeout=0.2)
+    torch.cuda.synchronize(dev)
+    assert int(flags_c[0]) == 2 and (int(flags_c[2]) & 0xFF) == 4
+    assert (int(flags_c[2]) >> 8) & 0xFF == 1
+    assert float(slot.float().abs().sum()) == 0.0 and counter.tolist() == [0, 0, 0, 0]
