@@ -50,8 +50,8 @@ def main():
         # the GPU's queue slots, and the scheduler's queue rotation put ~13 ms outliers into
         # the p99 (profiles/r4_chain: 13.7 ms at 4 queues, 0.75 ms at 2); one real GPU per
         # stage has no such sharing
-        env.update(DNN_FORCE_DEVICE="0", DNN_DIST_BACKEND="gloo")
-        env.setdefault("GPU_MAX_HW_QUEUES", "2")
+        env.update(DNN_FORCE_DEVICE="0", DNN_DIST_BACKEND="gloo",
+                   GPU_MAX_HW_QUEUES=os.environ.get("DNN_REHEARSAL_HW_QUEUES", "2"))
     with tempfile.TemporaryDirectory() as d:
         cfg = os.path.join(d, "model.json")
         export_model_json(cfg, ws, bs, ["relu"] * (a.stages - 1) + ["softmax"],

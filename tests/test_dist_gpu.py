@@ -241,13 +241,14 @@ def test_relayed_ipc_hops_bitwise_equal_direct(dev, world, relays):
                               np.load(os.path.join(d, "nrelay_loss.npy")))
 
 
-@pytest.mark.parametrize("world,relays", [(2, 0), (4, 0), (4, 2), (4, "auto")])
-def test_native_multirank_step_graph_capture(dev, world, relays):
+@pytest.mark.parametrize("world,relays,nm", [(2, 0, 4), (4, 0, 4), (4, 2, 8), (4, "auto", 4)])
+def test_native_multirank_step_graph_capture(dev, world, relays, nm):
     """The native multi-rank step (IPC hops: device step-number flag kernels) captured into a
     HIP graph and replayed gives bit-identical training to eager plan runs, and a replayed
     step costs the host only the graph launch. Relayed hops included (VERDICT r3 #4: capture
-    now records the slotted single-stream form, Trainer.capture)."""
-    steps, nm = 6, 4
+    now records the slotted single-stream form, Trainer.capture). pp4 x 8 micro-batches with
+    2 relays: the host time per replayed rank-step stays under 100 us (VERDICT r3 #4)."""
+    steps = 6
     with tempfile.TemporaryDirectory() as d:
         for tag, graph in (("eager", False), ("graph", True)):
             mp.start_processes(_native_worker,
@@ -262,8 +263,9 @@ def test_native_multirank_step_graph_capture(dev, world, relays):
                               np.load(os.path.join(d, "ngraph_loss.npy")))
         host = [float(np.median(np.load(os.path.join(d, f"ngraph_host_r{r}.npy"))))
                 for r in range(world)]
-        print("graph replay host s/step per rank:", host)
-        assert max(host) < 5e-4, host
+        print(f"graph replay host us/step per rank (pp{world}, {nm} micro-batches, relays "
+              f"{relays}):", [round(h * 1e6, 1) for h in host])
+        assert max(host) < 1e-4, host
 
 
 @pytest.mark.parametrize("world,relays", [(3, 1), (4, "auto")])
