@@ -15,7 +15,9 @@ import json
 import os
 import sys
 
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")  # one hardware queue per stage stream
+# one hardware queue per stage stream (the box exports 4: with stages + the host stream
+# sharing queues, a spinning receive would sit in front of the signal that releases it)
+os.environ["GPU_MAX_HW_QUEUES"] = "16"
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 import numpy as np  # noqa: E402
@@ -25,7 +27,9 @@ from docker_dist_nn_amd.utils.devmem import uncached_zeros  # noqa: E402
 from docker_dist_nn_amd.utils.native import native  # noqa: E402
 
 
-def run(n, dev, S, iters, W=1024, rows=1, fused=True):
+def run(n, dev, S, iters, W=1024, rows=1, form=1):
+    """form 1: one kernel per hop (receive folded into chain_gemv_send); 2: chain_recv +
+    chain_gemv_send; 3: chain_recv + gemv + chain_send."""
     flags = [uncached_zeros((64,), torch.int32, dev) for _ in range(S + 1)]  # [0] in, [2:4] hdr
     slots = [uncached_zeros((8, W), torch.bfloat16, dev) for _ in range(S + 1)]
     xl = [torch.zeros(8, W, dtype=torch.bfloat16, device=dev) for _ in range(S)]
@@ -43,9 +47,15 @@ def run(n, dev, S, iters, W=1024, rows=1, fused=True):
         for k in range(S):
             s = streams[k].cuda_stream
             fk, fn = flags[k].data_ptr(), flags[k + 1].data_ptr()
+            if form == 1:
+                n.chain_gemv_send(s, slots[k].data_ptr(), W, w[k].data_ptr(), W,
+                                  b[k].data_ptr(), 1, rows, W, W, 0, slots[k + 1].data_ptr(), W,
+                                  fn + 8, fk + 8, err[k].data_ptr(), k, 0, 0, 0, fn, it, 0,
+                                  ctr[k].data_ptr(), 5.0, in_flag=fk)
+                continue
             n.chain_recv(s, fk, slots[k].data_ptr(), rb, fk + 8, xl[k].data_ptr(), rb,
                          lh[k].data_ptr(), rows, rb, err[k].data_ptr(), it, 0, 5.0)
-            if fused:
+            if form == 2:
                 n.chain_gemv_send(s, xl[k].data_ptr(), W, w[k].data_ptr(), W, b[k].data_ptr(),
                                   1, rows, W, W, 0, slots[k + 1].data_ptr(), W, fn + 8,
                                   lh[k].data_ptr(), err[k].data_ptr(), k, 0, 0, 0, fn, it, 0,
@@ -66,21 +76,21 @@ def run(n, dev, S, iters, W=1024, rows=1, fused=True):
             raise RuntimeError(f"request {it} did not reach the end of the chain")
         ts.append(e0.elapsed_time(e1))
     t = np.asarray(ts[10:]) * 1e3
-    return {"stages": S, "fused": fused, "p50_us": round(float(np.percentile(t, 50)), 2),
+    return {"stages": S, "kernels_per_hop": form, "p50_us": round(float(np.percentile(t, 50)), 2),
             "p90_us": round(float(np.percentile(t, 90)), 2)}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--stages", default="1,2,4,8")
-    ap.add_argument("--iters", type=int, default=200)
+    ap.add_argument("--iters", type=int, default=100)
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
     n = native()
-    for fused in (True, False):
+    for form in (1, 2, 3):
         for S in (int(v) for v in a.stages.split(",")):
-            print(json.dumps(run(n, dev, S, a.iters, fused=fused)), flush=True)
+            print(json.dumps(run(n, dev, S, a.iters, form=form)), flush=True)
 
 
 if __name__ == "__main__":

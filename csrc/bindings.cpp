@@ -1078,8 +1078,9 @@ PYBIND11_MODULE(_native, m) {
           int rows, int N, int K, int out_f32, uintptr_t dst, long dst_ld, uintptr_t dst_hdr,
           uintptr_t in_hdr, uintptr_t err, int stage, uint32_t status, uintptr_t ack,
           uint32_t ack_target, uintptr_t next_flag, uint32_t seq, uintptr_t prev_ack,
-          uintptr_t counter, double timeout_s) {
+          uintptr_t counter, double timeout_s, uintptr_t in_flag) {
         dnn::ChainGemvSend p{};
+        p.in_flag = static_cast<const uint32_t*>(ptr(in_flag));
         p.x = static_cast<const uint16_t*>(ptr(x));
         p.ldx = ldx;
         p.w = static_cast<const uint16_t*>(ptr(w));
@@ -1111,7 +1112,7 @@ PYBIND11_MODULE(_native, m) {
       py::arg("out_f32"), py::arg("dst"), py::arg("dst_ld"), py::arg("dst_hdr"),
       py::arg("in_hdr"), py::arg("err"), py::arg("stage"), py::arg("status"), py::arg("ack"),
       py::arg("ack_target"), py::arg("next_flag"), py::arg("seq"), py::arg("prev_ack"),
-      py::arg("counter"), py::arg("timeout_s"));
+      py::arg("counter"), py::arg("timeout_s"), py::arg("in_flag") = 0);
   m.def(
       "chain_signal",
       [=](uintptr_t s, uintptr_t flag, uint32_t value) {

@@ -112,9 +112,11 @@ __global__ __launch_bounds__(256) void chain_send_kernel(ChainSend p) {
 // a missed input blames the producer, an ack timeout the consumer.
 __device__ __forceinline__ uint32_t hop_status(uint32_t status, const uint32_t* in_hdr,
                                                const uint32_t* err, int stage, bool ack_ok,
-                                               unsigned t) {
+                                               unsigned t, bool in_ok = true) {
   if (status) return status;
-  const uint32_t in = in_hdr ? in_hdr[t] : 0u;
+  if (!in_ok) return CHAIN_DEADLINE | ((uint32_t)(stage - 1) << 8);  // input never came
+  const uint32_t in = in_hdr ? __hip_atomic_load(in_hdr + t, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
   if (in & 0xffu) return in;
   if (__hip_atomic_load(err + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))
     return CHAIN_DEADLINE | ((uint32_t)(stage - 1) << 8);
@@ -130,14 +132,19 @@ __global__ __launch_bounds__(256) void chain_gemv_send_kernel(ChainGemvSend p) {
   const unsigned t = threadIdx.x;
   const int lane = t & 63;
   if (t == 0) {
+    // the input (folded receive) first, then the consumer's slot; both bounded
+    const bool in_ok = p.in_flag ? spin(p.in_flag + t, p.seq, p.timeout_ticks) : true;
     const bool ok = p.ack ? spin(p.ack + t, p.ack_target, p.timeout_ticks) : true;
-    if (!ok)  // a consumer that never freed the slot: remembered for the last workgroup
-      __hip_atomic_fetch_or(p.counter + 1 + t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_go = hop_status(p.status, p.in_hdr, p.err, p.stage, ok, t) == 0u ? 1u : 0u;
+    if (!ok || !in_ok)  // remembered for the last workgroup: bit 0 ack, bit 1 input
+      __hip_atomic_fetch_or(p.counter + 1 + t, (ok ? 0u : 1u) | (in_ok ? 0u : 2u),
+                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_go = hop_status(p.status, p.in_hdr, p.err, p.stage, ok, t, in_ok) == 0u ? 1u : 0u;
   }
   __syncthreads();
-  const int n = blockIdx.x * CG_WAVES + (int)(t >> 6);
-  if (s_go && n < p.N) {  // (no early return: every thread reaches the barrier below)
+  // a wave per output neuron; with fewer workgroups than N / 4 (the folded receive: every
+  // workgroup spins, so the grid is capped) a wave takes every (grid * 4)-th neuron
+  for (int n = blockIdx.x * CG_WAVES + (int)(t >> 6); s_go && n < p.N;
+       n += gridDim.x * CG_WAVES) {  // (no early return: every thread reaches the barrier)
     const uint16_t* wr = p.w + (long)n * p.ldw;
     float acc[M];
 #pragma unroll
@@ -190,7 +197,8 @@ __global__ __launch_bounds__(256) void chain_gemv_send_kernel(ChainGemvSend p) {
     if (prev == gridDim.x - 1) {  // the last workgroup: every row has landed
       const uint32_t fail = __hip_atomic_load(p.counter + 1 + t, __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t st = hop_status(p.status, p.in_hdr, p.err, p.stage, fail == 0u, t);
+      const uint32_t st = hop_status(p.status, p.in_hdr, p.err, p.stage, (fail & 1u) == 0u, t,
+                                     (fail & 2u) == 0u);
       __hip_atomic_store(p.counter + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(p.counter + 1 + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(p.err + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -296,7 +304,12 @@ int chain_gemv_send(const ChainGemvSend& p, hipStream_t stream) {
       p.ldw < p.K || p.ldx % 8 || p.ldw % 8 || p.dst_ld < p.N || misaligned16(p.x) ||
       misaligned16(p.w))
     return -2;
-  const dim3 grid((p.N + CG_WAVES - 1) / CG_WAVES), block(256);
+  // the folded receive makes every workgroup wait on the input flag: at most CG_RECV_WG of
+  // them, so a node's worth of waiting stages (a one-GPU rehearsal puts 8 on one GPU) stays
+  // far below what the GPU holds at once
+  constexpr int CG_RECV_WG = 64;
+  const int wg = (p.N + CG_WAVES - 1) / CG_WAVES;
+  const dim3 grid(p.in_flag ? std::min(wg, CG_RECV_WG) : wg), block(256);
 #define DNN_CG(MM)                                                                           \
   if (p.out_f32)                                                                             \
     hipLaunchKernelGGL((chain_gemv_send_kernel<MM, true>), grid, block, 0, stream, p);       \

@@ -75,8 +75,14 @@ int chain_signal(uint32_t* flag, uint32_t value, hipStream_t stream);
 // launch and no row copy instead of gemv + chain_send. Status / blame as chain_send: an
 // upstream failure or a missed input travels on, a consumer that never freed the slot
 // (ack timeout in any workgroup) is blamed, and then no workgroup writes rows.
+// With `in_flag` set the receive is folded in too (one kernel per hop): every workgroup
+// waits for the input slot's flag (>= seq) and reads the rows straight from the slot (`x`,
+// L2-uncached); `in_hdr` is then the slot's header, and the last workgroup also releases the
+// producer's ack (`prev_ack`: every workgroup has read the slot). A missed input blames the
+// producer, as chain_recv + chain_send do.
 struct ChainGemvSend {
-  const uint16_t* x;         // [rows][ldx] bf16 input rows (this stage's, L2-cached)
+  const uint32_t* in_flag;   // nullptr: x is already local (chain_recv ran, or stage 0)
+  const uint16_t* x;         // [rows][ldx] bf16 input rows
   long ldx;
   const uint16_t* w;         // [N][ldw] bf16 weights (nn.Linear layout)
   long ldw;

@@ -292,9 +292,11 @@ class FastChain:
                           self.cr.hop_timeout)  # (ack compares wrap: seq < NSLOT passes)
 
     def _gemv_send(self, s: torch.cuda.Stream, x: torch.Tensor, rows: int, seq: int,
-                   in_hdr: int) -> None:
+                   in_hdr: int, recv: bool = False) -> None:
         """The stage's layers up to the last, then the last one fused with the hop's send:
-        its rows go straight into the consumer's slot (csrc/kernels/chain.hip)."""
+        its rows go straight into the consumer's slot (csrc/kernels/chain.hip). ``recv``
+        (one-layer stages > 0): the receive is folded in too -- the kernel waits for this
+        stage's input flag and reads the rows from the slot itself, one launch per hop."""
         st = self.cr.stage
         L = len(st.layers)
         if L > 1:
@@ -303,12 +305,18 @@ class FastChain:
         slot = seq % NSLOT
         dst, dld, dhdr, dflag = self._dst(slot)
         f32 = self.rank == self.world - 1  # the last rank fills rank 0's fp32 result slots
-        self.n.chain_gemv_send(s.cuda_stream, x.data_ptr(), x.stride(0), w.data_ptr(),
-                               w.stride(0), b.data_ptr(), ops.kernels._act(st.acts[-1]), rows,
-                               w.shape[0], x.shape[1], int(f32), dst, dld // (4 if f32 else 2),
-                               dhdr, in_hdr, _ptr(self.flags, F_ERR), self.rank, 0,
-                               _ptr(self.flags, F_ACK), (seq - NSLOT) & 0xFFFFFFFF, dflag, seq,
-                               0, self.counter.data_ptr(), self.cr.hop_timeout)
+        if recv:
+            x_ptr, ldx = self.slots[slot].data_ptr(), self.in_w
+            in_flag, prev_ack = _ptr(self.flags, F_IN + slot), self.prev_flags + 4 * F_ACK
+        else:
+            x_ptr, ldx, in_flag, prev_ack = x.data_ptr(), x.stride(0), 0, 0
+        self.n.chain_gemv_send(s.cuda_stream, x_ptr, ldx, w.data_ptr(), w.stride(0),
+                               b.data_ptr(), ops.kernels._act(st.acts[-1]), rows, w.shape[0],
+                               self.in_w if recv else x.shape[1], int(f32), dst,
+                               dld // (4 if f32 else 2), dhdr, in_hdr, _ptr(self.flags, F_ERR),
+                               self.rank, 0, _ptr(self.flags, F_ACK),
+                               (seq - NSLOT) & 0xFFFFFFFF, dflag, seq, prev_ack,
+                               self.counter.data_ptr(), self.cr.hop_timeout, in_flag=in_flag)
 
     # ---- rank 0 -------------------------------------------------------------------------------
     def predict(self, x: np.ndarray, timeout: Optional[float]) -> np.ndarray:
@@ -423,6 +431,19 @@ class FastChain:
             if rows is None:
                 break
             slot = seq % NSLOT
+            one_launch = self.fused and len(self.cr.stage.layers) == 1 and \
+                self.cr.fault_stage != str(self.rank)
+            if one_launch:  # receive + layer + send in ONE kernel
+                with torch.cuda.stream(s):
+                    self._gemv_send(s, None, rows, seq, _ptr(self.flags, F_HDR + 2 * slot),
+                                    recv=True)
+                if self.trace:
+                    self._trace(seq, f"enqueued (one launch) rows={rows}")
+                    s.synchronize()
+                    self._trace(seq, "done")
+                self.processed = seq
+                self.cr._processed = seq
+                continue
             with torch.cuda.stream(s):
                 n.chain_recv(s.cuda_stream, _ptr(self.flags, F_IN + slot),
                              self.slots[slot].data_ptr(), row_b,

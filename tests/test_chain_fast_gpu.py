@@ -254,3 +254,54 @@ def test_chain_gemv_send_in_one_process(dev, rows):
     assert int(flags_c[0]) == 2 and (int(flags_c[2]) & 0xFF) == 4
     assert (int(flags_c[2]) >> 8) & 0xFF == 1
     assert float(slot.float().abs().sum()) == 0.0 and counter.tolist() == [0, 0, 0, 0]
+
+
+def test_chain_one_launch_hop_in_one_process(dev):
+    """chain_gemv_send with the receive folded in (in_flag): the kernel waits for the input
+    slot's flag, reads the rows from the slot itself, writes the layer's rows into the next
+    slot, raises its flag and acks the producer -- and a missing input blames the producer."""
+    import torch
+
+    from docker_dist_nn_amd import ops
+    from docker_dist_nn_amd.utils.devmem import uncached_zeros
+    from docker_dist_nn_amd.utils.native import native
+
+    n = native()
+    K, N, rows = 1024, 1024, 2
+    g = torch.Generator().manual_seed(7)
+    x = (torch.randn(8, K, generator=g) * 0.5).to(torch.bfloat16).to(dev)
+    w = (torch.randn(N, K, generator=g) * 0.05).to(torch.bfloat16).to(dev)
+    b = torch.randn(N, generator=g).to(dev)
+    ref = torch.empty(rows, N, dtype=torch.bfloat16, device=dev)
+    ops.gemv(x[:rows], w, b, ref, act="relu")
+    f_in = uncached_zeros((64,), torch.int32, dev)    # this stage: [0] flag, [2:4] header
+    f_out = uncached_zeros((64,), torch.int32, dev)   # consumer: [0] flag, [2:4] header
+    f_prod = uncached_zeros((64,), torch.int32, dev)  # producer: [8] ack
+    slot_in = uncached_zeros((8, K), torch.bfloat16, dev)
+    slot_out = uncached_zeros((8, N), torch.bfloat16, dev)
+    err = torch.zeros(4, dtype=torch.int32, device=dev)
+    counter = torch.zeros(4, dtype=torch.int32, device=dev)
+    s = torch.cuda.Stream(dev)
+
+    def hop(seq, timeout=2.0):
+        n.chain_gemv_send(s.cuda_stream, slot_in.data_ptr(), K, w.data_ptr(), K, b.data_ptr(),
+                          1, rows, N, K, 0, slot_out.data_ptr(), N, f_out.data_ptr() + 8,
+                          f_in.data_ptr() + 8, err.data_ptr(), 1, 0, 0, 0, f_out.data_ptr(),
+                          seq, f_prod.data_ptr() + 32, counter.data_ptr(), timeout,
+                          in_flag=f_in.data_ptr())
+
+    hop(1)  # enqueued before its input exists: it waits
+    slot_in.copy_(x)
+    f_in[2:4] = torch.tensor([0, rows], dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)
+    f_in[0] = 1  # the producer's flag
+    torch.cuda.synchronize(dev)
+    s.synchronize()
+    assert torch.equal(slot_out[:rows], ref)
+    assert int(f_out[0]) == 1 and f_out[2:4].tolist() == [0, rows] and int(f_prod[8]) == 1
+    # request 2 never arrives: no rows, the producer (stage 0) is blamed downstream
+    slot_out.zero_()
+    hop(2, timeout=0.2)
+    s.synchronize()
+    assert int(f_out[0]) == 2 and (int(f_out[2]) & 0xFF) == 4 and (int(f_out[2]) >> 8) == 0
+    assert float(slot_out.float().abs().sum()) == 0.0 and counter.tolist() == [0, 0, 0, 0]
