@@ -290,12 +290,12 @@ def test_chain_one_launch_hop_in_one_process(dev):
                           seq, f_prod.data_ptr() + 32, counter.data_ptr(), timeout,
                           in_flag=f_in.data_ptr())
 
-    hop(1)  # enqueued before its input exists: it waits
-    slot_in.copy_(x)
+    hop(1)  # enqueued before its input exists: it waits (on stream s; the writes below go
+    slot_in.copy_(x)  # through the current stream -- no device-wide sync while it spins)
     f_in[2:4] = torch.tensor([0, rows], dtype=torch.int32, device=dev)
-    torch.cuda.synchronize(dev)
+    torch.cuda.current_stream(dev).synchronize()
     f_in[0] = 1  # the producer's flag
-    torch.cuda.synchronize(dev)
+    torch.cuda.current_stream(dev).synchronize()
     s.synchronize()
     assert torch.equal(slot_out[:rows], ref)
     assert int(f_out[0]) == 1 and f_out[2:4].tolist() == [0, rows] and int(f_prod[8]) == 1
