@@ -51,25 +51,25 @@ def run(n, dev, S, iters, W=1024, rows=1, form=1):
                 n.chain_gemv_send(s, slots[k].data_ptr(), W, w[k].data_ptr(), W,
                                   b[k].data_ptr(), 1, rows, W, W, 0, slots[k + 1].data_ptr(), W,
                                   fn + 8, fk + 8, err[k].data_ptr(), k, 0, 0, 0, fn, it, 0,
-                                  ctr[k].data_ptr(), 5.0, in_flag=fk)
+                                  ctr[k].data_ptr(), 1.0, in_flag=fk)
                 continue
             n.chain_recv(s, fk, slots[k].data_ptr(), rb, fk + 8, xl[k].data_ptr(), rb,
-                         lh[k].data_ptr(), rows, rb, err[k].data_ptr(), it, 0, 5.0)
+                         lh[k].data_ptr(), rows, rb, err[k].data_ptr(), it, 0, 1.0)
             if form == 2:
                 n.chain_gemv_send(s, xl[k].data_ptr(), W, w[k].data_ptr(), W, b[k].data_ptr(),
                                   1, rows, W, W, 0, slots[k + 1].data_ptr(), W, fn + 8,
                                   lh[k].data_ptr(), err[k].data_ptr(), k, 0, 0, 0, fn, it, 0,
-                                  ctr[k].data_ptr(), 5.0)
+                                  ctr[k].data_ptr(), 1.0)
             else:
                 n.gemv_bf16(xl[k].data_ptr(), W, w[k].data_ptr(), W, b[k].data_ptr(),
                             out[k].data_ptr(), W, rows, W, W, 1, 0, s)
                 n.chain_send(s, out[k].data_ptr(), rb, slots[k + 1].data_ptr(), rb, rows, rb,
                              fn + 8, lh[k].data_ptr(), err[k].data_ptr(), k, 0, 0, 0, fn, it,
-                             0, 5.0)
+                             0, 1.0)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(host)
         n.chain_signal(host.cuda_stream, flags[0].data_ptr(), it)
-        n.chain_wait(host.cuda_stream, flags[S].data_ptr(), it, err[S].data_ptr(), 5.0)
+        n.chain_wait(host.cuda_stream, flags[S].data_ptr(), it, err[S].data_ptr(), 1.0)
         e1.record(host)
         torch.cuda.synchronize(dev)
         if int(err[S][0]):
@@ -83,14 +83,20 @@ def run(n, dev, S, iters, W=1024, rows=1, form=1):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--stages", default="1,2,4,8")
-    ap.add_argument("--iters", type=int, default=100)
+    ap.add_argument("--iters", type=int, default=60)
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
     n = native()
     for form in (1, 2, 3):
         for S in (int(v) for v in a.stages.split(",")):
-            print(json.dumps(run(n, dev, S, a.iters, form=form)), flush=True)
+            try:
+                r = run(n, dev, S, a.iters, form=form)
+            except RuntimeError as e:  # a request timed out (1 s): next form
+                print(json.dumps({"stages": S, "kernels_per_hop": form, "error": str(e)}),
+                      flush=True)
+                break
+            print(json.dumps(r), flush=True)
 
 
 if __name__ == "__main__":

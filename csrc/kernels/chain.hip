@@ -20,12 +20,17 @@ __device__ __forceinline__ bool reached(const uint32_t* flag, uint32_t target) {
          0;
 }
 
-// lane 0 of the calling wave: poll until reached or timed out
+// lane 0 of the calling wave: poll until reached or timed out. `relaxed`: a long sleep
+// between polls (~1000 clocks instead of ~64), for the many workgroups of a one-launch hop
+// that all wait on one flag -- their uncached polls otherwise flood the memory system the
+// flag's own write has to get through (profiles/r4_chain: 4 waiting stages, 144 vs 18 us)
+template <bool relaxed = false>
 __device__ __forceinline__ bool spin(const uint32_t* flag, uint32_t target,
                                      unsigned long long ticks) {
   const unsigned long long t0 = wall_clock64();
   while (!reached(flag, target)) {
-    __builtin_amdgcn_s_sleep(1);
+    if constexpr (relaxed) __builtin_amdgcn_s_sleep(16);
+    else __builtin_amdgcn_s_sleep(1);
     if (wall_clock64() - t0 > ticks) return false;
   }
   return true;
@@ -133,7 +138,9 @@ __global__ __launch_bounds__(256) void chain_gemv_send_kernel(ChainGemvSend p) {
   const int lane = t & 63;
   if (t == 0) {
     // the input (folded receive) first, then the consumer's slot; both bounded
-    const bool in_ok = p.in_flag ? spin(p.in_flag + t, p.seq, p.timeout_ticks) : true;
+    const bool in_ok = !p.in_flag ? true
+                       : blockIdx.x == 0 ? spin(p.in_flag + t, p.seq, p.timeout_ticks)
+                                         : spin<true>(p.in_flag + t, p.seq, p.timeout_ticks);
     const bool ok = p.ack ? spin(p.ack + t, p.ack_target, p.timeout_ticks) : true;
     if (!ok || !in_ok)  // remembered for the last workgroup: bit 0 ack, bit 1 input
       __hip_atomic_fetch_or(p.counter + 1 + t, (ok ? 0u : 1u) | (in_ok ? 0u : 2u),

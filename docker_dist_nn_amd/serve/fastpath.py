@@ -241,6 +241,7 @@ class FastChain:
         self.fused = (switches.get("DNN_CHAIN_FUSED") == "1" and
                       st.acts[-1] != "softmax")
         self.counter = torch.zeros(4, dtype=torch.int32, device=self.dev)
+        self.one_launch = self.fused and switches.get("DNN_CHAIN_ONE_LAUNCH") == "1"
         self.trace = switches.get("DNN_CHAIN_TRACE") == "1"
         self.lat: collections.deque = collections.deque(maxlen=100000)  # rank 0: seconds
         self.seq = 0
@@ -431,7 +432,7 @@ class FastChain:
             if rows is None:
                 break
             slot = seq % NSLOT
-            one_launch = self.fused and len(self.cr.stage.layers) == 1 and \
+            one_launch = self.one_launch and len(self.cr.stage.layers) == 1 and \
                 self.cr.fault_stage != str(self.rank)
             if one_launch:  # receive + layer + send in ONE kernel
                 with torch.cuda.stream(s):

@@ -108,6 +108,10 @@ SWITCHES: dict[str, tuple[str, str]] = {
     "DNN_CHAIN_FUSED": ("1", "device-side chain: a stage's last (non-softmax) layer runs fused "
                              "with the hop's send (chain_gemv_send: rows straight into the "
                              "consumer's slot); 0 = gemv + chain_send"),
+    "DNN_CHAIN_ONE_LAUNCH": ("0", "device-side chain, one-layer stages > 0: the receive folded into "
+                                  "chain_gemv_send too (one kernel per hop; every workgroup "
+                                  "waits on the input flag). Opt-in: slower with several waiting "
+                                  "stages on one GPU (profiles/r4_chain)"),
     "DNN_CHAIN_TRACE": ("0", "device-side chain: 1 = every rank logs each request's steps and, "
                              "after synchronising, its flag words (diagnosis; serialises)"),
     "DNN_CHAIN_FAST": ("1", "rank chain: serving-size requests (<= 8 rows) take the device-side "
