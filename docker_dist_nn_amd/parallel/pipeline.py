@@ -454,9 +454,12 @@ class PipelineExecutor:
             # main stream runs W0; then only layer 0's reduction + update is left at the end
             if plan[-1][1] != "@fork":
                 plan.append((None, "@fork", 0))
-            plan += [(st, f"FINO1-{L - 1}", 1), (st, "W0", 0), (st, "FINO0-0", 0),
-                     (None, "@join", 0)]
-            return plan
+            plan += [(st, f"FINO1-{L - 1}", 1), (st, "W0", 0)]
+            if switches.get("DNN_JOIN_EARLY") == "1":
+                # the join's wait packet in front of layer 0's update rather than in front of
+                # the next step's first kernel (the side stream finished long before W0)
+                return plan + [(None, "@join", 0), (st, "FINO0-0", 0)]
+            return plan + [(st, "FINO0-0", 0), (None, "@join", 0)]
         plan += [(st, "W0", 0), (None, "@join", 0)]
         plan.append((st, "FINO", 0) if "FINO" in segs else (st, "FIN", 0))
         if "FINO" not in segs:

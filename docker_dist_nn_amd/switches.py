@@ -68,6 +68,8 @@ SWITCHES: dict[str, tuple[str, str]] = {
                                "priority so side-stream wgrads only fill in"),
     "DNN_SIDE_PRIORITY": ("0", "overlap plans: create the side stream at high priority "
                                "(measured no effect: 0.374 vs 0.373 ms)"),
+    "DNN_JOIN_EARLY": ("0", "overlap plan with the split reduction: the side stream's join "
+                            "before layer 0's update instead of at the end of the step"),
     "DNN_FORK_ELIDE": ("0", "overlap plans: drop a side-stream fork when the main stream "
                             "enqueued nothing since the previous one (~6 us per event "
                             "packet); headline 0.403 vs 0.373 ms: the wgrads then all start "

@@ -25,10 +25,12 @@ def test_overlap_plan_bitwise(dev, monkeypatch, model, rows):
     # 1eK: plan 1 with DNN_FORK_ELIDE=K; 1s: plan 1 with DNN_SPLIT_FINO (layers 1.. reduced and
     # updated on the side stream during W0)
     # 5 / 5s: small wgrads on the side, W1 then W0 on the main stream (unsplit / split FINO)
-    for flag in ("0", "1", "2", "3", "4", "1e1", "1e2", "1s", "5", "5s"):
+    # 1j: plan 1 with the split reduction and the join in front of layer 0's update
+    for flag in ("0", "1", "2", "3", "4", "1e1", "1e2", "1s", "5", "5s", "1j"):
         monkeypatch.setenv("DNN_BW_OVERLAP", flag[0])
         monkeypatch.setenv("DNN_FORK_ELIDE", flag[2:] if flag[1:2] == "e" else "0")
-        monkeypatch.setenv("DNN_SPLIT_FINO", "1" if flag.endswith("s") else "0")
+        monkeypatch.setenv("DNN_SPLIT_FINO", "1" if flag[-1] in "sj" else "0")
+        monkeypatch.setenv("DNN_JOIN_EARLY", "1" if flag == "1j" else "0")
         tr = Trainer(spec, micro_batch=rows, num_micro=1,
                      optim=OptimConfig(lr=0.1, momentum=0.9), device=dev)
         losses = []
