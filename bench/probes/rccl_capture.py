@@ -12,6 +12,15 @@ NCCL_DEBUG=WARN so RCCL says what it rejects. The cases separate the suspects:
   plan_self_torch the same plan captured inside torch.cuda.graph (torch's capture path)
   plan_self_warm  plan_self after one eager run of the same plan (RCCL's lazy per-peer
                   connection set-up then happens outside the capture)
+  plan_fork_signal  a 2-stream StepPlan with only a SIGNAL kernel on the side stream captured
+                  (the plan's own fork / join under capture, no RCCL)
+  plan_group_only   GSTART + GEND with nothing inside, captured (RCCL group calls alone)
+  plan_send_only    the warm plan with the SEND alone inside the group (no matching RECV
+                  issued under capture: only whether the capture call itself crashes)
+
+Round-4 box run: eager_self ok; torch_allreduce "ok" but its graph is EMPTY (a 1-rank
+all-reduce launches nothing), so it proves nothing; plan_self_warm segfaults inside
+StepPlan.run under capture after the eager run succeeded. RCCL plans therefore stay eager.
 
 Output: one JSON line per case {case, rc, ok, stderr_tail}. One GPU.
 Usage: python bench/probes/rccl_capture.py
@@ -25,7 +34,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 # least to most likely to crash: a crash ends the probe (nothing more runs on the GPU after it)
-CASES = ["eager_self", "torch_allreduce", "plan_self_warm", "plan_self_torch", "plan_self"]
+CASES = ["eager_self", "torch_allreduce", "plan_fork_signal", "plan_group_only",
+         "plan_send_only", "plan_self_warm", "plan_self_torch", "plan_self"]
 
 
 def child(case: str) -> None:
@@ -56,8 +66,44 @@ def child(case: str) -> None:
         print(f"replayed ok, t[0]={float(t[0])}", flush=True)
         dist.destroy_process_group()
         return
+    if case == "plan_fork_signal":
+        from docker_dist_nn_amd.parallel.native_step import SIGNAL
+        flag = torch.zeros(4, dtype=torch.int32, device=dev)
+        p = n.StepPlan(2, 1)
+        p.add(kind=SIGNAL, stream=1, a=flag.data_ptr(), delta=0)
+        s = torch.cuda.Stream(dev)
+        g = n.GraphExec()
+        g.begin_capture(s.cuda_stream)
+        try:
+            p.run(s.cuda_stream)
+        finally:
+            g.end_capture()
+        g.replay(s.cuda_stream)
+        torch.cuda.synchronize()
+        print(f"fork/signal plan captured ({g.num_nodes} nodes) and replayed", flush=True)
+        dist.destroy_process_group()
+        return
     n.nccl_load(torch_rccl_path())
     comm = comm_ptr(dist.group.WORLD, dev)
+    if case in ("plan_group_only", "plan_send_only"):
+        buf = torch.zeros(4096, dtype=torch.uint8, device=dev)
+        p = n.StepPlan(2, 1)
+        p.add(kind=GSTART, stream=1)
+        if case == "plan_send_only":
+            p.add(kind=SEND, stream=1, comm=comm, a=buf.data_ptr(), count=buf.numel(),
+                  dtype=NCCL_U8, peer=0)
+        p.add(kind=GEND, stream=1)
+        s = torch.cuda.Stream(dev)
+        g = n.GraphExec()
+        print("capturing", flush=True)
+        g.begin_capture(s.cuda_stream)
+        try:
+            p.run(s.cuda_stream)
+        finally:
+            g.end_capture()
+        print(f"captured {g.num_nodes} nodes (not replayed)", flush=True)
+        dist.destroy_process_group()
+        return
     buf = torch.arange(4096, dtype=torch.int32, device=dev).view(torch.uint8)
     rb = torch.zeros_like(buf)
     p = n.StepPlan(2, 1)
