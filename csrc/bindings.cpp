@@ -20,6 +20,7 @@
 #include "kernels/gemv.hpp"
 #include "kernels/mlp_tail.hpp"
 #include "runtime/blaslt.hpp"
+#include "runtime/chain_host.hpp"
 #include "runtime/graph.hpp"
 #include "runtime/json_weights.hpp"
 #include "runtime/matrix_codec.hpp"
@@ -1113,6 +1114,71 @@ PYBIND11_MODULE(_native, m) {
       py::arg("in_hdr"), py::arg("err"), py::arg("stage"), py::arg("status"), py::arg("ack"),
       py::arg("ack_target"), py::arg("next_flag"), py::arg("seq"), py::arg("prev_ack"),
       py::arg("counter"), py::arg("timeout_s"), py::arg("in_flag") = 0);
+  py::class_<dnn::ChainHost>(m, "ChainHost",
+                             "rank 0's native request path of the device-side chain "
+                             "(runtime/chain_host.hpp)")
+      .def(py::init<int>(), py::arg("slots"))
+      .def(
+          "request",
+          [=](dnn::ChainHost& h, int slot, uintptr_t stream, uintptr_t res_stream,
+              uintptr_t x_dev, uintptr_t x_host, size_t x_bytes, uintptr_t w, long ldw,
+              uintptr_t bias, int act, int rows, int N, int K, uintptr_t dst, long dst_ld,
+              uintptr_t dst_hdr, uintptr_t err, uintptr_t ack, uint32_t ack_target,
+              uintptr_t next_flag, uint32_t seq, uintptr_t counter, double hop_timeout_s,
+              uintptr_t res_flag, uintptr_t res_err, uintptr_t res_dev, uintptr_t res_host,
+              size_t res_bytes, uintptr_t last_ack, double wait_timeout_s) {
+            dnn::ChainRequest r{};
+            r.stream = S(stream);
+            r.res_stream = S(res_stream);
+            r.x_dev = ptr(x_dev);
+            r.x_host = ptr(x_host);
+            r.x_bytes = x_bytes;
+            dnn::ChainGemvSend& p = r.send;
+            p.x = static_cast<const uint16_t*>(ptr(x_dev));
+            p.ldx = K;
+            p.w = static_cast<const uint16_t*>(ptr(w));
+            p.ldw = ldw;
+            p.bias = static_cast<const float*>(ptr(bias));
+            p.act = act;
+            p.rows = rows;
+            p.N = N;
+            p.K = K;
+            p.dst = ptr(dst);
+            p.dst_ld = dst_ld;
+            p.dst_hdr = static_cast<uint32_t*>(ptr(dst_hdr));
+            p.err = static_cast<uint32_t*>(ptr(err));
+            p.ack = static_cast<const uint32_t*>(ptr(ack));
+            p.ack_target = ack_target;
+            p.next_flag = static_cast<uint32_t*>(ptr(next_flag));
+            p.seq = seq;
+            p.counter = static_cast<uint32_t*>(ptr(counter));
+            p.timeout_ticks = dnn::chain_ticks(hop_timeout_s);
+            r.res_flag = static_cast<const uint32_t*>(ptr(res_flag));
+            r.res_err = static_cast<uint32_t*>(ptr(res_err));
+            r.res_dev = ptr(res_dev);
+            r.res_host = ptr(res_host);
+            r.res_bytes = res_bytes;
+            r.last_ack = static_cast<uint32_t*>(ptr(last_ack));
+            r.wait_timeout_s = wait_timeout_s;
+            chk(h.enqueue(r, slot), "ChainHost.request");
+          },
+          py::arg("slot"), py::arg("stream"), py::arg("res_stream"), py::arg("x_dev"),
+          py::arg("x_host"), py::arg("x_bytes"), py::arg("w"), py::arg("ldw"), py::arg("bias"),
+          py::arg("act"), py::arg("rows"), py::arg("N"), py::arg("K"), py::arg("dst"),
+          py::arg("dst_ld"), py::arg("dst_hdr"), py::arg("err"), py::arg("ack"),
+          py::arg("ack_target"), py::arg("next_flag"), py::arg("seq"), py::arg("counter"),
+          py::arg("hop_timeout_s"), py::arg("res_flag"), py::arg("res_err"), py::arg("res_dev"),
+          py::arg("res_host"), py::arg("res_bytes"), py::arg("last_ack"),
+          py::arg("wait_timeout_s"))
+      .def(
+          "wait",
+          [](dnn::ChainHost& h, int slot, double timeout_s) {
+            py::gil_scoped_release nogil;
+            const int rc = h.wait(slot, timeout_s);
+            if (rc < 0) throw std::runtime_error("ChainHost.wait: hipEventQuery failed");
+            return rc;
+          },
+          py::arg("slot"), py::arg("timeout_s"));
   m.def(
       "chain_signal",
       [=](uintptr_t s, uintptr_t flag, uint32_t value) {

@@ -244,6 +244,7 @@ class FastChain:
         self.one_launch = self.fused and switches.get("DNN_CHAIN_ONE_LAUNCH") == "1"
         self.trace = switches.get("DNN_CHAIN_TRACE") == "1"
         self.lat: collections.deque = collections.deque(maxlen=100000)  # rank 0: seconds
+        self.host = None  # rank 0: runtime ChainHost (the native request path)
         self.seq = 0
         self.lock = threading.Lock()
         self.processed = 0
@@ -256,6 +257,10 @@ class FastChain:
             self.x0 = torch.zeros(self.max_rows, self.in_w, dtype=torch.bfloat16,
                                   device=self.dev)
             self.events = [torch.cuda.Event() for _ in range(NSLOT)]
+            # one-layer stage 0 on the fused path: the whole request is one native call
+            # (runtime/chain_host.cpp), its completion a GIL-free spin
+            self.host = (self.n.ChainHost(NSLOT) if self.fused and len(st.layers) == 1 and
+                         switches.get("DNN_CHAIN_NATIVE") == "1" else None)
         self.ok = True
         self.why = (f"device-side chain ({NSLOT} slots per hop"
                     + (", last layer fused with the send" if self.fused else "") + ")")
@@ -337,6 +342,19 @@ class FastChain:
             hin = self.h_in[slot]
             hin[:rows, :x.shape[1]].copy_(torch.from_numpy(np.ascontiguousarray(x, np.float32)))
             self.ann.announce(seq, rows)
+            if self.host is not None:
+                self._native_request(seq, slot, rows)
+        if self.host is not None:
+            limit = self.cr.hop_timeout * self.world
+            if timeout is not None:
+                limit = min(limit, max(0.0, timeout))
+            if self.host.wait(slot, limit):
+                k = self.cr.blame(seq) if self.cr.store is not None else self.world - 1
+                raise StageFailure(self.cr.names[k], grpc.StatusCode.DEADLINE_EXCEEDED,
+                                   f"Deadline Exceeded (request {seq} not answered within "
+                                   f"{limit:.1f} s)")
+            return self._result(seq, slot, rows, t_in)
+        with self.lock:
             if self.trace:
                 self._trace(seq, f"announced rows={rows}")
             with torch.cuda.stream(self.stream):
@@ -378,6 +396,34 @@ class FastChain:
             spins += 1
             if spins > 2000:
                 time.sleep(20e-6)
+        return self._result(seq, slot, rows, t_in)
+
+    def _native_request(self, seq: int, slot: int, rows: int) -> None:
+        """Rank 0, one-layer stage, fused path: H2D + layer-and-send + result wait + D2H +
+        ack + event as one native call (runtime/chain_host.cpp)."""
+        st = self.cr.stage
+        w, b = st.w[0], st.b[0]
+        dst, dld, dhdr, dflag = self._dst(slot)
+        base = self.res[slot]
+        f32 = self.world == 1  # (rank 0 feeds rank 1's bf16 slot)
+        self.host.request(
+            slot, self.stream.cuda_stream, self.res_stream.cuda_stream, self.x0.data_ptr(),
+            self.h_in[slot].data_ptr(), rows * self.in_w * 2, w.data_ptr(), w.stride(0),
+            b.data_ptr(), ops.kernels._act(st.acts[0]), rows, w.shape[0], self.in_w, dst,
+            dld // (4 if f32 else 2), dhdr, _ptr(self.flags, F_ERR), _ptr(self.flags, F_ACK),
+            (seq - NSLOT) & 0xFFFFFFFF, dflag, seq, self.counter.data_ptr(),
+            self.cr.hop_timeout, _ptr(self.flags, F_RES + slot), _ptr(base, 2),
+            base.data_ptr(), self.h_out[slot].data_ptr(),
+            HDR + rows * self.res_w * 4, self.prev_flags_of_last() + 4 * F_ACK,
+            self.cr.hop_timeout * self.world)
+
+    def _result(self, seq: int, slot: int, rows: int, t_in: float) -> np.ndarray:
+        """Decode the result slot's host copy (header, then fp32 rows) of request ``seq``."""
+        import grpc
+
+        from .ingress import StageFailure
+
+        ho = self.h_out[slot]
         hdr = ho[:4].tolist()
         if self.trace:
             self._trace(seq, f"result hdr {hdr}")

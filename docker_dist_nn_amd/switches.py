@@ -110,6 +110,9 @@ SWITCHES: dict[str, tuple[str, str]] = {
     "DNN_CHAIN_FUSED": ("1", "device-side chain: a stage's last (non-softmax) layer runs fused "
                              "with the hop's send (chain_gemv_send: rows straight into the "
                              "consumer's slot); 0 = gemv + chain_send"),
+    "DNN_CHAIN_NATIVE": ("1", "device-side chain: rank 0 with a one-layer stage runs each request "
+                              "as one native call (runtime/chain_host.cpp: H2D, layer + send, "
+                              "result wait, D2H, ack, GIL-free completion spin)"),
     "DNN_CHAIN_ONE_LAUNCH": ("0", "device-side chain, one-layer stages > 0: the receive folded into "
                                   "chain_gemv_send too (one kernel per hop; every workgroup "
                                   "waits on the input flag). Opt-in: slower with several waiting "
