@@ -560,7 +560,7 @@ class Stage:
         L = len(self.geoms)
         if not self.tail or switches.get("DNN_FWD_TAIL") != "1":
             return False
-        g1, g2, g3 = self.geoms[L - 3], self.geoms[L - 2], self.geoms[L - 1]
+        g1, g2 = self.geoms[L - 3], self.geoms[L - 2]
         return (g1.spec.activation == "relu" and g2.spec.activation == "relu" and
                 self.relu_mask[L - 3] is None and (L - 3) not in self.actT and
                 ops.fwd_tail_supported(self.mb, g1.np_, g2.kp, g2.np_))

@@ -446,7 +446,6 @@ class FragMask:
         wm_n, wn_n = FRAG_WAVES[self.tiles]
         fm, sn = bm // wm_n // 16, bn // wn_n
         fn = sn // 16
-        nb = fm * fn // 2
         tm_n, tn_n = -(-self.m // bm), -(-self.n // bn)
         dev = self.buf.device
         raw = self.buf[:tm_n * tn_n * bm * bn // 8].view(tm_n, tn_n, wm_n, wn_n, 64, fn // 2, fm)
@@ -459,7 +458,6 @@ class FragMask:
         bit = (raw.unsqueeze(-1).to(torch.int32) >> ar(8).to(torch.int32)) & 1
         out = torch.zeros(tm_n * bm, tn_n * bn, dtype=torch.bool, device=dev)
         out[row.reshape(-1), col.reshape(-1)] = bit.reshape(-1).bool()
-        assert nb == fm * fn // 2
         return out[:self.m, :self.n]
 
 
