@@ -242,10 +242,19 @@ def measure(a, spec, n, world, dev, text):
     for _ in range(a.warmup):
         one_step()
 
+    # DNN_BENCH_STEP_EVENTS=1 (diagnosis): a HIP event before every timed step and after the
+    # last, so the JSON carries the per-step GPU times of the timed window
+    evs = [] if switches.get("DNN_BENCH_STEP_EVENTS") == "1" else None
     barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
+        if evs is not None:
+            evs.append(torch.cuda.Event(enable_timing=True))
+            evs[-1].record()
         one_step()
+    if evs is not None:
+        evs.append(torch.cuda.Event(enable_timing=True))
+        evs[-1].record()
     host_s = time.perf_counter() - t0  # enqueue time of the K steps (no sync inside)
     tr.flush()  # the last step's deferred DP update belongs to the timed region
     barrier()
@@ -274,6 +283,8 @@ def measure(a, spec, n, world, dev, text):
         "boundary": tr.boundary, "dp_reduce": tr.dp_reduce if plan.dp > 1 else None,
         "hip_graph": use_graph, "graph_copies": a.graph_copies if use_graph else 0,
         "graph_trial": graph_trial, "host_ms_per_step": round(host_s / a.steps * 1e3, 4),
+        "step_ms": ([round(e0.elapsed_time(e1), 4) for e0, e1 in zip(evs, evs[1:])]
+                    if evs else None),
         "loss": loss, "planner_predicted": round(plan.samples_per_s, 1),
     }
     del tr, data
@@ -427,6 +438,7 @@ def main(argv=None):
         "last_loss": None if m["loss"] is None else round(m["loss"], 5),
         "planner_predicted": m["planner_predicted"],
         "host_ms_per_step": m.get("host_ms_per_step"),
+        **({"step_ms": m["step_ms"]} if m.get("step_ms") else {}),
         "graph_trial": m.get("graph_trial"),
         "dp_only": dp_only,
         "native_fallback": m["native_fallback"],  # why the Python executor ran, if it did

@@ -41,6 +41,8 @@ SWITCHES: dict[str, tuple[str, str]] = {
                                   "per micro-batch hop (0 = the schedule on one stream)"),
     "DNN_NATIVE_DIST": ("1", "multi-rank step as one StepPlan call (parallel/native_step.py)"),
     "DNN_WGRAD_STREAMS": ("1", "concurrent wgrad streams in native single-process plans"),
+    "DNN_BENCH_STEP_EVENTS": ("0", "bench.py: 1 = a HIP event around every timed step; the JSON "
+                                   "gets the per-step GPU times (diagnosis)"),
     "DNN_BW_OVERLAP": ("1", "wgrad_i on a side stream concurrent with dgrad_i (1 stage, one "
                             "micro-batch): mlp8 3.43 -> 3.31 ms; 2 = only the small wgrads "
                             "on the side (headline 0.377 vs 0.372 ms, rejected); 3 = those under "
