@@ -22,11 +22,15 @@ def rnd(*shape, scale=1.0):
     return (torch.randn(*shape, device=dev) * scale).to(torch.bfloat16)
 
 
+EPI = 0  # --epi-probe
+
+
 def fwd(M, K, N):
     x, w, b = rnd(M, K, scale=0.1), rnd(N, K, scale=0.05), torch.randn(N, device=dev)
     y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
     return lambda tile, st, tl: ops.gemm(x, w, y, layout_a=KMAJ, layout_b=KMAJ, M=M, N=N, K=K,
-                                         bias=b, act="relu", tiles=tile, stages=st, timeline=tl)
+                                         bias=b, act="relu", tiles=tile, stages=st, timeline=tl,
+                                         epi_probe=EPI)
 
 
 def fwd_mask(M, K, N):
@@ -80,7 +84,7 @@ def dgrad(M, K, N):
     y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
     return lambda tile, st, tl: ops.gemm(dz, wt, y, layout_a=KMAJ, layout_b=KMAJ, M=M, N=N,
                                          K=K, aux=h, act="relu", tiles=tile, stages=st,
-                                         timeline=tl)
+                                         timeline=tl, epi_probe=EPI)
 
 
 CASES = {"f0": lambda: fwd(65536, 832, 512), "f1": lambda: fwd(65536, 512, 256),
@@ -100,10 +104,14 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--cases", default="f0,f1,w0,m8f")
 ap.add_argument("--variants", default="256x256:2,256x256:6")
 ap.add_argument("--wvariants", default="128x128:2,128x128:6")
+ap.add_argument("--epi-probe", type=int, default=0,
+                help="GemmParams::epi_probe bits for the register-direct epilogue (1: no stores, "
+                     "2: no bias loads); outputs are wrong, only the phases are timed")
 ap.add_argument("--cold", action="store_true",
                 help="evict the Infinity Cache (write 1 GiB) before the timed run: operands "
                      "come from HBM, as inside the training step")
 a = ap.parse_args()
+EPI = a.epi_probe
 flush = torch.empty(1 << 29, dtype=torch.bfloat16, device=dev) if a.cold else None
 tl = torch.zeros(4 * 65536, dtype=torch.int64, device=dev)
 for name in a.cases.split(","):
@@ -125,7 +133,7 @@ for name in a.cases.split(","):
         start, pro, loop, epi = (d[:, 0] - t0), (d[:, 1] - d[:, 0]), (d[:, 2] - d[:, 1]), \
             (d[:, 3] - d[:, 2])
         print(json.dumps({
-            "case": name, "cold": bool(a.cold), "tile": list(tile), "stages": int(st), "wgs": int(d.shape[0]),
+            "case": name, "cold": bool(a.cold), "epi_probe": EPI, "tile": list(tile), "stages": int(st), "wgs": int(d.shape[0]),
             "span_us": round(float(d[:, 3].max() - t0), 2),
             "start_us_p10_p50_p90": [round(float(q(start.tolist(), f)), 2) for f in (.1, .5, .9)],
             "prologue_us_med": round(float(q(pro.tolist(), .5)), 2),

@@ -79,9 +79,10 @@ PYBIND11_MODULE(_native, m) {
          uintptr_t loss_part, uintptr_t correct, int k_total, int stages, int group_m,
          int persist, uintptr_t mask_out, uintptr_t mask_in, long ld_mask, uintptr_t ct,
          long ld_ct, uintptr_t upd_master, uintptr_t upd_mom, uintptr_t upd_shadow,
-         uintptr_t upd_lr, float upd_mu, float upd_wd, uintptr_t timeline) {
+         uintptr_t upd_lr, float upd_mu, float upd_wd, uintptr_t timeline, int epi_probe) {
         GemmParams p{};
         p.timeline = P<unsigned long long>(timeline);
+        p.epi_probe = epi_probe;
         p.upd_master = P<float>(upd_master);
         p.upd_mom = P<float>(upd_mom);
         p.upd_shadow = P<uint16_t>(upd_shadow);
@@ -154,7 +155,8 @@ PYBIND11_MODULE(_native, m) {
       py::arg("mask_out") = 0, py::arg("mask_in") = 0, py::arg("ld_mask") = 0,
       py::arg("ct") = 0, py::arg("ld_ct") = 0, py::arg("upd_master") = 0,
       py::arg("upd_mom") = 0, py::arg("upd_shadow") = 0, py::arg("upd_lr") = 0,
-      py::arg("upd_mu") = 0.f, py::arg("upd_wd") = 0.f, py::arg("timeline") = 0);
+      py::arg("upd_mu") = 0.f, py::arg("upd_wd") = 0.f, py::arg("timeline") = 0,
+      py::arg("epi_probe") = 0);
   m.def("gemm_default_stages", &dnn::default_stages);
 
   m.def("gemv_max_rows", []() { return dnn::GEMV_MAX_ROWS; });

@@ -73,6 +73,9 @@ struct GemmParams {
   // timeline[4 * blockIdx.x + i] = s_memrealtime (100 MHz) at kernel entry (i = 0), after the
   // ring prologue (1), after the main loop (2) and at the end of the epilogue (3).
   unsigned long long* timeline;
+  // Diagnosis only (bench/probes/gemm_timeline.py --epi-probe; results are WRONG when set):
+  // bit 0 = the register-direct epilogue stores nothing, bit 1 = it loads no bias (zeros).
+  int epi_probe;
 };
 
 // Returns 0 on success, a negative code when a shape/alignment precondition fails

@@ -1053,7 +1053,7 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&a
               cs[2 * q + 1] += __uint_as_float(w[q] & 0xffff0000u);
             }
           }
-          if (row < p.M && scol < p.N)
+          if (row < p.M && scol < p.N && !(p.epi_probe & 1))
             *(uint4*)((u16*)p.C + (long)row * p.ldc + scol) = make_uint4(w[0], w[1], w[2], w[3]);
         }
         if (want_sum) {  // the 8 columns this lane stores, summed over the wave's rows
@@ -1086,7 +1086,7 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&a
             yv[j][i] = *(const uint2*)(ya + min(row0 + 16 * i, p.M - 1) * p.ld_aux);
         } else {
           bv[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-          if (p.bias && c < p.N) bv[j] = *(const f32x4_t*)(p.bias + c);
+          if (p.bias && c < p.N && !(p.epi_probe & 2)) bv[j] = *(const f32x4_t*)(p.bias + c);
         }
       }
 #pragma unroll
@@ -1149,7 +1149,7 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&a
           const auto s0 = __builtin_amdgcn_permlane16_swap(x0, z0, false, false);
           const auto s1 = __builtin_amdgcn_permlane16_swap(x1, z1, false, false);
           const int scol = scol0 + 16 * j;
-          if (row < p.M && scol < p.N) {
+          if (row < p.M && scol < p.N && !(p.epi_probe & 1)) {
             *(uint4*)((u16*)p.C + (long)row * p.ldc + scol) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
             if (!AUX && p.mask_out) {  // forward ReLU mask: bit e = stored bf16 of column e > 0
               const unsigned w[4] = {s0[0], s1[0], s0[1], s1[1]};

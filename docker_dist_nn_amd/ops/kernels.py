@@ -252,8 +252,9 @@ def wgrad_config(M: int, N: int, K_total: int, max_splits: int = 48) -> tuple[in
 def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=None, aux=None,
          act=0, accumulate: bool = False, splits: int = 1, tiles: tuple[int, int] | None = None,
          colsum=None, k_total: int = 0, stages: int = 0, group_m: int = 0, persist: int = 0,
-         mask_out=None, mask_in=None, ct=None, upd=None, timeline=None):
+         mask_out=None, mask_in=None, ct=None, upd=None, timeline=None, epi_probe: int = 0):
     """C (+)= epilogue(A.B). See csrc/kernels/gemm.hpp for the layout/epilogue contract.
+    ``epi_probe`` (diagnosis only, results WRONG): GemmParams::epi_probe.
 
     ``timeline`` (int64 GPU tensor, >= 4 per workgroup; one-tile kernels): per-workgroup phase
     timestamps for bench/probes/gemm_timeline.py (GemmParams::timeline).
@@ -371,7 +372,7 @@ def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=
                            upd_shadow=_p(upd.get("shadow")), upd_lr=_p(upd["lr_dev"]),
                            upd_mu=float(upd.get("momentum", 0.0)),
                            upd_wd=float(upd.get("weight_decay", 0.0)))),
-                       timeline=_p(timeline))
+                       timeline=_p(timeline), epi_probe=int(epi_probe))
     return c
 
 
