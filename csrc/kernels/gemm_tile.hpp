@@ -1071,8 +1071,14 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&a
         }
       }
       };
-      auto body = [&](auto has_aux) {
+      // `act_c`: the forward activation as a compile-time constant (ACT_RELU / ACT_LINEAR), or
+      // -1 = read p.act per element. A runtime activation costs two scalar compare + branch
+      // pairs per ELEMENT (128 per lane of a 256x256 tile): the ISA of the bias + ReLU
+      // epilogue was mostly those branches (profiles/r4_timeline: 5.9 of its 6.2 us per round
+      // remained with no stores and no bias loads)
+      auto body = [&](auto has_aux, auto act_c) {
       constexpr bool AUX = decltype(has_aux)::value;
+      constexpr int ACTC = decltype(act_c)::value;
       [[maybe_unused]] unsigned fw[NB >= 4 ? NB / 4 : 1] = {};  // fragment-order mask_out
       [[maybe_unused]] f32x4_t bv[AUX ? 1 : FN];
       [[maybe_unused]] uint2 yv[AUX ? FN : 1][FM];
@@ -1127,8 +1133,8 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&a
           } else {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              v0[e] = act_fwd(v0[e], p.act);
-              v1[e] = act_fwd(v1[e], p.act);
+              v0[e] = act_fwd(v0[e], ACTC >= 0 ? ACTC : p.act);
+              v1[e] = act_fwd(v1[e], ACTC >= 0 ? ACTC : p.act);
             }
           }
           const unsigned x0 = pack_bf16x2(v0[0], v0[1]), x1 = pack_bf16x2(v0[2], v0[3]);
@@ -1192,8 +1198,11 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&a
       };
       if (p.aux && p.act == ACT_RELU) relu_body(std::false_type{});
       else if (p.mask_in) relu_body(std::true_type{});
-      else if (p.aux) body(std::true_type{});
-      else body(std::false_type{});
+      else if (p.aux) body(std::true_type{}, std::integral_constant<int, -1>{});
+      else if (p.act == ACT_RELU) body(std::false_type{}, std::integral_constant<int, ACT_RELU>{});
+      else if (p.act == ACT_LINEAR)
+        body(std::false_type{}, std::integral_constant<int, ACT_LINEAR>{});
+      else body(std::false_type{}, std::integral_constant<int, -1>{});
       if (want_sum) {
         lds_barrier();
         if ((int)threadIdx.x < BN) {
