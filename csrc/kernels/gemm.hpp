@@ -74,7 +74,8 @@ struct GemmParams {
   // ring prologue (1), after the main loop (2) and at the end of the epilogue (3).
   unsigned long long* timeline;
   // Diagnosis only (bench/probes/gemm_timeline.py --epi-probe; results are WRONG when set):
-  // bit 0 = the register-direct epilogue stores nothing, bit 1 = it loads no bias (zeros).
+  // bit 0 = the register-direct epilogue stores nothing, bit 1 = it loads no bias (zeros);
+  // bit 2 (results correct) = the activation read per element, as before round 4 (A/B).
   int epi_probe;
 };
 

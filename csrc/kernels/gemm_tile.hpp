@@ -1199,8 +1199,9 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&a
       if (p.aux && p.act == ACT_RELU) relu_body(std::false_type{});
       else if (p.mask_in) relu_body(std::true_type{});
       else if (p.aux) body(std::true_type{}, std::integral_constant<int, -1>{});
-      else if (p.act == ACT_RELU) body(std::false_type{}, std::integral_constant<int, ACT_RELU>{});
-      else if (p.act == ACT_LINEAR)
+      else if (p.act == ACT_RELU && !(p.epi_probe & 4))
+        body(std::false_type{}, std::integral_constant<int, ACT_RELU>{});
+      else if (p.act == ACT_LINEAR && !(p.epi_probe & 4))
         body(std::false_type{}, std::integral_constant<int, ACT_LINEAR>{});
       else body(std::false_type{}, std::integral_constant<int, -1>{});
       if (want_sum) {

@@ -46,6 +46,8 @@ def _parse_stages(spec: str) -> dict:
 # LDS pipeline depth (2..4) per GEMM kind; see mma_tile in csrc/kernels/gemm.hip. 8 selects the
 # ping-pong half-tile-streamed form of the 256x256 tile (csrc/kernels/gemm_pp.hip).
 STAGES = _parse_stages(switches.get("DNN_GEMM_STAGES"))
+# A/B of the activation-specialised register-direct epilogue (GemmParams::epi_probe bit 2)
+_EPI_GENERIC = 4 if switches.get("DNN_GEMM_EPI_GENERIC") == "1" else 0
 
 
 def _parse_persist(spec: str) -> dict:
@@ -372,7 +374,7 @@ def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=
                            upd_shadow=_p(upd.get("shadow")), upd_lr=_p(upd["lr_dev"]),
                            upd_mu=float(upd.get("momentum", 0.0)),
                            upd_wd=float(upd.get("weight_decay", 0.0)))),
-                       timeline=_p(timeline), epi_probe=int(epi_probe))
+                       timeline=_p(timeline), epi_probe=int(epi_probe) | _EPI_GENERIC)
     return c
 
 

@@ -17,6 +17,8 @@ SWITCHES: dict[str, tuple[str, str]] = {
     "DNN_TUNED_TABLE": ("", "path of another tuned table (A/B of two tunings)"),
     "DNN_BLAS": ("", "hipBLASLt comparison path: '' never (own kernels), 1 = every product "
                      "it supports, or per kind 'fwd=1,dgrad=0,wgrad=1' (bench only)"),
+    "DNN_GEMM_EPI_GENERIC": ("0", "1 = the register-direct GEMM epilogue reads the activation per "
+                                  "element (the pre-round-4 form; A/B only)"),
     "DNN_GEMM_STAGES": ("", "LDS pipeline depth per GEMM kind ('3' or 'fwd=3,dgrad=2'); 8 = "
                             "ping-pong 256x256 form"),
     "DNN_GEMM_PERSIST": ("", "persistent-workgroup GEMM form per kind ('1', 'fwd=1,wgrad=0')"),
