@@ -794,9 +794,14 @@ __device__ __forceinline__ void epilogue_staged(const GemmParams& p,
           continue;
         }
         float* c = (float*)p.C + (long)split * p.c_split_stride + gm * p.ldc + gn;
-        if (!p.accumulate && p.act != ACT_LINEAR) {
+        if (!p.accumulate && p.act != ACT_LINEAR) {  // (one uniform test per row, not per element)
+          if (p.act == ACT_RELU) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = act_fwd(v[e], p.act);
+            for (int e = 0; e < 8; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = act_fwd(v[e], p.act);
+          }
         }
         f32x4_t o0 = {v[0], v[1], v[2], v[3]}, o1 = {v[4], v[5], v[6], v[7]};
         if (p.accumulate) {
@@ -808,13 +813,21 @@ __device__ __forceinline__ void epilogue_staged(const GemmParams& p,
       } else {
         if (xent) {
           // dz already computed in LDS
-        } else if (p.aux) {
+        } else if (p.aux) {  // activation tests hoisted out of the element loops (uniform)
+          if (p.act == ACT_RELU) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = act_bwd(v[e], bf2f((u16)yv[it][e]), p.act);
+            for (int e = 0; e < 8; ++e) v[e] = bf2f((u16)yv[it][e]) > 0.f ? v[e] : 0.f;
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = act_bwd(v[e], bf2f((u16)yv[it][e]), p.act);
+          }
         } else if (p.mask_in) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = (mk[it] >> e) & 1u ? v[e] : 0.f;
-        } else {
+        } else if (p.act == ACT_RELU) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+        } else if (p.act != ACT_LINEAR) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = act_fwd(v[e], p.act);
         }
@@ -949,7 +962,8 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&a
           if (p.bias) v[j] += *(const f32x4_t*)(p.bias + col0 + 16 * j);
           if (!p.accumulate && p.act != ACT_LINEAR) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[j][e] = act_fwd(v[j][e], p.act);
+            for (int e = 0; e < 4; ++e)
+              v[j][e] = p.act == ACT_RELU ? (v[j][e] > 0.f ? v[j][e] : 0.f) : act_fwd(v[j][e], p.act);
           }
           *(f32x4_t*)(crow + 16 * j) = v[j];
         }
