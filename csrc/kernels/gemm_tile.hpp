@@ -994,8 +994,12 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&a
       // per row and 8-column chunk -- exactly the chunk a lane stores) instead of the activation
       constexpr int NB = FM * FN / 2;  // fragment-order mask bytes per lane
       const bool frag = p.ld_mask < 0;  // uniform
-      auto relu_body = [&](auto from_mask) {
+      // FULL: the whole tile is inside C (uniform, tested once below), so the per-row /
+      // per-column bounds tests -- divergent exec-mask regions around every store and
+      // column-sum update -- compile away
+      auto relu_body = [&](auto from_mask, auto full_t) {
       constexpr bool MASK = decltype(from_mask)::value;
+      constexpr bool FULL = decltype(full_t)::value;
       [[maybe_unused]] uint4 yv[MASK ? 1 : FN / 2][FM];
       [[maybe_unused]] unsigned mv[MASK ? FN / 2 : 1][FM];
       [[maybe_unused]] unsigned fw[MASK && NB >= 4 ? NB / 4 : 1];
@@ -1060,14 +1064,14 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&a
               w[q] &= keep;
             }
           }
-          if (want_sum && row < p.M) {
+          if (want_sum && (FULL || row < p.M)) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
               cs[2 * q] += __uint_as_float(w[q] << 16);
               cs[2 * q + 1] += __uint_as_float(w[q] & 0xffff0000u);
             }
           }
-          if (row < p.M && scol < p.N && !(p.epi_probe & 1))
+          if ((FULL || (row < p.M && scol < p.N)) && !(p.epi_probe & 1))
             *(uint4*)((u16*)p.C + (long)row * p.ldc + scol) = make_uint4(w[0], w[1], w[2], w[3]);
         }
         if (want_sum) {  // the 8 columns this lane stores, summed over the wave's rows
@@ -1090,9 +1094,10 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&a
       // pairs per ELEMENT (128 per lane of a 256x256 tile): the ISA of the bias + ReLU
       // epilogue was mostly those branches (profiles/r4_timeline: 5.9 of its 6.2 us per round
       // remained with no stores and no bias loads)
-      auto body = [&](auto has_aux, auto act_c) {
+      auto body = [&](auto has_aux, auto act_c, auto full_t) {
       constexpr bool AUX = decltype(has_aux)::value;
       constexpr int ACTC = decltype(act_c)::value;
+      constexpr bool FULL = decltype(full_t)::value;
       [[maybe_unused]] unsigned fw[NB >= 4 ? NB / 4 : 1] = {};  // fragment-order mask_out
       [[maybe_unused]] f32x4_t bv[AUX ? 1 : FN];
       [[maybe_unused]] uint2 yv[AUX ? FN : 1][FM];
@@ -1106,7 +1111,8 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&a
             yv[j][i] = *(const uint2*)(ya + min(row0 + 16 * i, p.M - 1) * p.ld_aux);
         } else {
           bv[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-          if (p.bias && c < p.N && !(p.epi_probe & 2)) bv[j] = *(const f32x4_t*)(p.bias + c);
+          if (p.bias && (FULL || c < p.N) && !(p.epi_probe & 2))
+            bv[j] = *(const f32x4_t*)(p.bias + c);
         }
       }
 #pragma unroll
@@ -1153,7 +1159,7 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&a
           }
           const unsigned x0 = pack_bf16x2(v0[0], v0[1]), x1 = pack_bf16x2(v0[2], v0[3]);
           const unsigned z0 = pack_bf16x2(v1[0], v1[1]), z1 = pack_bf16x2(v1[2], v1[3]);
-          if (want_sum && row < p.M) {  // sums of the STORED (bf16-rounded) values
+          if (want_sum && (FULL || row < p.M)) {  // sums of the STORED (bf16-rounded) values
             cs0[0] += __uint_as_float(x0 << 16);
             cs0[1] += __uint_as_float(x0 & 0xffff0000u);
             cs0[2] += __uint_as_float(x1 << 16);
@@ -1169,7 +1175,7 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&a
           const auto s0 = __builtin_amdgcn_permlane16_swap(x0, z0, false, false);
           const auto s1 = __builtin_amdgcn_permlane16_swap(x1, z1, false, false);
           const int scol = scol0 + 16 * j;
-          if (row < p.M && scol < p.N && !(p.epi_probe & 1)) {
+          if ((FULL || (row < p.M && scol < p.N)) && !(p.epi_probe & 1)) {
             *(uint4*)((u16*)p.C + (long)row * p.ldc + scol) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
             if (!AUX && p.mask_out) {  // forward ReLU mask: bit e = stored bf16 of column e > 0
               const unsigned w[4] = {s0[0], s1[0], s0[1], s1[1]};
@@ -1210,14 +1216,20 @@ __device__ __forceinline__ void epilogue_direct(const GemmParams& p, f32x4_t (&a
                                                                                wn, lane), fw);
       }
       };
-      if (p.aux && p.act == ACT_RELU) relu_body(std::false_type{});
-      else if (p.mask_in) relu_body(std::true_type{});
-      else if (p.aux) body(std::true_type{}, std::integral_constant<int, -1>{});
-      else if (p.act == ACT_RELU && !(p.epi_probe & 4))
-        body(std::false_type{}, std::integral_constant<int, ACT_RELU>{});
-      else if (p.act == ACT_LINEAR && !(p.epi_probe & 4))
-        body(std::false_type{}, std::integral_constant<int, ACT_LINEAR>{});
-      else body(std::false_type{}, std::integral_constant<int, -1>{});
+      const bool full = (tm + 1) * (WM * 16 * FM) <= p.M && (tn + 1) * BN <= p.N &&
+                        !(p.epi_probe & 4);  // uniform
+      auto dispatch = [&](auto full_t) {
+        if (p.aux && p.act == ACT_RELU) relu_body(std::false_type{}, full_t);
+        else if (p.mask_in) relu_body(std::true_type{}, full_t);
+        else if (p.aux) body(std::true_type{}, std::integral_constant<int, -1>{}, full_t);
+        else if (p.act == ACT_RELU && !(p.epi_probe & 4))
+          body(std::false_type{}, std::integral_constant<int, ACT_RELU>{}, full_t);
+        else if (p.act == ACT_LINEAR && !(p.epi_probe & 4))
+          body(std::false_type{}, std::integral_constant<int, ACT_LINEAR>{}, full_t);
+        else body(std::false_type{}, std::integral_constant<int, -1>{}, full_t);
+      };
+      if (full) dispatch(std::true_type{});
+      else dispatch(std::false_type{});
       if (want_sum) {
         lds_barrier();
         if ((int)threadIdx.x < BN) {
