@@ -1,5 +1,6 @@
-# Runtime image of the framework (replaces the reference's per-stage python:3.11-slim image,
-# SURVEY R15): one image for every rank; the launcher starts one process per GPU inside it.
+# Runtime image of the framework (replaces the reference's per-stage python:3.9-slim image,
+# /root/reference/src/dockerfile:1, SURVEY R15): one image for every rank; the launcher starts
+# one process per GPU inside it.
 #   docker build -t dnn-amd .
 #   docker run --device=/dev/kfd --device=/dev/dri --group-add video --ipc=host \
 #       dnn-amd python bench.py --gpus 1
@@ -17,5 +18,6 @@ WORKDIR /opt/dnn
 COPY . /opt/dnn
 RUN python -m pip install --no-deps --no-build-isolation -e . && \
     python -m docker_dist_nn_amd._build
-EXPOSE 5000-5015
+# stage ports keep the reference's scheme 5100 + 100*i + 1 (partition.py): 5101, 5201, ... 5801
+EXPOSE 5101 5201 5301 5401 5501 5601 5701 5801
 CMD ["python", "bench.py"]

@@ -337,41 +337,76 @@ DP_ONLY_KEYS = ("parallelism", "global_batch", "transport", "native_step", "dp_r
 def supervise(a, argv) -> int:
     """WORLD_SIZE > 1: this process is the rank's supervisor (ladder.py). It never touches the
     GPU; every attempt runs ``bench.py`` again as a fresh child per rank (new rendezvous port),
-    climbing the fallback ladder until one attempt succeeds on every rank. Then the
-    data-parallel comparison runs the same way. Rank 0 prints the one JSON line, with every
-    attempt (rung, exit codes, last heartbeat of a stalled child) listed."""
+    climbing the fallback ladder until one attempt succeeds on every rank. Then, if the time
+    left allows, the data-parallel comparison runs the same way. Rank 0 prints the one JSON
+    line, with every attempt (rung, exit codes, last heartbeat of a stalled child) listed --
+    also when the job is ended by SIGTERM (ladder.OneLine), so a bench the driver stops at its
+    deadline still reports.
+
+    Time: a failing rung costs at most a child's start-up + the first-step guard
+    (DNN_FIRST_STEP_TIMEOUT, 30 s) or a heartbeat stall (DNN_LADDER_STALL, 60 s); past
+    DNN_LADDER_BUDGET (360 s) only the last rung is tried, and nothing runs past
+    DNN_LADDER_DEADLINE (540 s from start) -- inside a 600-second driver window."""
+    t_start = time.monotonic()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ["WORLD_SIZE"])
     base = [sys.executable, "-u", os.path.abspath(__file__),
             *(sys.argv[1:] if argv is None else argv)]
+    st = {"res": None, "rung": None, "attempts": [], "dp_only": None, "dp_attempts": None}
+    sup = None
+
+    def build(reason):
+        attempts = list(sup.attempts) if sup is not None else []
+        main_att = attempts[:len(st["attempts"])] if st["res"] is not None else attempts
+        if st["res"] is None:
+            out = {"metric": METRIC, "value": None, "unit": "samples/s", "n_gpus": world,
+                   "steps": a.steps, "warmup": a.warmup, "higher_is_better": True,
+                   "error": ("terminated before any rung succeeded" if reason else
+                             "every rung of the fallback ladder failed"),
+                   "ladder": {"attempts": main_att}}
+        else:
+            out = dict(st["res"])
+            dp_att = attempts[len(st["attempts"]):] or st["dp_attempts"]
+            out["dp_only"] = st["dp_only"] if st["dp_only"] is not None else (
+                {"value": None, "skipped": "terminated"} if reason else None)
+            out["ladder"] = {"rung": st["rung"], "attempts": st["attempts"],
+                             "dp_attempts": dp_att}
+        out["ladder"]["seconds"] = round(time.monotonic() - t_start, 1)
+        if reason:
+            out["terminated"] = reason
+        return out
+
+    line = ladder.OneLine(rank, build)
+    line.install_sigterm()  # before the Supervisor's handler, which chains to it
     sup = ladder.Supervisor(lambda r: [*base, *r.args, "--no-dp-compare"], rank=rank,
-                            world=world, stall=float(switches.get("DNN_LADDER_STALL")))
+                            world=world, stall=float(switches.get("DNN_LADDER_STALL")),
+                            startup=float(switches.get("DNN_LADDER_STARTUP")),
+                            deadline=t_start + float(switches.get("DNN_LADDER_DEADLINE")))
     if a.parallelism.startswith("tp"):
         rungs = [ladder.Rung("default")]
     else:
         rungs = ladder.bench_rungs(world, dp_only=a.parallelism.startswith("dp"))
     res, rung = sup.climb(rungs, budget_s=float(switches.get("DNN_LADDER_BUDGET")))
-    attempts = list(sup.attempts)
-    dp_only = dp_attempts = None
+    st.update(res=res, rung=rung.name if rung else None, attempts=list(sup.attempts))
     if res is not None and not a.no_dp_compare and \
             not res["config"]["parallelism"].startswith(("dp", "tp")):
-        d, _ = sup.climb(ladder.bench_rungs(world, dp_only=True))
-        dp_attempts = sup.attempts[len(attempts):]
-        dp_only = ({"value": d["value"], "ms_per_step": d["ms_per_step"],
-                    **{k: d["config"].get(k) for k in DP_ONLY_KEYS}} if d is not None else
-                   {"value": None, "error": "every data-parallel rung failed"})
-    if rank == 0:
-        if res is None:
-            out = {"metric": METRIC, "value": None, "unit": "samples/s", "n_gpus": world,
-                   "steps": a.steps, "warmup": a.warmup, "higher_is_better": True,
-                   "error": "every rung of the fallback ladder failed",
-                   "ladder": {"attempts": attempts}}
+        # the comparison only when the attempt that just succeeded would fit again before
+        # the deadline (the decision must be the same on every rank: rank 0's, via the store)
+        need = 1.5 * sup.attempts[-1]["seconds"] + 30
+        key = "dp_compare/decision"
+        if rank == 0:
+            sup.store.set(key, "run" if (sup.seconds_left() or 0) > need else "skip")
+        if sup.store.get(key).decode() == "run":
+            d, _ = sup.climb(ladder.bench_rungs(world, dp_only=True))
+            st["dp_attempts"] = sup.attempts[len(st["attempts"]):]
+            st["dp_only"] = ({"value": d["value"], "ms_per_step": d["ms_per_step"],
+                              **{k: d["config"].get(k) for k in DP_ONLY_KEYS}} if d is not None
+                             else {"value": None, "error": "every data-parallel rung failed"})
         else:
-            out = res
-            out["dp_only"] = dp_only
-            out["ladder"] = {"rung": rung.name, "attempts": attempts,
-                             "dp_attempts": dp_attempts}
-        print(json.dumps(out), flush=True)
+            st["dp_only"] = {"value": None, "skipped": "budget",
+                             "seconds_left": round(sup.seconds_left() or 0, 1),
+                             "seconds_needed": round(need, 1)}
+    line.emit()
     return 0 if res is not None else 1
 
 

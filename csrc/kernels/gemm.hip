@@ -151,24 +151,6 @@ static gemm_fn pick4(int ns, int la, int lb, int f32) {
                    : pick_layout<Cfg<BM, BN, 2, 2, 4>>(la, lb, f32);
 }
 
-// Stage codes 12 / 13 / 14: 32-deep k-steps (Cfg BK = 32) with 2 / 3 / 4 ring stages -- e.g. a
-// 64-KiB 256x256 ring, so two workgroups share a CU. Instantiated for the tiles where that
-// changes the residency: 256x256, 256x128, 128x128.
-static gemm_fn pick_bk32(int bm, int bn, int ns, int la, int lb, int f32) {
-  if (bm == 256 && bn == 256) {
-    if (ns == 12) return pick_layout<Cfg<256, 256, 4, 2, 2, 2, 32>>(la, lb, f32);
-    if (ns == 13) return pick_layout<Cfg<256, 256, 4, 2, 3, 3, 32>>(la, lb, f32);
-    if (ns == 14) return pick_layout<Cfg<256, 256, 4, 2, 4, 4, 32>>(la, lb, f32);
-  } else if (bm == 256 && bn == 128) {
-    if (ns == 12) return pick_layout<Cfg<256, 128, 4, 2, 2, 2, 32>>(la, lb, f32);
-    if (ns == 13) return pick_layout<Cfg<256, 128, 4, 2, 3, 3, 32>>(la, lb, f32);
-  } else if (bm == 128 && bn == 128) {
-    if (ns == 12) return pick_layout<Cfg<128, 128, 2, 2, 2, 2, 32>>(la, lb, f32);
-    if (ns == 14) return pick_layout<Cfg<128, 128, 2, 2, 4, 4, 32>>(la, lb, f32);
-  }
-  return nullptr;
-}
-
 bool gemm_tile_supported(int bm, int bn) {
   const bool small = (bm == 64 || bm == 128) && (bn == 64 || bn == 128);
   const bool big = (bm == 256 && (bn == 64 || bn == 128 || bn == 256)) || (bm == 128 && bn == 256);
@@ -182,7 +164,7 @@ const char* gemm_error_string(int code) {
     case 0: return "ok";
     case -1: return "unsupported tile (64|128 x 64|128, 256 x 64|128|256, 128 x 256)";
     case -2: return "M and N must be positive multiples of 8 (edge tiles are partial)";
-    case -3: return "per-split K must be a positive multiple of 64 (32 for the 32-deep k-step codes 12-14)";
+    case -3: return "per-split K must be a positive multiple of 64";
     case -4: return "leading dimensions must be multiples of 8 elements (16-byte rows)";
     case -5: return "pointers must be 16-byte aligned";
     case -6: return "bad layout code";
@@ -191,8 +173,8 @@ const char* gemm_error_string(int code) {
     case -9: return "hip launch failed";
     case -10: return "colsum needs bf16 output and ld_colsum >= N";
     case -11: return "fused cross-entropy needs bf16 output, N == bn <= 128, a bias and 0 < n_cls <= N";
-    case -13: return "relu bit masks need bf16 output, act = relu, ld_mask >= N/8 (or < 0: fragment order, stage codes 9-11 / 15-17), no aux/xent, one-tile form";
-    case -12: return "pipeline stages must be 2..4, 5 = A3/B2 ring, 6 / 7 = register-prefetched 2 / 3-deep ring (256x256: 6; 256x128, 128x128, 128x64, 64x64: 6, 7), 9 / 10 = the same with the register-direct epilogue (no ct / fused update), 11 = register-direct epilogue on the A3/B2 ring (256x256, 256x128, 128x128), 12..14 = 32-deep k-steps with 2..4 stages (256x256: 12-14, 256x128: 12-13, 128x128: 12, 14), 15 / 16 = code 9 with an L2 touch-prefetch 1 / 2 k-steps ahead (256x256, 256x128, 128x128, 64x64), 17 = code 11 with touch distance 1 (256x128, 128x128) (8-wave tiles: 2, 3, 5; 256x256: 2, 5 or 8 = ping-pong; 5, 12-14: one-tile form, no fused xent)";
+    case -13: return "relu bit masks need bf16 output, act = relu, ld_mask >= N/8 (or < 0: fragment order, stage codes 9 / 11), no aux/xent, one-tile form";
+    case -12: return "pipeline stages must be 2..4, 5 = A3/B2 ring, 6 = register-prefetched 2-deep ring (staged epilogue), 9 = the same with the register-direct epilogue (no ct / fused update), 11 = register-direct epilogue on the A3/B2 ring (256x256, 256x128, 128x128) (8-wave tiles: 2, 3, 5; 256x256: 2, 5 or 8 = ping-pong; 5: one-tile form, no fused xent)";
     case -14: return "transposed output ct needs bf16 output (or the fused update), no xent, one split, one-tile form, ld_ct >= M, 16-byte alignment";
     case -15: return "fused SGD epilogue needs f32 output, one split, no accumulate/bias/xent, a device lr, 16-byte aligned buffers, N % 8 == 0, one-tile form";
     default: return "unknown gemm error";
@@ -205,15 +187,14 @@ int default_stages(int bm, int bn) {
   return 2;
 }
 
-int gemm_check(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, int splits,
-               int kq) {
+int gemm_check(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, int splits) {
   if (!gemm_tile_supported(bm, bn)) return -1;
   // partial edge tiles: M and N need only be multiples of 8 (16-byte rows / chunks)
   if (p.M <= 0 || p.N <= 0 || p.M % 8 || p.N % 8) return -2;
   if (splits < 1) return -3;
   if (p.k_total > 0) {  // uneven split-K ranges are cut in 64-deep units
     if (p.k_total % 64 || splits > p.k_total / 64) return -3;
-  } else if (p.K <= 0 || p.K % kq) {  // kq: the kernel's k-step (64, or 32 for codes 12-14)
+  } else if (p.K <= 0 || p.K % 64) {
     return -3;
   }
   const long ktot = p.k_total > 0 ? (long)p.k_total : (long)p.K * splits;
@@ -247,12 +228,11 @@ int gemm_check(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn,
 
 int gemm_bf16(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, int splits,
               hipStream_t stream, int stages, int persist) {
-  const int rc = gemm_check(p, la, lb, out_f32, bm, bn, splits,
-                            stages >= 12 && stages <= 14 ? 32 : 64);
+  const int rc = gemm_check(p, la, lb, out_f32, bm, bn, splits);
   if (rc) return rc;
   if ((p.mask_out || p.mask_in) && persist) return -13;
   // fragment-order masks (ld_mask < 0) exist only in the register-direct epilogue
-  const bool direct = stages == 9 || stages == 10 || stages == 11 || (stages >= 15 && stages <= 17);
+  const bool direct = stages == 9 || stages == 11;
   if ((p.mask_out || p.mask_in) && p.ld_mask < 0 && !direct) return -13;
   if (p.ct && persist) return -14;
   if (p.upd_master && persist) return -15;
@@ -270,20 +250,9 @@ int gemm_bf16(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, 
   }
   const int nt = gemm_tile_threads(bm, bn);
   const int ns = stages ? stages : default_stages(bm, bn);
-  if (ns >= 12 && ns <= 14) {  // 32-deep k-steps (one-tile form, no fused xent)
+  if (ns == 6 || ns == 9 || ns == 11) {  // register-prefetched loop
     if (persist || p.xent_labels) return -12;
-    gemm_fn f = pick_bk32(bm, bn, ns, la, lb, out_f32);
-    if (!f) return -12;
-    const int tiles_n = (p.N + bn - 1) / bn, tiles_m = (p.M + bm - 1) / bm;
-    const int nwg = tiles_n * tiles_m * splits;
-    GemmParams q = p;
-    if (q.group_m <= 0) q.group_m = tiles_n >= 8 ? 4 : 1;
-    hipLaunchKernelGGL(f, dim3(nwg), dim3(nt), 0, stream, q, tiles_n, tiles_m, nwg);
-    return hipGetLastError() == hipSuccess ? 0 : -9;
-  }
-  if (ns == 6 || ns == 7 || (ns >= 9 && ns <= 11) || (ns >= 15 && ns <= 17)) {  // RP loop
-    if (persist || p.xent_labels) return -12;
-    if (ns >= 9) {  // register-direct epilogue (9-11, 15-17): no transposed copy / fused update
+    if (ns >= 9) {  // register-direct epilogue (9, 11): no transposed copy / fused update
       if (p.ct) return -14;
       if (p.upd_master) return -15;
     }

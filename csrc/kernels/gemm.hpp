@@ -98,13 +98,13 @@ int gemm_bf16_group(const GemmParams* ps, const int* splits, int n, int layout_a
                     int out_f32, int bm, int bn, int stages, hipStream_t stream);
 // The argument checks of gemm_bf16 (0 or its error code).
 int gemm_check(const GemmParams& p, int layout_a, int layout_b, int out_f32, int bm, int bn,
-               int splits, int kq = 64);
+               int splits);
 int gemm_bf16(const GemmParams& p, int layout_a, int layout_b, int out_f32, int bm, int bn,
               int splits, hipStream_t stream, int stages = 0, int persist = 0);
 // stages == 8 with 256x256 tiles: the ping-pong, half-tile-streamed main loop (gemm_pp.hip).
 int gemm_pp_launch(const GemmParams& q, int la, int lb, int out_f32, int splits,
                    hipStream_t stream);
-// stages == 6 / 7: the register-prefetched main loop with a 2- / 3-deep ring (gemm_rp.hip).
+// stages == 6 / 9 / 11: the register-prefetched main loop (gemm_rp.hip).
 int gemm_rp_launch(const GemmParams& q, int la, int lb, int out_f32, int bm, int bn, int splits,
                    int ns, hipStream_t stream);
 int gemm_persist_launch(const GemmParams& q, int la, int lb, int out_f32, int bm, int bn,

@@ -68,10 +68,6 @@ struct Cfg {
   // first)
   static constexpr bool RP = RP_ != 0, DIRECT = (RP_ & 3) == 2;
   static constexpr int RP_PATTERN = (RP_ >> 2) & 3;
-  // RP_ bits 4-5: L2 touch-prefetch distance D (0 = off; touch_tiles): every k-step also
-  // touches the streamed operand tiles D k-steps beyond the newest LDS-DMA tile, so HBM
-  // misses are in flight further ahead than the LDS ring can hold
-  static constexpr int TOUCH = (RP_ >> 4) & 3;
   static_assert(!RP || (BK == 64 && NS <= 3), "register prefetch: BK 64, NS 2..3 (or A3/B2)");
   static_assert(NSB == NS || (NS == 3 && NSB == 2), "asymmetric ring: A 3 deep, B 2 deep only");
   static_assert(BK == 64 || BK == 32, "k-step depth 64 or 32");
@@ -89,9 +85,7 @@ struct Cfg {
   static constexpr int CHUNKS = BM / EPI_ROWS, WPC = EPI_ROWS / SM;  // wave-rows per chunk
   static constexpr int CS_BYTES = EPI_ROWS * CS_LD * 4;
   static constexpr int RED_BYTES = NT * 32;  // colsum partial staging
-  // touch-prefetch scratch: the 256 B every touch instruction writes (never read)
-  static constexpr int TOUCH_OFF = RING, RING_T = RING + (TOUCH ? 256 : 0);
-  static constexpr int SMEM = cmax<cmax<RING_T, CS_BYTES + 64>::v, RED_BYTES>::v;
+  static constexpr int SMEM = cmax<cmax<RING, CS_BYTES + 64>::v, RED_BYTES>::v;
   // per-wave LDS-DMA instructions of one A / one B tile (vmcnt units of the asymmetric ring)
   static constexpr int PER_A = BM * BK / (512 * NW), PER_B = BN * BK / (512 * NW);
   static_assert(FM >= 1 && FN >= 1 && SM % 16 == 0 && SN % 16 == 0, "wave sub-tile");
@@ -129,87 +123,59 @@ __device__ __forceinline__ void stage_tile(const u16* __restrict__ g, long ld, i
   }
 }
 
-// stage_tile with the LDS-DMA issued from inline asm. The compiler's wait-count pass tracks
-// LDS-DMA it emits itself and, finding no alias information, puts an s_waitcnt vmcnt(0) in
-// front of every later ds_read_b64_tr_b16 -- i.e. each k-step of an MN-major operand waited
-// for the tile just issued for the NEXT k-step. Issued from asm, the loads are invisible to that
-// pass; the pipeline's own counted vmcnt waits (wait_stage) already order them.
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Winline-asm"  // M0 in the clobber list (see below)
-template <int L, int T, int NW, int BK = 64>
-__device__ __forceinline__ void stage_tile_asm(const u16* __restrict__ g, long ld, int mn0, int k0,
-                                               char LDS_AS* dst, int wave, int lane, int mn_lim) {
-  constexpr int NI = T * BK / (512 * NW);
-#pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const int piece = i * NW + wave;
-    const int chunk = piece * 64 + lane;
-    const u16* src;
-    if constexpr (L == KMAJ) {
-      constexpr int CPR = BK / 8;
-      const int r = chunk / CPR, ph = chunk % CPR;
-      const int c = ph ^ k_swz<BK>(r);
-      src = g + (long)min(mn0 + r, mn_lim - 1) * ld + k0 + c * 8;
-    } else {
-      constexpr int CPR = T / 8;
-      const int r = chunk / CPR, ph = chunk % CPR;
-      const int c = ph ^ mn_swz<T>(r);
-      src = g + (long)(k0 + r) * ld + min(mn0 + c * 8, mn_lim - 8);
-    }
-    const unsigned m0v =
-        __builtin_amdgcn_readfirstlane((unsigned)(size_t)(dst + piece * 1024));
-    // M0 is written inside the asm and listed as clobbered; kernels that use this form issue
-    // all of their LDS-DMA from it (the compiler keeps nothing else in M0 there).
-    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off"
-                 :: "v"(src), "s"(m0v) : "memory", "m0");
-  }
-}
-#pragma clang diagnostic pop
-
-// L2 touch-prefetch of the k-step at k0 (Cfg TOUCH): one 4-byte LDS-DMA per 128-byte line of
-// the streamed operand tiles (A always; B when it is MN-major, i.e. an activation of the weight
-// gradient rather than a weight), into a 256-byte LDS scratch nobody reads. The load brings the
-// line into L2 / the Infinity Cache, so the real LDS-DMA of that tile a few k-steps later finds
-// it on-die instead of waiting for HBM: the bytes in flight per CU are no longer bounded by the
-// LDS ring. Every wave issues exactly touch_count<C, LA, LB>() instructions (lanes past the
-// line count repeat a line), which is what the ring's counted vmcnt waits allow for.
-template <int L, int T>
-__device__ __forceinline__ constexpr int touch_lines() {
-  return L == KMAJ ? T : 64 * ((T * 2 + 127) / 128);  // T rows of 128 B | 64 k-rows of T*2 B
-}
-template <class C, int LA, int LB>
-__device__ __forceinline__ constexpr int touch_count() {
-  constexpr int NL = touch_lines<LA, C::BM>() + (LB == MNMAJ ? touch_lines<LB, C::BN>() : 0);
-  return (NL + C::NT - 1) / C::NT;
-}
-
-template <int L, int T>
-__device__ __forceinline__ const u16* touch_addr(const u16* __restrict__ g, long ld, int mn0,
-                                                 int k0, int line, int mn_lim) {
-  if constexpr (L == KMAJ) return g + (long)min(mn0 + line, mn_lim - 1) * ld + k0;
-  constexpr int LPR = (T * 2 + 127) / 128;  // lines per k-row
-  const int r = line / LPR, c = line - r * LPR;
-  return g + (long)(k0 + r) * ld + max(0, min(mn0 + c * 64, mn_lim - 64));
-}
-
+// LDS-DMA source of one operand for the register-prefetched loop, strength-reduced (round 5).
+// The loads are issued from inline asm: the compiler's wait-count pass tracks LDS-DMA it emits
+// itself and, finding no alias information, puts an s_waitcnt vmcnt(0) in front of every later
+// ds_read_b64_tr_b16 -- each k-step of an MN-major operand would wait for the tile just issued
+// for the NEXT k-step; issued from asm the loads are invisible to that pass and the pipeline's
+// own counted vmcnt waits order them. Until round 5 every lane's source address was recomputed
+// per k-step -- for an MN-major operand `(k0 + r) * ld` as a 64-bit multiply per piece (16
+// quarter-rate v_mul_lo_u32 + 8 v_mad_u64_u32 per 64-deep k-step of the 128x128 wgrad: more
+// VALU issue than its 32 MFMAs, docs/DESIGN.md section 7). Now every lane's byte offset inside
+// the tile (edge clamp included) is computed ONCE and a k-step only moves a scalar base: the
+// load is the SADDR form `global_load_lds_dwordx4 voff, s[base]` (address = base + voff), so
+// the loop issues no vector ALU for its loads (profiles/r5_isa).
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
-template <class C, int LA, int LB>
-__device__ __forceinline__ void touch_tiles(const GemmParams& p, int m0, int n0, int k0,
-                                            char LDS_AS* scratch, int wave, int lane) {
-  constexpr int NA = touch_lines<LA, C::BM>();
-  constexpr int NL = NA + (LB == MNMAJ ? touch_lines<LB, C::BN>() : 0);
-  constexpr int TI = touch_count<C, LA, LB>();
-  const unsigned m0v = __builtin_amdgcn_readfirstlane((unsigned)(size_t)scratch);
+template <int L, int T, int NW>
+struct DmaSrc {
+  static constexpr int NI = T * 64 / (512 * NW);
+  unsigned voff[NI];  // per-lane byte offset of piece i from the tile's (k0, mn0) corner
+  const char* base;   // operand + mn0 (row offset for K-major), bytes; uniform
+  long kstride;       // bytes per unit of k: ld * 2 (MN-major) or 2 (K-major)
+
+  __device__ __forceinline__ DmaSrc(const u16* __restrict__ g, long ld, int mn0, int wave,
+                                    int lane, int mn_lim) {
 #pragma unroll
-  for (int i = 0; i < TI; ++i) {
-    const int line = (i * C::NT + wave * 64 + lane) % NL;
-    const u16* src = line < NA ? touch_addr<LA, C::BM>(p.A, p.lda, m0, k0, line, p.M)
-                               : touch_addr<LB, C::BN>(p.B, p.ldb, n0, k0, line - NA, p.N);
-    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off"
-                 :: "v"(src), "s"(m0v) : "memory", "m0");
+    for (int i = 0; i < NI; ++i) {
+      const int chunk = (i * NW + wave) * 64 + lane;
+      if constexpr (L == KMAJ) {
+        const int r = chunk / 8, ph = chunk % 8;
+        const int c = ph ^ k_swz<64>(r);
+        voff[i] = (unsigned)((long)(min(mn0 + r, mn_lim - 1) - mn0) * ld * 2 + c * 16);
+      } else {
+        constexpr int CPR = T / 8;
+        const int r = chunk / CPR, ph = chunk % CPR;
+        const int c = ph ^ mn_swz<T>(r);
+        voff[i] = (unsigned)((long)r * ld * 2 + (min(mn0 + c * 8, mn_lim - 8) - mn0) * 2);
+      }
+    }
+    base = (const char*)(g + (L == KMAJ ? (long)mn0 * ld : (long)mn0));
+    kstride = L == KMAJ ? 2 : ld * 2;
   }
-}
+
+  // the k-step starting at contraction index k0 -> LDS tile `dst` (T x 64 image)
+  __device__ __forceinline__ void issue(int k0, char LDS_AS* dst, int wave) const {
+    const char* b = base + (long)k0 * kstride;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const unsigned m0v =
+          __builtin_amdgcn_readfirstlane((unsigned)(size_t)(dst + (i * NW + wave) * 1024));
+      asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1"
+                   :: "v"(voff[i]), "s"(b), "s"(m0v) : "memory", "m0");
+    }
+  }
+};
 #pragma clang diagnostic pop
 
 // Fragment of v_mfma_f32_16x16x32_bf16 for 16-wide block `blk` of the tile and k-step s (32 k):
@@ -460,23 +426,10 @@ __device__ __forceinline__ void mma_tile_rp(const GemmParams& p, int m0, int n0,
   auto b_at = [&](int slot) -> char LDS_AS* {
     return C::ASYM ? lds + NA * A_BYTES + slot * B_BYTES : lds + slot * C::STAGE + A_BYTES;
   };
-  auto st_a = [&](int k, int slot) {
-    stage_tile_asm<LA, C::BM, C::NW>(p.A, p.lda, m0, kbase + k * 64, a_at(slot), wave, lane,
-                                     p.M);
-  };
-  auto st_b = [&](int k, int slot) {
-    stage_tile_asm<LB, C::BN, C::NW>(p.B, p.ldb, n0, kbase + k * 64, b_at(slot), wave, lane,
-                                     p.N);
-  };
-  // L2 touch-prefetch (C::TOUCH = D > 0): tile kt + NA + D is touched right after the DMA of
-  // tile kt + NA; TI instructions per wave younger than that DMA are allowed in the waits
-  constexpr int D = C::TOUCH;
-  constexpr int TI = D ? touch_count<C, LA, LB>() : 0;
-  auto touch = [&](int k) {
-    if constexpr (D > 0)
-      touch_tiles<C, LA, LB>(p, m0, n0, kbase + min(k, nk - 1) * 64, lds + C::TOUCH_OFF, wave,
-                             lane);
-  };
+  const DmaSrc<LA, C::BM, C::NW> src_a(p.A, p.lda, m0, wave, lane, p.M);
+  const DmaSrc<LB, C::BN, C::NW> src_b(p.B, p.ldb, n0, wave, lane, p.N);
+  auto st_a = [&](int k, int slot) { src_a.issue(kbase + k * 64, a_at(slot), wave); };
+  auto st_b = [&](int k, int slot) { src_b.issue(kbase + k * 64, b_at(slot), wave); };
   // Prologue: every slot staged (tiles past the end clamp to the last one: same load counts
   // whatever nk is), then tile 0 landed.
   if constexpr (C::ASYM) {  // issue order A0 B0 A1 B1 A2
@@ -485,18 +438,14 @@ __device__ __forceinline__ void mma_tile_rp(const GemmParams& p, int m0, int n0,
     st_a(min(1, nk - 1), 1);
     st_b(min(1, nk - 1), 1);
     st_a(min(2, nk - 1), 2);
-#pragma unroll
-    for (int d = 0; d < D; ++d) touch(NA + d);
-    wait_vmcnt<2 * C::PER_A + C::PER_B + D * TI>();
+    wait_vmcnt<2 * C::PER_A + C::PER_B>();
   } else {
 #pragma unroll
     for (int s = 0; s < NA; ++s) {
       st_a(min(s, nk - 1), s);
       st_b(min(s, nk - 1), s);
     }
-#pragma unroll
-    for (int d = 0; d < D; ++d) touch(NA + d);
-    wait_vmcnt<(NA - 1) * C::PER_STAGE + D * TI>();
+    wait_vmcnt<(NA - 1) * C::PER_STAGE>();
   }
   lds_barrier();
   tl_mark(p, 1);
@@ -520,8 +469,8 @@ __device__ __forceinline__ void mma_tile_rp(const GemmParams& p, int m0, int n0,
     rp_interleave<C::RP_PATTERN, NR, NM>();
     // own loads of tile kt+1 landed: asymmetric -- only A(kt+2) was issued after B(kt+1);
     // symmetric -- tiles kt+2 .. kt+NS-1 may stay in flight
-    if constexpr (C::ASYM) wait_vmcnt<C::PER_A + TI>();
-    else wait_vmcnt<(NA - 2) * C::PER_STAGE + TI>();
+    if constexpr (C::ASYM) wait_vmcnt<C::PER_A>();
+    else wait_vmcnt<(NA - 2) * C::PER_STAGE>();
     __builtin_amdgcn_s_waitcnt(0xC07F);
     asm volatile("s_barrier" ::: "memory");
     // Tile kt's slots are free: B(kt+NB) and A(kt+NA) into them; past the end the last tile is
@@ -529,7 +478,6 @@ __device__ __forceinline__ void mma_tile_rp(const GemmParams& p, int m0, int n0,
     // branch and every k-step leaves the same loads in flight.
     st_b(min(kt + NB, nk - 1), rb);
     st_a(min(kt + NA, nk - 1), ra);
-    touch(kt + NA + D);
     ra = ra + 1 == NA ? 0 : ra + 1;
     rb = rb + 1 == NB ? 0 : rb + 1;
     read_half<C, LA, LB>(a_at(ra), b_at(rb), a0, b0, wm, wn, 0, lane);

@@ -266,11 +266,23 @@ class Trainer:
                 raise
             self.transport_reason = f"IPC set-up failed: {e}"[:300]
             return DistPipe(mesh, st)
-        if mode == "auto" and 4 + len(ipc.duties) > hwq:
-            ipc.close()
-            self.transport_reason = (f"IPC plan needs {4 + len(ipc.duties)} hardware queues, "
-                                     f"GPU_MAX_HW_QUEUES={hwq}")
-            return DistPipe(mesh, st)
+        # Every rank reaches this point (all earlier exits are agreed), and the queue check
+        # must be agreed too: with an explicit DNN_IPC_RELAYS=k ranks carry different relay
+        # duty counts, and a rank that fell back alone would free relay slots its peers have
+        # mapped and still write into. Decide on the busiest rank's count.
+        if mode == "auto":
+            import torch.distributed as dist
+
+            from ..parallel.comm import _cpu_group
+
+            tt = torch.tensor([len(ipc.duties), -hwq], dtype=torch.int64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX, group=_cpu_group())
+            most_duties, least_hwq = int(tt[0].item()), -int(tt[1].item())
+            if 4 + most_duties > least_hwq:
+                ipc.close()
+                self.transport_reason = (f"IPC plan needs {4 + most_duties} hardware queues on "
+                                         f"its busiest rank, GPU_MAX_HW_QUEUES={least_hwq}")
+                return DistPipe(mesh, st)
         kdesc = (f"{k} relays per hop" if isinstance(k, int) else
                  "per-hop relays " + "/".join(str(len(v)) for h, v in sorted(k.items())
                                               if h[2] == "f" and h[0] < mesh.pp))

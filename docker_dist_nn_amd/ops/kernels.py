@@ -310,7 +310,7 @@ def gemm(a, b, c, *, layout_a: int, layout_b: int, M: int, N: int, K: int, bias=
                                   t.shape[1] < N or t.stride(0) != (c if c.dim() == 2
                                                                     else c[0]).stride(0)):
                 raise ValueError(f"fused update: {k} must be [M][N] with C's row stride")
-    if stages in (9, 10, 11, 15, 16, 17) and (ct is not None or upd is not None):
+    if stages in DIRECT_STAGES and (ct is not None or upd is not None):
         stages = 6  # the register-direct epilogue has neither: RP loop, staged epilogue
     if not a.is_cuda:
         ref.gemm(a, b, c, layout_a=layout_a, layout_b=layout_b, M=M, N=N, K=K, bias=bias,
@@ -407,7 +407,7 @@ def gemv(x, w, bias, y, act="relu"):
 # wave grid (WM, WN) of the register-direct tiles that take fragment-order masks (NB >= 4 bytes
 # per lane; gemm_rp.hip pick_rp)
 FRAG_WAVES = {(256, 256): (4, 2), (256, 128): (4, 2), (128, 128): (2, 2), (128, 64): (2, 2)}
-DIRECT_STAGES = (9, 10, 11, 15, 16, 17)
+DIRECT_STAGES = (9, 11)
 
 
 class FragMask:

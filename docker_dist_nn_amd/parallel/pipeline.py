@@ -427,9 +427,7 @@ class PipelineExecutor:
             # main stream right after the last dgrad, then W0 -- so W1 and W0 never share the
             # chip whatever the dgrads cost (with the fragment-mask dgrad the default plan lets
             # W0 start before W1: profiles/r4_timeline)
-            plan = [(st, "F0", 0), (None, "@fork", 0)]
-            plan += [(st, f"W{i}", 1) for i in range(L - 1, 1, -1)]
-            plan += [(st, f"B0.L{i}", 0) for i in range(L - 1, 0, -1)] + [(st, "W1", 0)]
+            plan = self._mode5_head(st, L) + [(st, "W1", 0)]
             if split:
                 return plan + [(None, "@fork", 0), (st, f"FINO1-{L - 1}", 1), (st, "W0", 0),
                                (st, "FINO0-0", 0), (None, "@join", 0)]
@@ -464,6 +462,31 @@ class PipelineExecutor:
         plan.append((st, "FINO", 0) if "FINO" in segs else (st, "FIN", 0))
         if "FINO" not in segs:
             plan.append((st, "O", 0))
+        return plan
+
+    @staticmethod
+    def _mode5_head(st, L: int):
+        """Forward, then the small wgrads W{L-1} .. W2 on the side stream and every dgrad on
+        the main stream (overlap mode 5). W_i reads dZ_i, which the dgrad of layer i+1
+        (B0.L{i+1}) writes -- or the forward F0, when i = L-1 or when the classifier tail
+        already ran that dgrad (an empty segment). So before each side W_i whose dZ comes from
+        a real dgrad, that dgrad is placed on the main stream and a fresh fork orders the side
+        stream after it (a single fork after F0 let W_i race the dgrad producing its
+        input for L >= 5, or L = 4 without the tail)."""
+        plan = [(st, "F0", 0)]
+        emitted, fork_due = set(), True
+        for i in range(L - 1, 1, -1):
+            src = i + 1  # the dgrad writing dZ_i (none for the last layer: F0 does)
+            if src <= L - 1 and src not in emitted:
+                plan.append((st, f"B0.L{src}", 0))
+                emitted.add(src)
+                if st._prog.segment_size(f"B0.L{src}") > 0:
+                    fork_due = True  # the side stream must wait for this dgrad
+            if fork_due:
+                plan.append((None, "@fork", 0))
+                fork_due = False
+            plan.append((st, f"W{i}", 1))
+        plan += [(st, f"B0.L{i}", 0) for i in range(L - 1, 0, -1) if i not in emitted]
         return plan
 
     @staticmethod

@@ -61,7 +61,9 @@ class StageWorker:
 
         from ..engine.inference import InferenceEngine
 
-        want = env.get("DNN_WORKER_DEVICE", "auto")
+        from .. import switches
+
+        want = switches.get("DNN_WORKER_DEVICE", env)
         if want == "cpu" or not torch.cuda.is_available():
             dev = torch.device("cpu")
         else:

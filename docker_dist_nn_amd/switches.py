@@ -86,15 +86,20 @@ SWITCHES: dict[str, tuple[str, str]] = {
     "DNN_IPC_PLAN": ("streams", "native IPC step form: streams (a stream per direction and relay "
                                 "duty) | slotted (ONE stream in global logical-clock order: "
                                 "no co-scheduling assumption, a captured graph is one chain)"),
-    "DNN_FIRST_STEP_TIMEOUT": ("60", "bench.py: seconds the first multi-rank step may take "
+    "DNN_FIRST_STEP_TIMEOUT": ("30", "bench.py: seconds the first multi-rank step may take "
                                "before the plan trace is printed and the run exits"),
     "DNN_LADDER": ("1", "bench.py with WORLD_SIZE > 1: a supervisor per rank runs each attempt "
                         "in fresh child processes and climbs the fallback ladder (ladder.py) "
                         "on a hang or crash; 0 = measure in this process"),
-    "DNN_LADDER_STALL": ("180", "ladder: seconds a child may go without a heartbeat before "
+    "DNN_LADDER_STALL": ("60", "ladder: seconds a child may go without a heartbeat before "
                                 "it is killed and the next rung runs"),
-    "DNN_LADDER_BUDGET": ("900", "ladder: seconds of attempts after which only the last, "
+    "DNN_LADDER_BUDGET": ("360", "ladder: seconds of attempts after which only the last, "
                                  "most conservative rung is still tried"),
+    "DNN_LADDER_STARTUP": ("120", "ladder: seconds a freshly spawned child may take to its first "
+                                  "heartbeat (import torch on a cold box), if above the stall"),
+    "DNN_LADDER_DEADLINE": ("540", "ladder: seconds from the supervisor's start after which "
+                                   "no attempt runs on (a running child is killed); the "
+                                   "data-parallel comparison runs only if it fits before it"),
     "DNN_LADDER_FAULT": ("", "ladder fault injection (tests): 'rung=stage:S,step:N,kind:K;...' "
                              "-- the child of that rung gets DNN_FAULT (stage = rank)"),
     "DNN_PIPE": ("auto", "pipeline transport: auto (IPC with relays on RCCL jobs when every "
@@ -129,6 +134,8 @@ SWITCHES: dict[str, tuple[str, str]] = {
     "DNN_SERVE_REPLAY": ("graph", "serving engine replay: graph | native | eager"),
     "DNN_SYNC_DEBUG": ("0", "synchronise + check after every kernel (race / fault hunting)"),
     "DNN_AUTOBUILD": ("1", "build the native extension on import if it is missing"),
+    "DNN_NATIVE_PATH": ("", "load the native extension from this file instead of the in-tree "
+                            "build (same-box A/B of two kernel builds; bench / probes only)"),
     # multi-rank rehearsal on one GPU
     "DNN_FORCE_DEVICE": ("", "run every rank on this device (one-GPU rehearsals)"),
     "DNN_DIST_BACKEND": ("nccl", "process-group backend of bench.py (gloo for rehearsals)"),
@@ -142,10 +149,13 @@ SWITCHES: dict[str, tuple[str, str]] = {
 }
 
 
-def get(name: str) -> str:
+def get(name: str, env=None) -> str:
+    """The switch's value from ``env`` (default: the process environment) or its default. A
+    stage worker passes the environment it was configured with (the reference's per-container
+    env contract, serve/worker.py)."""
     if name not in SWITCHES:
         raise KeyError(f"undeclared switch {name}")
-    return os.environ.get(name, SWITCHES[name][0])
+    return (os.environ if env is None else env).get(name, SWITCHES[name][0])
 
 
 def flag(name: str) -> bool:

@@ -10,7 +10,9 @@ falling back, so a GPU test can never pass on an eager/PyTorch path by accident.
 from __future__ import annotations
 
 import importlib
+import importlib.util
 import os
+import sys
 import threading
 
 import torch  # noqa: F401  (must precede the extension import, see module doc)
@@ -25,6 +27,13 @@ def _try_import():
     global _mod, _err
     with _lock:
         if _mod is not None or _err is not None:
+            return
+        alt = switches.get("DNN_NATIVE_PATH")
+        if alt:  # A/B of another build: same module name, different file
+            spec = importlib.util.spec_from_file_location("docker_dist_nn_amd._native", alt)
+            _mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(_mod)
+            sys.modules["docker_dist_nn_amd._native"] = _mod
             return
         try:
             _mod = importlib.import_module("docker_dist_nn_amd._native")

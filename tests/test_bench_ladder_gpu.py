@@ -52,3 +52,44 @@ def test_bench_ladder_survives_hang_and_crash(tmp_path):
     assert out["ladder_rung"] == "rccl-slotted"
     assert out["dp_only"]["value"] > 0 and out["dp_only"]["parallelism"] == "dp2"
     assert [a["rung"] for a in lad["dp_attempts"]] == ["dp-native"]
+
+
+@pytest.mark.timeout(300)
+def test_bench_ladder_steady_state_hangs_and_sigterm(tmp_path):
+    """rungs 1 and 2 hang AFTER their first step (steady state: only the
+    heartbeat stall detector can see it), rung 3 hangs too, and the job is SIGTERMed at a set
+    wall time, as the driver ends an overrunning bench. Rank 0 must still print exactly ONE
+    JSON line, marked terminated, listing the stalled attempts -- within the SIGTERM grace."""
+    import signal
+    import time
+
+    env = dict(os.environ)
+    env.update(DNN_FORCE_DEVICE="0", DNN_DIST_BACKEND="gloo", DNN_FIRST_STEP_TIMEOUT="15",
+               DNN_LADDER_STALL="12", TMPDIR=str(tmp_path),
+               DNN_LADDER_FAULT="default=stage:0,step:3,kind:hang;"
+                                "ipc-slotted=stage:1,step:3,kind:hang;"
+                                "rccl-slotted=stage:0,step:3,kind:hang")
+    t0 = time.monotonic()
+    p = subprocess.Popen([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                          "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+                          "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
+                          "--gpus", "2", "--steps", "20", "--warmup", "2", "--batch", "2048"],
+                         env=env, stdout=subprocess.PIPE, stderr=None, text=True, cwd=ROOT)
+    # two stalled attempts (spawn + steps + 12 s stall each) fit well inside 150 s
+    deadline = t0 + 150
+    while time.monotonic() < deadline and p.poll() is None:
+        time.sleep(1)
+    assert p.poll() is None, "the ladder ended before the SIGTERM"
+    p.send_signal(signal.SIGTERM)
+    t_term = time.monotonic()
+    out, _ = p.communicate(timeout=60)
+    assert time.monotonic() - t_term < 45  # printed and gone within the grace period
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out
+    rec = json.loads(lines[0])
+    assert rec["terminated"] == "terminated" and rec["value"] is None
+    att = rec["ladder"]["attempts"]
+    assert [a["rung"] for a in att[:2]] == ["default", "ipc-slotted"], att
+    for a in att[:2]:  # the hung rank and its blocked peer: whichever stall is seen first
+        assert "stall" in a["rc"].values() and set(a["rc"].values()) <= {"stall", "killed"}, att
+    assert "step" in att[0].get("last_heartbeat", ""), att  # it hung after stepping

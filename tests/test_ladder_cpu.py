@@ -123,3 +123,69 @@ def test_rung_fault_parse():
     assert [r.name for r in bench_rungs(4, dp_only=True)] == ["dp-native", "dp-python"]
     assert bench_rungs(4)[-1].args == ["--parallelism", "dp4", "--graph", "off"]
     assert bench_rungs(4)[0].args == [] and bench_rungs(4)[1].args == ["--graph", "off"]
+
+
+# Children that stay alive and keep beating forever (a slow or steady-state-stuck attempt the
+# stall detector cannot see); supervisors with a deadline and rank 0's OneLine report.
+DEADLINE_SCRIPT = textwrap.dedent("""
+    import json, os, sys, time
+    sys.path.insert(0, {root!r})
+    from docker_dist_nn_amd import ladder
+    rank = int(os.environ["RANK"])
+    if ladder.is_child():
+        while True:
+            ladder.heartbeat("busy")
+            time.sleep(0.2)
+    world = int(os.environ["WORLD_SIZE"])
+    sup = None
+    def build(reason):
+        return {{"value": None, "terminated": reason,
+                 "attempts": list(sup.attempts) if sup else []}}
+    line = ladder.OneLine(rank, build)
+    line.install_sigterm()
+    sup = ladder.Supervisor(lambda r: [sys.executable, __file__], rank=rank, world=world,
+                            stall=3.0, deadline=time.monotonic() + float({deadline}))
+    res, rung = sup.climb([ladder.Rung("a"), ladder.Rung("b")], budget_s=1.0)
+    line.emit()
+""")
+
+
+@pytest.mark.timeout(120)
+def test_ladder_deadline_kills_and_skips(tmp_path):
+    """An attempt still running at the deadline is killed ("deadline") and no further rung is
+    tried (skipped: "deadline"); rank 0 prints one line."""
+    script = tmp_path / "sup.py"
+    script.write_text(DEADLINE_SCRIPT.format(root=ROOT, deadline=6))
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+                        "--master-port", str(_port()), str(script)],
+                       env=_env(tmp_path), capture_output=True, text=True, timeout=110)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, (r.stdout, r.stderr[-2000:])
+    att = json.loads(lines[0])["attempts"]
+    assert att[0]["rung"] == "a" and not att[0]["ok"]
+    assert set(att[0]["rc"].values()) <= {"deadline", "killed"} and \
+        "deadline" in att[0]["rc"].values(), att
+    assert att[1] == {"rung": "b", "ok": False, "skipped": "deadline"}, att
+
+
+@pytest.mark.timeout(120)
+def test_ladder_sigterm_still_prints_one_line(tmp_path):
+    """The driver ends an overrunning bench with SIGTERM: rank 0's supervisor must still print
+    exactly one JSON line (marked terminated) and take its child down."""
+    import signal
+    import time
+
+    script = tmp_path / "sup.py"
+    script.write_text(DEADLINE_SCRIPT.format(root=ROOT, deadline=600))
+    p = subprocess.Popen([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                          "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+                          "--master-port", str(_port()), str(script)],
+                         env=_env(tmp_path), stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                         text=True)
+    time.sleep(8)  # supervisors up, first attempt's children running
+    p.send_signal(signal.SIGTERM)
+    out, err = p.communicate(timeout=90)
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, (out, err[-3000:])
+    assert json.loads(lines[0])["terminated"] == "terminated"

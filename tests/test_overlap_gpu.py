@@ -46,6 +46,40 @@ def test_overlap_plan_bitwise(dev, monkeypatch, model, rows):
         assert torch.equal(res[0][1], r[1])
 
 
+def test_mode5_without_tail_bitwise(dev, monkeypatch):
+    """Overlap mode 5 with the classifier tail off: W2 on the side stream reads dZ_2, which the
+    main stream's dgrad of layer 3 writes, so the plan must fork after that dgrad.
+    Bitwise equal to the sequential plan."""
+    from docker_dist_nn_amd import NAMED_MODELS
+    from docker_dist_nn_amd.data import synthetic_mnist
+    from docker_dist_nn_amd.engine import OptimConfig, Trainer
+
+    rows = 8192
+    monkeypatch.setenv("DNN_BW_OVERLAP_MIN_ROWS", "0")
+    monkeypatch.setenv("DNN_TAIL", "0")
+    x, y = synthetic_mnist(rows, seed=6)
+    xb = torch.zeros(rows, 832, dtype=torch.bfloat16)
+    xb[:, :784] = torch.from_numpy(x).to(torch.bfloat16)
+    xb, yb = xb.to(dev), torch.from_numpy(y).to(dev)
+    res = []
+    for flag in ("0", "5"):
+        monkeypatch.setenv("DNN_BW_OVERLAP", flag)
+        tr = Trainer(NAMED_MODELS["mnist-fcnn"], micro_batch=rows, num_micro=1,
+                     optim=OptimConfig(lr=0.1, momentum=0.9), device=dev)
+        losses = []
+        for _ in range(4):
+            tr.set_batch(xb, yb)
+            tr.step()
+            losses.append(tr.loss())
+        segs = [seg for _, seg, _ in tr.executor._native_plan()]
+        if flag == "5":
+            assert segs.index("B0.L3") < segs.index("W2") and \
+                "@fork" in segs[segs.index("B0.L3"):segs.index("W2")], segs
+        res.append((losses, tr.stages[0].params.master.clone()))
+    assert res[0][0] == res[1][0]
+    assert torch.equal(res[0][1], res[1][1])
+
+
 @pytest.mark.parametrize("model,rows,split", [("mnist-fcnn", 8192, True),
                                               ("784-8192-8192-10", 2048, False)])
 def test_split_fino_auto_plan(dev, monkeypatch, model, rows, split):

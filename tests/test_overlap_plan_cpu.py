@@ -46,3 +46,31 @@ def test_fork_after_real_main_work_is_kept():
     plan = [(st if e[0] == "st" else None, e[1], e[2]) for e in PLAN]
     out = [e[1] for e in PipelineExecutor._elide_forks(st, plan)]
     assert out == ["F0", "@fork", "W3", "B0.L3", "@fork", "W2", "B0.L2", "W1", "B0.L1"]
+
+
+def _mode5(sizes, L):
+    st = _Stage(sizes)
+    return [e[1] for e in PipelineExecutor._mode5_head(st, L)]
+
+
+def test_mode5_forks_after_each_dgrad_a_side_wgrad_reads():
+    """overlap mode 5 put every small wgrad on the side stream behind ONE fork after
+    F0, but W_i reads dZ_i, which B0.L{i+1} writes. Every side W_i whose dgrad is real must come
+    after that dgrad and a fork on the main stream."""
+    L = 6
+    sizes = {"F0": 4, **{f"B0.L{i}": 1 for i in range(1, L)}, **{f"W{i}": 1 for i in range(L)}}
+    out = _mode5(sizes, L)
+    for i in range(2, L - 1):
+        b, w = out.index(f"B0.L{i + 1}"), out.index(f"W{i}")
+        assert b < w and "@fork" in out[b:w], (i, out)
+    # every dgrad exactly once, in order
+    assert [s for s in out if s.startswith("B0")] == [f"B0.L{i}" for i in range(L - 1, 0, -1)]
+    assert out.index(f"W{L - 1}") > out.index("@fork") > out.index("F0")
+
+
+def test_mode5_with_tail_keeps_one_fork():
+    """The headline's tail already ran the dgrads of layers 3 and 2 (empty segments): their
+    wgrads read dZ written by F0, so one fork suffices, as before."""
+    out = _mode5(SIZES, 4)
+    assert out.count("@fork") == 1
+    assert out == ["F0", "@fork", "W3", "B0.L3", "W2", "B0.L2", "B0.L1"]
