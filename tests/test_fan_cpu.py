@@ -1,0 +1,171 @@
+"""Replicated-stage ("fan") pipelines on CPU: the list schedule is a linear extension of the
+dependency graph for every layout (deadlock-free), replicas run exactly their micro-batches,
+and gloo multi-process training with fan-in / fan-out hops and per-stage gradient groups
+reproduces single-process training of the same global batch."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from docker_dist_nn_amd import MLPSpec
+from docker_dist_nn_amd.data import synthetic_mnist
+from docker_dist_nn_amd.parallel.fan import (FanLayout, check_schedule, fan_rows, fan_schedule,
+                                             parse_fan, stage_costs)
+
+
+@pytest.mark.parametrize("reps", [(1, 1), (2, 1), (1, 3), (3, 1), (2, 3), (3, 2), (1, 2, 1),
+                                  (2, 1, 3), (1, 1, 1, 1), (6, 2), (1, 7), (2, 2, 2, 2)])
+@pytest.mark.parametrize("M", [7, 8, 12])
+def test_schedule_is_a_linear_extension(reps, M):
+    if M < max(reps):
+        pytest.skip("fewer micro-batches than replicas")
+    lay = FanLayout(tuple([1] * len(reps)), reps)
+    for f, b, hop in (([1.0] * len(reps), [2.0] * len(reps), 0.0),
+                      ([1.0, 0.2, 3.0, 0.5][:len(reps)], [2.0, 0.4, 6.0, 1.0][:len(reps)], 0.7)):
+        sch = fan_schedule(lay, M, f, b, hop)
+        check_schedule(sch)  # raises on any violation
+        # every rank's sends to one peer are in its own op order (FIFO matching)
+        for (s, q), ops in sch.ops.items():
+            for d, t in (("f", s + 1), ("b", s - 1)):
+                if 0 <= t < lay.S:
+                    for p in range(reps[t]):
+                        seq = sch.send_order(s, q, d, p)
+                        op = "F" if d == "f" else "B"
+                        assert seq == [j for o, j in ops if o == op and j % reps[t] == p]
+
+
+def test_schedule_replays_deadlock_free_as_blocking_ranks():
+    """Execute the per-rank orders with rendezvous semantics (a receive waits for the matching
+    send, sends are buffered): every rank must finish -- for many random cost profiles."""
+    rng = np.random.default_rng(0)
+    for reps in [(3, 1), (1, 3), (2, 3, 1), (6, 2), (1, 7), (2, 1, 2, 1)]:
+        lay = FanLayout(tuple([1] * len(reps)), reps)
+        for _ in range(5):
+            f = list(rng.uniform(0.1, 3, len(reps)))
+            b = list(rng.uniform(0.1, 6, len(reps)))
+            sch = fan_schedule(lay, 16, f, b, float(rng.uniform(0, 2)))
+            pos = {w: 0 for w in sch.ops}
+            done = set()
+            progress = True
+            while progress:
+                progress = False
+                for w, ops in sch.ops.items():
+                    s, _ = w
+                    while pos[w] < len(ops):
+                        o, j = ops[pos[w]]
+                        need = [(s - 1, "F", j)] if o == "F" and s > 0 else []
+                        if o == "B" and s + 1 < lay.S:
+                            need.append((s + 1, "B", j))
+                        if all(n in done for n in need):
+                            done.add((s, o, j))
+                            pos[w] += 1
+                            progress = True
+                        else:
+                            break
+            assert all(pos[w] == len(ops) for w, ops in sch.ops.items()), (reps, f, b)
+
+
+def test_layout_helpers():
+    lay = FanLayout((1, 2), (3, 1))
+    assert lay.world == 4 and lay.offsets == [0, 3]
+    assert [lay.stage_of(r) for r in range(4)] == [(0, 0), (0, 1), (0, 2), (1, 0)]
+    assert lay.local_micros(0, 1, 8) == [1, 4, 7]
+    assert fan_rows(lay, 0, 1, 8, 16) == [slice(16, 32), slice(64, 80), slice(112, 128)]
+    assert parse_fan("fan:1x3,2x1") == ([1, 2], [3, 1])
+    assert parse_fan("fan:3,1") == (None, [3, 1])
+    assert parse_fan("pp4") is None
+    f, b = stage_costs(MLPSpec.parse("784-512-256-128-10"), [1, 3])
+    assert max(f + b) == 1.0 and b[0] > b[1]
+
+
+# ---- gloo training parity ---------------------------------------------------------------
+SPEC = "784-128-64-32-10"
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _global(rows):
+    x, y = synthetic_mnist(rows, seed=9)
+    xt = torch.zeros(rows, 832, dtype=torch.bfloat16)
+    xt[:, :784] = torch.from_numpy(x).to(torch.bfloat16)
+    return xt, torch.from_numpy(y)
+
+
+def _worker(rank, world, port, dist_, reps, mb, M, steps, shard, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from docker_dist_nn_amd.engine import OptimConfig
+    from docker_dist_nn_amd.engine.fan_trainer import FanTrainer
+    from docker_dist_nn_amd.parallel.fan import build_fan_mesh
+
+    lay = FanLayout(tuple(dist_), tuple(reps))
+    mesh = build_fan_mesh(lay)
+    tr = FanTrainer(MLPSpec.parse(SPEC), lay, mesh, micro_batch=mb, num_micro=M,
+                    optim=OptimConfig(lr=0.1, momentum=0.9), device=torch.device("cpu"),
+                    dp_reduce="shard" if shard else "allreduce")
+    xt, yt = _global(mb * M)
+    losses = []
+    for _ in range(steps):
+        tr.set_global_batch(xt, yt)
+        tr.step()
+        losses.append(tr.loss())
+    for k, (w, b) in tr.local_weights().items():
+        np.save(os.path.join(out_dir, f"w{k}_s{mesh.stage}_q{mesh.replica}.npy"), w)
+    if losses[-1] is not None:
+        np.save(os.path.join(out_dir, f"loss_q{mesh.replica}.npy"), np.array(losses))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _single(mb, M, steps):
+    from docker_dist_nn_amd.engine import OptimConfig, Trainer
+
+    tr = Trainer(MLPSpec.parse(SPEC), micro_batch=mb * M, num_micro=1,
+                 optim=OptimConfig(lr=0.1, momentum=0.9), device=torch.device("cpu"))
+    xt, yt = _global(mb * M)
+    losses = []
+    for _ in range(steps):
+        tr.set_batch(xt, yt)
+        tr.step()
+        losses.append(tr.loss())
+    return losses, {k: w for k, (w, b) in tr.local_weights().items()}
+
+
+@pytest.mark.parametrize("dist_,reps,shard,M", [([1, 3], [3, 1], False, 6),
+                                                ([2, 2], [1, 2], False, 6),
+                                                ([1, 3], [3, 1], False, 7),  # uneven counts
+                                                ([1, 1, 2], [2, 1, 2], True, 6),
+                                                ([3, 1], [2, 3], True, 7)])
+def test_fan_training_matches_single_process(tmp_path, dist_, reps, shard, M):
+    mb, steps = 64, 3
+    world = sum(reps)
+    mp.spawn(_worker, args=(world, _port(), dist_, reps, mb, M, steps, shard, str(tmp_path)),
+             nprocs=world, join=True)
+    ref_losses, ref_w = _single(mb, M, steps)
+    lay = FanLayout(tuple(dist_), tuple(reps))
+    # the loss is the sum of the last stage's replicas' shares
+    got = sum(np.load(tmp_path / f"loss_q{q}.npy") for q in range(reps[-1]))
+    # all-reduce: fp32 gradients, only the summation order differs; shard: the gradients
+    # cross the DP group in bf16 (as tests/test_dp_shard_cpu.py)
+    tol = dict(rtol=2e-2, atol=3e-4) if shard else dict(rtol=1e-4, atol=2e-5)
+    np.testing.assert_allclose(got, ref_losses, rtol=1e-4 if not shard else 1e-2)
+    g = 0
+    for s, k in enumerate(dist_):
+        for i in range(g, g + k):
+            ws = [np.load(tmp_path / f"w{i}_s{s}_q{q}.npy") for q in range(reps[s])]
+            for w in ws[1:]:  # replicas stay identical
+                np.testing.assert_array_equal(w, ws[0])
+            np.testing.assert_allclose(ws[0], ref_w[i], **tol)
+        g += k
