@@ -21,7 +21,8 @@ from ..parallel.fan import FanLayout, FanMesh, FanPipe, fan_rows, fan_schedule, 
 from ..parallel.pipeline import GradSync, PipelineExecutor
 from ..partition import plan_stages
 from .stage import OptimConfig, Stage
-from .trainer import Trainer
+from .trainer import Trainer, _any_rank, _warm_groups
+from .. import switches
 
 
 class FanTrainer(Trainer):
@@ -75,6 +76,25 @@ class FanTrainer(Trainer):
         self.transport = "rccl" if mesh.backend == "nccl" else mesh.backend
         self.transport_reason = (f"fan layout {layout.describe()}: fan-in / fan-out P2P "
                                  f"({self.transport}), Python executor")
+        if mesh.backend == "nccl" and self.native_exec and \
+                switches.get("DNN_NATIVE_DIST") != "0":
+            # the rank's whole step as one StepPlan call (fan.FanNativeStep, slotted RCCL form);
+            # agreed over the world like the uniform mesh's native step (trainer.py)
+            from ..parallel.fan import FanNativeStep
+
+            _warm_groups(mesh, self.device)
+            err = None
+            try:
+                self.native_step = FanNativeStep(self.executor, mesh, self.sched)
+            except Exception as e:
+                err = e
+            if _any_rank(self.native_step is None, self.device):
+                self.native_fallback = repr(err) if err is not None else "another rank"
+                self.native_step = None
+            else:
+                self.executor.native_step = self.native_step
+                self.transport_reason = (f"fan layout {layout.describe()}: slotted RCCL plan "
+                                         "(one group per clock slot), native step")
         self._ipc_verify = None
         self._fallback_step = None
         self._graph = None

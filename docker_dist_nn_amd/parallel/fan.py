@@ -416,3 +416,184 @@ def lcm_reps(reps: Sequence[int]) -> int:
     for r in reps:
         out = out * r // math.gcd(out, r)
     return out
+
+
+# ---- native step -------------------------------------------------------------------------
+def fan_slots(sched: FanSchedule) -> dict:
+    """Integer logical clock of every compute op of a fan step (the slotted plan's clock): an
+    op runs one slot after its worker's previous op and TWO slots after the op producing its
+    input (the slot between carries the hop). Computed over the schedule's global start order,
+    a linear extension of the dependency graph, so every dependency is placed first."""
+    sch = sched
+    lay = sch.layout
+    order = sorted(sch.start, key=lambda k: (sch.start[k], k[0], k[1], k[2]))
+    worker_last: dict = {}
+    slot: dict = {}
+    for key in order:
+        s, op, j = key
+        w = (s, lay.replica_of(s, j))
+        t = worker_last.get(w, -1) + 1
+        if op == "F" and s > 0:
+            t = max(t, slot[(s - 1, "F", j)] + 2)
+        if op == "B":
+            t = max(t, slot[(s, "F", j)] + 1)
+            if s + 1 < lay.S:
+                t = max(t, slot[(s + 1, "B", j)] + 2)
+        slot[key] = t
+        worker_last[w] = t
+    return slot
+
+
+def fan_messages(sched: FanSchedule) -> list[tuple[int, str, int, int, int]]:
+    """Every hop of a step: (slot, direction, j, src rank, dst rank); a message leaves in the
+    slot after the compute that produced it."""
+    lay, slot = sched.layout, fan_slots(sched)
+    out = []
+    for (s, op, j), t in slot.items():
+        if op == "F" and s + 1 < lay.S:
+            out.append((t + 1, "f", j, lay.rank_of(s, lay.replica_of(s, j)),
+                        lay.rank_of(s + 1, lay.replica_of(s + 1, j))))
+        elif op == "B" and s > 0:
+            out.append((t + 1, "b", j, lay.rank_of(s, lay.replica_of(s, j)),
+                        lay.rank_of(s - 1, lay.replica_of(s - 1, j))))
+    return sorted(out)
+
+
+def _fan_native_step_class():
+    from .native_step import (COMM, GROUP, MAIN, NCCL_BF16, REC, RECV, SEG, SEND, WAIT,
+                              NativeStep, comm_ptr, flatten, torch_rccl_path, PLAN_KEYS)
+    from ..utils.native import native
+
+    class FanNativeStep(NativeStep):
+        """The RCCL step of one fan-layout rank as ONE StepPlan call, in the ``slotted`` form
+        (parallel/native_step.py): every hop of a step has a slot of the global clock
+        (fan_slots), and at slot t each rank issues one ncclGroupStart/End with all its sends
+        and receives of slot t on the boundary communicators -- whose partners are in the
+        partner's slot-t group by construction -- so group t completes once every group < t
+        has, whatever the RCCL kernel residency (checked with one resident RCCL kernel per
+        rank by the plan simulator, tests/test_fan_cpu.py). Compute on stream 0, RCCL on
+        stream 1; the DP buckets of a replicated stage follow the last group."""
+
+        def __init__(self, executor, mesh: FanMesh, sched: FanSchedule,
+                     comms: Optional[dict] = None, build_only: bool = False):
+            if len(executor.stages) != 1:
+                raise ValueError("native fan step: one stage per rank")
+            st = executor.stages[0]
+            if st._prog is None or not st._has_w or not st._o_native:
+                raise ValueError("native fan step needs a recorded stage (compile_native)")
+            self.ex, self.mesh, self.st, self.sched = executor, mesh, st, sched
+            self.lay = mesh.layout
+            self.transport, self.ipc, self.mode = "rccl", None, "fan-slotted"
+            self.dp = mesh.dp
+            self.sharded = st.params.sharded
+            self.pp = self.lay.S
+            self.comms = dict(comms or {})
+            if comms is None and not build_only:
+                self.n = native()
+                self.n.nccl_load(torch_rccl_path())
+                for name, g in (("f_in", mesh.fwd_in), ("f_out", mesh.fwd_out),
+                                ("b_in", mesh.bwd_in), ("b_out", mesh.bwd_out)):
+                    if g is not None:
+                        self.comms[name] = comm_ptr(g, st.device)
+                if self.dp > 1 or self.sharded:
+                    self.comms["dp"] = comm_ptr(mesh.dp_group, st.device)
+                self._check_comm_ranks()
+            self._ev = 0
+            self.ops = []
+            self._build()
+            self.n_streams = 2
+            if build_only:
+                return
+            import os
+
+            hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+            if self.n_streams > hwq:
+                raise RuntimeError(f"native fan step needs {self.n_streams} hardware queues")
+            self.n = native()
+            self.plan = self.n.StepPlan(self.n_streams, max(1, self._ev))
+            for o in flatten(self.ops):
+                self.plan.add(**{k: v for k, v in o.items() if k in PLAN_KEYS})
+
+        def _base(self, name: str) -> int:
+            """First global rank of the boundary group a link channel lives on."""
+            s = self.mesh.stage
+            b = s - 1 if name in ("f_in", "b_out") else s
+            return self.lay.offsets[b]
+
+        def _check_comm_ranks(self) -> None:
+            n, m, lay = self.n, self.mesh, self.lay
+            for name, comm in self.comms.items():
+                size, rank = n.nccl_comm_info(comm)
+                if name == "dp":
+                    want = (self.dp, m.replica)
+                else:
+                    b = self._base(name)
+                    s = m.stage - 1 if name in ("f_in", "b_out") else m.stage
+                    want = (lay.reps[s] + lay.reps[s + 1], m.rank - b)
+                if (size, rank) != want:
+                    raise RuntimeError(f"communicator {name}: (size, rank) = {(size, rank)}, "
+                                       f"the plan assumes {want}")
+
+        def _fan_p2p(self, kind: int, direction: str, j: int, other: int) -> dict:
+            inbound = kind == RECV
+            name = ("f_in" if inbound else "f_out") if direction == "f" else \
+                ("b_in" if inbound else "b_out")
+            st = self.st
+            t = (st.x_in if direction == "f" else st.grad_out) if inbound else \
+                (st.output if direction == "f" else st.dx_send)
+            v = t[st.rows_of(self.lay.local_index(self.mesh.stage, j))]
+            return dict(kind=kind, stream=COMM, comm=self.comms.get(name, 0), a=v.data_ptr(),
+                        count=v.numel(), dtype=NCCL_BF16, peer=other - self._base(name),
+                        gpeer=other, tag=(direction, j, 0))
+
+        def _build(self) -> None:
+            self._check_w(self.ex.ops[0])
+            m, st, lay = self.mesh, self.st, self.lay
+            me = m.rank
+            slot = fan_slots(self.sched)
+            msgs = fan_messages(self.sched)
+            sends, recvs = {}, {}
+            for t, d, j, src, dst in msgs:
+                if src == me:
+                    sends.setdefault(t, []).append((d, j, dst))
+                if dst == me:
+                    recvs.setdefault(t, []).append((d, j, src))
+            consumed, produced = {}, {}
+            group_ev = {}
+            for t in sorted(recvs):
+                group_ev[t] = self._event()
+                for d, j, _src in recvs[t]:
+                    consumed[(d, j)] = group_ev[t]
+            entries = []
+            s = m.stage
+            for op, j in self.sched.ops[(s, m.replica)]:
+                d, ops = op.lower(), []
+                if (d, j) in consumed:
+                    ops.append(dict(kind=WAIT, stream=MAIN, event=consumed[(d, j)]))
+                jj = lay.local_index(s, j)
+                ops.append(dict(kind=SEG, stream=MAIN, prog=st._prog, seg=f"{op}{jj}"))
+                if (d == "f" and s + 1 < lay.S) or (d == "b" and s > 0):
+                    produced[(d, j)] = e = self._event()
+                    ops.append(dict(kind=REC, stream=MAIN, event=e))
+                entries.append((slot[(s, op, j)], 1, ops))
+            for t in sorted(set(sends) | set(recvs)):
+                ops, members = [], []
+                for d, j, dst in sends.get(t, []):
+                    ops.append(dict(kind=WAIT, stream=COMM, event=produced[(d, j)]))
+                    members.append(self._fan_p2p(SEND, d, j, dst))
+                for d, j, src in recvs.get(t, []):
+                    members.append(self._fan_p2p(RECV, d, j, src))
+                ops.append(dict(kind=GROUP, stream=COMM, ops=members, tag=("slot", t)))
+                if t in group_ev:
+                    ops.append(dict(kind=REC, stream=COMM, event=group_ev[t]))
+                entries.append((t, 0, ops))
+            for _, _, ops in sorted(entries, key=lambda e: (e[0], e[1])):
+                self.ops += ops
+            self._wgrad_update(COMM)
+
+    return FanNativeStep
+
+
+def FanNativeStep(*args, **kw):
+    """See ``_fan_native_step_class`` (built lazily: native_step imports the pipeline)."""
+    return _fan_native_step_class()(*args, **kw)

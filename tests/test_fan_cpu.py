@@ -169,3 +169,89 @@ def test_fan_training_matches_single_process(tmp_path, dist_, reps, shard, M):
                 np.testing.assert_array_equal(w, ws[0])
             np.testing.assert_allclose(ws[0], ref_w[i], **tol)
         g += k
+
+
+# ---- native plans: the timed plan simulator ------------------------------------------------
+class _FT:
+    """Fake device tensor: addresses only (as tests/test_step_plan_sim_cpu.py)."""
+
+    def __init__(self, base, rows, cols, esize=2):
+        self.base, self.rows, self.cols, self.esize = base, rows, cols, esize
+
+    def __getitem__(self, sl):
+        return _FT(self.base + sl.start * self.cols * self.esize, sl.stop - sl.start, self.cols,
+                   self.esize)
+
+    def data_ptr(self):
+        return self.base
+
+    def numel(self):
+        return self.rows * self.cols
+
+
+def _fan_builds(dist_, reps, M, mb=256, spec="784-512-256-128-10", dp_reduce="allreduce"):
+    from types import SimpleNamespace as NS
+
+    from docker_dist_nn_amd.engine.stage import OptimConfig, StageParams
+    from docker_dist_nn_amd.models.mlp import LayerGeom
+    from docker_dist_nn_amd.parallel.fan import FanNativeStep
+    from docker_dist_nn_amd.partition import plan_stages
+
+    spec = MLPSpec.parse(spec)
+    lay = FanLayout(tuple(dist_), tuple(reps))
+    f, b = stage_costs(spec, dist_)
+    sch = fan_schedule(lay, M, f, b)
+    plans = plan_stages(len(spec.layers), list(dist_))
+    out = {}
+    for rank in range(lay.world):
+        s, q = lay.stage_of(rank)
+        p = plans[s]
+        geoms = [LayerGeom(i, spec.layers[i]) for i in range(p.layer_start, p.layer_end)]
+        shard = (reps[s], q) if dp_reduce == "shard" and reps[s] > 1 else None
+        params = StageParams(geoms, torch.device("cpu"), OptimConfig(), shard=shard)
+        nm = len(lay.local_micros(s, q, M))
+        base = (rank + 1) << 40
+        st = NS(nm=nm, mb=mb, boundary="bf16", _has_w=True, _o_native=True,
+                _prog=NS(segments=lambda: {"FINO", "W"}), params=params, geoms=geoms,
+                rows_of=lambda j, mb=mb: slice(j * mb, (j + 1) * mb))
+        for k, (key, w) in enumerate((("x_in", geoms[0].kp), ("grad_out", geoms[-1].np_),
+                                      ("output", geoms[-1].np_), ("dx_send", geoms[0].kp))):
+            setattr(st, key, _FT(base | (k + 1) << 32, nm * mb, w))
+        mesh = NS(rank=rank, stage=s, replica=q, layout=lay, dp=reps[s])
+        comms = {"dp": ("dp", s)}
+        if s > 0:
+            comms["f_in"], comms["b_out"] = ("f", s - 1), ("b", s - 1)
+        if s + 1 < lay.S:
+            comms["f_out"], comms["b_in"] = ("f", s), ("b", s)
+        ex = NS(stages=[st], ops=[sch.local_ops(s, q)], kind="fan")
+        out[rank] = FanNativeStep(ex, mesh, sch, comms=comms, build_only=True)
+    return out
+
+
+@pytest.mark.parametrize("dist_,reps", [([1, 3], [3, 1]), ([1, 3], [1, 3]), ([2, 2], [6, 2]),
+                                        ([1, 1, 2], [2, 1, 2]), ([1, 1, 1, 1], [3, 2, 2, 1]),
+                                        ([1, 3], [7, 1])])
+@pytest.mark.parametrize("dp_reduce", ["allreduce", "shard"])
+def test_fan_native_plans_deadlock_free_with_one_rccl_kernel(dist_, reps, dp_reduce):
+    """Every rank's slotted fan plan (fan-in / fan-out groups per clock slot, DP buckets of the
+    replicated stages) completes in the timed plan simulator, also when each rank can have only
+    ONE RCCL kernel resident -- and every hop is one send matched by one receive."""
+    from docker_dist_nn_amd.parallel import native_step as nsmod
+    from docker_dist_nn_amd.parallel import plan_sim
+
+    M = 2 * max(reps) + 1
+    builds = _fan_builds(dist_, reps, M, dp_reduce=dp_reduce)
+    plans = {r: plan_sim.RankPlan(ns.ops, ns.n_streams) for r, ns in builds.items()}
+    for serial in (False, True):
+        res = plan_sim.simulate(plans, steps=2, serial_rccl=serial)
+        assert res.makespan > 0
+    sends, recvs = [], []
+    for r, ns in builds.items():
+        for o in nsmod.flatten(ns.ops):
+            if o["kind"] == nsmod.SEND:
+                sends.append((r, o["gpeer"], o["tag"][:2]))
+            elif o["kind"] == nsmod.RECV:
+                recvs.append((o["gpeer"], r, o["tag"][:2]))
+    assert sorted(sends) == sorted(recvs)
+    lay = FanLayout(tuple(dist_), tuple(reps))
+    assert len(sends) == 2 * M * (lay.S - 1)

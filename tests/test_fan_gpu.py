@@ -1,0 +1,96 @@
+"""Replicated-stage (fan) pipelines on the GPU: processes sharing cuda:0 (gloo), the EXACT op
+list of the native fan step (fan.FanNativeStep: slotted RCCL groups on the boundary
+communicators, DP buckets of the replicated stages) executed by the gloo plan interpreter
+trains bit for bit like the op-by-op Python executor (FanPipe)."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+SPEC = "784-256-128-64-10"
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, dist_, reps, M, dp_reduce, use_interp, steps, out_dir, tag):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DNN_DP_DEFER="0")
+    import torch.distributed as dist
+
+    from docker_dist_nn_amd import MLPSpec
+    from docker_dist_nn_amd.data import synthetic_mnist
+    from docker_dist_nn_amd.engine import OptimConfig
+    from docker_dist_nn_amd.engine.fan_trainer import FanTrainer
+    from docker_dist_nn_amd.parallel.fan import FanLayout, FanNativeStep, build_fan_mesh
+    from docker_dist_nn_amd.parallel.plan_interp import PlanInterpreter
+
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lay = FanLayout(tuple(dist_), tuple(reps))
+    mesh = build_fan_mesh(lay)
+    mb = 256
+    tr = FanTrainer(MLPSpec.parse(SPEC), lay, mesh, micro_batch=mb, num_micro=M, device=dev,
+                    dp_reduce=dp_reduce, optim=OptimConfig(name="sgd", lr=0.05, momentum=0.9))
+    assert tr.native_step is None  # gloo: the Python executor, unless interpreted below
+    it = None
+    if use_interp:
+        names = {"f_in": mesh.fwd_in, "f_out": mesh.fwd_out, "b_in": mesh.bwd_in,
+                 "b_out": mesh.bwd_out, "dp": mesh.dp_group}
+        comms = {k: k for k, g in names.items() if g is not None}
+        groups = {k: g for k, g in names.items() if g is not None}
+        ns = FanNativeStep(tr.executor, mesh, tr.sched, comms=comms, build_only=True)
+        it = PlanInterpreter(ns, groups, timeout_s=60)
+    x, y = synthetic_mnist(mb * M, seed=3)
+    xt = torch.zeros(mb * M, 832, dtype=torch.bfloat16)
+    xt[:, :784] = torch.from_numpy(x).to(torch.bfloat16)
+    xt, yt = xt.to(dev), torch.from_numpy(y).to(dev)
+    for _ in range(steps):
+        tr.set_global_batch(xt, yt)
+        if it is None:
+            tr.step()
+        else:
+            for st in tr.stages:
+                st.begin_step()
+            it.run_step()
+    torch.cuda.synchronize()
+    for k, (w, b) in tr.local_weights().items():
+        if mesh.replica == 0:
+            np.save(os.path.join(out_dir, f"{tag}_w{k}.npy"), w)
+            np.save(os.path.join(out_dir, f"{tag}_b{k}.npy"), b)
+    if tr.last is not None:
+        np.save(os.path.join(out_dir, f"{tag}_loss{mesh.replica}.npy"), np.array([tr.loss()]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("dist_,reps,M,dp_reduce", [([1, 3], [3, 1], 7, "allreduce"),
+                                                    ([2, 2], [1, 3], 6, "shard"),
+                                                    ([1, 1, 2], [2, 1, 2], 5, "allreduce")])
+def test_fan_plan_interpreted_bitwise_equals_python(dev, dist_, reps, M, dp_reduce):
+    world, steps = sum(reps), 3
+    with tempfile.TemporaryDirectory() as d:
+        for use, tag in ((False, "py"), (True, "plan")):
+            mp.start_processes(_worker, args=(world, _port(), dist_, reps, M, dp_reduce, use,
+                                              steps, d, tag),
+                               nprocs=world, join=True, start_method="spawn")
+        for k in range(4):
+            for wb in ("w", "b"):
+                a = np.load(os.path.join(d, f"py_{wb}{k}.npy"))
+                b = np.load(os.path.join(d, f"plan_{wb}{k}.npy"))
+                assert np.array_equal(a, b), (wb, k)
+        for q in range(reps[-1]):
+            assert np.array_equal(np.load(os.path.join(d, f"py_loss{q}.npy")),
+                                  np.load(os.path.join(d, f"plan_loss{q}.npy")))
