@@ -53,6 +53,7 @@ from docker_dist_nn_amd import ladder, switches  # noqa: E402
 from docker_dist_nn_amd.faults import FaultInjector  # noqa: E402
 from docker_dist_nn_amd.data import DeviceDataset, synthetic_mnist  # noqa: E402
 from docker_dist_nn_amd.engine import OptimConfig, Trainer  # noqa: E402
+from docker_dist_nn_amd.parallel.fan import FanLayout, parse_fan  # noqa: E402
 from docker_dist_nn_amd.parallel.planner import Planner, parse_parallelism  # noqa: E402
 
 METRIC = "samples/sec (whole node) MNIST FCNN training at 1/2/4/8-stage pipeline"
@@ -112,15 +113,38 @@ def _plan(a, spec, n, world, text):
     planner = Planner.calibrated(spec, relays=relays,
                                  dp_grad_bytes=2.0 if a.dp_reduce == "shard" else 4.0)
     loopback = world == 1
-    pp, dp = parse_parallelism(text, n, loopback=loopback)
+    fan = parse_fan(text)
+    if fan is not None:  # 'fan:1x1,2x7' (layers x GPUs per stage) or 'fan:1,7' (GPUs only)
+        dist_, reps = fan
+        if not reps or sum(reps) != n:
+            raise SystemExit(f"--parallelism {text}: the replica counts must add up to {n}")
+        if not dist_:
+            from docker_dist_nn_amd.parallel.planner import compositions
+
+            dist_ = max(compositions(len(spec.layers), len(reps)),
+                        key=lambda d: planner.evaluate_fan(spec, d, reps, a.batch).samples_per_s)
+        return planner.evaluate_fan(spec, dist_, reps, a.batch)
+    pp, dp = parse_parallelism("pipeline" if text == "uniform" else text, n, loopback=loopback)
     if pp is None:
         if text == "best":
             return planner.best(spec, n, a.batch)
         if n == 1:
             return planner.evaluate(spec, 1, 1, a.batch)
-        return planner.pipeline_layout(spec, n, a.batch)
+        if text == "uniform" or loopback:  # the literal ppS x dpD grid (BASELINE's layouts)
+            return planner.pipeline_layout(spec, n, a.batch)
+        # the pipeline the planner scores best over every layer split and every split of
+        # the GPUs into per-stage replica groups (parallel/fan.py; equal counts = ppS x dpD)
+        return planner.best_fan(spec, n, a.batch)
     rows = a.batch * (1 if loopback else pp)  # loopback: every stage on the one GPU
     return planner.evaluate(spec, pp, dp, rows, loopback=loopback)
+
+
+def _uniform_prediction(a, spec, n, world):
+    if n < 2 or a.parallelism not in ("pipeline", "auto"):
+        return None
+    p = _plan(a, spec, n, world, "uniform")
+    return {"parallelism": p.parallelism, "layer_distribution": p.distribution,
+            "planner_predicted": round(p.samples_per_s, 1)}
 
 
 def first_step_guard(tr, one_step, dev, timeout_s):
@@ -155,33 +179,64 @@ def first_step_guard(tr, one_step, dev, timeout_s):
 def measure(a, spec, n, world, dev, text):
     """Build the trainer for one layout, W warm-up + K timed steps; returns the JSON fields."""
     plan = _plan(a, spec, n, world, text)
+    fan = plan.reps is not None and len(set(plan.reps)) > 1
+    if fan and world != sum(plan.reps):
+        raise SystemExit(f"fan layout {plan.parallelism} needs {sum(plan.reps)} ranks")
+    if plan.reps is not None and not fan:  # equal replica counts: the uniform ppS x dpD grid
+        plan.dp = plan.reps[0]
+        plan.reps = None
     mb = a.micro or plan.micro_batch
-    rows = a.batch * (1 if world == 1 else plan.pp)  # rows per replica per step
-    nm = max(1, rows // mb)
-    if mb * nm != rows or mb % 64:
-        raise SystemExit(f"batch {rows} must split into micro-batches of a multiple of 64")
+    if fan:  # replicated-stage pipeline (parallel/fan.py): nm = the GLOBAL micro-batch count
+        rows = nm = None
+        nm = max(1, plan.micro_batch * plan.num_micro // mb)
+        if mb * nm != plan.micro_batch * plan.num_micro or mb % 64:
+            raise SystemExit(f"batch {plan.micro_batch * plan.num_micro} must split into "
+                             "micro-batches of a multiple of 64")
+    else:
+        rows = a.batch * (1 if world == 1 else plan.pp)  # rows per replica per step
+        nm = max(1, rows // mb)
+        if mb * nm != rows or mb % 64:
+            raise SystemExit(f"batch {rows} must split into micro-batches of a multiple of 64")
     mesh = None
-    if world > 1:
-        from docker_dist_nn_amd.parallel.groups import build_mesh
+    if fan:
+        from docker_dist_nn_amd.data import FanDataset
+        from docker_dist_nn_amd.engine.fan_trainer import FanTrainer
+        from docker_dist_nn_amd.parallel.fan import build_fan_mesh
 
-        mesh = build_mesh(plan.pp, plan.dp)
-        # communicator set-up happens at a group's first collective: do it here, outside the
-        # W warm-up steps and the timed region
-        t = torch.ones(1024, device=dev)
-        for g in (mesh.fwd_group, mesh.bwd_group, mesh.dp_group, None):
-            torch.distributed.all_reduce(t, group=g)
-        torch.cuda.synchronize(dev)
-    sched = a.schedule
-    if sched == "auto":
-        sched = "1f1b_lh" if world > 1 and plan.pp > 1 else "1f1b"
-    tr = Trainer(spec, micro_batch=mb, num_micro=nm, distribution=plan.distribution,
-                 pp=plan.pp, dp=plan.dp, schedule=sched,
-                 optim=OptimConfig(name=a.optimizer, lr=a.lr),
-                 device=dev, seed=a.seed, mesh=mesh, boundary=a.boundary,
-                 dp_reduce=a.dp_reduce)
-    replica = mesh.replica if mesh else 0
-    x, y = synthetic_mnist(max(60000, 2 * rows), seed=a.seed + 1000 * replica)
-    data = DeviceDataset(x, y, rows, dev, kp=tr.stages[0].x_in.shape[1] if tr.first else None)
+        lay = FanLayout(tuple(plan.distribution), tuple(plan.reps))
+        mesh = build_fan_mesh(lay)
+        sched = "fan"
+        tr = FanTrainer(spec, lay, mesh, micro_batch=mb, num_micro=nm,
+                        optim=OptimConfig(name=a.optimizer, lr=a.lr), device=dev, seed=a.seed,
+                        dp_reduce=a.dp_reduce)
+        data = FanDataset(lay.local_micros(mesh.stage, mesh.replica, nm), mb, dev,
+                          kp=tr.stages[0].x_in.shape[1] if tr.first else None, seed=a.seed,
+                          inputs=tr.first is not None, labels=tr.last is not None)
+        global_batch = mb * nm
+    else:
+        if world > 1:
+            from docker_dist_nn_amd.parallel.groups import build_mesh
+
+            mesh = build_mesh(plan.pp, plan.dp)
+            # communicator set-up happens at a group's first collective: do it here, outside
+            # the W warm-up steps and the timed region
+            t = torch.ones(1024, device=dev)
+            for g in (mesh.fwd_group, mesh.bwd_group, mesh.dp_group, None):
+                torch.distributed.all_reduce(t, group=g)
+            torch.cuda.synchronize(dev)
+        sched = a.schedule
+        if sched == "auto":
+            sched = "1f1b_lh" if world > 1 and plan.pp > 1 else "1f1b"
+        tr = Trainer(spec, micro_batch=mb, num_micro=nm, distribution=plan.distribution,
+                     pp=plan.pp, dp=plan.dp, schedule=sched,
+                     optim=OptimConfig(name=a.optimizer, lr=a.lr),
+                     device=dev, seed=a.seed, mesh=mesh, boundary=a.boundary,
+                     dp_reduce=a.dp_reduce)
+        replica = mesh.replica if mesh else 0
+        x, y = synthetic_mnist(max(60000, 2 * rows), seed=a.seed + 1000 * replica)
+        data = DeviceDataset(x, y, rows, dev,
+                             kp=tr.stages[0].x_in.shape[1] if tr.first else None)
+        global_batch = rows * plan.dp
 
     # --graph: the step as a HIP graph (one GPU, or a native multi-rank step: opt-in, the
     # plan's flag waits are kernels so the whole rank step -- hops included -- is captured)
@@ -264,23 +319,28 @@ def measure(a, spec, n, world, dev, text):
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     loss = tr.loss()
-    if world > 1:  # the last stage of replica 0 owns the loss; rank 0 prints
+    if world > 1 and fan:  # the last stage's replicas hold shares of the global mean loss
+        lt = torch.tensor([loss if loss is not None else 0.0], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(lt)
+        loss = float(lt.item())
+    elif world > 1:  # the last stage of replica 0 owns the loss; rank 0 prints
         lt = torch.tensor([loss if loss is not None else -1.0], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(lt, op=torch.distributed.ReduceOp.MAX)
         loss = float(lt.item())
-    global_batch = rows * plan.dp
     value = global_batch * a.steps / elapsed
     out = {
         "value": round(value, 1), "ms_per_step": round(elapsed / a.steps * 1e3, 4),
         "global_batch": global_batch,
         "parallelism": plan.parallelism + ("-loopback" if world == 1 and plan.pp > 1 else ""),
         "layer_distribution": plan.distribution, "micro_batch": mb, "num_micro": nm,
+        "stage_gpus": plan.reps if fan else None,
         "schedule": sched if plan.pp > 1 else "none",
         "transport": tr.transport, "transport_reason": tr.transport_reason,
         "native_step": tr.native_step is not None or world == 1,
         "rccl_plan": tr.native_step.mode if tr.native_step is not None else None,
         "native_fallback": tr.native_fallback,
-        "boundary": tr.boundary, "dp_reduce": tr.dp_reduce if plan.dp > 1 else None,
+        "boundary": tr.boundary,
+        "dp_reduce": tr.dp_reduce if (plan.dp > 1 or (fan and max(plan.reps) > 1)) else None,
         "hip_graph": use_graph, "graph_copies": a.graph_copies if use_graph else 0,
         "graph_trial": graph_trial, "host_ms_per_step": round(host_s / a.steps * 1e3, 4),
         "step_ms": ([round(e0.elapsed_time(e1), 4) for e0, e1 in zip(evs, evs[1:])]
@@ -385,7 +445,13 @@ def supervise(a, argv) -> int:
     if a.parallelism.startswith("tp"):
         rungs = [ladder.Rung("default")]
     else:
-        rungs = ladder.bench_rungs(world, dp_only=a.parallelism.startswith("dp"))
+        # the planner runs on the CPU: the supervisor knows whether the default layout is a
+        # replicated-stage pipeline without touching the GPU
+        spec = NAMED_MODELS.get(a.model) or MLPSpec.parse(a.model)
+        is_fan = (not a.parallelism.startswith("dp") and
+                  _plan(a, spec, world, world, a.parallelism).reps is not None and
+                  len(set(_plan(a, spec, world, world, a.parallelism).reps)) > 1)
+        rungs = ladder.bench_rungs(world, dp_only=a.parallelism.startswith("dp"), fan=is_fan)
     res, rung = sup.climb(rungs, budget_s=float(switches.get("DNN_LADDER_BUDGET")))
     st.update(res=res, rung=rung.name if rung else None, attempts=list(sup.attempts))
     if res is not None and not a.no_dp_compare and \
@@ -462,7 +528,8 @@ def main(argv=None):
             "model": MODEL_LABEL.get(a.model, spec.describe()),
             "global_batch": m["global_batch"],
             "seq_len": None,
-            **{k: m[k] for k in ("parallelism", "layer_distribution", "micro_batch", "num_micro",
+            **{k: m.get(k) for k in ("parallelism", "layer_distribution", "stage_gpus",
+                                 "micro_batch", "num_micro",
                                  "schedule", "transport", "transport_reason", "native_step",
                                  "rccl_plan",
                                  "boundary", "dp_reduce", "hip_graph", "graph_copies")},
@@ -476,6 +543,9 @@ def main(argv=None):
         **({"step_ms": m["step_ms"]} if m.get("step_ms") else {}),
         "graph_trial": m.get("graph_trial"),
         "dp_only": dp_only,
+        # the literal uniform ppS x dpD grid of BASELINE.json, predicted by the same planner
+        # (measured with --parallelism uniform)
+        "uniform_pipeline": _uniform_prediction(a, spec, n, world),
         "native_fallback": m["native_fallback"],  # why the Python executor ran, if it did
         "switches": switches.active(),  # non-default DNN_* switches of this run
     }

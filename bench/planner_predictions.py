@@ -1,7 +1,9 @@
 """Planner predictions for every BASELINE config at N = 1, 2, 4, 8 GPUs (weak scaling):
-the pipeline layout bench.py runs (bf16 and fp8 hops) and the data-parallel-only layout.
+the uniform pipeline (bf16 and fp8 hops, relays), the best replicated-stage ("fan") pipeline
+bench.py runs (parallel/fan.py; bf16 hops, direct links), and the data-parallel-only layout,
+each with its efficiency against N x the one-GPU rate.
 
-    python bench/planner_predictions.py > profiles/r4_planner/predictions.jsonl
+    python bench/planner_predictions.py > profiles/r5_planner/predictions.jsonl
 """
 from __future__ import annotations
 
@@ -30,6 +32,9 @@ def main():
             c = pr.evaluate(spec, a.pp, a.dp, rows * a.pp, distribution=a.distribution)
             e = pa.pipeline_layout(spec, n, rows)
             d = pl.evaluate(spec, 1, n, rows)
+            one = pl.evaluate(spec, 1, 1, rows).samples_per_s
+            f = pl.best_fan(spec, n, rows) if n > 1 else a
+            f8 = p8.best_fan(spec, n, rows) if n > 1 else a
             print(json.dumps({"model": model, "n": n, "layout": a.parallelism,
                               "dist": a.distribution, "nm": a.num_micro,
                               "pipe_bf16_Msps": round(a.samples_per_s / 1e6, 1),
@@ -37,7 +42,17 @@ def main():
                               "pipe_ipc_relay2_Msps": round(c.samples_per_s / 1e6, 1),
                               "pipe_ipc_planned_Msps": round(e.samples_per_s / 1e6, 1),
                               "planned_dist": e.distribution,
+                              "fan_layout": f.parallelism, "fan_dist": f.distribution,
+                              "fan_reps": f.reps, "fan_nm": f.num_micro,
+                              "fan_bf16_Msps": round(f.samples_per_s / 1e6, 1),
+                              "fan_eff": round(f.samples_per_s / (n * one), 3),
+                              "fan_detail": f.detail if n > 1 else None,
+                              "fan_fp8_layout": f8.parallelism,
+                              "fan_fp8_Msps": round(f8.samples_per_s / 1e6, 1),
+                              "fan_fp8_eff": round(f8.samples_per_s / (n * one), 3),
+                              "uniform_eff": round(a.samples_per_s / (n * one), 3),
                               "dp_only_Msps": round(d.samples_per_s / 1e6, 1),
+                              "dp_eff": round(d.samples_per_s / (n * one), 3),
                               "dp_allreduce_ms": d.detail["allreduce_ms"]}))
 
 

@@ -145,3 +145,33 @@ class DeviceDataset:
         b = i % self.num_batches
         r0 = b * self.batch_rows
         return self.x[r0:r0 + self.batch_rows], self.labels[r0:r0 + self.batch_rows]
+
+
+class FanDataset:
+    """The rows one rank of a replicated-stage pipeline (parallel/fan.py) holds: micro-batch j
+    of the global batch is ``synthetic_mnist(mb, seed + 7919 * b + j)`` for alternating batch
+    b in {0, 1}, so the first stage's replica of j and the last stage's replica of j -- on
+    different ranks -- hold the inputs and labels of the SAME samples without any rank
+    generating the whole global batch. ``batch(i)`` returns this rank's rows (its
+    micro-batches in local order), resident in HBM like DeviceDataset."""
+
+    def __init__(self, micros, mb: int, device: torch.device, kp: Optional[int] = None,
+                 seed: int = 0, inputs: bool = True, labels: bool = True):
+        self.batches = []
+        for b in range(2):
+            xs, ys = [], []
+            for j in micros:
+                x, y = synthetic_mnist(mb, seed=seed + 7919 * b + j)
+                xs.append(x)
+                ys.append(y)
+            dim = xs[0].shape[1]
+            kpp = kp or round_up(dim, 64)
+            xt = None
+            if inputs:
+                xt = torch.zeros(len(micros) * mb, kpp, dtype=torch.bfloat16, device=device)
+                xt[:, :dim] = torch.from_numpy(np.concatenate(xs)).to(device, torch.bfloat16)
+            yt = torch.from_numpy(np.concatenate(ys)).to(device) if labels else None
+            self.batches.append((xt, yt))
+
+    def batch(self, i: int):
+        return self.batches[i % 2]

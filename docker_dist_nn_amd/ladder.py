@@ -33,6 +33,10 @@ Rungs of the training benchmark (``bench_rungs``), most capable first:
   4. ``rccl-streams``  -- RCCL, one stream + communicator per link channel;
   5. ``python``        -- the Python executor over torch.distributed P2P;
   6. ``dp-native`` / ``dp-python`` -- data parallelism only (no pipeline hops at all).
+
+When the default layout is a replicated-stage pipeline (parallel/fan.py) the rungs are
+``default`` (its native slotted RCCL step) -> ``fan-python`` -> ``uniform-rccl-slotted`` /
+``uniform-python`` (the literal ppS x dpD grid) -> ``dp-native`` / ``dp-python``.
 """
 from __future__ import annotations
 
@@ -58,9 +62,11 @@ class Rung:
     args: list = field(default_factory=list)    # extra command-line arguments (appended)
 
 
-def bench_rungs(n: int, dp_only: bool = False) -> list[Rung]:
+def bench_rungs(n: int, dp_only: bool = False, fan: bool = False) -> list[Rung]:
     """The training benchmark's ladder for ``n`` ranks. ``dp_only``: the layout is already
-    data-parallel (no hops), only the executor can fall back."""
+    data-parallel (no hops), only the executor can fall back. ``fan``: the default layout is
+    a replicated-stage pipeline (parallel/fan.py: RCCL slotted plan, no IPC form): its Python
+    executor, then the uniform ppS x dpD grid with its own rungs, then data parallelism."""
     # every rung after the first replays eagerly: a failed first attempt may have been the
     # graph replay itself (bench --graph auto)
     eager = ["--graph", "off"]
@@ -68,6 +74,14 @@ def bench_rungs(n: int, dp_only: bool = False) -> list[Rung]:
           Rung("dp-python", {"DNN_NATIVE_DIST": "0"}, ["--parallelism", f"dp{n}", *eager])]
     if dp_only:
         return dp
+    if fan:
+        uni = ["--parallelism", "uniform", *eager]
+        return [Rung("default"),
+                Rung("fan-python", {"DNN_NATIVE_DIST": "0"}, eager),
+                Rung("uniform-rccl-slotted", {"DNN_PIPE": "rccl", "DNN_RCCL_PLAN": "slotted"},
+                     uni),
+                Rung("uniform-python", {"DNN_PIPE": "rccl", "DNN_NATIVE_DIST": "0"}, uni),
+                *dp]
     return [Rung("default"),
             Rung("ipc-slotted", {"DNN_IPC_PLAN": "slotted"}, eager),
             Rung("rccl-slotted", {"DNN_PIPE": "rccl", "DNN_RCCL_PLAN": "slotted"}, eager),

@@ -25,6 +25,7 @@ WIDTH (hop bytes) against compute balance, not FLOPs alone. ``best`` searches ev
 from __future__ import annotations
 
 import itertools
+import math
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -41,9 +42,15 @@ class Plan:
     step_time_s: float
     samples_per_s: float
     detail: dict = field(default_factory=dict)
+    reps: Optional[list] = None  # fan layout: GPUs per stage (parallel/fan.py)
 
     @property
     def parallelism(self) -> str:
+        if self.reps is not None and len(set(self.reps)) > 1:
+            return "fan" + ",".join(f"{k}x{r}" for k, r in zip(self.distribution, self.reps))
+        if self.reps is not None:  # equal replica counts: the uniform grid
+            d = self.reps[0]
+            return f"pp{self.pp}" + (f"dp{d}" if d > 1 else "")
         if self.pp == 1:
             return f"dp{self.dp}"
         if self.dp == 1:
@@ -205,6 +212,84 @@ class Planner:
         if not cands:
             raise ValueError(f"no valid layout for {n_gpus} GPUs and {len(spec.layers)} layers")
         return max(cands, key=lambda p: p.samples_per_s)
+
+    # ---- replicated-stage ("fan") pipelines (parallel/fan.py) -----------------------------
+    def evaluate_fan(self, spec: MLPSpec, dist: list[int], reps: list[int], rows_per_gpu: int,
+                     num_micro: Optional[int] = None) -> Plan:
+        """Predicted step of a fan layout: stage s (layers dist[s]) on reps[s] GPUs, micro-batch
+        j on replica j % r_s of every stage (parallel/fan.py).
+
+        * compute: a replica of stage s runs ceil(M / r_s) micro-batches of ``c_s`` each;
+        * hops: the pair (producer p, consumer c) of boundary b carries the micro-batches with
+          j % r_b == p and j % r_{b+1} == c over its own direct xGMI link (every GPU pair of an
+          MI355X node has one), forward and backward on the two directions; the slowest pair
+          bounds the boundary (``link_gbps`` per direction, ``hop_latency_us`` per message);
+        * the pipeline fills and drains once per step: one micro-batch's trip through every
+          other stage and hop;
+        * a replicated stage exchanges its gradient over its own DP group of r_s GPUs (half
+          hidden behind the weight gradients, as ``evaluate``)."""
+        from .fan import lcm_reps
+
+        S, N = len(reps), sum(reps)
+        L = spec.layers
+        G = rows_per_gpu * N
+        if num_micro is None:  # ~8 micro-batches per GPU: GEMMs of >= 8192 rows at 65536
+            num_micro = max(8 * N, 2 * max(reps))
+            while G % num_micro or (G // num_micro) % 64:
+                num_micro += 1
+                if num_micro > G // 64:
+                    num_micro = max(reps)
+                    break
+        M = num_micro
+        mb = G // M
+        fl = layer_train_flops(spec)
+        comp, g = [], 0
+        for k in dist:
+            comp.append(sum(fl[g:g + k]) * mb / self.rate)
+            g += k
+        busy = [math.ceil(M / r) * c for r, c in zip(reps, comp)]
+        hops, g = [], 0
+        for b in range(S - 1):
+            g += dist[b]
+            width = L[g - 1].out_dim
+            per_msg = self.lat + mb * width * self.bb / self.link
+            ra, rb = reps[b], reps[b + 1]
+            most = max(sum(1 for j in range(M) if j % ra == p and j % rb == c)
+                       for p in range(ra) for c in range(rb))
+            hops.append((most * per_msg, per_msg))
+        fill = sum(comp) - max(comp) + 2 * sum(h[1] for h in hops)
+        pipe = max(busy + [h[0] for h in hops]) + fill
+        ar, g = 0.0, 0
+        for k, r in zip(dist, reps):
+            params = sum(l.params for l in L[g:g + k])
+            g += k
+            if r > 1:
+                ar = max(ar, 2 * (r - 1) / r * params * self.gb / self.ar)
+        t = pipe + 0.5 * ar + self.ovh
+        detail = {"fan_reps": list(reps), "stage_ms_per_micro": [round(c * 1e3, 4) for c in comp],
+                  "stage_busy_ms": [round(x * 1e3, 4) for x in busy],
+                  "boundary_link_ms": [round(h[0] * 1e3, 4) for h in hops],
+                  "fill_ms": round(fill * 1e3, 4), "allreduce_ms": round(ar * 1e3, 4),
+                  "lcm_reps": lcm_reps(reps)}
+        plan = Plan(S, 1, list(dist), M, mb, t, G / t, detail)
+        plan.reps = list(reps)
+        return plan
+
+    def best_fan(self, spec: MLPSpec, n_gpus: int, rows_per_gpu: int,
+                 min_stages: int = 2) -> Plan:
+        """The best fan layout with at least ``min_stages`` stages over every contiguous layer
+        split and every split of the N GPUs (uniform ppS x dpD is the case of equal replica
+        counts; a single stage is plain data parallelism)."""
+        best = None
+        for S in range(min_stages, min(n_gpus, len(spec.layers)) + 1):
+            for dist in compositions(len(spec.layers), S):
+                for reps in compositions(n_gpus, S):
+                    p = self.evaluate_fan(spec, dist, reps, rows_per_gpu)
+                    if best is None or p.samples_per_s > best.samples_per_s:
+                        best = p
+        if best is None:
+            raise ValueError(f"no fan layout of >= {min_stages} stages for {n_gpus} GPUs")
+        return best
 
     def pipeline_layout(self, spec: MLPSpec, n_gpus: int, rows_per_gpu: int) -> Plan:
         """The deepest pipeline for N GPUs: pp = largest divisor of N that is <= #layers,

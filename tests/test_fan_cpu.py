@@ -255,3 +255,27 @@ def test_fan_native_plans_deadlock_free_with_one_rccl_kernel(dist_, reps, dp_red
     assert sorted(sends) == sorted(recvs)
     lay = FanLayout(tuple(dist_), tuple(reps))
     assert len(sends) == 2 * M * (lay.S - 1)
+
+
+def test_bench_plans_fan_layouts_at_the_default_batch():
+    """What bench.py runs by default across GPUs (the planner's best replicated-stage pipeline)
+    and the uniform grid it reports beside it."""
+    import importlib.util
+    import os as _os
+
+    root = _os.path.dirname(_os.path.dirname(_os.path.abspath(__file__)))
+    sp = importlib.util.spec_from_file_location("bench_mod", _os.path.join(root, "bench.py"))
+    b = importlib.util.module_from_spec(sp)
+    sp.loader.exec_module(b)
+    from docker_dist_nn_amd import NAMED_MODELS
+
+    a = b.parse_args(["--gpus", "8"])
+    spec = NAMED_MODELS["mnist-fcnn"]
+    assert b._plan(a, spec, 4, 4, "pipeline").parallelism == "fan3x3,1x1"
+    assert b._plan(a, spec, 8, 8, "pipeline").parallelism == "fan3x7,1x1"
+    assert b._plan(a, spec, 2, 2, "pipeline").parallelism == "pp2"
+    assert b._uniform_prediction(a, spec, 4, 4)["parallelism"] == "pp4"
+    w = NAMED_MODELS["wide"]
+    assert b._plan(a, w, 8, 8, "pipeline").parallelism == "fan1x1,2x7"
+    p = b._plan(a, spec, 4, 4, "fan:3x3,1x1")
+    assert p.reps == [3, 1] and p.distribution == [3, 1]

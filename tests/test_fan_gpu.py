@@ -94,3 +94,34 @@ def test_fan_plan_interpreted_bitwise_equals_python(dev, dist_, reps, M, dp_redu
         for q in range(reps[-1]):
             assert np.array_equal(np.load(os.path.join(d, f"py_loss{q}.npy")),
                                   np.load(os.path.join(d, f"plan_loss{q}.npy")))
+
+
+@pytest.mark.timeout(300)
+def test_bench_runs_the_fan_layout(tmp_path):
+    """bench.py at N = 4 (four ranks sharing cuda:0 over gloo, launched by torch.distributed.run
+    as the driver launches it) runs the replicated-stage layout the planner picks for the
+    headline model at the default batch (tests/test_fan_cpu.py) -- 3 layers on three GPUs, the
+    classifier layer on one -- through the ladder (at a small batch here), and reports it with
+    a uniform pipeline grid's prediction beside it."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, DNN_FORCE_DEVICE="0", DNN_DIST_BACKEND="gloo", TMPDIR=str(tmp_path))
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "4", "--master-addr", "127.0.0.1",
+                        "--master-port", str(_port()), os.path.join(root, "bench.py"),
+                        "--gpus", "4", "--steps", "3", "--warmup", "1", "--batch", "4096",
+                        "--parallelism", "fan:3x3,1x1", "--no-dp-compare"],
+                       env=env, stdout=subprocess.PIPE, stderr=None, text=True, timeout=280,
+                       cwd=root)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert r.returncode == 0 and len(lines) == 1, r.stdout[-3000:]
+    out = json.loads(lines[0])
+    assert out["value"] > 0 and out["n_gpus"] == 4
+    assert out["config"]["parallelism"] == "fan3x3,1x1", out["config"]
+    assert out["config"]["stage_gpus"] == [3, 1]
+    assert out["ladder"]["rung"] == "default"
+    assert out["ladder"]["attempts"][0]["rung"] == "default"
+    assert 0 < out["last_loss"] < 10

@@ -189,3 +189,12 @@ def test_ladder_sigterm_still_prints_one_line(tmp_path):
     lines = [l for l in out.splitlines() if l.startswith("{")]
     assert len(lines) == 1, (out, err[-3000:])
     assert json.loads(lines[0])["terminated"] == "terminated"
+
+
+def test_fan_rungs():
+    from docker_dist_nn_amd.ladder import bench_rungs
+
+    names = [r.name for r in bench_rungs(8, fan=True)]
+    assert names == ["default", "fan-python", "uniform-rccl-slotted", "uniform-python",
+                     "dp-native", "dp-python"]
+    assert "--parallelism" in bench_rungs(8, fan=True)[2].args
