@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cstring>
 #include <stdexcept>
+#include <map>
 #include <string>
 #include <tuple>
 #include <vector>
@@ -723,16 +724,46 @@ PYBIND11_MODULE(_native, m) {
   m.def(
       "run_plan",
       [](const std::vector<std::tuple<const dnn::Program*, std::string, int>>& plan,
-         uintptr_t stream, uintptr_t side) {
+         uintptr_t stream, uintptr_t side, bool device_fence) {
         py::gil_scoped_release nogil;
-        static thread_local hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+        // fork / join events: both streams are on this device, so the ordering needs no
+        // system-scope fence (cache write-back / invalidate at every record: the ~6 us
+        // "event packets" of profiles/r2_sched). device_fence = hipEventDisableSystemFence.
+        static thread_local hipEvent_t evs[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};
+        hipEvent_t& ev_fork = evs[device_fence][0];
+        hipEvent_t& ev_join = evs[device_fence][1];
         if (!ev_fork) {
-          if (hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming) != hipSuccess ||
-              hipEventCreateWithFlags(&ev_join, hipEventDisableTiming) != hipSuccess)
+          const unsigned fl =
+              hipEventDisableTiming | (device_fence ? hipEventDisableSystemFence : 0u);
+          if (hipEventCreateWithFlags(&ev_fork, fl) != hipSuccess ||
+              hipEventCreateWithFlags(&ev_join, fl) != hipSuccess)
             throw std::runtime_error("run_plan: hipEventCreate failed");
         }
+        // cross-step events ("@xmark:<k>" records on the side stream, "@xwait:<k>" makes the
+        // main stream wait on the LAST such record -- possibly made by the previous step's
+        // call: a step's first kernels overlap the previous step's side-stream tail)
+        static thread_local std::map<std::string, hipEvent_t> xev[2];
+        auto xevent = [&](const std::string& k) {
+          hipEvent_t& e = xev[device_fence][k];
+          if (!e) {
+            const unsigned fl =
+                hipEventDisableTiming | (device_fence ? hipEventDisableSystemFence : 0u);
+            if (hipEventCreateWithFlags(&e, fl) != hipSuccess)
+              throw std::runtime_error("run_plan: hipEventCreate failed");
+          }
+          return e;
+        };
         std::vector<std::string> one(1);
         for (const auto& [pr, seg, si] : plan) {
+          if (seg.rfind("@xmark:", 0) == 0 || seg.rfind("@xwait:", 0) == 0) {
+            if (!side) throw std::invalid_argument("run_plan: cross-step event without a side");
+            hipEvent_t e = xevent(seg.substr(7));
+            const bool mark = seg[2] == 'm';
+            if ((mark ? hipEventRecord(e, S(side)) : hipStreamWaitEvent(S(stream), e, 0)) !=
+                hipSuccess)
+              throw std::runtime_error("run_plan: cross-step event failed");
+            continue;
+          }
           if (seg == "@rewait") {  // side waits on the last fork again: a side-queue packet only
             if (!side || hipStreamWaitEvent(S(side), ev_fork, 0) != hipSuccess)
               throw std::runtime_error("run_plan: @rewait failed");
@@ -751,7 +782,7 @@ PYBIND11_MODULE(_native, m) {
           pr->run(one, si ? S(side) : S(stream));
         }
       },
-      py::arg("plan"), py::arg("stream"), py::arg("side") = 0);
+      py::arg("plan"), py::arg("stream"), py::arg("side") = 0, py::arg("device_fence") = false);
   m.def("record_begin", [](dnn::Program& pr) {
     if (dnn::recording_program()) throw std::runtime_error("already recording a Program");
     dnn::recording_program() = &pr;

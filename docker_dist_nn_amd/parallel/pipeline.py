@@ -259,6 +259,7 @@ class PipelineExecutor:
 
     def flush(self) -> None:
         """Apply every deferred update now (end of training / before reading weights)."""
+        self.xstep_join()
         for st in self.stages:
             pend = self._pending.pop(id(st), None)
             if pend is not None:
@@ -576,6 +577,9 @@ class PipelineExecutor:
                     st.params.step_count += 1
                 self.pipe.end_step()
                 return
+        if plan is not None and len(self.stages) == 1 and \
+                not getattr(self, "capturing", False) and switches.get("DNN_XSTEP") == "1":
+            plan = self._xstep_plan(plan)
         if plan is not None:
             dev = self.stages[0].device
             for st in self.stages:
@@ -599,7 +603,8 @@ class PipelineExecutor:
             native().run_plan([(st._prog if st is not None else None, seg, si)
                                for st, seg, si in plan],
                               main.cuda_stream,
-                              self._side.cuda_stream if self._side is not None else 0)
+                              self._side.cuda_stream if self._side is not None else 0,
+                              switches.get("DNN_EVENT_FENCE") == "device")
             if main is not cur:
                 cur.wait_stream(main)
             for st in self.stages:
@@ -614,6 +619,52 @@ class PipelineExecutor:
         else:
             self._run_interleaved()
         self.pipe.end_step()
+
+    def _xstep_plan(self, plan):
+        """Cross-step overlap of a single-stage overlap plan (DNN_XSTEP=1): the step no longer
+        ends with a join of the side stream. The side stream marks "w" after its last weight
+        gradient and "end" after its last op (the reduce + update of layers 1..L-1); the NEXT
+        step waits for "w" before its layer-0 forward (which overwrites the activation those
+        weight gradients read) and for "end" only before its layer-1 forward (which needs the
+        updated W_1). So the next step's first GEMM runs beside this step's side-stream tail
+        instead of after it. Bitwise the same step (only the join moves); applied only to plans
+        of the form [F0, ..., side W's, ..., main FINO0-0, @join] (split reduction)."""
+        if getattr(self, "_xplan_src", None) is plan:
+            out = self._xplan
+        else:
+            out = None
+            st = self.stages[0]
+            L = len(st.geoms)
+            side_w = [k for k, e in enumerate(plan) if e[2] == 1 and e[1].startswith("W")]
+            if (plan and plan[0][1] == "F0" and plan[-1][1] == "@join" and side_w and
+                    plan[-2][1] == "FINO0-0" and all(f"F0.L{i}" in st._prog.segments()
+                                                     for i in range(L))):
+                out = [(None, "@xwait:w", 0), (st, "F0.L0", 0), (None, "@xwait:end", 0)]
+                out += [(st, f"F0.L{i}", 0) for i in range(1, L)]
+                last_w = side_w[-1]
+                for k, e in enumerate(plan[1:-1], start=1):
+                    out.append(e)
+                    if k == last_w:
+                        out.append((None, "@xmark:w", 1))
+                out.append((None, "@xmark:end", 1))
+            self._xplan_src, self._xplan = plan, out
+        if out is None:
+            return plan
+        if not getattr(self, "_xprimed", False):  # nothing recorded yet: no waits this step
+            self._xprimed = True
+            return [e for e in out if not e[1].startswith("@xwait")]
+        self._xpending = True
+        return out
+
+    def xstep_join(self) -> None:
+        """Order the current stream after the last cross-step side-stream work (before
+        reading weights / ending a timed region)."""
+        if getattr(self, "_xprimed", False) and self._side is not None:
+            st = self.stages[0]
+            cur = torch.cuda.current_stream(st.device)
+            native().run_plan([(None, "@xwait:end", 0)], cur.cuda_stream,
+                              self._side.cuda_stream,
+                              switches.get("DNN_EVENT_FENCE") == "device")
 
     def _run_interleaved(self):
         self._traverse(lambda s, op, j, nxt: self._run_op(self.stages[s], op, j, nxt))

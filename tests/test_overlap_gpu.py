@@ -104,3 +104,39 @@ def test_split_fino_auto_plan(dev, monkeypatch, model, rows, split):
     L = len(spec.layers)
     assert ((f"FINO1-{L - 1}", 1) in segs and ("FINO0-0", 0) in segs) == split, segs
     assert (("FINO", 0) in segs) == (not split), segs
+
+
+def test_cross_step_overlap_bitwise(dev, monkeypatch):
+    """DNN_XSTEP=1 moves the side stream's join from the end of a step to in front of the
+    next step's layer-1 forward (the layer-0 forward runs beside the reduce + update of layers
+    1..L-1). Bitwise the same training as the joined plan, for the losses of every step and
+    the weights after flush."""
+    from docker_dist_nn_amd import NAMED_MODELS
+    from docker_dist_nn_amd.data import synthetic_mnist
+    from docker_dist_nn_amd.engine import OptimConfig, Trainer
+
+    rows = 8192
+    monkeypatch.setenv("DNN_BW_OVERLAP_MIN_ROWS", "0")
+    monkeypatch.setenv("DNN_SPLIT_FINO", "1")
+    x, y = synthetic_mnist(2 * rows, seed=7)
+    xb = torch.zeros(2 * rows, 832, dtype=torch.bfloat16)
+    xb[:, :784] = torch.from_numpy(x).to(torch.bfloat16)
+    xb, yb = xb.to(dev), torch.from_numpy(y).to(dev)
+    res = []
+    for xs in ("0", "1"):
+        monkeypatch.setenv("DNN_XSTEP", xs)
+        tr = Trainer(NAMED_MODELS["mnist-fcnn"], micro_batch=rows, num_micro=1,
+                     optim=OptimConfig(lr=0.1, momentum=0.9), device=dev)
+        losses = []
+        for k in range(6):  # alternating batches, zero-copy views as in the bench
+            r = slice((k % 2) * rows, (k % 2 + 1) * rows)
+            tr.set_batch(xb[r], yb[r], zero_copy=True)
+            tr.step()
+            losses.append(tr.loss())
+        tr.flush()
+        if xs == "1":
+            segs = [seg for _, seg, _ in tr.executor._xstep_plan(tr.executor._native_plan())]
+            assert "@xwait:w" in segs and segs[-1] == "@xmark:end", segs
+        res.append((losses, tr.stages[0].params.master.clone()))
+    assert res[0][0] == res[1][0]
+    assert torch.equal(res[0][1], res[1][1])
