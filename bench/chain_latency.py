@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--rows", type=int, default=1)
     ap.add_argument("--stages", type=int, default=8)
     ap.add_argument("--width", type=int, default=1024)
+    ap.add_argument("--log", default=None, help="write the servers' log here")
     a = ap.parse_args()
     import torch
 
@@ -65,17 +66,26 @@ def main():
                               "--mode", "ranks", "--device", "cuda" if n_gpu else "cpu",
                               "--cache-dir", os.path.join(d, "cache"), "--run-for", "600"],
                              env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+        ok = True
         try:
             c = LayerClient(f"127.0.0.1:{port}", timeout=30, wait_ready=180)
             q = x[:a.rows]
+            print("servers ready", file=sys.stderr, flush=True)
             for _ in range(50):
                 c.process(q)
+            print("warm-up done", file=sys.stderr, flush=True)
             ts = []
-            for _ in range(a.iters):
+            for i in range(a.iters):
                 t0 = time.perf_counter()
                 c.process(q)
                 ts.append(time.perf_counter() - t0)
+                if (i + 1) % 100 == 0:  # progress (a long run must not look hung)
+                    print(f"{i + 1} requests, p50 so far {np.median(ts) * 1e3:.3f} ms",
+                          file=sys.stderr, flush=True)
             c.close()
+        except Exception:
+            ok = False
+            raise
         finally:
             p.terminate()
             try:
@@ -83,6 +93,11 @@ def main():
             except subprocess.TimeoutExpired:
                 p.kill()
                 log, _ = p.communicate()
+            if a.log:
+                with open(a.log, "w") as f:
+                    f.write(log or "")
+            if not ok:
+                print((log or "")[-6000:], file=sys.stderr, flush=True)
     fast = "device-side chain" in (log or "")
     import re
     m = re.search(r"predict latency over (\d+) requests: p50 ([\d.]+) ms p90 ([\d.]+) ms "
@@ -97,6 +112,7 @@ def main():
                                    (", one-GPU rehearsal: every stage on cuda:0"
                                     if rehearsal else ""),
                       "gpu_max_hw_queues": env.get("GPU_MAX_HW_QUEUES"),
+                      "persistent_stages": env.get("DNN_CHAIN_PERSIST", "1") == "1",
                       # rank 0's predict() alone (request in -> logits out, no gRPC): the
                       # device-side chain's own latency, warm-up requests included
                       "chain_only": inner,

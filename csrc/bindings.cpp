@@ -1016,6 +1016,47 @@ PYBIND11_MODULE(_native, m) {
   m.def(
       "free_device", [](uintptr_t p) { dnn::free_device(reinterpret_cast<void*>(p)); },
       py::arg("ptr"));
+  m.def(
+      "host_alloc_mapped",
+      [](size_t bytes) {
+        // pinned, coherent host memory the GPU reads and writes directly (a persistent
+        // kernel's stop word and progress counter: no stream operation needed while it runs)
+        void* p = nullptr;
+        if (hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+          throw std::runtime_error("hipHostMalloc failed");
+        std::memset(p, 0, bytes);
+        void* d = nullptr;
+        if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+          (void)hipHostFree(p);
+          throw std::runtime_error("hipHostGetDevicePointer failed");
+        }
+        return py::make_tuple(reinterpret_cast<uintptr_t>(p), reinterpret_cast<uintptr_t>(d));
+      },
+      py::arg("bytes"), "(host pointer, device pointer) of zeroed coherent pinned memory");
+  m.def(
+      "host_free", [](uintptr_t p) { (void)hipHostFree(reinterpret_cast<void*>(p)); },
+      py::arg("ptr"));
+  m.def(
+      "stream_create_dedicated",
+      []() {
+        // a stream on a hardware queue of its own (the runtime gives a CU-masked stream a new
+        // queue instead of a slot in the shared pool): a persistent kernel on it cannot stall
+        // the work of other streams queued behind it on a shared queue
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+          throw std::runtime_error("stream_create_dedicated: no device");
+        std::vector<uint32_t> mask((cus + 31) / 32, 0xffffffffu);
+        hipStream_t st = nullptr;
+        if (hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()) != hipSuccess)
+          throw std::runtime_error("hipExtStreamCreateWithCUMask failed");
+        return reinterpret_cast<uintptr_t>(st);
+      },
+      "a stream with a hardware queue of its own (all CUs)");
+  m.def(
+      "stream_destroy",
+      [](uintptr_t st) { (void)hipStreamDestroy(reinterpret_cast<hipStream_t>(st)); },
+      py::arg("stream"));
   m.def("can_access_peer", &dnn::can_access_peer, py::arg("dev"), py::arg("peer"));
   m.def(
       "copy_async",
@@ -1212,6 +1253,55 @@ PYBIND11_MODULE(_native, m) {
             return rc;
           },
           py::arg("slot"), py::arg("timeout_s"));
+  m.def(
+      "chain_stage_run",
+      [=](uintptr_t s, uintptr_t in_flags, uintptr_t in_hdrs, uintptr_t in_slots, long ldx,
+          uintptr_t prev_ack, uintptr_t w, long ldw, uintptr_t bias, int act, int N, int K,
+          int out_f32, uintptr_t dst, long dst_slot_bytes, long dst_ld, uintptr_t dst_hdr,
+          long hdr_stride, uintptr_t next_flags, uintptr_t ack, uintptr_t stop, uintptr_t done,
+          uintptr_t sync, uint32_t start_seq, uint32_t epoch, int stage, int nslot,
+          int max_rows, double idle_s, double timeout_s, int workgroups) {
+        dnn::ChainStage p{};
+        p.in_flags = static_cast<const uint32_t*>(ptr(in_flags));
+        p.in_hdrs = static_cast<const uint32_t*>(ptr(in_hdrs));
+        p.in_slots = static_cast<const uint16_t*>(ptr(in_slots));
+        p.ldx = ldx;
+        p.prev_ack = static_cast<uint32_t*>(ptr(prev_ack));
+        p.w = static_cast<const uint16_t*>(ptr(w));
+        p.ldw = ldw;
+        p.bias = static_cast<const float*>(ptr(bias));
+        p.act = act;
+        p.N = N;
+        p.K = K;
+        p.out_f32 = out_f32;
+        p.dst = static_cast<char*>(ptr(dst));
+        p.dst_slot_bytes = dst_slot_bytes;
+        p.dst_ld = dst_ld;
+        p.dst_hdr = static_cast<uint32_t*>(ptr(dst_hdr));
+        p.hdr_stride = hdr_stride;
+        p.next_flags = static_cast<uint32_t*>(ptr(next_flags));
+        p.ack = static_cast<const uint32_t*>(ptr(ack));
+        p.stop = static_cast<const uint32_t*>(ptr(stop));
+        p.done = static_cast<uint32_t*>(ptr(done));
+        p.sync = static_cast<uint32_t*>(ptr(sync));
+        p.start_seq = start_seq;
+        p.epoch = epoch;
+        p.stage = stage;
+        p.nslot = nslot;
+        p.max_rows = max_rows;
+        p.idle_ticks = dnn::chain_ticks(idle_s);
+        p.timeout_ticks = dnn::chain_ticks(timeout_s);
+        const int wg = workgroups > 0 ? workgroups : dnn::chain_stage_workgroups(N, act);
+        chk(dnn::chain_stage_run(p, wg, S(s)), "chain_stage_run");
+        return wg;
+      },
+      py::arg("stream"), py::arg("in_flags"), py::arg("in_hdrs"), py::arg("in_slots"),
+      py::arg("ldx"), py::arg("prev_ack"), py::arg("w"), py::arg("ldw"), py::arg("bias"),
+      py::arg("act"), py::arg("N"), py::arg("K"), py::arg("out_f32"), py::arg("dst"),
+      py::arg("dst_slot_bytes"), py::arg("dst_ld"), py::arg("dst_hdr"), py::arg("hdr_stride"),
+      py::arg("next_flags"), py::arg("ack"), py::arg("stop"), py::arg("done"), py::arg("sync"),
+      py::arg("start_seq"), py::arg("epoch"), py::arg("stage"), py::arg("nslot"),
+      py::arg("max_rows"), py::arg("idle_s"), py::arg("timeout_s"), py::arg("workgroups") = 0);
   m.def(
       "chain_signal",
       [=](uintptr_t s, uintptr_t flag, uint32_t value) {

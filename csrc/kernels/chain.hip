@@ -141,7 +141,11 @@ __global__ __launch_bounds__(256) void chain_gemv_send_kernel(ChainGemvSend p) {
     const bool in_ok = !p.in_flag ? true
                        : blockIdx.x == 0 ? spin(p.in_flag + t, p.seq, p.timeout_ticks)
                                          : spin<true>(p.in_flag + t, p.seq, p.timeout_ticks);
-    const bool ok = p.ack ? spin(p.ack + t, p.ack_target, p.timeout_ticks) : true;
+    // (the grid can be N / 4 workgroups: all but one poll the consumer's ack relaxed, as the
+    // folded receive's input flag, so a wide layer does not flood the memory system)
+    const bool ok = !p.ack ? true
+                    : blockIdx.x == 0 ? spin(p.ack + t, p.ack_target, p.timeout_ticks)
+                                      : spin<true>(p.ack + t, p.ack_target, p.timeout_ticks);
     if (!ok || !in_ok)  // remembered for the last workgroup: bit 0 ack, bit 1 input
       __hip_atomic_fetch_or(p.counter + 1 + t, (ok ? 0u : 1u) | (in_ok ? 0u : 2u),
                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -216,6 +220,223 @@ __global__ __launch_bounds__(256) void chain_gemv_send_kernel(ChainGemvSend p) {
       __hip_atomic_store(p.next_flag + t, p.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       if (p.prev_ack)
         __hip_atomic_store(p.prev_ack + t, p.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+// ---- persistent stage (ChainStage, chain.hpp) ---------------------------------------------
+// sync words: [0, nslot) per-slot arrival counters, [nslot, 2 nslot) per-slot ack failures
+// (written by workgroup 0 before it releases the slot), then go, exit.
+
+// One request's layer for `rows` <= M rows staged in LDS (xs, row stride K). A wave takes NB
+// neurons at once (their weight loads in flight together, the x vectors read once for all);
+// per neuron the loop and reduction order are chain_gemv_send's, so the outputs are bitwise
+// the same. `logits` != nullptr (softmax, one workgroup): the pre-activation rows go there.
+template <int M, int NB>
+__device__ __forceinline__ void cs_layer(const ChainStage& p, const u16* xs, int rows, char* dst,
+                                         float* logits) {
+  const unsigned t = threadIdx.x;
+  const int lane = t & 63;
+  constexpr int U = 4;
+  for (int n0 = (blockIdx.x * CG_WAVES + (int)(t >> 6)) * NB; n0 < p.N;
+       n0 += gridDim.x * CG_WAVES * NB) {
+    float acc[NB][M];
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+      for (int m = 0; m < M; ++m) acc[j][m] = 0.f;
+    for (int k0 = 0; k0 < p.K; k0 += 512 * U) {
+      bf16x8_t wv[NB][U], xv[U][M];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = k0 + u * 512 + lane * 8;
+        if (k < p.K) {
+#pragma unroll
+          for (int j = 0; j < NB; ++j)
+            wv[j][u] = n0 + j < p.N ? *(const bf16x8_t*)(p.w + (long)(n0 + j) * p.ldw + k)
+                                    : bf16x8_t{};
+#pragma unroll
+          for (int m = 0; m < M; ++m)
+            xv[u][m] = m < rows ? *(const bf16x8_t*)(xs + m * p.K + k) : bf16x8_t{};
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = k0 + u * 512 + lane * 8;
+        if (k < p.K) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+#pragma unroll
+            for (int j = 0; j < NB; ++j) {
+              const float we = bf2f((u16)wv[j][u][e]);
+#pragma unroll
+              for (int m = 0; m < M; ++m) acc[j][m] += we * bf2f((u16)xv[u][m][e]);
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+#pragma unroll
+      for (int m = 0; m < M; ++m) acc[j][m] = wave_sum(acc[j][m]);
+      const int n = n0 + j;
+      if (n < p.N && lane < rows) {
+        float v = 0.f;
+#pragma unroll
+        for (int m = 0; m < M; ++m)
+          if (m == lane) v = acc[j][m];
+        v += p.bias ? p.bias[n] : 0.f;
+        if (logits) {
+          logits[lane * p.N + n] = v;
+        } else {
+          v = act_fwd(v, p.act);
+          if (p.out_f32)
+            ((float*)dst)[(long)lane * p.dst_ld + n] = v;
+          else
+            ((u16*)dst)[(long)lane * p.dst_ld + n] = f2bf(v);
+        }
+      }
+    }
+  }
+}
+
+constexpr int CS_NB = 4;  // neurons per wave in flight (chain_stage_kernel)
+
+__global__ __launch_bounds__(256) void chain_stage_kernel(ChainStage p) {
+  extern __shared__ __attribute__((aligned(16))) char cs_lds[];
+  __shared__ uint32_t s_cmd[4];  // run, input status, rows, ack failure
+  u16* xs = (u16*)cs_lds;
+  float* logits = p.act == ACT_SOFTMAX ? (float*)(cs_lds + (long)p.max_rows * p.K * 2) : nullptr;
+  const unsigned t = threadIdx.x;
+  uint32_t* cnt = p.sync;
+  uint32_t* fail = p.sync + p.nslot;
+  uint32_t* go = p.sync + 2 * p.nslot;  // workgroup 0: the last request it let through
+  uint32_t* ex = go + 1;                // == epoch: this launch ends before request *go + 1
+  for (uint32_t seq = p.start_seq + 1;; ++seq) {
+    const int slot = (int)(seq % (uint32_t)p.nslot);
+    if (t == 0) {
+      uint32_t run = 1;
+      if (blockIdx.x == 0) {
+        // the stop word lives in host memory (a read crosses the host link): looked at every
+        // ~20 us of waiting, not every poll of the (local) input flag
+        const unsigned long long t0 = wall_clock64();
+        unsigned long long t_stop = t0;
+        for (;;) {
+          if ((int)(__hip_atomic_load(p.in_flags + slot, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_SYSTEM) - seq) >= 0)
+            break;
+          const unsigned long long now = wall_clock64();
+          if (now - t_stop > 2000) {
+            t_stop = now;
+            if (__hip_atomic_load(p.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+              run = 0;
+              break;
+            }
+          }
+          if (now - t0 > p.idle_ticks) {
+            run = 0;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if (run) {
+          // the consumer drained the slot this request reuses (bounded: a stuck consumer is
+          // reported downstream as DEADLINE naming it, the request's rows are not written)
+          const bool ok = spin(p.ack, seq - (uint32_t)p.nslot, p.timeout_ticks);
+          __hip_atomic_store(fail + slot, ok ? 0u : 1u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(go, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          __hip_atomic_store(ex, p.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      } else {
+        // the other workgroups follow workgroup 0's decision (it alone polls the input flag
+        // and owns the idle / stop exit, so every workgroup leaves at the same request)
+        for (;;) {
+          if ((int)(__hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - seq) >= 0)
+            break;
+          if (__hip_atomic_load(ex, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p.epoch) {
+            run = 0;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      if (run) {
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);  // system scope: the producer's rows + header
+        s_cmd[1] = __hip_atomic_load(p.in_hdrs + 2 * slot, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_SYSTEM);
+        s_cmd[2] = __hip_atomic_load(p.in_hdrs + 2 * slot + 1, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_SYSTEM);
+        s_cmd[3] = __hip_atomic_load(fail + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      s_cmd[0] = run;
+    }
+    __syncthreads();
+    if (!s_cmd[0]) break;  // uniform: the launch ends here
+    const uint32_t in_st = s_cmd[1];
+    const int rows = (int)s_cmd[2];
+    const bool rows_ok = rows >= 1 && rows <= p.max_rows;
+    const uint32_t ack_fail = s_cmd[3];
+    const bool compute = (in_st & 0xffu) == 0u && ack_fail == 0u && rows_ok;
+    char* dst = p.dst + slot * p.dst_slot_bytes;
+    if (compute) {
+      const u16* src = p.in_slots + (long)slot * p.max_rows * p.ldx;
+      const int cpr = p.K >> 3;
+      for (int i = t; i < rows * cpr; i += blockDim.x) {
+        const int r = i / cpr, c = i - r * cpr;
+        *(uint4*)(xs + r * p.K + 8 * c) = *(const uint4*)(src + r * p.ldx + 8 * c);
+      }
+      __syncthreads();
+      switch (rows) {
+        case 1: cs_layer<1, CS_NB>(p, xs, rows, dst, logits); break;
+        case 2: cs_layer<2, CS_NB>(p, xs, rows, dst, logits); break;
+        case 3:
+        case 4: cs_layer<4, CS_NB>(p, xs, rows, dst, logits); break;
+        default: cs_layer<8, CS_NB>(p, xs, rows, dst, logits); break;
+      }
+      if (logits) {  // row softmax (one workgroup): a wave per row
+        __syncthreads();
+        const int lane = t & 63;
+        for (int m = (int)(t >> 6); m < rows; m += CG_WAVES) {
+          float mx = -INFINITY;
+          for (int n = lane; n < p.N; n += 64) mx = fmaxf(mx, logits[m * p.N + n]);
+          mx = wave_max(mx);
+          float s = 0.f;
+          for (int n = lane; n < p.N; n += 64) s += __expf(logits[m * p.N + n] - mx);
+          s = wave_sum(s);
+          const float inv = 1.f / s;
+          for (int n = lane; n < p.N; n += 64) {
+            const float v = __expf(logits[m * p.N + n] - mx) * inv;
+            if (p.out_f32)
+              ((float*)dst)[(long)m * p.dst_ld + n] = v;
+            else
+              ((u16*)dst)[(long)m * p.dst_ld + n] = f2bf(v);
+          }
+        }
+      }
+    }
+    __threadfence_system();  // this thread's rows are visible before the workgroup counts in
+    __syncthreads();
+    if (t == 0) {
+      const uint32_t prev = __hip_atomic_fetch_add(cnt + slot, 1u, __ATOMIC_ACQ_REL,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == gridDim.x - 1) {  // the last workgroup: every row of the request landed
+        uint32_t st = 0u;
+        if (in_st & 0xffu) st = in_st;  // an upstream failure travels on unchanged
+        else if (ack_fail) st = CHAIN_DEADLINE | ((uint32_t)(p.stage + 1) << 8);
+        else if (!rows_ok) st = CHAIN_INTERNAL | ((uint32_t)p.stage << 8);
+        __hip_atomic_store(cnt + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t* hdr = p.dst_hdr + slot * p.hdr_stride;
+        __hip_atomic_store(hdr, st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(hdr + 1, (uint32_t)(rows_ok ? rows : 0), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        __threadfence_system();
+        __hip_atomic_store(p.next_flags + slot, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(p.prev_ack, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(p.done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
     }
   }
 }
@@ -330,6 +551,30 @@ int chain_gemv_send(const ChainGemvSend& p, hipStream_t stream) {
     default: DNN_CG(8) break;
   }
 #undef DNN_CG
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
+int chain_stage_workgroups(int N, int act) {
+  if (act == ACT_SOFTMAX) return 1;  // the row pass needs every logit in one workgroup
+  // a neuron group (CS_NB neurons) per wave, at most 64 workgroups: a one-GPU rehearsal keeps
+  // 7 persistent stages resident at once (448 workgroups, far below the GPU's ~2048)
+  return std::max(1, std::min(64, (N + CG_WAVES * CS_NB - 1) / (CG_WAVES * CS_NB)));
+}
+
+int chain_stage_run(const ChainStage& p, int workgroups, hipStream_t stream) {
+  if (!p.in_flags || !p.in_hdrs || !p.in_slots || !p.prev_ack || !p.w || !p.dst || !p.dst_hdr ||
+      !p.next_flags || !p.ack || !p.stop || !p.done || !p.sync || misaligned4(p.in_flags) ||
+      misaligned4(p.sync) || misaligned4(p.next_flags) || misaligned4(p.dst_hdr))
+    return -1;
+  if (p.N < 1 || p.K < 8 || p.K % 8 || p.ldx < p.K || p.ldx % 8 || p.ldw < p.K || p.ldw % 8 ||
+      p.dst_ld < p.N || p.nslot < 2 || p.max_rows < 1 || p.max_rows > GEMV_MAX_ROWS ||
+      misaligned16(p.in_slots) || misaligned16(p.w) || p.epoch == 0)
+    return -2;
+  const long lds = (long)p.max_rows * p.K * 2 +
+                   (p.act == ACT_SOFTMAX ? (long)p.max_rows * p.N * 4 : 0);
+  if (lds > 64 * 1024) return -3;  // rows staged in LDS: K (and a softmax's N) bounded
+  if (workgroups < 1 || (p.act == ACT_SOFTMAX && workgroups != 1)) return -4;
+  hipLaunchKernelGGL(chain_stage_kernel, dim3(workgroups), dim3(256), (size_t)lds, stream, p);
   return hipGetLastError() == hipSuccess ? 0 : -9;
 }
 

@@ -107,6 +107,46 @@ struct ChainGemvSend {
 };
 int chain_gemv_send(const ChainGemvSend& p, hipStream_t stream);
 
+// Persistent stage of the serving chain (one-layer stages > 0): ONE launch serves request after
+// request with no host work per request. Workgroup 0 polls the input flag of the next slot
+// (and the stop word, and an idle timer) and releases the other workgroups through `go`; every
+// workgroup stages the slot's rows in LDS, computes its share of the layer (chain_gemv_send's
+// math, bitwise), writes straight into the consumer's slot and counts in on the slot's
+// counter; the last one writes the header, raises the consumer's flag, acks the producer and
+// publishes `done`. The rows of a request come from the slot header its producer wrote. The
+// kernel returns when the host sets `*stop` or after `idle_ticks` without a request (the host
+// relaunches it with start_seq = *done); either way every wave leaves through the same
+// decision of workgroup 0.
+struct ChainStage {
+  const uint32_t* in_flags;  // [nslot] this stage's input flags (written by the producer)
+  const uint32_t* in_hdrs;   // [nslot][2] input slot headers (status, rows)
+  const uint16_t* in_slots;  // [nslot][max_rows][ldx] bf16 rows (L2-uncached)
+  long ldx;                  // elements (= K padded)
+  uint32_t* prev_ack;        // producer's ack word (IPC-mapped)
+  const uint16_t* w;         // [N][ldw]
+  long ldw;
+  const float* bias;
+  int act;                   // Act code; ACT_SOFTMAX: row softmax (one workgroup, N <= 1024)
+  int N, K;
+  int out_f32;
+  char* dst;                 // consumer's slot 0 rows; slot s at dst + s * dst_slot_bytes
+  long dst_slot_bytes;
+  long dst_ld;               // elements
+  uint32_t* dst_hdr;         // consumer's slot 0 header; slot s at dst_hdr + s * hdr_stride
+  long hdr_stride;           // words
+  uint32_t* next_flags;      // [nslot] the consumer's flags for the slots
+  const uint32_t* ack;       // this stage's ack word (the consumer writes it)
+  const uint32_t* stop;      // != 0 -> return (coherent host memory, set by the host)
+  uint32_t* done;            // the last request finished (coherent host memory: progress)
+  uint32_t* sync;            // [nslot + 4] zeroed: per-slot arrival counters, go, exit
+  uint32_t start_seq;        // serve start_seq + 1, start_seq + 2, ...
+  uint32_t epoch;            // this launch's id (exit word value)
+  int stage, nslot, max_rows;
+  unsigned long long idle_ticks, timeout_ticks;
+};
+int chain_stage_run(const ChainStage& p, int workgroups, hipStream_t stream);
+int chain_stage_workgroups(int N, int act);  // the grid chain_stage_run is given by default
+
 // Training step plans (runtime/step_plan.cpp COPYSIG): a peer copy followed by its flag in ONE
 // launch. Every workgroup copies its share, fences, and bumps `counter`; the last one to
 // arrive resets the counter and stores *flag = *seq + delta (system-scope release), so the

@@ -40,6 +40,7 @@ the stage reports INTERNAL) or ``hang`` (the stage stops responding after
 from __future__ import annotations
 
 import argparse
+from contextlib import nullcontext
 import itertools
 import json
 import logging
@@ -350,47 +351,51 @@ class ChainRank:
                     self._send_msg([0, 0, 0, ST_STOP, 0], None, self.rank + 1, self.fwd_group,
                                    self.out_pad)
                 return
-            if status != ST_OK:  # propagate an upstream failure
-                self._processed = req
-                self._forward_hdr(last, req, R, 0, status, extra)
-                continue
-            buf = self.stage.buffers(R)
-            if R <= self.small:
-                buf["x"].reshape(-1).view(torch.uint8).copy_(
-                    pk[HDR_BYTES:HDR_BYTES + R * width * 2])
-            elif not self._recv_payload(buf["x"], prev, self.fwd_group, self.hop_timeout):
-                # the hop is broken: the posted receive would take the next message from prev
-                # (on NCCL the timed-out wait aborts the communicator), so nothing later on it
-                # can be trusted. Report this request, then stop serving; rank 0 blames this
-                # stage for every later request from the progress it no longer publishes.
-                log.error(f"({self.names[self.rank]}) payload of request {req} did not arrive "
-                          f"within {self.hop_timeout:.1f} s; the hop from rank {prev} is broken, "
-                          f"this stage stops serving")
-                self._forward_hdr(last, req, R, 0, ST_DEADLINE, prev)
-                return
-            try:
-                self._maybe_fault(served)
-                out = self.stage.forward(R)
-                if self.comm_dev.type == "cpu":
-                    self._sync()
-            except ValueError:
-                self._processed = req
-                self._forward_hdr(last, req, R, 0, ST_VALUE, self.rank)
-                continue
-            except Exception:  # noqa: BLE001
-                log.exception(f"({self.names[self.rank]}) stage failure")
-                self._processed = req
-                self._forward_hdr(last, req, R, 0, ST_INTERNAL, self.rank)
-                continue
-            finally:
-                served += 1
-            self._processed = req  # received + computed: what rank 0's blame reads
-            if last:
-                self._send(self._hdr(req, R, self.stage.out_dim, ST_OK, 0), 0, self.ret_group)
-                self._send(out[:, :self.stage.out_dim].contiguous(), 0, self.ret_group)
-            else:
-                self._send_msg([req, R, out.shape[1], ST_OK, 0], out, self.rank + 1,
-                               self.fwd_group, self.out_pad)
+            # the GPU is this request's: a persistent device-chain kernel steps aside
+            with (self.fast.paused() if self.fast is not None else nullcontext()):
+                if status != ST_OK:  # propagate an upstream failure
+                    self._processed = req
+                    self._forward_hdr(last, req, R, 0, status, extra)
+                    continue
+                buf = self.stage.buffers(R)
+                if R <= self.small:
+                    buf["x"].reshape(-1).view(torch.uint8).copy_(
+                        pk[HDR_BYTES:HDR_BYTES + R * width * 2])
+                elif not self._recv_payload(buf["x"], prev, self.fwd_group, self.hop_timeout):
+                    # the hop is broken: the posted receive would take the next message from
+                    # prev (on NCCL the timed-out wait aborts the communicator), so nothing
+                    # later on it can be trusted. Report this request, then stop serving; rank 0
+                    # blames this stage for every later request from the progress it no longer
+                    # publishes.
+                    log.error(f"({self.names[self.rank]}) payload of request {req} did not "
+                              f"arrive within {self.hop_timeout:.1f} s; the hop from rank {prev} "
+                              f"is broken, this stage stops serving")
+                    self._forward_hdr(last, req, R, 0, ST_DEADLINE, prev)
+                    return
+                try:
+                    self._maybe_fault(served)
+                    out = self.stage.forward(R)
+                    if self.comm_dev.type == "cpu":
+                        self._sync()
+                except ValueError:
+                    self._processed = req
+                    self._forward_hdr(last, req, R, 0, ST_VALUE, self.rank)
+                    continue
+                except Exception:  # noqa: BLE001
+                    log.exception(f"({self.names[self.rank]}) stage failure")
+                    self._processed = req
+                    self._forward_hdr(last, req, R, 0, ST_INTERNAL, self.rank)
+                    continue
+                finally:
+                    served += 1
+                self._processed = req  # received + computed: what rank 0's blame reads
+                if last:
+                    self._send(self._hdr(req, R, self.stage.out_dim, ST_OK, 0), 0,
+                               self.ret_group)
+                    self._send(out[:, :self.stage.out_dim].contiguous(), 0, self.ret_group)
+                else:
+                    self._send_msg([req, R, out.shape[1], ST_OK, 0], out, self.rank + 1,
+                                   self.fwd_group, self.out_pad)
 
     def _forward_hdr(self, last: bool, req, R, width, status, extra) -> None:
         if last:

@@ -24,12 +24,20 @@ header read and a host send per hop. Here:
   whose input does not arrive within the per-hop deadline (10 s, grpc_node.py:133) sends
   DEADLINE_EXCEEDED naming its producer -- the stage that stopped -- and every later stage
   forwards the status unchanged;
+* one-layer stages > 0 run as ONE persistent kernel each (``chain_stage_run``, DNN_CHAIN_PERSIST):
+  it polls its input flags itself, takes a request's rows from the slot header the producer
+  wrote, and serves request after request with no host work at all -- no announcement read, no
+  launch; the host thread only relaunches it after an idle exit and publishes its progress
+  counter (coherent host memory) for rank 0's blame. A stage that must use the GPU for
+  something else (a message-chain request) pauses it first (``paused``);
 * larger requests and any set-up that cannot map its peers keep using the message-passing
   chain (serve/chain.py), which stays the fallback.
 """
 from __future__ import annotations
 
 import collections
+import contextlib
+import ctypes
 import logging
 import mmap
 import os
@@ -58,6 +66,8 @@ F_ERR = F_ACK + 1           # this rank's recv-timeout word
 F_LHDR = F_ACK + 4          # [2] local copy of the current request's input header
 F_RES = F_ACK + 8           # rank 0: [NSLOT] result flags (written by the last rank)
 F_WORDS = F_RES + NSLOT + 8
+PERSIST_IDLE_S = 1.0   # a persistent stage kernel returns after this long without a request
+PERSIST_POLL_S = 5e-4  # its host thread's poll period (progress, stop, pause)
 
 
 class Announcer:
@@ -114,6 +124,9 @@ class Announcer:
         while a[i] != seq:  # the head is written last; the entry is there
             if a[i] > seq:  # lapped: rank 0 ran a whole ring ahead of this stage
                 raise RuntimeError(f"announcement ring overrun at request {seq}")
+            if a[1]:
+                return None
+            time.sleep(0)
         return int(a[i + 1])
 
     def close(self) -> None:
@@ -246,6 +259,7 @@ class FastChain:
         self.lat: collections.deque = collections.deque(maxlen=100000)  # rank 0: seconds
         self.host = None  # rank 0: runtime ChainHost (the native request path)
         self.seq = 0
+        self.inflight = 0  # rank 0: requests announced and not yet answered (back-pressure)
         self.lock = threading.Lock()
         self.processed = 0
         if self.rank == 0:
@@ -261,9 +275,30 @@ class FastChain:
             # (runtime/chain_host.cpp), its completion a GIL-free spin
             self.host = (self.n.ChainHost(NSLOT) if self.fused and len(st.layers) == 1 and
                          switches.get("DNN_CHAIN_NATIVE") == "1" else None)
+        self.failed = False
+        self.persist = self._persist_ok()
+        if self.persist:
+            # the kernel never returns while requests flow: it gets a hardware queue of its own
+            # (work of this process's other streams would otherwise wait behind it whenever
+            # the runtime maps their stream onto the same queue)
+            self._pstream_ptr = self.n.stream_create_dedicated()
+            self.pstream = torch.cuda.ExternalStream(self._pstream_ptr, device=self.dev)
+            # per-slot arrival counters, ack failures, go, exit (chain.hip ChainStage) and
+            # the stop word / progress counter in coherent host memory
+            self.sync = torch.zeros(2 * NSLOT + 4, dtype=torch.int32, device=self.dev)
+            self._ctl_host, self._ctl_dev = self.n.host_alloc_mapped(64)
+            self.ctl = np.ctypeslib.as_array((ctypes.c_uint32 * 16).from_address(self._ctl_host))
+            self._want_pause = False
+            self._pause_lock = threading.Lock()
+            self._parked = threading.Event()
+            self._resume = threading.Event()
+            self._runner_done = threading.Event()
+            self.workgroups = 0
         self.ok = True
         self.why = (f"device-side chain ({NSLOT} slots per hop"
-                    + (", last layer fused with the send" if self.fused else "") + ")")
+                    + (", last layer fused with the send" if self.fused else "")
+                    + (", one-layer stages as persistent kernels"
+                       if switches.get("DNN_CHAIN_PERSIST") == "1" else "") + ")")
 
     def _agree(self, ok: bool) -> bool:
         from ..parallel.comm import _cpu_group
@@ -326,7 +361,26 @@ class FastChain:
 
     # ---- rank 0 -------------------------------------------------------------------------------
     def predict(self, x: np.ndarray, timeout: Optional[float]) -> np.ndarray:
-        """One request of <= max_rows rows through the device-side chain -> float64 outputs."""
+        """One request of <= max_rows rows through the device-side chain -> float64 outputs.
+        Back-pressure: the stages read the announcement ring in order, so rank 0 never has
+        more than half a ring of requests in flight (RESOURCE_EXHAUSTED beyond that)."""
+        import grpc
+
+        from .ingress import StageFailure
+
+        with self.lock:
+            if self.inflight >= ANN_SLOTS // 2:
+                raise StageFailure(self.cr.names[0], grpc.StatusCode.RESOURCE_EXHAUSTED,
+                                   f"{self.inflight} requests in flight on the device-side "
+                                   f"chain")
+            self.inflight += 1
+        try:
+            return self._predict(x, timeout)
+        finally:
+            with self.lock:
+                self.inflight -= 1
+
+    def _predict(self, x: np.ndarray, timeout: Optional[float]) -> np.ndarray:
         import grpc
 
         from .ingress import StageFailure
@@ -467,7 +521,20 @@ class FastChain:
 
     # ---- ranks > 0 ----------------------------------------------------------------------------
     def loop(self) -> None:
-        """Serve announced requests in order until the ring stops."""
+        """Serve announced requests in order until the ring stops. A failure of this thread is
+        logged and ends the stage's device-side serving: its progress stops, so rank 0 blames
+        this stage by name for every later request (chain.ChainRank.blame)."""
+        try:
+            if self.persist:
+                self._persist_loop()
+            else:
+                self._host_loop()
+        except Exception:  # noqa: BLE001
+            self.failed = True
+            log.exception(f"({self.cr.names[self.rank]}) device-side chain thread failed; this "
+                          f"stage stops serving serving-size requests")
+
+    def _host_loop(self) -> None:
         n = self.n
         seq = 0
         s = self.stream
@@ -521,6 +588,89 @@ class FastChain:
             self.cr._processed = seq
         torch.cuda.synchronize(self.dev)
 
+    # ---- ranks > 0: the persistent stage kernel -----------------------------------------------
+    def _persist_ok(self) -> bool:
+        st = self.cr.stage
+        if self.rank == 0 or switches.get("DNN_CHAIN_PERSIST") != "1" or len(st.layers) != 1:
+            return False
+        if self.cr.fault_stage == str(self.rank) or self.trace:
+            return False  # fault injection and tracing act per request on the host
+        n = st.dims[-1] if st.acts[0] == "softmax" else st.w[0].shape[0]
+        lds = self.max_rows * self.in_w * 2 + (self.max_rows * n * 4
+                                                if st.acts[0] == "softmax" else 0)
+        return lds <= 64 * 1024 and st.w[0].shape[1] == self.in_w
+
+    def _persist_launch(self, start: int, epoch: int) -> None:
+        st = self.cr.stage
+        w, b, act = st.w[0], st.b[0], st.acts[0]
+        last = self.rank == self.world - 1
+        if last:  # rank 0's result slots: header, then fp32 rows
+            dst, slot_b = self.dst + HDR, self.res_bytes
+            hdr, hstride, nflags = self.dst, self.res_bytes // 4, self.next_flags + 4 * F_RES
+        else:
+            dst, slot_b = self.dst, self.max_rows * self.out_w * 2
+            hdr, hstride, nflags = self.next_flags + 4 * F_HDR, 2, self.next_flags + 4 * F_IN
+        n_out = st.dims[-1] if act == "softmax" else w.shape[0]
+        self.workgroups = self.n.chain_stage_run(
+            self.pstream.cuda_stream, _ptr(self.flags, F_IN), _ptr(self.flags, F_HDR),
+            self.slots.data_ptr(), self.in_w, self.prev_flags + 4 * F_ACK, w.data_ptr(),
+            w.stride(0), b.data_ptr(), ops.kernels._act(act), n_out, self.in_w, int(last), dst,
+            slot_b, self.out_w, hdr, hstride, nflags, _ptr(self.flags, F_ACK), self._ctl_dev,
+            self._ctl_dev + 4, self.sync.data_ptr(), start & 0xFFFFFFFF, epoch, self.rank, NSLOT,
+            self.max_rows, PERSIST_IDLE_S, self.cr.hop_timeout)
+
+    def _persist_loop(self) -> None:
+        """Keep the stage kernel running until the ring stops: relaunch it after an idle exit,
+        park it while ``paused`` holds the GPU, publish its progress for rank 0's blame."""
+        s = self.pstream
+        start, epoch = 0, 0
+        try:
+            while not self.ann.a[1]:
+                if self._want_pause:
+                    self._parked.set()
+                    self._resume.wait()
+                    self._resume.clear()
+                    continue
+                self.ctl[0] = 0
+                epoch += 1
+                with torch.cuda.stream(s):
+                    self._persist_launch(start, epoch)
+                ev = torch.cuda.Event()
+                ev.record(s)
+                asked = False
+                while not ev.query():
+                    d = int(self.ctl[1])
+                    if d != self.processed:  # (the message chain's progress shares the key)
+                        self.processed = self.cr._processed = d
+                    if not asked and (self.ann.a[1] or self._want_pause):
+                        self.ctl[0] = 1  # the kernel returns within ~20 us of waiting
+                        asked = True
+                    time.sleep(PERSIST_POLL_S)
+                start = int(self.ctl[1])
+                if start != self.processed:
+                    self.processed = self.cr._processed = start
+        finally:
+            self._runner_done.set()
+            self._parked.set()
+
+    @contextlib.contextmanager
+    def paused(self):
+        """Ranks > 0: hold the GPU for other work (a message-chain request: its kernels, a
+        device-wide sync) with the persistent stage kernel stopped; requests arriving meanwhile
+        wait in their slots and are served on resume."""
+        if not getattr(self, "persist", False):
+            yield
+            return
+        with self._pause_lock:
+            self._want_pause = True
+            self._parked.wait(self.cr.hop_timeout)
+            try:
+                yield
+            finally:
+                self._want_pause = False
+                self._parked.clear()
+                self._resume.set()
+
     def stop(self) -> None:
         if self.rank == 0 and self.ok:
             self.ann.stop()
@@ -529,3 +679,9 @@ class FastChain:
     def close(self) -> None:
         if self.ok:
             self.ann.close()
+            if self.persist and self._runner_done.is_set():
+                # (a runner still alive may have a kernel that writes these words: leaked)
+                self.pstream.synchronize()
+                self.n.host_free(self._ctl_host)
+                self.n.stream_destroy(self._pstream_ptr)
+                self.persist = False

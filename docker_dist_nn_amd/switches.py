@@ -132,6 +132,9 @@ SWITCHES: dict[str, tuple[str, str]] = {
                                   "chain_gemv_send too (one kernel per hop; every workgroup "
                                   "waits on the input flag). Opt-in: slower with several waiting "
                                   "stages on one GPU (profiles/r4_chain)"),
+    "DNN_CHAIN_PERSIST": ("1", "device-side chain, one-layer stages > 0: one persistent kernel "
+                               "per stage (chain_stage_run) serves every request with no host "
+                               "work per request; 0 = the host enqueues each request's kernels"),
     "DNN_CHAIN_TRACE": ("0", "device-side chain: 1 = every rank logs each request's steps and, "
                              "after synchronising, its flag words (diagnosis; serialises)"),
     "DNN_CHAIN_FAST": ("1", "rank chain: serving-size requests (<= 8 rows) take the device-side "

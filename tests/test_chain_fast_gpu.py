@@ -305,3 +305,162 @@ def test_chain_one_launch_hop_in_one_process(dev):
     s.synchronize()
     assert int(f_out[0]) == 2 and (int(f_out[2]) & 0xFF) == 4 and (int(f_out[2]) >> 8) == 0
     assert float(slot_out.float().abs().sum()) == 0.0 and counter.tolist() == [0, 0, 0, 0]
+
+
+def _persistent_stage(dev, K, N, act, nslot=4, out_f32=False, n_out=None):
+    """A persistent stage kernel (chain_stage_run) between a simulated producer (this test
+    writes the input slots, headers and flags) and a simulated consumer (it reads the output
+    slots and writes the ack)."""
+    import ctypes
+
+    import torch
+
+    from docker_dist_nn_amd.utils.devmem import uncached_zeros
+    from docker_dist_nn_amd.utils.native import native
+
+    n = native()
+    st = type("S", (), {})()
+    st.n, st.K, st.N, st.nslot = n, K, N, nslot
+    st.n_out = n_out or N
+    st.f_in = uncached_zeros((64,), torch.int32, dev)    # [0:nslot] flags, [16:] headers
+    st.f_out = uncached_zeros((64,), torch.int32, dev)   # consumer: same layout
+    st.f_ack = uncached_zeros((16,), torch.int32, dev)   # [0] the consumer's ack (ours)
+    st.f_prod = uncached_zeros((16,), torch.int32, dev)  # [0] the producer's ack (we write)
+    st.slots_in = uncached_zeros((nslot, 8, K), torch.bfloat16, dev)
+    st.slots_out = uncached_zeros((nslot, 8, N), torch.float32 if out_f32 else torch.bfloat16,
+                                  dev)
+    st.sync = torch.zeros(2 * nslot + 4, dtype=torch.int32, device=dev)
+    st.hp, st.dp = n.host_alloc_mapped(64)
+    st.ctl = np.ctypeslib.as_array((ctypes.c_uint32 * 16).from_address(st.hp))
+    g = torch.Generator().manual_seed(K + N)
+    st.w = (torch.randn(N, K, generator=g) * 0.05).to(torch.bfloat16).to(dev)
+    st.b = torch.randn(N, generator=g).to(dev)
+    # the persistent kernel's stream has a hardware queue of its own (as in serve/fastpath.py):
+    # this test's writes on the current stream must never queue behind it
+    st.s_ptr = n.stream_create_dedicated()
+    st.s = torch.cuda.ExternalStream(st.s_ptr, device=dev)
+    st.act, st.out_f32 = act, out_f32
+    st.epoch = 0
+
+    def launch(start, idle=5.0, timeout=2.0):
+        st.epoch += 1
+        st.ctl[0] = 0
+        es = st.slots_out.element_size()
+        return n.chain_stage_run(
+            st.s.cuda_stream, st.f_in.data_ptr(), st.f_in.data_ptr() + 64,
+            st.slots_in.data_ptr(), K, st.f_prod.data_ptr(), st.w.data_ptr(), K, st.b.data_ptr(),
+            {"relu": 1, "softmax": 3}[act], st.n_out, K, int(out_f32), st.slots_out.data_ptr(),
+            8 * N * es, N, st.f_out.data_ptr() + 64, 2, st.f_out.data_ptr(), st.f_ack.data_ptr(),
+            st.dp, st.dp + 4, st.sync.data_ptr(), start, st.epoch, 1, nslot, 8, idle, timeout)
+
+    def feed(seq, x, status=0):
+        slot = seq % nslot
+        rows = x.shape[0]
+        st.slots_in[slot, :rows].copy_(x)
+        st.f_in[16 + 2 * slot:18 + 2 * slot] = torch.tensor([status, rows], dtype=torch.int32,
+                                                            device=dev)
+        torch.cuda.current_stream(dev).synchronize()
+        st.f_in[slot] = seq
+        torch.cuda.current_stream(dev).synchronize()
+
+    def wait_out(seq, limit=10.0):
+        slot = seq % nslot
+        t0 = time.monotonic()
+        while int(st.f_out[slot]) != seq:
+            assert time.monotonic() - t0 < limit, f"request {seq} never reached the consumer"
+            time.sleep(1e-3)
+        return st.f_out[16 + 2 * slot:18 + 2 * slot].tolist(), st.slots_out[slot].clone()
+
+    st.launch, st.feed, st.wait_out = launch, feed, wait_out
+    return st
+
+
+@pytest.mark.timeout(120)
+def test_chain_stage_persistent_in_one_process(dev):
+    """chain_stage_run: ONE launch serves a sequence of requests of varying rows -- each
+    output bitwise equal to ops.gemv (chain_gemv_send's math), the producer acked and the
+    progress counter published in host memory; an upstream failure travels on unchanged; a
+    consumer that never drains is blamed; the host's stop word and the idle timer end the
+    launch, and a relaunch from the published progress continues the sequence."""
+    import torch
+
+    from docker_dist_nn_amd import ops
+
+    K, N = 1024, 1024
+    st = _persistent_stage(dev, K, N, "relu")
+    g = torch.Generator().manual_seed(11)
+    xs = (torch.randn(64, K, generator=g) * 0.5).to(torch.bfloat16).to(dev)
+    wg = st.launch(0)
+    assert wg >= 16
+    seq, off = 0, 0
+    for rows in (1, 3, 8, 2, 5, 1, 8, 4, 7):
+        seq += 1
+        x = xs[off:off + rows]
+        off += rows
+        st.feed(seq, x)
+        hdr, out = st.wait_out(seq)
+        ref = torch.empty(rows, N, dtype=torch.bfloat16, device=dev)
+        ops.gemv(x, st.w, st.b, ref, act="relu")
+        assert hdr == [0, rows], (seq, hdr)
+        assert torch.equal(out[:rows], ref), f"request {seq} ({rows} rows) differs"
+        assert int(st.f_prod[0]) == seq and int(st.ctl[1]) == seq
+        st.f_ack[0] = seq  # the consumer drained it
+    # an upstream failure (stage 0 blamed for a deadline) travels on, no rows written
+    seq += 1
+    st.slots_out[seq % st.nslot].zero_()
+    st.feed(seq, xs[:2], status=4 | (0 << 8))
+    hdr, out = st.wait_out(seq)
+    assert hdr == [4, 2] and float(out.float().abs().sum()) == 0.0
+    # the consumer stops draining: a request reusing an undrained slot blames it (stage 2)
+    seq += 1
+    st.f_ack[0] = seq - 1 - st.nslot  # too old for request `seq`
+    st.feed(seq, xs[:1])
+    hdr, _ = st.wait_out(seq)
+    assert (hdr[0] & 0xFF) == 4 and (hdr[0] >> 8) == 2, hdr
+    st.f_ack[0] = seq
+    # the host's stop word ends the launch promptly
+    t0 = time.monotonic()
+    st.ctl[0] = 1
+    st.s.synchronize()
+    assert time.monotonic() - t0 < 1.0
+    done = int(st.ctl[1])
+    assert done == seq
+    # a relaunch from the progress counter continues; then the idle timer ends it alone
+    st.launch(done, idle=0.3)
+    seq += 1
+    st.feed(seq, xs[:3])
+    hdr, out = st.wait_out(seq)
+    ref = torch.empty(3, N, dtype=torch.bfloat16, device=dev)
+    ops.gemv(xs[:3], st.w, st.b, ref, act="relu")
+    assert hdr == [0, 3] and torch.equal(out[:3], ref)
+    t0 = time.monotonic()
+    st.s.synchronize()
+    assert time.monotonic() - t0 < 3.0 and int(st.sync[2 * st.nslot + 1]) == st.epoch
+    assert st.sync[:st.nslot].tolist() == [0] * st.nslot  # counters left at zero
+    st.n.host_free(st.hp)
+    st.n.stream_destroy(st.s_ptr)
+
+
+@pytest.mark.timeout(120)
+def test_chain_stage_persistent_softmax_last_stage(dev):
+    """The last stage's persistent kernel: one workgroup, fp32 rows into rank 0's result
+    slot layout, row softmax over the real outputs against the fp32 torch reference."""
+    import torch
+
+    K, N, n_out = 1024, 64, 10
+    st = _persistent_stage(dev, K, N, "softmax", out_f32=True, n_out=n_out)
+    g = torch.Generator().manual_seed(5)
+    x = (torch.randn(8, K, generator=g) * 0.5).to(torch.bfloat16).to(dev)
+    assert st.launch(0) == 1
+    for seq, rows in enumerate((1, 8, 3), start=1):
+        st.feed(seq, x[:rows])
+        hdr, out = st.wait_out(seq)
+        z = x[:rows].float() @ st.w[:n_out].float().t() + st.b[:n_out]
+        ref = torch.softmax(z, dim=1)
+        assert hdr == [0, rows]
+        torch.testing.assert_close(out[:rows, :n_out], ref, atol=1e-5, rtol=1e-4)
+        st.f_ack[0] = seq
+    st.ctl[0] = 1
+    st.s.synchronize()
+    st.n.host_free(st.hp)
+    st.n.stream_destroy(st.s_ptr)
