@@ -1260,7 +1260,7 @@ PYBIND11_MODULE(_native, m) {
           int out_f32, uintptr_t dst, long dst_slot_bytes, long dst_ld, uintptr_t dst_hdr,
           long hdr_stride, uintptr_t next_flags, uintptr_t ack, uintptr_t stop, uintptr_t done,
           uintptr_t sync, uint32_t start_seq, uint32_t epoch, int stage, int nslot,
-          int max_rows, double idle_s, double timeout_s, int workgroups) {
+          int max_rows, double idle_s, double timeout_s, int workgroups, int share) {
         dnn::ChainStage p{};
         p.in_flags = static_cast<const uint32_t*>(ptr(in_flags));
         p.in_hdrs = static_cast<const uint32_t*>(ptr(in_hdrs));
@@ -1291,8 +1291,9 @@ PYBIND11_MODULE(_native, m) {
         p.max_rows = max_rows;
         p.idle_ticks = dnn::chain_ticks(idle_s);
         p.timeout_ticks = dnn::chain_ticks(timeout_s);
-        const int wg = workgroups > 0 ? workgroups : dnn::chain_stage_workgroups(N, act);
-        chk(dnn::chain_stage_run(p, wg, S(s)), "chain_stage_run");
+        const int want = workgroups > 0 ? workgroups : dnn::chain_stage_workgroups(N, act);
+        const int wg = dnn::chain_stage_run(p, want, share, S(s));
+        if (wg < 1) chk(wg, "chain_stage_run");
         return wg;
       },
       py::arg("stream"), py::arg("in_flags"), py::arg("in_hdrs"), py::arg("in_slots"),
@@ -1301,7 +1302,8 @@ PYBIND11_MODULE(_native, m) {
       py::arg("dst_slot_bytes"), py::arg("dst_ld"), py::arg("dst_hdr"), py::arg("hdr_stride"),
       py::arg("next_flags"), py::arg("ack"), py::arg("stop"), py::arg("done"), py::arg("sync"),
       py::arg("start_seq"), py::arg("epoch"), py::arg("stage"), py::arg("nslot"),
-      py::arg("max_rows"), py::arg("idle_s"), py::arg("timeout_s"), py::arg("workgroups") = 0);
+      py::arg("max_rows"), py::arg("idle_s"), py::arg("timeout_s"), py::arg("workgroups") = 0,
+      py::arg("share") = 1);
   m.def(
       "chain_signal",
       [=](uintptr_t s, uintptr_t flag, uint32_t value) {

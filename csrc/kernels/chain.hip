@@ -36,6 +36,20 @@ __device__ __forceinline__ bool spin(const uint32_t* flag, uint32_t target,
   return true;
 }
 
+// spin() without the acquire: a relaxed system-scope poll (no cache invalidation). For flags
+// whose writer's data this wave does not read (the consumer's ack: only orders our later
+// stores, which are issued after the load returns).
+__device__ __forceinline__ bool spin_relaxed(const uint32_t* flag, uint32_t target,
+                                             unsigned long long ticks) {
+  const unsigned long long t0 = wall_clock64();
+  while ((int)(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - target) <
+         0) {
+    __builtin_amdgcn_s_sleep(1);
+    if (wall_clock64() - t0 > ticks) return false;
+  }
+  return true;
+}
+
 // rows x row_bytes from src (ld sld bytes) to dst (ld dld bytes), 16-byte vectors
 __device__ __forceinline__ void copy_rows(const char* src, long sld, char* dst, long dld,
                                           int rows, int row_bytes) {
@@ -237,7 +251,7 @@ __device__ __forceinline__ void cs_layer(const ChainStage& p, const u16* xs, int
                                          float* logits) {
   const unsigned t = threadIdx.x;
   const int lane = t & 63;
-  constexpr int U = 4;
+  constexpr int U = 2;  // (the loop order per lane is U-independent: bitwise as U = 4)
   for (int n0 = (blockIdx.x * CG_WAVES + (int)(t >> 6)) * NB; n0 < p.N;
        n0 += gridDim.x * CG_WAVES * NB) {
     float acc[NB][M];
@@ -313,11 +327,17 @@ __global__ __launch_bounds__(256) void chain_stage_kernel(ChainStage p) {
   uint32_t* fail = p.sync + p.nslot;
   uint32_t* go = p.sync + 2 * p.nslot;  // workgroup 0: the last request it let through
   uint32_t* ex = go + 1;                // == epoch: this launch ends before request *go + 1
+                                        // (ex[1]: why -- 1 stop, 2 idle; ex[2]: the stop
+                                        // word read / the idle ticks)
   for (uint32_t seq = p.start_seq + 1;; ++seq) {
     const int slot = (int)(seq % (uint32_t)p.nslot);
     if (t == 0) {
       uint32_t run = 1;
       if (blockIdx.x == 0) {
+        // the consumer drained the slot this request will reuse -- checked BEFORE the input
+        // arrives (it nearly always has: the wait is off the request's path). Bounded: a stuck
+        // consumer is reported downstream as DEADLINE naming it, no rows are written.
+        const bool ack_ok = spin_relaxed(p.ack, seq - (uint32_t)p.nslot, p.timeout_ticks);
         // the stop word lives in host memory (a read crosses the host link): looked at every
         // ~20 us of waiting, not every poll of the (local) input flag
         const unsigned long long t0 = wall_clock64();
@@ -329,22 +349,26 @@ __global__ __launch_bounds__(256) void chain_stage_kernel(ChainStage p) {
           const unsigned long long now = wall_clock64();
           if (now - t_stop > 2000) {
             t_stop = now;
-            if (__hip_atomic_load(p.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+            const uint32_t sv = __hip_atomic_load(p.stop, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_SYSTEM);
+            if (sv) {
               run = 0;
+              __hip_atomic_store(ex + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              __hip_atomic_store(ex + 2, sv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
               break;
             }
           }
           if (now - t0 > p.idle_ticks) {
             run = 0;
+            __hip_atomic_store(ex + 1, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(ex + 2, (uint32_t)(now - t0), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
             break;
           }
           __builtin_amdgcn_s_sleep(1);
         }
         if (run) {
-          // the consumer drained the slot this request reuses (bounded: a stuck consumer is
-          // reported downstream as DEADLINE naming it, the request's rows are not written)
-          const bool ok = spin(p.ack, seq - (uint32_t)p.nslot, p.timeout_ticks);
-          __hip_atomic_store(fail + slot, ok ? 0u : 1u, __ATOMIC_RELAXED,
+          __hip_atomic_store(fail + slot, ack_ok ? 0u : 1u, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(go, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         } else {
@@ -364,7 +388,9 @@ __global__ __launch_bounds__(256) void chain_stage_kernel(ChainStage p) {
         }
       }
       if (run) {
-        __atomic_thread_fence(__ATOMIC_ACQUIRE);  // system scope: the producer's rows + header
+        // no acquire fence: it would invalidate the L2 that keeps this stage's weights resident
+        // between requests. The header and rows are read with system-scope loads instead
+        // (they bypass every cache level), issued after the flag / go was seen.
         s_cmd[1] = __hip_atomic_load(p.in_hdrs + 2 * slot, __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_SYSTEM);
         s_cmd[2] = __hip_atomic_load(p.in_hdrs + 2 * slot + 1, __ATOMIC_RELAXED,
@@ -383,10 +409,12 @@ __global__ __launch_bounds__(256) void chain_stage_kernel(ChainStage p) {
     char* dst = p.dst + slot * p.dst_slot_bytes;
     if (compute) {
       const u16* src = p.in_slots + (long)slot * p.max_rows * p.ldx;
-      const int cpr = p.K >> 3;
+      const int cpr = p.K >> 2;  // 8-byte words per row
       for (int i = t; i < rows * cpr; i += blockDim.x) {
         const int r = i / cpr, c = i - r * cpr;
-        *(uint4*)(xs + r * p.K + 8 * c) = *(const uint4*)(src + r * p.ldx + 8 * c);
+        *(uint64_t*)(xs + r * p.K + 4 * c) = __hip_atomic_load(
+            (const uint64_t*)(src + r * p.ldx + 4 * c), __ATOMIC_RELAXED,
+            __HIP_MEMORY_SCOPE_SYSTEM);
       }
       __syncthreads();
       switch (rows) {
@@ -417,10 +445,12 @@ __global__ __launch_bounds__(256) void chain_stage_kernel(ChainStage p) {
         }
       }
     }
-    __threadfence_system();  // this thread's rows are visible before the workgroup counts in
+    // this thread's rows are visible before the workgroup counts in: a release-only fence
+    // (a full __threadfence_system would also invalidate the L2 holding the weights)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     __syncthreads();
     if (t == 0) {
-      const uint32_t prev = __hip_atomic_fetch_add(cnt + slot, 1u, __ATOMIC_ACQ_REL,
+      const uint32_t prev = __hip_atomic_fetch_add(cnt + slot, 1u, __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_AGENT);
       if (prev == gridDim.x - 1) {  // the last workgroup: every row of the request landed
         uint32_t st = 0u;
@@ -432,7 +462,7 @@ __global__ __launch_bounds__(256) void chain_stage_kernel(ChainStage p) {
         __hip_atomic_store(hdr, st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(hdr + 1, (uint32_t)(rows_ok ? rows : 0), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
-        __threadfence_system();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
         __hip_atomic_store(p.next_flags + slot, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(p.prev_ack, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(p.done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -561,7 +591,7 @@ int chain_stage_workgroups(int N, int act) {
   return std::max(1, std::min(64, (N + CG_WAVES * CS_NB - 1) / (CG_WAVES * CS_NB)));
 }
 
-int chain_stage_run(const ChainStage& p, int workgroups, hipStream_t stream) {
+int chain_stage_run(const ChainStage& p, int workgroups, int share, hipStream_t stream) {
   if (!p.in_flags || !p.in_hdrs || !p.in_slots || !p.prev_ack || !p.w || !p.dst || !p.dst_hdr ||
       !p.next_flags || !p.ack || !p.stop || !p.done || !p.sync || misaligned4(p.in_flags) ||
       misaligned4(p.sync) || misaligned4(p.next_flags) || misaligned4(p.dst_hdr))
@@ -574,8 +604,19 @@ int chain_stage_run(const ChainStage& p, int workgroups, hipStream_t stream) {
                    (p.act == ACT_SOFTMAX ? (long)p.max_rows * p.N * 4 : 0);
   if (lds > 64 * 1024) return -3;  // rows staged in LDS: K (and a softmax's N) bounded
   if (workgroups < 1 || (p.act == ACT_SOFTMAX && workgroups != 1)) return -4;
+  // every workgroup of every persistent stage on this GPU must be resident at once (a request
+  // completes only when all of a stage's workgroups count in, and resident ones never yield):
+  // `share` stages split what the GPU holds, with a quarter kept for everything else
+  int per_cu = 0, dev = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chain_stage_kernel, 256,
+                                                   (size_t)lds) != hipSuccess ||
+      hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return -9;
+  const int cap = std::max(1, per_cu * cus * 3 / 4 / std::max(1, share));
+  workgroups = std::min(workgroups, cap);
   hipLaunchKernelGGL(chain_stage_kernel, dim3(workgroups), dim3(256), (size_t)lds, stream, p);
-  return hipGetLastError() == hipSuccess ? 0 : -9;
+  return hipGetLastError() == hipSuccess ? workgroups : -9;
 }
 
 int chain_signal(uint32_t* flag, uint32_t value, hipStream_t stream) {

@@ -138,13 +138,16 @@ struct ChainStage {
   const uint32_t* ack;       // this stage's ack word (the consumer writes it)
   const uint32_t* stop;      // != 0 -> return (coherent host memory, set by the host)
   uint32_t* done;            // the last request finished (coherent host memory: progress)
-  uint32_t* sync;            // [nslot + 4] zeroed: per-slot arrival counters, go, exit
+  uint32_t* sync;            // [2 nslot + 4] zeroed: per-slot arrival counters, per-slot ack
+                             // failures, go, exit (+ exit reason, its value)
   uint32_t start_seq;        // serve start_seq + 1, start_seq + 2, ...
   uint32_t epoch;            // this launch's id (exit word value)
   int stage, nslot, max_rows;
   unsigned long long idle_ticks, timeout_ticks;
 };
-int chain_stage_run(const ChainStage& p, int workgroups, hipStream_t stream);
+// Returns the workgroups launched (>= 1; capped so that `share` persistent stages on this GPU
+// are all resident at once) or < 0 on a parameter / launch error.
+int chain_stage_run(const ChainStage& p, int workgroups, int share, hipStream_t stream);
 int chain_stage_workgroups(int N, int act);  // the grid chain_stage_run is given by default
 
 // Training step plans (runtime/step_plan.cpp COPYSIG): a peer copy followed by its flag in ONE

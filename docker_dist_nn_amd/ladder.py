@@ -137,12 +137,16 @@ def write_result(obj: dict) -> bool:
 
 def rung_fault(rung: str, spec: str) -> str:
     """``DNN_LADDER_FAULT`` = 'rung=fault;rung=fault' (fault in DNN_FAULT syntax): the fault
-    the child of ``rung`` injects (tests of the ladder itself)."""
+    the child of ``rung`` injects (tests of the ladder itself); rung '*' = every rung not named
+    on its own."""
+    wild = ""
     for item in filter(None, (s.strip() for s in spec.split(";"))):
         name, _, fault = item.partition("=")
         if name.strip() == rung:
             return fault.strip()
-    return ""
+        if name.strip() == "*":
+            wild = fault.strip()
+    return wild
 
 
 # ---- supervisor side ----------------------------------------------------------------------

@@ -41,6 +41,7 @@ import ctypes
 import logging
 import mmap
 import os
+import socket
 import threading
 import time
 from typing import Optional
@@ -177,7 +178,10 @@ class FastChain:
                                            device=self.dev)
             torch.cuda.synchronize(self.dev)
             mine = {"flags": self.n.ipc_export(self.flags.data_ptr()),
-                    "in_w": self.in_w, "out_w": self.out_w, "out_dim": st.out_dim}
+                    "in_w": self.in_w, "out_w": self.out_w, "out_dim": st.out_dim,
+                    # which GPU: persistent stages sharing one split its workgroup slots
+                    "gpu": (socket.gethostname(), str(torch.cuda.get_device_properties(
+                        self.dev).uuid))}
             if self.rank > 0:
                 mine["slots"] = self.n.ipc_export(self.slots.data_ptr())
         except Exception as e:  # noqa: BLE001 -- agreed on below
@@ -212,6 +216,9 @@ class FastChain:
         for r in range(self.world - 1):
             if not bad and everyone[r]["out_w"] != everyone[r + 1]["in_w"]:
                 bad.append((r, f"width {everyone[r]['out_w']} -> {everyone[r + 1]['in_w']}"))
+        if not bad:  # ranks > 0 on this rank's GPU: the persistent stages that share it
+            self.gpu_share = sum(1 for r in range(1, self.world)
+                                 if everyone[r].get("gpu") == everyone[self.rank].get("gpu"))
         if bad:
             self.why = f"fast path unavailable: {bad}"[:300]
             log.info(self.why)
@@ -617,7 +624,7 @@ class FastChain:
             w.stride(0), b.data_ptr(), ops.kernels._act(act), n_out, self.in_w, int(last), dst,
             slot_b, self.out_w, hdr, hstride, nflags, _ptr(self.flags, F_ACK), self._ctl_dev,
             self._ctl_dev + 4, self.sync.data_ptr(), start & 0xFFFFFFFF, epoch, self.rank, NSLOT,
-            self.max_rows, PERSIST_IDLE_S, self.cr.hop_timeout)
+            self.max_rows, PERSIST_IDLE_S, self.cr.hop_timeout, share=max(1, self.gpu_share))
 
     def _persist_loop(self) -> None:
         """Keep the stage kernel running until the ring stops: relaunch it after an idle exit,

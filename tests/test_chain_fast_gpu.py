@@ -339,6 +339,9 @@ def _persistent_stage(dev, K, N, act, nslot=4, out_f32=False, n_out=None):
     # this test's writes on the current stream must never queue behind it
     st.s_ptr = n.stream_create_dedicated()
     st.s = torch.cuda.ExternalStream(st.s_ptr, device=dev)
+    # ... and it is a blocking stream: the test's own work goes on a non-blocking stream, or
+    # the null stream would wait for the kernel (serve/fastpath.py pauses it instead)
+    st.side = torch.cuda.Stream(dev)
     st.act, st.out_f32 = act, out_f32
     st.epoch = 0
 
@@ -384,10 +387,21 @@ def test_chain_stage_persistent_in_one_process(dev):
     launch, and a relaunch from the published progress continues the sequence."""
     import torch
 
-    from docker_dist_nn_amd import ops
-
     K, N = 1024, 1024
     st = _persistent_stage(dev, K, N, "relu")
+    prev = torch.cuda.current_stream(dev)
+    torch.cuda.set_stream(st.side)
+    try:
+        _persistent_relu_body(st, dev, K, N)
+    finally:
+        torch.cuda.set_stream(prev)
+
+
+def _persistent_relu_body(st, dev, K, N):
+    import torch
+
+    from docker_dist_nn_amd import ops
+
     g = torch.Generator().manual_seed(11)
     xs = (torch.randn(64, K, generator=g) * 0.5).to(torch.bfloat16).to(dev)
     wg = st.launch(0)
@@ -449,6 +463,17 @@ def test_chain_stage_persistent_softmax_last_stage(dev):
 
     K, N, n_out = 1024, 64, 10
     st = _persistent_stage(dev, K, N, "softmax", out_f32=True, n_out=n_out)
+    prev = torch.cuda.current_stream(dev)
+    torch.cuda.set_stream(st.side)
+    try:
+        _persistent_softmax_body(st, dev, K, N, n_out)
+    finally:
+        torch.cuda.set_stream(prev)
+
+
+def _persistent_softmax_body(st, dev, K, N, n_out):
+    import torch
+
     g = torch.Generator().manual_seed(5)
     x = (torch.randn(8, K, generator=g) * 0.5).to(torch.bfloat16).to(dev)
     assert st.launch(0) == 1

@@ -117,6 +117,9 @@ def test_rung_fault_parse():
 
     assert rung_fault("b", FAULT) == "stage:1,step:0,kind:crash"
     assert rung_fault("z", FAULT) == ""
+    wild = "*=stage:0,step:3,kind:hang;b=stage:1,step:3,kind:hang"
+    assert rung_fault("b", wild) == "stage:1,step:3,kind:hang"  # a named rung wins
+    assert rung_fault("z", wild) == "stage:0,step:3,kind:hang"
     names = [r.name for r in bench_rungs(8)]
     assert names == ["default", "ipc-slotted", "rccl-slotted", "rccl-streams", "python",
                      "dp-native", "dp-python"]
