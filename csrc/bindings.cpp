@@ -1037,6 +1037,25 @@ PYBIND11_MODULE(_native, m) {
       "host_free", [](uintptr_t p) { (void)hipHostFree(reinterpret_cast<void*>(p)); },
       py::arg("ptr"));
   m.def(
+      "host_register",
+      [](uintptr_t p, size_t bytes) {
+        // page-locks and maps existing host memory (e.g. a /dev/shm mapping shared by two
+        // processes) for the GPU; returns its device pointer
+        if (hipHostRegister(reinterpret_cast<void*>(p), bytes, hipHostRegisterMapped) !=
+            hipSuccess)
+          throw std::runtime_error("hipHostRegister failed");
+        void* d = nullptr;
+        if (hipHostGetDevicePointer(&d, reinterpret_cast<void*>(p), 0) != hipSuccess) {
+          (void)hipHostUnregister(reinterpret_cast<void*>(p));
+          throw std::runtime_error("hipHostGetDevicePointer failed");
+        }
+        return reinterpret_cast<uintptr_t>(d);
+      },
+      py::arg("ptr"), py::arg("bytes"));
+  m.def(
+      "host_unregister",
+      [](uintptr_t p) { (void)hipHostUnregister(reinterpret_cast<void*>(p)); }, py::arg("ptr"));
+  m.def(
       "stream_create_dedicated",
       []() {
         // a stream on a hardware queue of its own (the runtime gives a CU-masked stream a new

@@ -36,20 +36,6 @@ __device__ __forceinline__ bool spin(const uint32_t* flag, uint32_t target,
   return true;
 }
 
-// spin() without the acquire: a relaxed system-scope poll (no cache invalidation). For flags
-// whose writer's data this wave does not read (the consumer's ack: only orders our later
-// stores, which are issued after the load returns).
-__device__ __forceinline__ bool spin_relaxed(const uint32_t* flag, uint32_t target,
-                                             unsigned long long ticks) {
-  const unsigned long long t0 = wall_clock64();
-  while ((int)(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - target) <
-         0) {
-    __builtin_amdgcn_s_sleep(1);
-    if (wall_clock64() - t0 > ticks) return false;
-  }
-  return true;
-}
-
 // rows x row_bytes from src (ld sld bytes) to dst (ld dld bytes), 16-byte vectors
 __device__ __forceinline__ void copy_rows(const char* src, long sld, char* dst, long dld,
                                           int rows, int row_bytes) {
@@ -337,12 +323,32 @@ __global__ __launch_bounds__(256) void chain_stage_kernel(ChainStage p) {
         // the consumer drained the slot this request will reuse -- checked BEFORE the input
         // arrives (it nearly always has: the wait is off the request's path). Bounded: a stuck
         // consumer is reported downstream as DEADLINE naming it, no rows are written.
-        const bool ack_ok = spin_relaxed(p.ack, seq - (uint32_t)p.nslot, p.timeout_ticks);
-        // the stop word lives in host memory (a read crosses the host link): looked at every
-        // ~20 us of waiting, not every poll of the (local) input flag
+        // The stop word lives in host memory (a read crosses the host link): looked at every
+        // ~20 us of waiting, not every poll of a (local) flag -- in this ack wait too, so a
+        // stage whose consumer is stuck still returns promptly when asked.
+        bool ack_ok = true;
+        unsigned long long t_stop = wall_clock64();
+        {
+          const unsigned long long ta = t_stop;
+          while ((int)(__hip_atomic_load(p.ack, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) -
+                       (seq - (uint32_t)p.nslot)) < 0) {
+            const unsigned long long now = wall_clock64();
+            if (now - t_stop > 2000) {
+              t_stop = now;
+              if (__hip_atomic_load(p.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+                run = 0;
+                break;
+              }
+            }
+            if (now - ta > p.timeout_ticks) {
+              ack_ok = false;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+        }
         const unsigned long long t0 = wall_clock64();
-        unsigned long long t_stop = t0;
-        for (;;) {
+        for (; run;) {
           if ((int)(__hip_atomic_load(p.in_flags + slot, __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_SYSTEM) - seq) >= 0)
             break;

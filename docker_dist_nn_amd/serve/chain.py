@@ -110,6 +110,10 @@ class ChainRank:
         self._packets: dict = {}
         self.store = dist.distributed_c10d._get_default_store() if world > 1 else None
         self.fast = None  # serve/fastpath.FastChain once enable_fast() agreed on it
+        # every thread of a chain rank does its GPU work on this non-blocking stream, never on
+        # the null stream: a persistent device-chain kernel runs on a blocking stream of its
+        # own (serve/fastpath.py), and null-stream work would wait for it to return
+        self.work_stream = torch.cuda.Stream(device) if device.type == "cuda" else None
         self._processed = 0
         self._published = 0
         if rank > 0 and world > 1:
@@ -117,9 +121,16 @@ class ChainRank:
             t.start()
         if rank == 0 and world > 1:
             for fn, nm in ((self._sender, "chain-send"), (self._receiver, "chain-recv")):
-                t = threading.Thread(target=fn, name=nm, daemon=True)
+                t = threading.Thread(target=self._on_work_stream, args=(fn,), name=nm,
+                                     daemon=True)
                 t.start()
                 self._threads.append(t)
+
+    def _on_work_stream(self, fn, *args):
+        """Run ``fn`` with this thread's current stream set to the work stream (thread-local)."""
+        if self.work_stream is not None:
+            torch.cuda.set_stream(self.work_stream)
+        return fn(*args)
 
     # -- transport ----------------------------------------------------------------------------
     def _hdr(self, *vals) -> torch.Tensor:
@@ -248,6 +259,8 @@ class ChainRank:
         self.stage.check_input_dim(cols)  # ValueError -> INVALID_ARGUMENT
         if self.fast is not None and rows <= self.small:
             return self.fast.predict(x, timeout)
+        if self.work_stream is not None:  # (an ingress worker thread: see work_stream)
+            torch.cuda.set_stream(self.work_stream)
         R = bucket(rows)
         with self.compute_lock:  # this rank's per-bucket buffers are shared
             buf = self.stage.buffers(R)
@@ -337,6 +350,8 @@ class ChainRank:
         raise RuntimeError("injected fault")
 
     def loop(self) -> None:
+        if self.work_stream is not None:
+            torch.cuda.set_stream(self.work_stream)
         prev = self.rank - 1
         last = self.rank == self.world - 1
         in_w = self.stage.in_pad

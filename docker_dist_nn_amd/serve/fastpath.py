@@ -216,8 +216,8 @@ class FastChain:
         for r in range(self.world - 1):
             if not bad and everyone[r]["out_w"] != everyone[r + 1]["in_w"]:
                 bad.append((r, f"width {everyone[r]['out_w']} -> {everyone[r + 1]['in_w']}"))
-        if not bad:  # ranks > 0 on this rank's GPU: the persistent stages that share it
-            self.gpu_share = sum(1 for r in range(1, self.world)
+        if not bad:  # the ranks on this rank's GPU: the persistent stages that may share it
+            self.gpu_share = sum(1 for r in range(self.world)
                                  if everyone[r].get("gpu") == everyone[self.rank].get("gpu"))
         if bad:
             self.why = f"fast path unavailable: {bad}"[:300]
@@ -255,6 +255,8 @@ class FastChain:
         if not self._agree(good):
             self.why = "fast path unavailable: no shared-memory announcement ring"
             return
+        self.ack_ptr = _ptr(self.flags, F_ACK)  # this rank's "consumer drained" word
+        self.res_flags_ptr = self.next_flags + 4 * F_RES if self.rank == self.world - 1 else 0
         self.stream = torch.cuda.Stream(self.dev)
         # the stage's last layer fused with the send of its hop (chain_gemv_send): not for a
         # softmax output (a row-wise second pass)
@@ -284,28 +286,117 @@ class FastChain:
                          switches.get("DNN_CHAIN_NATIVE") == "1" else None)
         self.failed = False
         self.persist = self._persist_ok()
+        self._setup_doorbell(ann_dir, st)
         if self.persist:
-            # the kernel never returns while requests flow: it gets a hardware queue of its own
-            # (work of this process's other streams would otherwise wait behind it whenever
-            # the runtime maps their stream onto the same queue)
-            self._pstream_ptr = self.n.stream_create_dedicated()
-            self.pstream = torch.cuda.ExternalStream(self._pstream_ptr, device=self.dev)
-            # per-slot arrival counters, ack failures, go, exit (chain.hip ChainStage) and
-            # the stop word / progress counter in coherent host memory
-            self.sync = torch.zeros(2 * NSLOT + 4, dtype=torch.int32, device=self.dev)
-            self._ctl_host, self._ctl_dev = self.n.host_alloc_mapped(64)
-            self.ctl = np.ctypeslib.as_array((ctypes.c_uint32 * 16).from_address(self._ctl_host))
-            self._want_pause = False
-            self._pause_lock = threading.Lock()
-            self._parked = threading.Event()
-            self._resume = threading.Event()
-            self._runner_done = threading.Event()
-            self.workgroups = 0
+            self._set_persist_state()
         self.ok = True
         self.why = (f"device-side chain ({NSLOT} slots per hop"
                     + (", last layer fused with the send" if self.fused else "")
                     + (", one-layer stages as persistent kernels"
-                       if switches.get("DNN_CHAIN_PERSIST") == "1" else "") + ")")
+                       if switches.get("DNN_CHAIN_PERSIST") == "1" else "")
+                    + (", requests and results through host-memory doorbells"
+                       if self.doorbell else "") + ")")
+        if self.doorbell and self.rank == 0:  # rank 0's own stage kernel and its runner
+            t = threading.Thread(target=self.loop, name="chain-doorbell", daemon=True)
+            t.start()
+            self._runner = t
+
+    # ---- doorbells (rank 0 <-> host memory) ---------------------------------------------------
+    def _setup_doorbell(self, ann_dir: str, st) -> None:
+        """DNN_CHAIN_DOORBELL: rank 0's stage is a persistent kernel too, reading each request
+        from host memory the ingress thread writes (rows, header, then the flag), and the last
+        rank writes results into a host-memory ring shared with rank 0 (a /dev/shm mapping
+        page-locked in both processes), which rank 0's thread polls on the CPU. A request then
+        costs rank 0 a bf16 conversion, a few stores and a spin: no HIP call at all."""
+        self.doorbell = False
+        name = [None]
+        if self.rank == 0 and switches.get("DNN_CHAIN_DOORBELL") == "1" and \
+                self._persist_ok(rank0=True):
+            path = f"{ann_dir}/dnn_res_{os.getpid()}_{os.environ.get('MASTER_PORT', '0')}"
+            try:
+                fd = os.open(path, os.O_RDWR | os.O_CREAT | os.O_TRUNC, 0o600)
+                os.ftruncate(fd, NSLOT * self.res_bytes + 4096)
+                os.close(fd)
+                name = [path]
+            except OSError as e:
+                log.info(f"doorbell result ring unavailable: {e!r}")
+        dist.broadcast_object_list(name, src=0)
+        if name[0] is None:
+            return
+        good = True
+        try:
+            if self.rank in (0, self.world - 1):
+                self._open_results(name[0])
+            if self.rank == 0:
+                self._open_requests()
+        except Exception as e:  # noqa: BLE001 -- agreed on below
+            log.warning(f"doorbell set-up failed: {e!r}")
+            good = False
+        self.doorbell = self._agree(good)
+        if not self.doorbell:
+            self._close_doorbell()
+            return
+        if self.rank == self.world - 1:  # results go to the shared host ring
+            self.dst = self._res_dev
+            self.res_flags_ptr = self._res_dev + self._res_flag_off
+            self.ack_ptr = self._res_dev + self._res_flag_off + 4 * NSLOT
+        if self.rank == 0:
+            self.persist = True
+
+    def _open_results(self, path: str) -> None:
+        size = NSLOT * self.res_bytes + 4096
+        fd = os.open(path, os.O_RDWR)
+        try:
+            mm = mmap.mmap(fd, size)
+        finally:
+            os.close(fd)
+        self._res_mm, self._res_path, self._res_size = mm, path, size
+        self._res_anchor = ctypes.c_char.from_buffer(mm)  # (released before mm.close())
+        self._res_host = ctypes.addressof(self._res_anchor)
+        self._res_flag_off = NSLOT * self.res_bytes
+        self.res_np = np.ndarray((size // 4,), dtype=np.int32, buffer=mm)
+        self._res_dev = self.n.host_register(self._res_host, size)
+
+    def _open_requests(self) -> None:
+        row_b = self.max_rows * self.in_w * 2
+        self._req_rows_off = 0
+        self._req_hdr_off = NSLOT * row_b
+        self._req_flag_off = self._req_hdr_off + 8 * NSLOT
+        self._req_ack_off = self._req_flag_off + 4 * NSLOT
+        size = self._req_ack_off + 64
+        self._req_host, self._req_dev = self.n.host_alloc_mapped(size)
+        buf = (ctypes.c_char * size).from_address(self._req_host)
+        words = np.frombuffer(buf, dtype=np.int32)
+        self.req_hdr = words[self._req_hdr_off // 4:self._req_flag_off // 4].reshape(NSLOT, 2)
+        self.req_flag = words[self._req_flag_off // 4:self._req_ack_off // 4]
+        self.req_ack = words[self._req_ack_off // 4:self._req_ack_off // 4 + 1]
+        self.req_rows = torch.from_numpy(
+            np.frombuffer(buf, dtype=np.int16, count=NSLOT * self.max_rows * self.in_w)
+            .reshape(NSLOT, self.max_rows, self.in_w)).view(torch.bfloat16)
+        self._res_acked = 0
+        self._res_done: set = set()
+
+    def _close_doorbell(self) -> None:
+        if getattr(self, "_res_mm", None) is not None:
+            if getattr(self, "_res_dev", None):
+                self.n.host_unregister(self._res_host)
+                self._res_dev = 0
+            self.res_np = None
+            self._res_anchor = None
+            try:
+                self._res_mm.close()
+            except (BufferError, ValueError):
+                pass
+            self._res_mm = None
+            if self.rank == 0:
+                try:
+                    os.unlink(self._res_path)
+                except FileNotFoundError:
+                    pass
+        if getattr(self, "_req_host", None):
+            self.req_rows = self.req_hdr = self.req_flag = self.req_ack = None
+            self.n.host_free(self._req_host)
+            self._req_host = 0
 
     def _agree(self, ok: bool) -> bool:
         from ..parallel.comm import _cpu_group
@@ -320,7 +411,7 @@ class FastChain:
         consumer's slot ``slot``."""
         if self.rank == self.world - 1:  # rank 0's result slot: header, then fp32 rows
             base = self.dst + slot * self.res_bytes
-            return base + HDR, self.out_w * 4, base, self.next_flags + 4 * (F_RES + slot)
+            return base + HDR, self.out_w * 4, base, self.res_flags_ptr + 4 * slot
         row_b = self.out_w * 2
         return (self.dst + slot * self.max_rows * row_b, row_b,
                 self.next_flags + 4 * (F_HDR + 2 * slot), self.next_flags + 4 * (F_IN + slot))
@@ -336,7 +427,7 @@ class FastChain:
             rb = self.out_w * out.element_size()
         self.n.chain_send(s.cuda_stream, src, sld, dst, dld, rows if out is not None else 0, rb,
                           dhdr, in_hdr, _ptr(self.flags, F_ERR), self.rank, status,
-                          _ptr(self.flags, F_ACK), (seq - NSLOT) & 0xFFFFFFFF, dflag, seq, 0,
+                          self.ack_ptr, (seq - NSLOT) & 0xFFFFFFFF, dflag, seq, 0,
                           self.cr.hop_timeout)  # (ack compares wrap: seq < NSLOT passes)
 
     def _gemv_send(self, s: torch.cuda.Stream, x: torch.Tensor, rows: int, seq: int,
@@ -362,7 +453,7 @@ class FastChain:
                                b.data_ptr(), ops.kernels._act(st.acts[-1]), rows, w.shape[0],
                                self.in_w if recv else x.shape[1], int(f32), dst,
                                dld // (4 if f32 else 2), dhdr, in_hdr, _ptr(self.flags, F_ERR),
-                               self.rank, 0, _ptr(self.flags, F_ACK),
+                               self.rank, 0, self.ack_ptr,
                                (seq - NSLOT) & 0xFFFFFFFF, dflag, seq, prev_ack,
                                self.counter.data_ptr(), self.cr.hop_timeout, in_flag=in_flag)
 
@@ -382,6 +473,8 @@ class FastChain:
                                    f"chain")
             self.inflight += 1
         try:
+            if self.doorbell:
+                return self._predict_doorbell(x, timeout)
             return self._predict(x, timeout)
         finally:
             with self.lock:
@@ -458,6 +551,79 @@ class FastChain:
             if spins > 2000:
                 time.sleep(20e-6)
         return self._result(seq, slot, rows, t_in)
+
+    def _predict_doorbell(self, x: np.ndarray, timeout: Optional[float]) -> np.ndarray:
+        """The request through host memory: rows (bf16), header, flag -> rank 0's persistent
+        stage kernel; the logits come back in the shared result ring, polled here."""
+        import grpc
+
+        from .ingress import StageFailure
+
+        t_in = time.perf_counter()
+        rows, cols = x.shape
+        xb = torch.from_numpy(np.ascontiguousarray(x, np.float32)).to(torch.bfloat16)
+        limit = self.cr.hop_timeout * self.world
+        if timeout is not None:
+            limit = min(limit, max(0.0, timeout))
+        t_end = time.monotonic() + limit
+        with self.lock:
+            self.seq += 1
+            seq = self.seq
+            slot = seq % NSLOT
+            # the slot's previous request was read by the stage kernel (practically always)
+            while int(self.req_ack[0]) - (seq - NSLOT) < 0:
+                if time.monotonic() > t_end:
+                    raise StageFailure(self.cr.names[0], grpc.StatusCode.DEADLINE_EXCEEDED,
+                                       f"Deadline Exceeded (request slot {slot} not free)")
+                time.sleep(0)
+            self.req_rows[slot, :rows, :cols].copy_(xb)
+            self.req_hdr[slot, 0] = 0
+            self.req_hdr[slot, 1] = rows
+            self.req_flag[slot] = seq  # last: the kernel reads rows and header after it
+            self.ann.announce(seq, rows)  # (stages on the host loop follow the ring)
+        base = slot * self.res_bytes // 4
+        flag_i = self._res_flag_off // 4 + slot
+        res = self.res_np
+        spins = 0
+        try:
+            while res[flag_i] != seq:
+                spins += 1
+                if spins > 2000:
+                    if time.monotonic() > t_end:
+                        k = self.cr.blame(seq) if self.cr.store is not None else self.world - 1
+                        raise StageFailure(self.cr.names[k], grpc.StatusCode.DEADLINE_EXCEEDED,
+                                           f"Deadline Exceeded (request {seq} not answered "
+                                           f"within {limit:.1f} s)")
+                    time.sleep(20e-6)
+            hdr = res[base:base + 2].tolist()
+            out = res[base + HDR // 4:base + HDR // 4 + rows * self.res_w].view(np.float32)
+            out = out.reshape(rows, self.res_w)[:, :self.n_out].astype(np.float64)
+        finally:
+            self._consume(seq)
+        code, who = hdr[0] & 0xFF, (hdr[0] >> 8) & 0xFF
+        if code != ST_OK:
+            bad = self.cr.names[who % self.world]
+            if code == ST_DEADLINE:
+                raise StageFailure(bad, grpc.StatusCode.DEADLINE_EXCEEDED,
+                                   f"Deadline Exceeded (request {seq}: {bad} did not answer "
+                                   f"within {self.cr.hop_timeout:.1f} s)")
+            raise StageFailure(bad, grpc.StatusCode.INVALID_ARGUMENT if code == ST_VALUE
+                               else grpc.StatusCode.INTERNAL, f"stage {bad} failed (status "
+                               f"{code})")
+        self.lat.append(time.perf_counter() - t_in)
+        return out
+
+    def _consume(self, seq: int) -> None:
+        """Result slot of ``seq`` read (or abandoned): the shared ack word advances over the
+        contiguous run of consumed requests (the last rank reuses a slot only behind it)."""
+        with self.lock:
+            self._res_done.add(seq)
+            a = self._res_acked
+            while a + 1 in self._res_done:
+                a += 1
+                self._res_done.discard(a)
+            self._res_acked = a
+            self.res_np[self._res_flag_off // 4 + NSLOT] = a
 
     def _native_request(self, seq: int, slot: int, rows: int) -> None:
         """Rank 0, one-layer stage, fused path: H2D + layer-and-send + result wait + D2H +
@@ -595,10 +761,29 @@ class FastChain:
             self.cr._processed = seq
         torch.cuda.synchronize(self.dev)
 
-    # ---- ranks > 0: the persistent stage kernel -----------------------------------------------
-    def _persist_ok(self) -> bool:
+    # ---- the persistent stage kernel (ranks > 0; rank 0 with the doorbell) --------------------
+    def _set_persist_state(self) -> None:
+        # the kernel never returns while requests flow: it gets a hardware queue of its own
+        # (work of this process's other streams would otherwise wait behind it whenever the
+        # runtime maps their stream onto the same queue)
+        self._pstream_ptr = self.n.stream_create_dedicated()
+        self.pstream = torch.cuda.ExternalStream(self._pstream_ptr, device=self.dev)
+        # per-slot arrival counters, ack failures, go, exit (chain.hip ChainStage) and the
+        # stop word / progress counter in coherent host memory
+        self.sync = torch.zeros(2 * NSLOT + 4, dtype=torch.int32, device=self.dev)
+        self._ctl_host, self._ctl_dev = self.n.host_alloc_mapped(64)
+        self.ctl = np.ctypeslib.as_array((ctypes.c_uint32 * 16).from_address(self._ctl_host))
+        self._want_pause = False
+        self._pause_lock = threading.Lock()
+        self._parked = threading.Event()
+        self._resume = threading.Event()
+        self._runner_done = threading.Event()
+        self.workgroups = 0
+
+    def _persist_ok(self, rank0: bool = False) -> bool:
         st = self.cr.stage
-        if self.rank == 0 or switches.get("DNN_CHAIN_PERSIST") != "1" or len(st.layers) != 1:
+        if (self.rank == 0) != rank0 or switches.get("DNN_CHAIN_PERSIST") != "1" or \
+                len(st.layers) != 1:
             return False
         if self.cr.fault_stage == str(self.rank) or self.trace:
             return False  # fault injection and tracing act per request on the host
@@ -613,16 +798,23 @@ class FastChain:
         last = self.rank == self.world - 1
         if last:  # rank 0's result slots: header, then fp32 rows
             dst, slot_b = self.dst + HDR, self.res_bytes
-            hdr, hstride, nflags = self.dst, self.res_bytes // 4, self.next_flags + 4 * F_RES
+            hdr, hstride, nflags = self.dst, self.res_bytes // 4, self.res_flags_ptr
         else:
             dst, slot_b = self.dst, self.max_rows * self.out_w * 2
             hdr, hstride, nflags = self.next_flags + 4 * F_HDR, 2, self.next_flags + 4 * F_IN
+        if self.rank == 0:  # the doorbell: requests from host memory
+            in_flags = self._req_dev + self._req_flag_off
+            in_hdrs = self._req_dev + self._req_hdr_off
+            in_slots = self._req_dev + self._req_rows_off
+            prev_ack = self._req_dev + self._req_ack_off
+        else:
+            in_flags, in_hdrs = _ptr(self.flags, F_IN), _ptr(self.flags, F_HDR)
+            in_slots, prev_ack = self.slots.data_ptr(), self.prev_flags + 4 * F_ACK
         n_out = st.dims[-1] if act == "softmax" else w.shape[0]
         self.workgroups = self.n.chain_stage_run(
-            self.pstream.cuda_stream, _ptr(self.flags, F_IN), _ptr(self.flags, F_HDR),
-            self.slots.data_ptr(), self.in_w, self.prev_flags + 4 * F_ACK, w.data_ptr(),
-            w.stride(0), b.data_ptr(), ops.kernels._act(act), n_out, self.in_w, int(last), dst,
-            slot_b, self.out_w, hdr, hstride, nflags, _ptr(self.flags, F_ACK), self._ctl_dev,
+            self.pstream.cuda_stream, in_flags, in_hdrs, in_slots, self.in_w, prev_ack,
+            w.data_ptr(), w.stride(0), b.data_ptr(), ops.kernels._act(act), n_out, self.in_w,
+            int(last), dst, slot_b, self.out_w, hdr, hstride, nflags, self.ack_ptr, self._ctl_dev,
             self._ctl_dev + 4, self.sync.data_ptr(), start & 0xFFFFFFFF, epoch, self.rank, NSLOT,
             self.max_rows, PERSIST_IDLE_S, self.cr.hop_timeout, share=max(1, self.gpu_share))
 
@@ -685,6 +877,8 @@ class FastChain:
 
     def close(self) -> None:
         if self.ok:
+            if self.doorbell and self.rank == 0:
+                self._runner.join(5.0)
             self.ann.close()
             if self.persist and self._runner_done.is_set():
                 # (a runner still alive may have a kernel that writes these words: leaked)
@@ -692,3 +886,5 @@ class FastChain:
                 self.n.host_free(self._ctl_host)
                 self.n.stream_destroy(self._pstream_ptr)
                 self.persist = False
+            if self.doorbell and (not self.persist or self.rank != 0):
+                self._close_doorbell()

@@ -135,6 +135,10 @@ SWITCHES: dict[str, tuple[str, str]] = {
     "DNN_CHAIN_PERSIST": ("1", "device-side chain, one-layer stages > 0: one persistent kernel "
                                "per stage (chain_stage_run) serves every request with no host "
                                "work per request; 0 = the host enqueues each request's kernels"),
+    "DNN_CHAIN_DOORBELL": ("1", "device-side chain with persistent stages: rank 0's one-layer "
+                                "stage is a persistent kernel too, fed through host memory "
+                                "(rows, header, flag), and the last rank writes results into a "
+                                "shared host-memory ring: no HIP call per request on rank 0"),
     "DNN_CHAIN_TRACE": ("0", "device-side chain: 1 = every rank logs each request's steps and, "
                              "after synchronising, its flag words (diagnosis; serialises)"),
     "DNN_CHAIN_FAST": ("1", "rank chain: serving-size requests (<= 8 rows) take the device-side "

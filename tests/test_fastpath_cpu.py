@@ -76,7 +76,7 @@ def _bare_chain():
 
     fc = FastChain.__new__(FastChain)
     fc.cr, fc.rank, fc.lock, fc.inflight = _CR(), 1, threading.Lock(), 0
-    fc.persist, fc.failed = False, False
+    fc.persist, fc.failed, fc.doorbell = False, False, False
     return fc
 
 
