@@ -1002,6 +1002,22 @@ class Stage:
                     if self.first else None)
         self._rl = (prog.region(self.labels_buf.data_ptr(), self.labels_buf.numel() * 4)
                     if self.labels is not None else None)
+        # DNN_H0_DOUBLE: the layer-0 activation alternates between two buffers from step to
+        # step (a relocatable region re-based by flip_h0), so the next step's layer-0 forward
+        # never has to wait for this step's side-stream weight gradient that reads it
+        # (pipeline._xstep_plan drops that wait)
+        L = len(self.geoms)
+        self.h0_double = (switches.get("DNN_H0_DOUBLE") == "1" and self.device.type == "cuda"
+                          and self.first and self.last and self.nm == 1 and L >= 2 and
+                          self.relu_mask[0] is None and 0 not in self.actT and
+                          not (self.tail and L - 2 <= 0))
+        self._rh0 = None
+        if self.h0_double:
+            a0 = self.acts[0]
+            self._h0_alt = torch.zeros_like(a0)
+            self._h0_ptrs = (a0.data_ptr(), self._h0_alt.data_ptr())
+            self._h0_flip = 0
+            self._rh0 = prog.region(a0.data_ptr(), a0.numel() * a0.element_size())
         self._recording = True
         nat.record_begin(prog)
         try:
@@ -1089,6 +1105,12 @@ class Stage:
 
     def _replay(self, seg: str) -> None:
         self._prog.run([seg], torch.cuda.current_stream(self.device).cuda_stream)
+
+    def flip_h0(self) -> None:
+        """Start a step on the other layer-0 activation buffer (DNN_H0_DOUBLE)."""
+        if self._rh0 is not None:
+            self._h0_flip ^= 1
+            self._prog.rebase(self._rh0, self._h0_ptrs[self._h0_flip])
 
     def bind_input(self, x: torch.Tensor) -> None:
         """First stage reads ``x`` in place (zero-copy) from now on."""

@@ -578,8 +578,11 @@ class PipelineExecutor:
                 self.pipe.end_step()
                 return
         if plan is not None and len(self.stages) == 1 and \
-                not getattr(self, "capturing", False) and switches.get("DNN_XSTEP") == "1":
-            plan = self._xstep_plan(plan)
+                not getattr(self, "capturing", False):
+            if getattr(self.stages[0], "h0_double", False):
+                self.stages[0].flip_h0()
+            if switches.get("DNN_XSTEP") == "1":
+                plan = self._xstep_plan(plan)
         if plan is not None:
             dev = self.stages[0].device
             for st in self.stages:
@@ -639,12 +642,16 @@ class PipelineExecutor:
             if (plan and plan[0][1] == "F0" and plan[-1][1] == "@join" and side_w and
                     plan[-2][1] == "FINO0-0" and all(f"F0.L{i}" in st._prog.segments()
                                                      for i in range(L))):
-                out = [(None, "@xwait:w", 0), (st, "F0.L0", 0), (None, "@xwait:end", 0)]
+                # with a double-buffered layer-0 activation (DNN_H0_DOUBLE) the layer-0
+                # forward writes the buffer the previous step's wgrads do NOT read: no wait
+                dbl = getattr(st, "h0_double", False)
+                out = ([] if dbl else [(None, "@xwait:w", 0)]) + \
+                    [(st, "F0.L0", 0), (None, "@xwait:end", 0)]
                 out += [(st, f"F0.L{i}", 0) for i in range(1, L)]
                 last_w = side_w[-1]
                 for k, e in enumerate(plan[1:-1], start=1):
                     out.append(e)
-                    if k == last_w:
+                    if k == last_w and not dbl:
                         out.append((None, "@xmark:w", 1))
                 out.append((None, "@xmark:end", 1))
             self._xplan_src, self._xplan = plan, out

@@ -123,8 +123,9 @@ def test_cross_step_overlap_bitwise(dev, monkeypatch):
     xb[:, :784] = torch.from_numpy(x).to(torch.bfloat16)
     xb, yb = xb.to(dev), torch.from_numpy(y).to(dev)
     res = []
-    for xs in ("0", "1"):
+    for xs, dbl in (("0", "0"), ("1", "0"), ("1", "1")):
         monkeypatch.setenv("DNN_XSTEP", xs)
+        monkeypatch.setenv("DNN_H0_DOUBLE", dbl)
         tr = Trainer(NAMED_MODELS["mnist-fcnn"], micro_batch=rows, num_micro=1,
                      optim=OptimConfig(lr=0.1, momentum=0.9), device=dev)
         losses = []
@@ -136,7 +137,9 @@ def test_cross_step_overlap_bitwise(dev, monkeypatch):
         tr.flush()
         if xs == "1":
             segs = [seg for _, seg, _ in tr.executor._xstep_plan(tr.executor._native_plan())]
-            assert "@xwait:w" in segs and segs[-1] == "@xmark:end", segs
+            assert ("@xwait:w" in segs) == (dbl == "0") and segs[-1] == "@xmark:end", segs
+            assert tr.stages[0].h0_double == (dbl == "1")
         res.append((losses, tr.stages[0].params.master.clone()))
-    assert res[0][0] == res[1][0]
-    assert torch.equal(res[0][1], res[1][1])
+    for r in res[1:]:  # DNN_XSTEP and DNN_H0_DOUBLE: bitwise the same training
+        assert r[0] == res[0][0]
+        assert torch.equal(r[1], res[0][1])
