@@ -72,7 +72,7 @@ SWITCHES: dict[str, tuple[str, str]] = {
                                "priority so side-stream wgrads only fill in"),
     "DNN_SIDE_PRIORITY": ("0", "overlap plans: create the side stream at high priority "
                                "(measured no effect: 0.374 vs 0.373 ms)"),
-    "DNN_H0_DOUBLE": ("0", "single-stage native steps: the layer-0 activation alternates between "
+    "DNN_H0_DOUBLE": ("1", "single-stage native steps: the layer-0 activation alternates between "
                            "two buffers from step to step (a relocatable Program region), so "
                            "with DNN_XSTEP the next step's layer-0 forward does not wait for "
                            "this step's side-stream weight gradient that reads it"),
