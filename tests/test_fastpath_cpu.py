@@ -125,3 +125,28 @@ def test_chain_thread_failure_is_logged_not_silent(caplog):
     with caplog.at_level("ERROR"):
         fc.loop()
     assert fc.failed and "device-side chain thread failed" in caplog.text
+
+
+def test_doorbell_result_ack_advances_over_contiguous_consumed_requests():
+    """Rank 0's shared result-ring ack (the last rank reuses a result slot only behind it)
+    advances over the contiguous run of consumed requests, whatever order concurrent callers
+    finish in; an abandoned (timed-out) request counts as consumed."""
+    import numpy as np
+
+    from docker_dist_nn_amd.serve.fastpath import NSLOT
+
+    fc = _bare_chain()
+    fc.res_bytes = 256
+    fc._res_flag_off = NSLOT * fc.res_bytes
+    fc.res_np = np.zeros((fc._res_flag_off // 4 + NSLOT + 8,), dtype=np.int32)
+    fc._res_acked, fc._res_done = 0, set()
+    ack = lambda: int(fc.res_np[fc._res_flag_off // 4 + NSLOT])  # noqa: E731
+    fc._consume(2)
+    assert ack() == 0  # request 1 still out
+    fc._consume(3)
+    fc._consume(1)
+    assert ack() == 3
+    fc._consume(5)
+    assert ack() == 3
+    fc._consume(4)  # e.g. a caller that timed out: abandoned, slot free again
+    assert ack() == 5 and not fc._res_done
