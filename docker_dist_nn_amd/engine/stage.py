@@ -34,6 +34,7 @@ from ..utils.native import native
 from .. import switches
 
 _ALIGN = 64  # elements; keeps every layer's region 256-B aligned
+RELU_MASK_AUTO_WIDTH = 1024  # DNN_RELU_MASK=auto: masks for hidden layers at least this wide
 
 
 @dataclass
@@ -453,9 +454,14 @@ class Stage:
         self.relu_mask = []
         for i, g in enumerate(self.geoms):
             m = None
-            if mask_mode == "1" and i < L - 1 and g.spec.activation == "relu":
+            # auto: fragment-order masks for layers >= 1024 wide, where the dgrad's activation
+            # read is the big term (wide 5.81 -> 5.44 ms, mlp8 2.73 -> 2.71; the headline's
+            # 512-wide layer 0 loses: profiles/r5_tables/relu_mask_*)
+            mode_i = ("2" if g.np_ >= RELU_MASK_AUTO_WIDTH else "0") if mask_mode == "auto" \
+                else mask_mode
+            if mode_i == "1" and i < L - 1 and g.spec.activation == "relu":
                 m = torch.zeros(R, g.np_ // 8, dtype=torch.uint8, device=dev)
-            elif mask_mode == "2" and i < L - 1 and g.spec.activation == "relu" and \
+            elif mode_i == "2" and i < L - 1 and g.spec.activation == "relu" and \
                     not (self.tail and i + 1 >= L - 2):
                 tiles = ops.frag_mask_tiles(self.mb, g.np_, g.kp, self.geoms[i + 1].np_)
                 if tiles is not None:

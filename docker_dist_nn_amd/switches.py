@@ -29,9 +29,10 @@ SWITCHES: dict[str, tuple[str, str]] = {
                              "the producing GEMMs: auto (layers >= 16M weights) | 1 | 0"),
     "DNN_TAIL": ("1", "fused classifier tail kernel (mlp_tail.hip)"),
     "DNN_FUSED_XENT": ("1", "softmax cross-entropy fused into the logits GEMM epilogue"),
-    "DNN_RELU_MASK": ("0", "1-bit ReLU masks instead of the activation in dgrad epilogues: "
-                              "1 = row-block-major bytes, 2 = fragment order (ops.FragMask, "
-                              "register-direct tiles only), 0 = off"),
+    "DNN_RELU_MASK": ("auto", "1-bit ReLU masks instead of the activation in dgrad epilogues: "
+                                 "1 = row-block-major bytes, 2 = fragment order (ops.FragMask, "
+                                 "register-direct tiles only), 0 = off, auto = 2 for hidden "
+                                 "layers >= 1024 wide"),
     "DNN_WGRAD_ALGO": ("splitk", "weight-gradient algorithm: splitk | streamk"),
     "DNN_WGRAD_GROUP": ("1", "one grouped launch for small split-K weight gradients"),
     "DNN_FUSE_FIN_SGD": ("1", "gradient reduction and optimizer step in one launch (FINO)"),

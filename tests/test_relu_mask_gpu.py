@@ -114,3 +114,37 @@ def test_engine_fragment_mask_bitwise_equals_activation_path(dev, monkeypatch):
         del tr
     assert res[0][0] == res[1][0]
     assert torch.equal(res[0][1], res[1][1])
+
+
+def test_engine_auto_mask_only_for_wide_layers_bitwise(dev, monkeypatch):
+    """DNN_RELU_MASK=auto (the default): fragment-order masks only for hidden layers at least
+    RELU_MASK_AUTO_WIDTH wide (here layer 0, 1024 wide; layer 1, 512 wide, reads its
+    activation), and the same losses and weights as reading every activation."""
+    from docker_dist_nn_amd import MLPSpec
+    from docker_dist_nn_amd.data import synthetic_mnist
+    from docker_dist_nn_amd.engine import OptimConfig, Trainer
+    from docker_dist_nn_amd.engine.stage import RELU_MASK_AUTO_WIDTH
+
+    R = 16384
+    spec = MLPSpec.parse("784-1024-512-10")
+    x, y = synthetic_mnist(R, seed=5)
+    xb = torch.zeros(R, 832, dtype=torch.bfloat16)
+    xb[:, :784] = torch.from_numpy(x).to(torch.bfloat16)
+    xb, yb = xb.to(dev), torch.from_numpy(y).to(dev)
+    res = []
+    for flag in ("0", "auto"):
+        monkeypatch.setenv("DNN_RELU_MASK", flag)
+        tr = Trainer(spec, micro_batch=R, num_micro=1, optim=OptimConfig(lr=0.1), device=dev)
+        st = tr.stages[0]
+        for g, m in zip(st.geoms, st.relu_mask):
+            if flag == "0" or g.np_ < RELU_MASK_AUTO_WIDTH:
+                assert m is None
+        losses = []
+        for _ in range(3):
+            tr.set_batch(xb, yb)
+            tr.step()
+            losses.append(tr.loss())
+        tr.flush()
+        res.append((losses, st.params.master.clone()))
+    assert res[0][0] == res[1][0]
+    assert torch.equal(res[0][1], res[1][1])
