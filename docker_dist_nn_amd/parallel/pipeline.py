@@ -327,7 +327,7 @@ class PipelineExecutor:
         mode = switches.get("DNN_BW_OVERLAP")
         # small steps are host-bound: every fork / join is an event record + wait (~6-8 us of
         # host time each), more than the overlap can win back on GEMMs of a few thousand rows
-        if mode in ("1", "2", "3", "4", "5") and len(self.stages) == 1 and \
+        if mode in ("1", "2", "3", "4", "5", "6") and len(self.stages) == 1 and \
                 self.stages[0].rows >= int(switches.get("DNN_BW_OVERLAP_MIN_ROWS")):
             ov = self._overlap_plan(self.stages[0], mode)
             if ov is not None:
@@ -423,6 +423,17 @@ class PipelineExecutor:
         sf = switches.get("DNN_SPLIT_FINO")
         split = ((sf == "1" or (sf == "auto" and not fused)) and L > 1 and
                  f"FINO1-{L - 1}" in segs and "FINO0-0" in segs and 0 not in fused)
+        if mode == "6" and L >= 3 and not fused and split and all(
+                st._prog.segment_size(f"B0.L{i}") == 0 for i in range(2, L)):
+            # one fork after the forward (every side wgrad's dZ comes from it: the classifier
+            # tail ran the dgrads of layers 2..L-1); the side stream runs W1 FIRST, beside the
+            # layer-1 dgrad, then the small ones -- so W0 (main, after that dgrad) shares the
+            # chip with small wgrads instead of W1
+            plan = [(st, "F0", 0), (None, "@fork", 0), (st, "W1", 1)]
+            plan += [(st, f"W{i}", 1) for i in range(L - 1, 1, -1)]
+            plan += [(st, f"B0.L{i}", 0) for i in range(L - 1, 0, -1)]
+            return plan + [(None, "@fork", 0), (st, f"FINO1-{L - 1}", 1), (st, "W0", 0),
+                           (st, "FINO0-0", 0), (None, "@join", 0)]
         if mode == "5" and L >= 3 and not fused:
             # one fork: the small wgrads (L-1 .. 2) on the side under the dgrads; W1 on the
             # main stream right after the last dgrad, then W0 -- so W1 and W0 never share the

@@ -51,7 +51,9 @@ SWITCHES: dict[str, tuple[str, str]] = {
                             "on the side (headline 0.377 vs 0.372 ms, rejected); 3 = those under "
                             "W0 (0.386 ms, rejected); 4 = one fork, W1..W3 on the side (0.407 ms, "
                             "rejected); 5 = small wgrads on the side, W1 then W0 on the main "
-                            "stream (fixes their order); 0 = off"),
+                            "stream (fixes their order); 6 = one fork, W1 first on the side "
+                            "then the small wgrads (the classifier-tail shape with the split "
+                            "reduction); 0 = off"),
     "DNN_BW_OVERLAP_MIN_ROWS": ("16384", "overlap plans only for steps of at least this many "
                                          "rows (below, the single-stream plan: no event "
                                          "packets, the host cost that bounds small steps; "

@@ -26,7 +26,9 @@ def test_overlap_plan_bitwise(dev, monkeypatch, model, rows):
     # updated on the side stream during W0)
     # 5 / 5s: small wgrads on the side, W1 then W0 on the main stream (unsplit / split FINO)
     # 1j: plan 1 with the split reduction and the join in front of layer 0's update
-    for flag in ("0", "1", "2", "3", "4", "1e1", "1e2", "1s", "5", "5s", "1j"):
+    # 6s: one fork, W1 first on the side stream, then the small wgrads (split reduction; the
+    # headline shape only -- elsewhere it falls back to plan 1)
+    for flag in ("0", "1", "2", "3", "4", "1e1", "1e2", "1s", "5", "5s", "1j", "6s"):
         monkeypatch.setenv("DNN_BW_OVERLAP", flag[0])
         monkeypatch.setenv("DNN_FORK_ELIDE", flag[2:] if flag[1:2] == "e" else "0")
         monkeypatch.setenv("DNN_SPLIT_FINO", "1" if flag[-1] in "sj" else "0")
