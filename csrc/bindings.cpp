@@ -764,6 +764,12 @@ PYBIND11_MODULE(_native, m) {
               throw std::runtime_error("run_plan: cross-step event failed");
             continue;
           }
+          if (seg.rfind("@delay:", 0) == 0) {  // a deliberate stagger on the op's stream
+            if (si && !side) throw std::invalid_argument("run_plan: @delay without a side");
+            if (dnn::stream_delay(std::stod(seg.substr(7)), si ? S(side) : S(stream)) != 0)
+              throw std::runtime_error("run_plan: @delay failed");
+            continue;
+          }
           if (seg == "@rewait") {  // side waits on the last fork again: a side-queue packet only
             if (!side || hipStreamWaitEvent(S(side), ev_fork, 0) != hipSuccess)
               throw std::runtime_error("run_plan: @rewait failed");

@@ -625,6 +625,21 @@ int chain_stage_run(const ChainStage& p, int workgroups, int share, hipStream_t 
   return hipGetLastError() == hipSuccess ? workgroups : -9;
 }
 
+// One lane sleeps `ticks` of the wall clock (bounded by construction): a deliberate delay of
+// the work queued behind it on its stream (the "@delay:<us>" plan op).
+__global__ void stream_delay_kernel(unsigned long long ticks) {
+  if (threadIdx.x != 0) return;
+  const unsigned long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+int stream_delay(double us, hipStream_t stream) {
+  if (!(us >= 0.0) || us > 1e6) return -1;  // at most one second
+  hipLaunchKernelGGL(stream_delay_kernel, dim3(1), dim3(64), 0, stream,
+                     chain_ticks(us * 1e-6));
+  return hipGetLastError() == hipSuccess ? 0 : -9;
+}
+
 int chain_signal(uint32_t* flag, uint32_t value, hipStream_t stream) {
   if (!flag || misaligned4(flag)) return -1;
   hipLaunchKernelGGL(chain_signal_kernel, dim3(1), dim3(64), 0, stream, flag, value);

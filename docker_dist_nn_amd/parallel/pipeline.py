@@ -458,6 +458,13 @@ class PipelineExecutor:
             plan = plan[:-1]
         if switches.get("DNN_FORK_ELIDE") in ("1", "2"):
             plan = self._elide_forks(st, plan, rewait=switches.get("DNN_FORK_ELIDE") == "2")
+        delay = float(switches.get("DNN_SIDE_DELAY_US"))
+        if delay > 0:
+            # the side stream starts its first wgrad `delay` us after the fork instead of the
+            # main stream paying event packets for that stagger (with DNN_FORK_ELIDE=1 the
+            # redundant forks are gone and the next dgrad starts right after the tail)
+            k = next(i for i, e in enumerate(plan) if e[1] == "@fork")
+            plan = plan[:k + 1] + [(None, f"@delay:{delay:g}", 1)] + plan[k + 1:]
         if split:
             # the side stream reduces + updates layers 1..L-1 (their wgrads are done; the fork
             # above orders it after the last dgrad, the last reader of their W^T) while the

@@ -85,6 +85,10 @@ SWITCHES: dict[str, tuple[str, str]] = {
     "DNN_EVENT_FENCE": ("device", "fork / join events of single-process step plans: device = "
                                   "no system-scope fence at the record (both streams on one "
                                   "GPU), system = HIP's default (cache write-back per record)"),
+    "DNN_SIDE_DELAY_US": ("0", "overlap plans: the side stream waits this many microseconds "
+                               "after the first fork (a delay kernel) before its first wgrad -- "
+                               "the stagger the redundant forks gave, without their event "
+                               "packets on the main stream (use with DNN_FORK_ELIDE=1)"),
     "DNN_JOIN_EARLY": ("0", "overlap plan with the split reduction: the side stream's join "
                             "before layer 0's update instead of at the end of the step"),
     "DNN_FORK_ELIDE": ("0", "overlap plans: drop a side-stream fork when the main stream "

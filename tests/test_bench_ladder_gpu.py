@@ -47,7 +47,9 @@ def test_bench_ladder_survives_hang_and_crash(tmp_path):
     att = lad["attempts"]
     assert [a["rung"] for a in att] == ["default", "ipc-slotted", "rccl-slotted"]
     assert att[0]["rc"]["0"] == "3" and att[0]["rc"]["1"] in ("killed", "3")  # watchdog exit
-    assert att[1]["rc"]["1"] == "87" and att[1]["rc"]["0"] == "killed"      # injected crash
+    # injected crash on rank 1; rank 0 is killed by its supervisor -- or gets there first
+    # itself, failing on the closed gloo connection (rc 1): the race is the machine's
+    assert att[1]["rc"]["1"] == "87" and att[1]["rc"]["0"] in ("killed", "1")
     assert att[2]["ok"] and att[2]["rc"] == {"0": "0", "1": "0"}
     assert out["ladder_rung"] == "rccl-slotted"
     assert out["dp_only"]["value"] > 0 and out["dp_only"]["parallelism"] == "dp2"

@@ -28,9 +28,11 @@ def test_overlap_plan_bitwise(dev, monkeypatch, model, rows):
     # 1j: plan 1 with the split reduction and the join in front of layer 0's update
     # 6s: one fork, W1 first on the side stream, then the small wgrads (split reduction; the
     # headline shape only -- elsewhere it falls back to plan 1)
-    for flag in ("0", "1", "2", "3", "4", "1e1", "1e2", "1s", "5", "5s", "1j", "6s"):
+    # 1e1d: plan 1, forks elided, the side stream staggered by a 10 us delay kernel
+    for flag in ("0", "1", "2", "3", "4", "1e1", "1e2", "1s", "5", "5s", "1j", "6s", "1e1d"):
         monkeypatch.setenv("DNN_BW_OVERLAP", flag[0])
-        monkeypatch.setenv("DNN_FORK_ELIDE", flag[2:] if flag[1:2] == "e" else "0")
+        monkeypatch.setenv("DNN_FORK_ELIDE", flag[2:3] if flag[1:2] == "e" else "0")
+        monkeypatch.setenv("DNN_SIDE_DELAY_US", "10" if flag.endswith("d") else "0")
         monkeypatch.setenv("DNN_SPLIT_FINO", "1" if flag[-1] in "sj" else "0")
         monkeypatch.setenv("DNN_JOIN_EARLY", "1" if flag == "1j" else "0")
         tr = Trainer(spec, micro_batch=rows, num_micro=1,
