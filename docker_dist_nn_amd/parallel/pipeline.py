@@ -17,7 +17,6 @@ S-stage pipelines on one device and checks that the schedules are deadlock-free.
 """
 from __future__ import annotations
 
-import os
 from typing import Callable, Optional, Sequence
 
 import torch
