@@ -74,3 +74,41 @@ def test_mode5_with_tail_keeps_one_fork():
     out = _mode5(SIZES, 4)
     assert out.count("@fork") == 1
     assert out == ["F0", "@fork", "W3", "B0.L3", "W2", "B0.L2", "B0.L1"]
+
+
+class _XProg(_Prog):
+    def segments(self):
+        return ["F0", "F0.L0", "F0.L1", "F0.L2", "F0.L3"]
+
+
+class _XStage:
+    def __init__(self, h0_double):
+        self._prog = _XProg({})
+        self.geoms = [None] * 4
+        self.h0_double = h0_double
+
+
+def _xplan(h0_double):
+    ex = PipelineExecutor.__new__(PipelineExecutor)
+    st = _XStage(h0_double)
+    ex.stages = [st]
+    plan = [(st, "F0", 0), (None, "@fork", 0), (st, "W3", 1), (st, "B0.L3", 0),
+            (None, "@fork", 0), (st, "W2", 1), (st, "B0.L2", 0), (None, "@fork", 0),
+            (st, "W1", 1), (st, "B0.L1", 0), (None, "@fork", 0), (st, "FINO1-3", 1),
+            (st, "W0", 0), (st, "FINO0-0", 0), (None, "@join", 0)]
+    first = [e[1] for e in ex._xstep_plan(plan)]
+    return first, [e[1] for e in ex._xstep_plan(plan)]
+
+
+def test_cross_step_plan_waits_for_the_side_wgrads_unless_h0_is_double_buffered():
+    """DNN_XSTEP: the next step's layer-0 forward waits for this step's side-stream wgrads
+    ("@xwait:w": W1 reads the activation it overwrites) -- unless that activation alternates
+    between two buffers (DNN_H0_DOUBLE); the layer-1 forward always waits for the side
+    stream's end (the updated W_1). The first step has nothing to wait for."""
+    first, steady = _xplan(False)
+    assert not any(s.startswith("@xwait") for s in first)
+    assert steady[:3] == ["@xwait:w", "F0.L0", "@xwait:end"] and steady[-1] == "@xmark:end"
+    assert steady.index("@xmark:w") == steady.index("W1") + 1
+    first, steady = _xplan(True)
+    assert steady[:2] == ["F0.L0", "@xwait:end"] and "@xmark:w" not in steady
+    assert "@join" not in steady and steady[-1] == "@xmark:end"
