@@ -503,7 +503,7 @@ PYBIND11_MODULE(_native, m) {
                            uintptr_t mom, uintptr_t shadow, float lr, float mu, float wd,
                            uintptr_t lr_dev, int adam, uintptr_t v, float b1, float b2,
                            float eps, int decoupled, uintptr_t step_dev, double db1, double db2,
-                           float bc1, float bc2) {
+                           float bc1, float bc2, int max_blocks) {
     std::vector<dnn::ReduceJob> J;
     J.reserve(jobs.size());
     for (const auto& t : jobs)
@@ -530,7 +530,7 @@ PYBIND11_MODULE(_native, m) {
       std::vector<dnn::ReduceJob> part(J.begin() + k, J.begin() + k + n);
       launch(
           "reduce_multi",
-          [part, fused, sg](hipStream_t s, const dnn::Program& R) mutable {
+          [part, fused, sg, max_blocks](hipStream_t s, const dnn::Program& R) mutable {
             std::vector<dnn::ReduceJob> q = part;
             for (auto& j : q) {
               j.src = R.fix(j.src);
@@ -543,7 +543,8 @@ PYBIND11_MODULE(_native, m) {
             f.mom = R.fix(f.mom);
             f.shadow = R.fix(f.shadow);
             f.v = R.fix(f.v);
-            return dnn::reduce_multi(q.data(), (int)q.size(), s, fused ? &f : nullptr);
+            return dnn::reduce_multi(q.data(), (int)q.size(), s, fused ? &f : nullptr,
+                                     max_blocks);
           },
           stream);
     }
@@ -552,7 +553,7 @@ PYBIND11_MODULE(_native, m) {
      py::arg("wd") = 0.f, py::arg("lr_dev") = 0, py::arg("adam") = 0, py::arg("v") = 0,
      py::arg("b1") = 0.f, py::arg("b2") = 0.f, py::arg("eps") = 0.f, py::arg("decoupled") = 0,
      py::arg("step_dev") = 0, py::arg("db1") = 0.0, py::arg("db2") = 0.0, py::arg("bc1") = 1.f,
-     py::arg("bc2") = 1.f);
+     py::arg("bc2") = 1.f, py::arg("max_blocks") = 0);
   m.def(
       "sgd_update",
       [](uintptr_t p, uintptr_t g, uintptr_t mom, uintptr_t shadow, long n, float lr, float mu,

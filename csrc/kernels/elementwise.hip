@@ -460,22 +460,28 @@ __device__ __forceinline__ void reduce_block(const ReduceJob& jb, long blk, f32x
 __global__ __launch_bounds__(256) void reduce_multi_kernel(ReduceJobs jobs, FusedSgd sg) {
   __shared__ f32x4_t red_s[256];
   f32x4_t LDS_AS* red = (f32x4_t LDS_AS*)red_s;
-  int j = 0;
-  while (j + 1 < jobs.n_jobs && (int)blockIdx.x >= jobs.block_start[j + 1]) ++j;
-  const ReduceJob& jb = jobs.job[j];
-  const long blk = (long)blockIdx.x - jobs.block_start[j];
-  switch (reduce_ty(jb.n_src)) {
-    case 64: reduce_block<64>(jb, blk, red, sg); break;
-    case 32: reduce_block<32>(jb, blk, red, sg); break;
-    case 16: reduce_block<16>(jb, blk, red, sg); break;
-    case 8: reduce_block<8>(jb, blk, red, sg); break;
-    case 4: reduce_block<4>(jb, blk, red, sg); break;
-    case 2: reduce_block<2>(jb, blk, red, sg); break;
-    default: reduce_block<1>(jb, blk, red, sg); break;
+  // a workgroup per block, or -- a capped grid (max_blocks) -- every gridDim.x-th block
+  const int total = jobs.block_start[jobs.n_jobs];
+  for (int vb = blockIdx.x; vb < total; vb += gridDim.x) {  // (uniform per workgroup)
+    int j = 0;
+    while (j + 1 < jobs.n_jobs && vb >= jobs.block_start[j + 1]) ++j;
+    const ReduceJob& jb = jobs.job[j];
+    const long blk = (long)vb - jobs.block_start[j];
+    switch (reduce_ty(jb.n_src)) {
+      case 64: reduce_block<64>(jb, blk, red, sg); break;
+      case 32: reduce_block<32>(jb, blk, red, sg); break;
+      case 16: reduce_block<16>(jb, blk, red, sg); break;
+      case 8: reduce_block<8>(jb, blk, red, sg); break;
+      case 4: reduce_block<4>(jb, blk, red, sg); break;
+      case 2: reduce_block<2>(jb, blk, red, sg); break;
+      default: reduce_block<1>(jb, blk, red, sg); break;
+    }
+    __syncthreads();  // `red` is rewritten by the next block
   }
 }
 
-int reduce_multi(const ReduceJob* job, int n_jobs, hipStream_t stream, const FusedSgd* sgd) {
+int reduce_multi(const ReduceJob* job, int n_jobs, hipStream_t stream, const FusedSgd* sgd,
+                 int max_blocks) {
   if (n_jobs <= 0 || n_jobs > REDUCE_MAX_JOBS) return -1;
   ReduceJobs J{};
   J.n_jobs = n_jobs;
@@ -502,7 +508,8 @@ int reduce_multi(const ReduceJob* job, int n_jobs, hipStream_t stream, const Fus
     if (job[k].wt && (!sgd || !sg.shadow || job[k].wt_cols <= 0 || job[k].wt_cols % 4 ||
                       job[k].n % job[k].wt_cols))
       return -1;
-  hipLaunchKernelGGL(reduce_multi_kernel, dim3(blocks), dim3(256), 0, stream, J, sg);
+  const int grid = max_blocks > 0 ? std::min(blocks, max_blocks) : blocks;
+  hipLaunchKernelGGL(reduce_multi_kernel, dim3(grid), dim3(256), 0, stream, J, sg);
   return hipGetLastError() == hipSuccess ? 0 : -9;
 }
 

@@ -65,8 +65,11 @@ struct FusedSgd {
   float bc1, bc2;
 };
 // All jobs in one launch, each bitwise identical to reduce_slabs on the same inputs.
+// max_blocks > 0: at most that many workgroups, each looping over the launch's blocks (the
+// same per-output arithmetic; a reduction running beside other kernels then occupies fewer
+// CUs).
 int reduce_multi(const ReduceJob* job, int n_jobs, hipStream_t stream,
-                 const FusedSgd* sgd = nullptr);
+                 const FusedSgd* sgd = nullptr, int max_blocks = 0);
 // lr_dev / step_dev (optional, device memory): see the kernels in elementwise.hip.
 int sgd_update(float* p, const float* g, float* mom, uint16_t* shadow, long n, float lr, float mu,
                float wd, hipStream_t stream, const float* lr_dev = nullptr);

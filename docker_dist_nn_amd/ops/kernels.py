@@ -974,7 +974,7 @@ def reduce_slabs(src, n_src, stride, n, out, scale=1.0, accumulate=False):
                           _stream(src))
 
 
-def reduce_multi(jobs, sgd=None):
+def reduce_multi(jobs, sgd=None, max_blocks: int = 0):
     """Several reduce_slabs in ONE launch. jobs: iterable of
     (src, n_src, stride, n, out, scale, accumulate) with reduce_slabs' meaning; the results are
     bitwise identical to running reduce_slabs on each job.
@@ -988,7 +988,10 @@ def reduce_multi(jobs, sgd=None):
 
     A job may carry an 8th element ``wt`` (GPU, fused update with a shadow only): the bf16
     W^T[cols][rows] of the layer whose [rows][cols] weight gradient the job reduces; the update
-    writes it too (bitwise the transpose of the refreshed shadow)."""
+    writes it too (bitwise the transpose of the refreshed shadow).
+
+    ``max_blocks`` (GPU, > 0): cap the launch at that many workgroups (each loops over the
+    blocks; same results) -- for a reduction that runs beside other kernels."""
     jobs = [tuple(j) + (None,) * (8 - len(j)) for j in jobs]
     if not jobs:
         return
@@ -1024,7 +1027,7 @@ def reduce_multi(jobs, sgd=None):
         packed.append((_p(src), int(stride), int(n_src), int(n), _p(out), float(scale),
                        int(acc), _p(wt), int(wt.shape[0]) if wt is not None else 0))
     if sgd is None:
-        native().reduce_multi(packed, _stream(jobs[0][0]))
+        native().reduce_multi(packed, _stream(jobs[0][0]), max_blocks=int(max_blocks))
         return
     g, m = sgd["grad"], sgd["master"]
     adam = bool(sgd.get("adam"))
@@ -1040,7 +1043,7 @@ def reduce_multi(jobs, sgd=None):
                           mom=_p(sgd.get("mom")), shadow=_p(sh), lr=float(sgd["lr"]),
                           mu=float(sgd.get("momentum", 0.0)),
                           wd=float(sgd.get("weight_decay", 0.0)), lr_dev=_p(sgd.get("lr_dev")),
-                          **(_adam_args(sgd) if adam else {}))
+                          max_blocks=int(max_blocks), **(_adam_args(sgd) if adam else {}))
 
 
 def _adam_args(sgd: dict) -> dict:

@@ -85,6 +85,9 @@ SWITCHES: dict[str, tuple[str, str]] = {
     "DNN_EVENT_FENCE": ("device", "fork / join events of single-process step plans: device = "
                                   "no system-scope fence at the record (both streams on one "
                                   "GPU), system = HIP's default (cache write-back per record)"),
+    "DNN_FINO_SIDE_BLOCKS": ("0", "workgroup cap of the side-stream reduce + SGD of layers "
+                                  "1..L-1 (it runs beside the next step's first forward with "
+                                  "DNN_XSTEP); 0 = one workgroup per block"),
     "DNN_SIDE_DELAY_US": ("0", "overlap plans: the side stream waits this many microseconds "
                                "after the first fork (a delay kernel) before its first wgrad -- "
                                "the stagger the redundant forks gave, without their event "

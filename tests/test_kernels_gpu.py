@@ -295,9 +295,11 @@ def test_reduce_slabs_many_sources(dev, n_src):
     torch.testing.assert_close(out, 1 + 0.25 * src.sum(0), rtol=1e-5, atol=1e-5)
 
 
-def test_reduce_multi_bitwise_equals_reduce_slabs(dev):
+@pytest.mark.parametrize("max_blocks", [0, 7, 128])
+def test_reduce_multi_bitwise_equals_reduce_slabs(dev, max_blocks):
     """One launch over jobs with every source-group class (1..64 groups of sources) and > 16
-    jobs (several launches) must reproduce per-job reduce_slabs bit for bit."""
+    jobs (several launches) must reproduce per-job reduce_slabs bit for bit -- also with the
+    grid capped (max_blocks: each workgroup loops over blocks)."""
     gen = torch.Generator().manual_seed(5)
     shapes = [(1, 64), (3, 4096), (7, 832 * 512), (16, 256), (512, 128), (40, 1024),
               (9, 2048), (18, 832 * 512), (64, 256 * 512), (128, 4096)] * 2
@@ -310,7 +312,7 @@ def test_reduce_multi_bitwise_equals_reduce_slabs(dev):
         ops.reduce_slabs(src, ns, n + 8, n, ref_out, scale=scale, accumulate=acc)
         jobs.append((src, ns, n + 8, n, out, scale, acc))
         expect.append(ref_out)
-    ops.reduce_multi(jobs)
+    ops.reduce_multi(jobs, max_blocks=max_blocks)
     for j, e in zip(jobs, expect):
         assert torch.equal(j[4], e)
 
