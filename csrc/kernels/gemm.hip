@@ -240,7 +240,11 @@ int gemm_bf16(const GemmParams& p, int la, int lb, int out_f32, int bm, int bn, 
   // (A 4-wave 256x256 form -- 128x128 per wave, one wave per SIMD, accumulators in AGPRs,
   // hipBLASLt's MT256x256 MIWT8_8 shape -- was built and measured: 7 % slower on 8192^3 fwd,
   // 20 % on K = 832, 3-4x on dgrad (spills); without hand-scheduled intra-wave pipelining one
-  // wave per SIMD cannot hide LDS latency, so the 8-wave form is the 256x256 tile.)
+  // wave per SIMD cannot hide LDS latency, so the 8-wave form is the 256x256 tile. Round 5
+  // re-measured it on the register-prefetched loop (stage code 13, bitwise equal to code 11):
+  // 6-43 % slower on every BASELINE GEMM, wgrad included, whose loop compiles clean; the
+  // K-major loops also shuffle accumulators between VGPRs and AGPRs -- 256 AGPRs of
+  // accumulators leave the allocator no spare. profiles/r5_blas/code13_*.)
   if (stages == 8) {  // ping-pong half-tile-streamed form (gemm_pp.hip)
     if (bm != 256 || bn != 256) return -12;
     if (p.xent_labels) return -11;
