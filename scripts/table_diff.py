@@ -18,6 +18,9 @@ def diff(full: dict, base: dict) -> dict:
 def main(paths):
     base = json.load(open(DEFAULT))["entries"]
     for p in paths:
+        if os.path.realpath(p) == os.path.realpath(DEFAULT):
+            print(p, "is the default table itself: skipped (it would be emptied)")
+            continue
         doc = json.load(open(p))
         if "override" in doc:
             continue
