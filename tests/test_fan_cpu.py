@@ -147,7 +147,11 @@ def _single(mb, M, steps):
                                                 ([2, 2], [1, 2], False, 6),
                                                 ([1, 3], [3, 1], False, 7),  # uneven counts
                                                 ([1, 1, 2], [2, 1, 2], True, 6),
-                                                ([3, 1], [2, 3], True, 7)])
+                                                ([3, 1], [2, 3], True, 7),
+                                                # the headline's bench layouts at N = 4 and
+                                                # N = 8: fan3x3,1x1 and fan3x7,1x1
+                                                ([3, 1], [3, 1], False, 6),
+                                                ([3, 1], [7, 1], False, 7)])
 def test_fan_training_matches_single_process(tmp_path, dist_, reps, shard, M):
     mb, steps = 64, 3
     world = sum(reps)
