@@ -11,6 +11,7 @@
 #include <cstring>
 #include <stdexcept>
 #include <map>
+#include <mutex>
 #include <string>
 #include <tuple>
 #include <vector>
@@ -720,12 +721,11 @@ PYBIND11_MODULE(_native, m) {
   // schedule order, one call, GIL released.
   // A whole step of a single-process (loopback) pipeline: (program, segment, stream) triples
   // in schedule order, one call, GIL released. stream 0 = `stream`, 1 = `side`; the pseudo
-  // segments "@fork" (side waits for main) and "@join" (main waits for side) order the two;
-  // "@rewait" makes the side wait on the last fork's record again (no packet on `stream`).
+  // segments "@fork" (side waits for main) and "@join" (main waits for side) order the two.
   m.def(
       "run_plan",
       [](const std::vector<std::tuple<const dnn::Program*, std::string, int>>& plan,
-         uintptr_t stream, uintptr_t side, bool device_fence) {
+         uintptr_t stream, uintptr_t side, bool device_fence, uint64_t xkey) {
         py::gil_scoped_release nogil;
         // fork / join events: both streams are on this device, so the ordering needs no
         // system-scope fence (cache write-back / invalidate at every record: the ~6 us
@@ -742,10 +742,15 @@ PYBIND11_MODULE(_native, m) {
         }
         // cross-step events ("@xmark:<k>" records on the side stream, "@xwait:<k>" makes the
         // main stream wait on the LAST such record -- possibly made by the previous step's
-        // call: a step's first kernels overlap the previous step's side-stream tail)
-        static thread_local std::map<std::string, hipEvent_t> xev[2];
+        // call: a step's first kernels overlap the previous step's side-stream tail). They
+        // belong to one executor (`xkey`, its id): two executors stepping in turn on one
+        // thread must each wait on their OWN side stream's marks. Process-wide,
+        // under a mutex, so a step issued from another thread finds the same events.
+        static std::mutex xmu;
+        static std::map<std::tuple<uint64_t, bool, std::string>, hipEvent_t> xev;
         auto xevent = [&](const std::string& k) {
-          hipEvent_t& e = xev[device_fence][k];
+          std::lock_guard<std::mutex> lk(xmu);
+          hipEvent_t& e = xev[{xkey, device_fence, k}];
           if (!e) {
             const unsigned fl =
                 hipEventDisableTiming | (device_fence ? hipEventDisableSystemFence : 0u);
@@ -765,17 +770,6 @@ PYBIND11_MODULE(_native, m) {
               throw std::runtime_error("run_plan: cross-step event failed");
             continue;
           }
-          if (seg.rfind("@delay:", 0) == 0) {  // a deliberate stagger on the op's stream
-            if (si && !side) throw std::invalid_argument("run_plan: @delay without a side");
-            if (dnn::stream_delay(std::stod(seg.substr(7)), si ? S(side) : S(stream)) != 0)
-              throw std::runtime_error("run_plan: @delay failed");
-            continue;
-          }
-          if (seg == "@rewait") {  // side waits on the last fork again: a side-queue packet only
-            if (!side || hipStreamWaitEvent(S(side), ev_fork, 0) != hipSuccess)
-              throw std::runtime_error("run_plan: @rewait failed");
-            continue;
-          }
           if (seg == "@fork" || seg == "@join") {
             if (!side) throw std::invalid_argument("run_plan: fork/join without a side stream");
             hipEvent_t ev = seg == "@fork" ? ev_fork : ev_join;
@@ -789,7 +783,8 @@ PYBIND11_MODULE(_native, m) {
           pr->run(one, si ? S(side) : S(stream));
         }
       },
-      py::arg("plan"), py::arg("stream"), py::arg("side") = 0, py::arg("device_fence") = false);
+      py::arg("plan"), py::arg("stream"), py::arg("side") = 0, py::arg("device_fence") = false,
+      py::arg("xkey") = 0);
   m.def("record_begin", [](dnn::Program& pr) {
     if (dnn::recording_program()) throw std::runtime_error("already recording a Program");
     dnn::recording_program() = &pr;

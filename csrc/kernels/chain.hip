@@ -315,11 +315,17 @@ __global__ __launch_bounds__(256) void chain_stage_kernel(ChainStage p) {
   uint32_t* ex = go + 1;                // == epoch: this launch ends before request *go + 1
                                         // (ex[1]: why -- 1 stop, 2 idle; ex[2]: the stop
                                         // word read / the idle ticks)
+  uint32_t stop_seen = 0;  // workgroup 0: the stop word read after the last request's go
   for (uint32_t seq = p.start_seq + 1;; ++seq) {
     const int slot = (int)(seq % (uint32_t)p.nslot);
     if (t == 0) {
       uint32_t run = 1;
-      if (blockIdx.x == 0) {
+      if (blockIdx.x == 0 && stop_seen) {  // asked to stop while the last request ran
+        run = 0;
+        __hip_atomic_store(ex + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ex + 2, stop_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ex, p.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      } else if (blockIdx.x == 0) {
         // the consumer drained the slot this request will reuse -- checked BEFORE the input
         // arrives (it nearly always has: the wait is off the request's path). Bounded: a stuck
         // consumer is reported downstream as DEADLINE naming it, no rows are written.
@@ -335,8 +341,12 @@ __global__ __launch_bounds__(256) void chain_stage_kernel(ChainStage p) {
             const unsigned long long now = wall_clock64();
             if (now - t_stop > 2000) {
               t_stop = now;
-              if (__hip_atomic_load(p.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+              const uint32_t sv = __hip_atomic_load(p.stop, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_SYSTEM);
+              if (sv) {  // the exit reason is recorded as on the input-wait path
                 run = 0;
+                __hip_atomic_store(ex + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(ex + 2, sv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 break;
               }
             }
@@ -377,6 +387,11 @@ __global__ __launch_bounds__(256) void chain_stage_kernel(ChainStage p) {
           __hip_atomic_store(fail + slot, ack_ok ? 0u : 1u, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(go, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+          // one look at the stop word per request, off the request's path (the other
+          // workgroups are already computing): back-to-back requests never wait the ~20 us
+          // the polls above need before they read it, so a paused() chain would otherwise
+          // run until its hop timeout
+          stop_seen = __hip_atomic_load(p.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         } else {
           __hip_atomic_store(ex, p.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -456,7 +471,11 @@ __global__ __launch_bounds__(256) void chain_stage_kernel(ChainStage p) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     __syncthreads();
     if (t == 0) {
-      const uint32_t prev = __hip_atomic_fetch_add(cnt + slot, 1u, __ATOMIC_RELAXED,
+      // acq_rel at agent scope: every workgroup's release (fence above) synchronizes with
+      // the last arriver's acquire, so the rows it publishes below are ordered by the memory
+      // model, not only by each writer's own fence. An agent-scope acquire invalidates the
+      // per-CU caches only, not the L2 that keeps this stage's weights resident
+      const uint32_t prev = __hip_atomic_fetch_add(cnt + slot, 1u, __ATOMIC_ACQ_REL,
                                                    __HIP_MEMORY_SCOPE_AGENT);
       if (prev == gridDim.x - 1) {  // the last workgroup: every row of the request landed
         uint32_t st = 0u;
@@ -623,21 +642,6 @@ int chain_stage_run(const ChainStage& p, int workgroups, int share, hipStream_t 
   workgroups = std::min(workgroups, cap);
   hipLaunchKernelGGL(chain_stage_kernel, dim3(workgroups), dim3(256), (size_t)lds, stream, p);
   return hipGetLastError() == hipSuccess ? workgroups : -9;
-}
-
-// One lane sleeps `ticks` of the wall clock (bounded by construction): a deliberate delay of
-// the work queued behind it on its stream (the "@delay:<us>" plan op).
-__global__ void stream_delay_kernel(unsigned long long ticks) {
-  if (threadIdx.x != 0) return;
-  const unsigned long long t0 = wall_clock64();
-  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
-}
-
-int stream_delay(double us, hipStream_t stream) {
-  if (!(us >= 0.0) || us > 1e6) return -1;  // at most one second
-  hipLaunchKernelGGL(stream_delay_kernel, dim3(1), dim3(64), 0, stream,
-                     chain_ticks(us * 1e-6));
-  return hipGetLastError() == hipSuccess ? 0 : -9;
 }
 
 int chain_signal(uint32_t* flag, uint32_t value, hipStream_t stream) {

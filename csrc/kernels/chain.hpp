@@ -65,9 +65,6 @@ unsigned long long chain_ticks(double seconds);  // wall_clock64 ticks
 int chain_wait(const uint32_t* flag, uint32_t target, uint32_t* err, double timeout_s,
                hipStream_t stream);
 int chain_send(const ChainSend& p, hipStream_t stream);
-// A kernel that only waits `us` microseconds (wall clock): delays the work behind it on its
-// stream (step plans' "@delay:<us>").
-int stream_delay(double us, hipStream_t stream);
 // *flag = value with system-scope release (one lane, a vector store).
 int chain_signal(uint32_t* flag, uint32_t value, hipStream_t stream);
 

@@ -878,14 +878,10 @@ class Stage:
         # layers whose W^T comes out of the update launch itself (no transpose launch after it)
         skip = frozenset(i for i in self._wt_by_update_layers()) if wt_fused else frozenset()
         if o.name == "sgd":
-            # the layer-range form of layers 1.. runs on the side stream beside the next
-            # step's first forward (DNN_XSTEP): DNN_FINO_SIDE_BLOCKS caps its workgroups
-            cap = int(switches.get("DNN_FINO_SIDE_BLOCKS")) if a >= 1 else 0
             ops.reduce_multi(jobs, sgd=dict(grad=p.grad, master=p.master,
                                             mom=p.state[0] if p.state else None,
                                             shadow=p.shadow, lr=o.lr, momentum=o.momentum,
-                                            weight_decay=o.weight_decay, lr_dev=p.lr_dev),
-                             max_blocks=cap)
+                                            weight_decay=o.weight_decay, lr_dev=p.lr_dev))
             p.refresh_t(a, b, step=True, skip=skip)
             return
         if (a, b) != (0, L):

@@ -492,6 +492,11 @@ class Trainer:
                                           mode="slotted")
             self.executor.native_step = self.native_step
         cur = torch.cuda.current_stream(self.device)
+        # an eager step before the capture may have left its cross-step side-stream tail (the
+        # reduce + update of layers 1..L-1) running: order the capture after it, and start the
+        # cross-step chain afresh when eager steps resume
+        self.executor.xstep_join()
+        self.executor._xprimed = False
         self._stream = torch.cuda.Stream(self.device)
         self._stream.wait_stream(cur)
         if self.first is not None and self.first.x_in.data_ptr() != self.first.x_buf.data_ptr():

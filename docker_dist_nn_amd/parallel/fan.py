@@ -339,20 +339,31 @@ class FanPipe:
             self._sends.append(dist.isend(t, dst=dst, group=group))
 
     def begin_step(self):
+        """Post every receive of the step in THIS rank's consumption order (its F / B op
+        order), not grouped per peer: RCCL runs a rank's point-to-point operations in posting
+        order on one stream, so a receive from replica 1 posted behind all of replica 0's
+        could wait for data replica 0 sends only after it got our gradient.
+        Restricted to one peer the order must still be that peer's send order, for the FIFO
+        matching of each rank pair -- checked here."""
         m, st, lay, sch = self.mesh, self.stage, self.lay, self.sched
         s, q = m.stage, m.replica
-        if s > 0:  # forward inputs, per producer replica in its send order
-            for p in range(lay.reps[s - 1]):
-                for j in sch.send_order(s - 1, p, "f", q):
-                    jj = lay.local_index(s, j)
-                    self._recv_f[jj] = self._irecv(st.x_in[st.rows_of(jj)],
-                                                   lay.rank_of(s - 1, p), m.fwd_in, ("rf", jj))
-        if s + 1 < lay.S:  # gradients, per consumer replica in its send order
-            for c in range(lay.reps[s + 1]):
-                for j in sch.send_order(s + 1, c, "b", q):
-                    jj = lay.local_index(s, j)
-                    self._recv_b[jj] = self._irecv(st.grad_out[st.rows_of(jj)],
-                                                   lay.rank_of(s + 1, c), m.bwd_in, ("rb", jj))
+        mine = sch.ops[(s, q)]
+        for op, t, direction, grp, key, buf in (
+                ("F", s - 1, "f", m.fwd_in, "rf", st.x_in),
+                ("B", s + 1, "b", m.bwd_in, "rb", getattr(st, "grad_out", None))):
+            if not 0 <= t < lay.S:
+                continue
+            order = [j for o, j in mine if o == op]
+            for p in range(lay.reps[t]):
+                sent = sch.send_order(t, p, direction, q)
+                if [j for j in order if lay.replica_of(t, j) == p] != sent:
+                    raise RuntimeError(f"fan schedule: rank {m.rank} consumes the {op} hops "
+                                       f"from replica {p} out of that replica's send order")
+            recs = self._recv_f if op == "F" else self._recv_b
+            for j in order:
+                jj = lay.local_index(s, j)
+                recs[jj] = self._irecv(buf[st.rows_of(jj)],
+                                       lay.rank_of(t, lay.replica_of(t, j)), grp, (key, jj))
 
     def recv_fwd(self, stage, jj):
         if self.mesh.stage > 0:

@@ -147,7 +147,6 @@ class PipelineExecutor:
         # concurrent wgrad streams in native single-process plans (DNN_WGRAD_STREAMS)
         self.wgrad_streams = int(switches.get("DNN_WGRAD_STREAMS"))
         self._side = None
-        self._main_hp = None  # DNN_MAIN_PRIORITY=1: the overlap plan's main stream
         # deferred data-parallel update (DNN_DP_DEFER=0 disables): see dp_split
         self.defer = (grad_sync is not None and grad_sync.world > 1 and
                       not grad_sync.shard and switches.get("DNN_DP_DEFER") != "0")
@@ -326,7 +325,7 @@ class PipelineExecutor:
         mode = switches.get("DNN_BW_OVERLAP")
         # small steps are host-bound: every fork / join is an event record + wait (~6-8 us of
         # host time each), more than the overlap can win back on GEMMs of a few thousand rows
-        if mode in ("1", "2", "3", "4", "5", "6") and len(self.stages) == 1 and \
+        if mode in ("1", "5") and len(self.stages) == 1 and \
                 self.stages[0].rows >= int(switches.get("DNN_BW_OVERLAP_MIN_ROWS")):
             ov = self._overlap_plan(self.stages[0], mode)
             if ov is not None:
@@ -383,56 +382,21 @@ class PipelineExecutor:
         ready before dgrad_i starts), so a memory-bound dgrad and a wgrad fill each other's
         tails. Ends with a join, the first layer's wgrad and the gradient reduction/update.
 
-        mode "2" (opt-in A/B): ONE fork after the forward; the side stream runs the small
-        wgrads of layers L-1 .. 2 under the remaining dgrads, and the main stream runs the
-        dgrads and then W1, W0 itself (fewer ~6 us event packets, no large wgrad competing
-        with W0). Measured SLOWER on the headline (0.377 vs 0.372 ms): concurrent kernels
-        slow each other about in proportion, and the stagger the extra packets add helps
-        (profiles/r2_sched). mode "3" (opt-in A/B): the same side wgrads forked after W1, under
-        W0 -- slower still (0.386 ms): W0's workgroups hold the CUs and the side GEMMs wait."""
+        Mode "5" (opt-in): the small wgrads on the side stream, W1 and W0 on the main stream.
+        The other variants measured over rounds 2-5 (one fork with every side wgrad under the
+        dgrads or under W0, W1 first on the side, fork elision, a delay kernel instead of event
+        packets, stream priorities, an early join, a workgroup cap on the side reduction) lost
+        or tied and were removed in round 6 (profiles/r6_prune)."""
         segs = st._prog.segments()
         if st.nm != 1 or not st.first or not st.last or "W0" not in segs:
             return None
         L = len(st.geoms)
         fused = st.params.fused_layers  # their wgrad also UPDATES W_i and W_i^T
-        if mode == "4" and L >= 2 and not fused:  # largest side wgrad first, one fork
-            plan = [(st, "F0", 0), (None, "@fork", 0)]
-            plan += [(st, f"W{i}", 1) for i in range(1, L)]
-            plan += [(st, f"B0.L{i}", 0) for i in range(L - 1, 0, -1)]
-            plan += [(st, "W0", 0), (None, "@join", 0)]
-            plan.append((st, "FINO", 0) if "FINO" in segs else (st, "FIN", 0))
-            if "FINO" not in segs:
-                plan.append((st, "O", 0))
-            return plan
-        if mode in ("2", "3") and L >= 3 and not fused:
-            plan = [(st, "F0", 0)]
-            side = [(None, "@fork", 0)] + [(st, f"W{i}", 1) for i in range(L - 1, 1, -1)]
-            if mode == "2":  # small wgrads under the dgrads
-                plan += side
-            plan += [(st, f"B0.L{i}", 0) for i in range(L - 1, 0, -1)] + [(st, "W1", 0)]
-            if mode == "3":  # small wgrads under W0 (room for their workgroups next to it)
-                plan += side
-            plan += [(st, "W0", 0), (None, "@join", 0)]
-            plan.append((st, "FINO", 0) if "FINO" in segs else (st, "FIN", 0))
-            if "FINO" not in segs:
-                plan.append((st, "O", 0))
-            return plan
         # auto: on unless a layer updates in its wgrad epilogue (the wide model: there the
         # side-stream update of layers 1.. competes with the fused W1; profiles/r3b_fino)
         sf = switches.get("DNN_SPLIT_FINO")
         split = ((sf == "1" or (sf == "auto" and not fused)) and L > 1 and
                  f"FINO1-{L - 1}" in segs and "FINO0-0" in segs and 0 not in fused)
-        if mode == "6" and L >= 3 and not fused and split and all(
-                st._prog.segment_size(f"B0.L{i}") == 0 for i in range(2, L)):
-            # one fork after the forward (every side wgrad's dZ comes from it: the classifier
-            # tail ran the dgrads of layers 2..L-1); the side stream runs W1 FIRST, beside the
-            # layer-1 dgrad, then the small ones -- so W0 (main, after that dgrad) shares the
-            # chip with small wgrads instead of W1
-            plan = [(st, "F0", 0), (None, "@fork", 0), (st, "W1", 1)]
-            plan += [(st, f"W{i}", 1) for i in range(L - 1, 1, -1)]
-            plan += [(st, f"B0.L{i}", 0) for i in range(L - 1, 0, -1)]
-            return plan + [(None, "@fork", 0), (st, f"FINO1-{L - 1}", 1), (st, "W0", 0),
-                           (st, "FINO0-0", 0), (None, "@join", 0)]
         if mode == "5" and L >= 3 and not fused:
             # one fork: the small wgrads (L-1 .. 2) on the side under the dgrads; W1 on the
             # main stream right after the last dgrad, then W0 -- so W1 and W0 never share the
@@ -455,15 +419,6 @@ class PipelineExecutor:
                 plan += [(st, f"W{i}", 1), (st, f"B0.L{i}", 0), (None, "@fork", 0)]
         if plan[-1][1] == "@fork" and not split:
             plan = plan[:-1]
-        if switches.get("DNN_FORK_ELIDE") in ("1", "2"):
-            plan = self._elide_forks(st, plan, rewait=switches.get("DNN_FORK_ELIDE") == "2")
-        delay = float(switches.get("DNN_SIDE_DELAY_US"))
-        if delay > 0:
-            # the side stream starts its first wgrad `delay` us after the fork instead of the
-            # main stream paying event packets for that stagger (with DNN_FORK_ELIDE=1 the
-            # redundant forks are gone and the next dgrad starts right after the tail)
-            k = next(i for i, e in enumerate(plan) if e[1] == "@fork")
-            plan = plan[:k + 1] + [(None, f"@delay:{delay:g}", 1)] + plan[k + 1:]
         if split:
             # the side stream reduces + updates layers 1..L-1 (their wgrads are done; the fork
             # above orders it after the last dgrad, the last reader of their W^T) while the
@@ -471,10 +426,6 @@ class PipelineExecutor:
             if plan[-1][1] != "@fork":
                 plan.append((None, "@fork", 0))
             plan += [(st, f"FINO1-{L - 1}", 1), (st, "W0", 0)]
-            if switches.get("DNN_JOIN_EARLY") == "1":
-                # the join's wait packet in front of layer 0's update rather than in front of
-                # the next step's first kernel (the side stream finished long before W0)
-                return plan + [(None, "@join", 0), (st, "FINO0-0", 0)]
             return plan + [(st, "FINO0-0", 0), (None, "@join", 0)]
         plan += [(st, "W0", 0), (None, "@join", 0)]
         plan.append((st, "FINO", 0) if "FINO" in segs else (st, "FIN", 0))
@@ -506,29 +457,6 @@ class PipelineExecutor:
             plan.append((st, f"W{i}", 1))
         plan += [(st, f"B0.L{i}", 0) for i in range(L - 1, 0, -1) if i not in emitted]
         return plan
-
-    @staticmethod
-    def _elide_forks(st, plan, rewait: bool = False):
-        """Drop a fork when the main stream enqueued nothing since the previous one (an empty
-        segment, e.g. the dgrads the fused classifier tail already ran): the side stream is
-        ordered after that earlier fork already. Each event record + wait is a barrier packet
-        that costs ~6 us of queue time on the main stream (kernel trace:
-        profiles/r2_sched), three of them sat between the tail and the next dgrad.
-        ``rewait``: keep the side stream's wait there ("@rewait": the same event again, a
-        packet on the side queue only), so the side kernels keep their stagger while the main
-        stream loses the records."""
-        out, main_work = [], True  # the first fork always follows real work (F0)
-        for e in plan:
-            if e[1] == "@fork":
-                if not main_work:
-                    if rewait:
-                        out.append((None, "@rewait", 0))
-                    continue
-                main_work = False
-            elif e[0] is not None and e[2] == 0 and st._prog.segment_size(e[1]) > 0:
-                main_work = True
-            out.append(e)
-        return out
 
     def _loopback_step_plan(self, plan):
         """Several stages in one process (loopback): run each stage on ITS OWN stream, with an
@@ -602,31 +530,23 @@ class PipelineExecutor:
                 plan = self._xstep_plan(plan)
         if plan is not None:
             dev = self.stages[0].device
+            if getattr(self, "_xprimed", False) and any(
+                    float(st.params.optim.lr) != getattr(st.params, "_lr_cur", None)
+                    for st in self.stages):
+                # the previous step's side-stream update still reads lr_dev: a new rate is
+                # written only after it
+                self.xstep_join()
             for st in self.stages:
                 st.params.set_lr(st.params.optim.lr)
             if self._side is None and (self.wgrad_streams > 1 or
                                        any(e[1] == "@fork" for e in plan)):
-                # DNN_SIDE_PRIORITY=1: the side stream (small wgrads) at high priority, so
-                # its workgroups are dispatched ahead of the main stream's pending ones
-                self._side = torch.cuda.Stream(
-                    dev, priority=-1 if switches.get("DNN_SIDE_PRIORITY") == "1" else 0)
-            cur = torch.cuda.current_stream(dev)
-            main = cur
-            if self._side is not None and switches.get("DNN_MAIN_PRIORITY") == "1":
-                # the critical path (forward, dgrads, the first layer's wgrad) on a
-                # high-priority stream: when its kernels and the side stream's wgrads are both
-                # pending, its workgroups are dispatched first and the wgrads fill in
-                if self._main_hp is None:
-                    self._main_hp = torch.cuda.Stream(dev, priority=-1)
-                main = self._main_hp
-                main.wait_stream(cur)
+                self._side = torch.cuda.Stream(dev)
+            main = cur = torch.cuda.current_stream(dev)
             native().run_plan([(st._prog if st is not None else None, seg, si)
                                for st, seg, si in plan],
                               main.cuda_stream,
                               self._side.cuda_stream if self._side is not None else 0,
-                              switches.get("DNN_EVENT_FENCE") == "device")
-            if main is not cur:
-                cur.wait_stream(main)
+                              switches.get("DNN_EVENT_FENCE") == "device", id(self))
             for st in self.stages:
                 st.params.step_count += 1
             self.pipe.end_step()
@@ -688,7 +608,7 @@ class PipelineExecutor:
             cur = torch.cuda.current_stream(st.device)
             native().run_plan([(None, "@xwait:end", 0)], cur.cuda_stream,
                               self._side.cuda_stream,
-                              switches.get("DNN_EVENT_FENCE") == "device")
+                              switches.get("DNN_EVENT_FENCE") == "device", id(self))
 
     def _run_interleaved(self):
         self._traverse(lambda s, op, j, nxt: self._run_op(self.stages[s], op, j, nxt))

@@ -47,13 +47,9 @@ SWITCHES: dict[str, tuple[str, str]] = {
     "DNN_BENCH_STEP_EVENTS": ("0", "bench.py: 1 = a HIP event around every timed step; the JSON "
                                    "gets the per-step GPU times (diagnosis)"),
     "DNN_BW_OVERLAP": ("1", "wgrad_i on a side stream concurrent with dgrad_i (1 stage, one "
-                            "micro-batch): mlp8 3.43 -> 3.31 ms; 2 = only the small wgrads "
-                            "on the side (headline 0.377 vs 0.372 ms, rejected); 3 = those under "
-                            "W0 (0.386 ms, rejected); 4 = one fork, W1..W3 on the side (0.407 ms, "
-                            "rejected); 5 = small wgrads on the side, W1 then W0 on the main "
-                            "stream (fixes their order); 6 = one fork, W1 first on the side "
-                            "then the small wgrads (the classifier-tail shape with the split "
-                            "reduction); 0 = off"),
+                            "micro-batch): mlp8 3.43 -> 3.31 ms; 5 = small wgrads on the side, "
+                            "W1 then W0 on the main stream (fixes their order); 0 = off. The "
+                            "rejected modes 2/3/4/6 were removed in round 6 (profiles/r6_prune)"),
     "DNN_BW_OVERLAP_MIN_ROWS": ("16384", "overlap plans only for steps of at least this many "
                                          "rows (below, the single-stream plan: no event "
                                          "packets, the host cost that bounds small steps; "
@@ -71,10 +67,6 @@ SWITCHES: dict[str, tuple[str, str]] = {
     "DNN_FWD_TAIL": ("0", "fuse the forward of the layer before the classifier tail into the "
                           "tail launch (mlp_fwd_tail_kernel; ReLU, 256-wide, 256-row tiles); "
                           "headline 0.375 vs 0.372 ms (71 us = the two kernels' sum), opt-in"),
-    "DNN_MAIN_PRIORITY": ("0", "overlap plans: run the main (critical-path) stream at high "
-                               "priority so side-stream wgrads only fill in"),
-    "DNN_SIDE_PRIORITY": ("0", "overlap plans: create the side stream at high priority "
-                               "(measured no effect: 0.374 vs 0.373 ms)"),
     "DNN_H0_DOUBLE": ("1", "single-stage native steps: the layer-0 activation alternates between "
                            "two buffers from step to step (a relocatable Program region), so "
                            "with DNN_XSTEP the next step's layer-0 forward does not wait for "
@@ -85,20 +77,6 @@ SWITCHES: dict[str, tuple[str, str]] = {
     "DNN_EVENT_FENCE": ("device", "fork / join events of single-process step plans: device = "
                                   "no system-scope fence at the record (both streams on one "
                                   "GPU), system = HIP's default (cache write-back per record)"),
-    "DNN_FINO_SIDE_BLOCKS": ("0", "workgroup cap of the side-stream reduce + SGD of layers "
-                                  "1..L-1 (it runs beside the next step's first forward with "
-                                  "DNN_XSTEP); 0 = one workgroup per block"),
-    "DNN_SIDE_DELAY_US": ("0", "overlap plans: the side stream waits this many microseconds "
-                               "after the first fork (a delay kernel) before its first wgrad -- "
-                               "the stagger the redundant forks gave, without their event "
-                               "packets on the main stream (use with DNN_FORK_ELIDE=1)"),
-    "DNN_JOIN_EARLY": ("0", "overlap plan with the split reduction: the side stream's join "
-                            "before layer 0's update instead of at the end of the step"),
-    "DNN_FORK_ELIDE": ("0", "overlap plans: drop a side-stream fork when the main stream "
-                            "enqueued nothing since the previous one (~6 us per event "
-                            "packet); headline 0.403 vs 0.373 ms: the wgrads then all start "
-                            "together and contend, rejected; 2 = side re-waits instead "
-                            "(0.406 ms, rejected)"),
     "DNN_DP_DEFER": ("1", "deferred data-parallel update (Python executor path)"),
     "DNN_RCCL_PLAN": ("auto", "native RCCL step form: streams (one stream per hop channel) | "
                       "slotted (one RCCL stream, per-slot groups: safe with one resident RCCL "

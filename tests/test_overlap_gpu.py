@@ -1,6 +1,6 @@
 """dgrad/wgrad overlap plans (DNN_BW_OVERLAP=1: wgrad_i on a side stream concurrent with the
-next dgrad; =2: only the small wgrads of layers >= 2 on the side stream, one fork): must be
-bitwise identical to the sequential native plan."""
+next dgrad; =5: the small wgrads on the side, W1 and W0 on the main stream): must be bitwise
+identical to the sequential native plan."""
 import pytest
 import torch
 
@@ -22,19 +22,12 @@ def test_overlap_plan_bitwise(dev, monkeypatch, model, rows):
     xb[:, :784] = torch.from_numpy(x).to(torch.bfloat16)
     xb, yb = xb.to(dev), torch.from_numpy(y).to(dev)
     res = []
-    # 1eK: plan 1 with DNN_FORK_ELIDE=K; 1s: plan 1 with DNN_SPLIT_FINO (layers 1.. reduced and
-    # updated on the side stream during W0)
-    # 5 / 5s: small wgrads on the side, W1 then W0 on the main stream (unsplit / split FINO)
-    # 1j: plan 1 with the split reduction and the join in front of layer 0's update
-    # 6s: one fork, W1 first on the side stream, then the small wgrads (split reduction; the
-    # headline shape only -- elsewhere it falls back to plan 1)
-    # 1e1d: plan 1, forks elided, the side stream staggered by a 10 us delay kernel
-    for flag in ("0", "1", "2", "3", "4", "1e1", "1e2", "1s", "5", "5s", "1j", "6s", "1e1d"):
+    # 1s: plan 1 with DNN_SPLIT_FINO (layers 1.. reduced and updated on the side stream
+    # during W0); 5 / 5s: small wgrads on the side, W1 then W0 on the main stream (unsplit /
+    # split FINO)
+    for flag in ("0", "1", "1s", "5", "5s"):
         monkeypatch.setenv("DNN_BW_OVERLAP", flag[0])
-        monkeypatch.setenv("DNN_FORK_ELIDE", flag[2:3] if flag[1:2] == "e" else "0")
-        monkeypatch.setenv("DNN_SIDE_DELAY_US", "10" if flag.endswith("d") else "0")
-        monkeypatch.setenv("DNN_SPLIT_FINO", "1" if flag[-1] in "sj" else "0")
-        monkeypatch.setenv("DNN_JOIN_EARLY", "1" if flag == "1j" else "0")
+        monkeypatch.setenv("DNN_SPLIT_FINO", "1" if flag[-1] == "s" else "0")
         tr = Trainer(spec, micro_batch=rows, num_micro=1,
                      optim=OptimConfig(lr=0.1, momentum=0.9), device=dev)
         losses = []
