@@ -114,16 +114,18 @@ def _plan(a, spec, n, world, text):
                                  dp_grad_bytes=2.0 if a.dp_reduce == "shard" else 4.0)
     loopback = world == 1
     fan = parse_fan(text)
-    if fan is not None:  # 'fan:1x1,2x7' (layers x GPUs per stage) or 'fan:1,7' (GPUs only)
-        dist_, reps = fan
-        if not reps or sum(reps) != n:
-            raise SystemExit(f"--parallelism {text}: the replica counts must add up to {n}")
+    if fan is not None:  # 'fan:1x1,2x7' (layers x GPUs per stage), 'fan:1,7' (GPUs only) or
+        # 'fan:3x4,1x1@3' (the last stage co-located on rank 3)
+        dist_, reps, place = fan
+        if not reps or FanLayout(tuple([1] * len(reps)), tuple(reps), place).world != n:
+            raise SystemExit(f"--parallelism {text}: the layout must use {n} GPUs")
         if not dist_:
             from docker_dist_nn_amd.parallel.planner import compositions
 
             dist_ = max(compositions(len(spec.layers), len(reps)),
-                        key=lambda d: planner.evaluate_fan(spec, d, reps, a.batch).samples_per_s)
-        return planner.evaluate_fan(spec, dist_, reps, a.batch)
+                        key=lambda d: planner.evaluate_fan(spec, d, reps, a.batch,
+                                                           place=place).samples_per_s)
+        return planner.evaluate_fan(spec, dist_, reps, a.batch, place=place)
     pp, dp = parse_parallelism("pipeline" if text == "uniform" else text, n, loopback=loopback)
     if pp is None:
         if text == "best":
@@ -179,9 +181,10 @@ def first_step_guard(tr, one_step, dev, timeout_s):
 def measure(a, spec, n, world, dev, text):
     """Build the trainer for one layout, W warm-up + K timed steps; returns the JSON fields."""
     plan = _plan(a, spec, n, world, text)
-    fan = plan.reps is not None and len(set(plan.reps)) > 1
-    if fan and world != sum(plan.reps):
-        raise SystemExit(f"fan layout {plan.parallelism} needs {sum(plan.reps)} ranks")
+    fan = plan.reps is not None and (len(set(plan.reps)) > 1 or plan.colocated)
+    lay = FanLayout(tuple(plan.distribution), tuple(plan.reps), plan.place) if fan else None
+    if fan and world != lay.world:
+        raise SystemExit(f"fan layout {plan.parallelism} needs {lay.world} ranks")
     if plan.reps is not None and not fan:  # equal replica counts: the uniform ppS x dpD grid
         plan.dp = plan.reps[0]
         plan.reps = None
@@ -203,15 +206,15 @@ def measure(a, spec, n, world, dev, text):
         from docker_dist_nn_amd.engine.fan_trainer import FanTrainer
         from docker_dist_nn_amd.parallel.fan import build_fan_mesh
 
-        lay = FanLayout(tuple(plan.distribution), tuple(plan.reps))
         mesh = build_fan_mesh(lay)
         sched = "fan"
         tr = FanTrainer(spec, lay, mesh, micro_batch=mb, num_micro=nm,
                         optim=OptimConfig(name=a.optimizer, lr=a.lr), device=dev, seed=a.seed,
                         dp_reduce=a.dp_reduce)
-        data = FanDataset(lay.local_micros(mesh.stage, mesh.replica, nm), mb, dev,
+        data = FanDataset(tr.input_micros, mb, dev,
                           kp=tr.stages[0].x_in.shape[1] if tr.first else None, seed=a.seed,
-                          inputs=tr.first is not None, labels=tr.last is not None)
+                          inputs=tr.first is not None, labels=tr.last is not None,
+                          label_micros=tr.label_micros)
         global_batch = mb * nm
     else:
         if world > 1:
@@ -334,6 +337,7 @@ def measure(a, spec, n, world, dev, text):
         "parallelism": plan.parallelism + ("-loopback" if world == 1 and plan.pp > 1 else ""),
         "layer_distribution": plan.distribution, "micro_batch": mb, "num_micro": nm,
         "stage_gpus": plan.reps if fan else None,
+        "stage_place": [list(p) for p in plan.place] if fan and plan.colocated else None,
         "schedule": sched if plan.pp > 1 else "none",
         "transport": tr.transport, "transport_reason": tr.transport_reason,
         "native_step": tr.native_step is not None or world == 1,
@@ -394,43 +398,68 @@ def measure_tp(a, spec, n, world, dev):
 DP_ONLY_KEYS = ("parallelism", "global_batch", "transport", "native_step", "dp_reduce")
 
 
+def _summary(d, keys):
+    return {"value": d["value"], "ms_per_step": d["ms_per_step"],
+            **{k: d["config"].get(k) for k in keys}}
+
+
 def supervise(a, argv) -> int:
     """WORLD_SIZE > 1: this process is the rank's supervisor (ladder.py). It never touches the
     GPU; every attempt runs ``bench.py`` again as a fresh child per rank (new rendezvous port),
-    climbing the fallback ladder until one attempt succeeds on every rank. Then, if the time
-    left allows, the data-parallel comparison runs the same way. Rank 0 prints the one JSON
-    line, with every attempt (rung, exit codes, last heartbeat of a stalled child) listed --
-    also when the job is ended by SIGTERM (ladder.OneLine), so a bench the driver stops at its
-    deadline still reports.
+    climbing the fallback ladder until one attempt succeeds on every rank. Then, while the time
+    left allows, two comparisons run the same way: the literal uniform ppS x dpD pipeline of
+    BASELINE.json (when the main layout was a replicated-stage "fan" pipeline) and pure data
+    parallelism. Rank 0 prints the one JSON line, with every attempt (rung, exit codes, last
+    heartbeat of a stalled child) listed -- also when the job is ended by SIGTERM
+    (ladder.OneLine), so a bench the driver stops at its deadline still reports.
 
     Time: a failing rung costs at most a child's start-up + the first-step guard
     (DNN_FIRST_STEP_TIMEOUT, 30 s) or a heartbeat stall (DNN_LADDER_STALL, 60 s); past
-    DNN_LADDER_BUDGET (360 s) only the last rung is tried, and nothing runs past
-    DNN_LADDER_DEADLINE (540 s from start) -- inside a 600-second driver window."""
+    DNN_LADDER_BUDGET (360 s) only the last rung is tried; a comparison starts only if 1.5 x the
+    main attempt's time + 30 s is left; nothing runs past DNN_LADDER_DEADLINE (540 s from
+    start) -- inside a 600-second driver window."""
     t_start = time.monotonic()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ["WORLD_SIZE"])
     base = [sys.executable, "-u", os.path.abspath(__file__),
             *(sys.argv[1:] if argv is None else argv)]
-    st = {"res": None, "rung": None, "attempts": [], "dp_only": None, "dp_attempts": None}
+    st = {"res": None, "rung": None, "attempts": [], "extra": {}}
     sup = None
+    spec = NAMED_MODELS.get(a.model) or MLPSpec.parse(a.model)
+
+    def entry_json(key, e):
+        if e is None:
+            return None
+        if "skipped" in e:
+            return {"value": None, **e}
+        d = e["result"]
+        if d is None:
+            return {"value": None, "error": "every rung failed"}
+        if key == "uniform_pipeline":
+            return {**_summary(d, ("parallelism", "layer_distribution", "transport",
+                                   "rccl_plan")),
+                    "planner_predicted": d.get("planner_predicted")}
+        return _summary(d, DP_ONLY_KEYS)
 
     def build(reason):
         attempts = list(sup.attempts) if sup is not None else []
-        main_att = attempts[:len(st["attempts"])] if st["res"] is not None else attempts
         if st["res"] is None:
             out = {"metric": METRIC, "value": None, "unit": "samples/s", "n_gpus": world,
                    "steps": a.steps, "warmup": a.warmup, "higher_is_better": True,
                    "error": ("terminated before any rung succeeded" if reason else
                              "every rung of the fallback ladder failed"),
-                   "ladder": {"attempts": main_att}}
+                   "ladder": {"attempts": attempts}}
         else:
             out = dict(st["res"])
-            dp_att = attempts[len(st["attempts"]):] or st["dp_attempts"]
-            out["dp_only"] = st["dp_only"] if st["dp_only"] is not None else (
-                {"value": None, "skipped": "terminated"} if reason else None)
+            n_main = len(st["attempts"])
+            for key in ("uniform_pipeline", "dp_only"):
+                e = st["extra"].get(key)
+                if e is not None:  # measured (or skipped) over the child's prediction
+                    out[key] = {**(out.get(key) or {}), **entry_json(key, e)}
+                elif reason and key in st["pending"]:
+                    out[key] = {**(out.get(key) or {}), "value": None, "skipped": "terminated"}
             out["ladder"] = {"rung": st["rung"], "attempts": st["attempts"],
-                             "dp_attempts": dp_att}
+                             "compare_attempts": attempts[n_main:]}
         out["ladder"]["seconds"] = round(time.monotonic() - t_start, 1)
         if reason:
             out["terminated"] = reason
@@ -442,36 +471,30 @@ def supervise(a, argv) -> int:
                             world=world, stall=float(switches.get("DNN_LADDER_STALL")),
                             startup=float(switches.get("DNN_LADDER_STARTUP")),
                             deadline=t_start + float(switches.get("DNN_LADDER_DEADLINE")))
+    is_fan = False
     if a.parallelism.startswith("tp"):
         rungs = [ladder.Rung("default")]
     else:
         # the planner runs on the CPU: the supervisor knows whether the default layout is a
         # replicated-stage pipeline without touching the GPU
-        spec = NAMED_MODELS.get(a.model) or MLPSpec.parse(a.model)
-        is_fan = (not a.parallelism.startswith("dp") and
-                  _plan(a, spec, world, world, a.parallelism).reps is not None and
-                  len(set(_plan(a, spec, world, world, a.parallelism).reps)) > 1)
+        if not a.parallelism.startswith("dp"):
+            p = _plan(a, spec, world, world, a.parallelism)
+            is_fan = p.reps is not None and (len(set(p.reps)) > 1 or p.colocated)
         rungs = ladder.bench_rungs(world, dp_only=a.parallelism.startswith("dp"), fan=is_fan)
+    st["pending"] = []
     res, rung = sup.climb(rungs, budget_s=float(switches.get("DNN_LADDER_BUDGET")))
     st.update(res=res, rung=rung.name if rung else None, attempts=list(sup.attempts))
-    if res is not None and not a.no_dp_compare and \
-            not res["config"]["parallelism"].startswith(("dp", "tp")):
-        # the comparison only when the attempt that just succeeded would fit again before
-        # the deadline (the decision must be the same on every rank: rank 0's, via the store)
+    if res is not None:
+        lay = res["config"]["parallelism"]
+        items = []
+        # the literal BASELINE grid, measured, when the main number came from a fan layout
+        if is_fan and lay.startswith("fan"):
+            items.append(("uniform_pipeline", ladder.uniform_rungs()))
+        if not a.no_dp_compare and not lay.startswith(("dp", "tp")):
+            items.append(("dp_only", ladder.bench_rungs(world, dp_only=True)))
+        st["pending"] = [k for k, _ in items]
         need = 1.5 * sup.attempts[-1]["seconds"] + 30
-        key = "dp_compare/decision"
-        if rank == 0:
-            sup.store.set(key, "run" if (sup.seconds_left() or 0) > need else "skip")
-        if sup.store.get(key).decode() == "run":
-            d, _ = sup.climb(ladder.bench_rungs(world, dp_only=True))
-            st["dp_attempts"] = sup.attempts[len(st["attempts"]):]
-            st["dp_only"] = ({"value": d["value"], "ms_per_step": d["ms_per_step"],
-                              **{k: d["config"].get(k) for k in DP_ONLY_KEYS}} if d is not None
-                             else {"value": None, "error": "every data-parallel rung failed"})
-        else:
-            st["dp_only"] = {"value": None, "skipped": "budget",
-                             "seconds_left": round(sup.seconds_left() or 0, 1),
-                             "seconds_needed": round(need, 1)}
+        sup.comparisons(items, need, on_done=lambda k, e: st["extra"].__setitem__(k, e))
     line.emit()
     return 0 if res is not None else 1
 
@@ -502,6 +525,13 @@ def main(argv=None):
         m = measure_tp(a, spec, n, world, dev)
     else:
         m = measure(a, spec, n, world, dev, a.parallelism)
+    uniform = _uniform_prediction(a, spec, n, world)
+    if world > 1 and not ladder.is_child() and m["parallelism"].startswith("fan"):
+        # without the ladder (DNN_LADDER=0): the literal grid measured in-process too
+        u = measure(a, spec, n, world, dev, "uniform")
+        uniform = {**(uniform or {}), "value": u["value"], "ms_per_step": u["ms_per_step"],
+                   "parallelism": u["parallelism"], "layer_distribution": u["layer_distribution"],
+                   "transport": u["transport"], "rccl_plan": u["rccl_plan"]}
     dp_only = None
     if world > 1 and not a.no_dp_compare and not m["parallelism"].startswith(("dp", "tp")):
         d = measure(a, spec, n, world, dev, f"dp{n}")
@@ -529,6 +559,7 @@ def main(argv=None):
             "global_batch": m["global_batch"],
             "seq_len": None,
             **{k: m.get(k) for k in ("parallelism", "layer_distribution", "stage_gpus",
+                                 "stage_place",
                                  "micro_batch", "num_micro",
                                  "schedule", "transport", "transport_reason", "native_step",
                                  "rccl_plan",
@@ -543,9 +574,10 @@ def main(argv=None):
         **({"step_ms": m["step_ms"]} if m.get("step_ms") else {}),
         "graph_trial": m.get("graph_trial"),
         "dp_only": dp_only,
-        # the literal uniform ppS x dpD grid of BASELINE.json, predicted by the same planner
-        # (measured with --parallelism uniform)
-        "uniform_pipeline": _uniform_prediction(a, spec, n, world),
+        # the literal uniform ppS x dpD grid of BASELINE.json: predicted by the same planner,
+        # measured too after a fan layout's number (the supervisor's comparison; in-process
+        # without the ladder)
+        "uniform_pipeline": uniform,
         "native_fallback": m["native_fallback"],  # why the Python executor ran, if it did
         "switches": switches.active(),  # non-default DNN_* switches of this run
     }

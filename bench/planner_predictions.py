@@ -3,7 +3,12 @@ the uniform pipeline (bf16 and fp8 hops, relays), the best replicated-stage ("fa
 bench.py runs (parallel/fan.py; bf16 hops, direct links), and the data-parallel-only layout,
 each with its efficiency against N x the one-GPU rate.
 
-    python bench/planner_predictions.py > profiles/r5_planner/predictions.jsonl
+    python bench/planner_predictions.py > profiles/r6_planner/predictions.jsonl
+
+Round 6: every planner here is calibrated on one MI355X (Planner.calibrated: the measured
+single-stage step and the measured replica steps of every layer range at every micro-batch
+size and count, docker_dist_nn_amd/parallel/stage_times_gfx950.json), and the fan search
+includes the light last stage co-located on a heavy replica's GPU.
 """
 from __future__ import annotations
 
@@ -34,6 +39,7 @@ def main():
             d = pl.evaluate(spec, 1, n, rows)
             one = pl.evaluate(spec, 1, 1, rows).samples_per_s
             f = pl.best_fan(spec, n, rows) if n > 1 else a
+            fs = pl.best_fan(spec, n, rows, colocate=False) if n > 1 else a
             f8 = p8.best_fan(spec, n, rows) if n > 1 else a
             print(json.dumps({"model": model, "n": n, "layout": a.parallelism,
                               "dist": a.distribution, "nm": a.num_micro,
@@ -46,6 +52,8 @@ def main():
                               "fan_reps": f.reps, "fan_nm": f.num_micro,
                               "fan_bf16_Msps": round(f.samples_per_s / 1e6, 1),
                               "fan_eff": round(f.samples_per_s / (n * one), 3),
+                              "fan_no_colocation": fs.parallelism,
+                              "fan_no_colocation_Msps": round(fs.samples_per_s / 1e6, 1),
                               "fan_detail": f.detail if n > 1 else None,
                               "fan_fp8_layout": f8.parallelism,
                               "fan_fp8_Msps": round(f8.samples_per_s / 1e6, 1),

@@ -156,21 +156,24 @@ class FanDataset:
     micro-batches in local order), resident in HBM like DeviceDataset."""
 
     def __init__(self, micros, mb: int, device: torch.device, kp: Optional[int] = None,
-                 seed: int = 0, inputs: bool = True, labels: bool = True):
+                 seed: int = 0, inputs: bool = True, labels: bool = True,
+                 label_micros=None):
+        """``micros``: the global micro-batches whose inputs this rank holds (its first-stage
+        replica's); ``label_micros``: those whose labels it holds (its last-stage replica's;
+        default ``micros`` -- they differ on a rank hosting co-located stages)."""
+        label_micros = micros if label_micros is None else label_micros
         self.batches = []
         for b in range(2):
-            xs, ys = [], []
-            for j in micros:
-                x, y = synthetic_mnist(mb, seed=seed + 7919 * b + j)
-                xs.append(x)
-                ys.append(y)
-            dim = xs[0].shape[1]
-            kpp = kp or round_up(dim, 64)
-            xt = None
-            if inputs:
+            xt = yt = None
+            if inputs and micros:
+                xs = [synthetic_mnist(mb, seed=seed + 7919 * b + j)[0] for j in micros]
+                dim = xs[0].shape[1]
+                kpp = kp or round_up(dim, 64)
                 xt = torch.zeros(len(micros) * mb, kpp, dtype=torch.bfloat16, device=device)
                 xt[:, :dim] = torch.from_numpy(np.concatenate(xs)).to(device, torch.bfloat16)
-            yt = torch.from_numpy(np.concatenate(ys)).to(device) if labels else None
+            if labels and label_micros:
+                ys = [synthetic_mnist(mb, seed=seed + 7919 * b + j)[1] for j in label_micros]
+                yt = torch.from_numpy(np.concatenate(ys)).to(device)
             self.batches.append((xt, yt))
 
     def batch(self, i: int):

@@ -16,13 +16,48 @@ from typing import Optional
 import torch
 
 from ..models.mlp import MLPSpec
-from ..parallel.fan import FanLayout, FanMesh, FanPipe, fan_rows, fan_schedule, gather_rows, \
-    stage_costs
+from ..parallel.fan import FanLayout, FanMesh, FanPipe, fan_schedule, gather_rows, stage_costs
 from ..parallel.pipeline import GradSync, PipelineExecutor
 from ..partition import plan_stages
 from .stage import OptimConfig, Stage
 from .trainer import Trainer, _any_rank, _warm_groups
 from .. import switches
+
+
+class _RankSteps:
+    """The Python step of a rank hosting several workers (co-located fan layout): each
+    worker's stage has an executor of its own (its own DP group), and the rank runs every
+    compute op of its workers in the schedule's rank order (FanSchedule.rank_ops: one GPU, one
+    compute stream), then each stage's batched weight gradient and update."""
+
+    def __init__(self, execs: dict, order: list, pipe):
+        self.execs, self.order, self.pipe = execs, order, pipe
+        self.stages = [ex.stages[0] for _, ex in sorted(execs.items())]
+        self.native_step = None
+        self.capturing = False
+
+    def run_step(self) -> None:
+        self.pipe.begin_step()
+        for ex in self.execs.values():
+            st = ex.stages[0]
+            st.begin_step()
+            if st.params.fused_layers:  # one-split wgrads update in their epilogue
+                st.params.set_lr(ex.lr_fn() if ex.lr_fn else st.params.optim.lr)
+        for s, op, jj in self.order:
+            ex = self.execs[s]
+            ex._run_op(ex.stages[0], op, jj, None)
+        for s, ex in sorted(self.execs.items(), reverse=True):
+            st = ex.stages[0]
+            ex._run_op(st, "W", -1, "O")
+            ex._run_op(st, "O", -1, None)
+        self.pipe.end_step()
+
+    def flush(self) -> None:
+        for ex in self.execs.values():
+            ex.flush()
+
+    def xstep_join(self) -> None:
+        pass
 
 
 class FanTrainer(Trainer):
@@ -33,10 +68,12 @@ class FanTrainer(Trainer):
                  hop_cost: float = 0.0):
         if sum(layout.dist) != len(spec.layers):
             raise ValueError(f"fan layout {layout.dist} does not cover {len(spec.layers)} layers")
+        layout.check_directions(num_micro)
         self.spec, self.mesh, self.layout = spec, mesh, layout
         self.device = device or (torch.device("cuda", torch.cuda.current_device())
                                  if torch.cuda.is_available() else torch.device("cpu"))
-        s, q = mesh.stage, mesh.replica
+        workers = mesh.workers or [(mesh.stage, mesh.replica)]
+        s, q = workers[0]
         r = layout.reps[s]
         self.pp, self.dp = layout.S, r
         self.plans = plan_stages(len(spec.layers), list(layout.dist))
@@ -47,44 +84,66 @@ class FanTrainer(Trainer):
         self.optim = optim or OptimConfig()
         if dp_reduce not in ("allreduce", "shard"):
             raise ValueError(f"dp_reduce must be allreduce | shard, got {dp_reduce!r}")
-        self.dp_reduce = dp_reduce if r > 1 else "allreduce"
+        self.dp_reduce = dp_reduce if max(layout.reps[w] for w, _ in workers) > 1 \
+            else "allreduce"
         self.local = layout.local_micros(s, q, num_micro)
-        p = self.plans[s]
-        st = Stage(spec, p.layer_start, p.layer_end, micro_batch=micro_batch,
-                   num_micro=len(self.local), device=self.device,
-                   global_batch=self.global_batch, optim=self.optim, wgrad="batched",
-                   stage_index=s, num_stages=layout.S,
-                   dp_shard=(r, q) if self.dp_reduce == "shard" else None)
-        st.params.init_default(seed)
-        self.stages = [st]
         f, b = stage_costs(spec, layout.dist)
         self.sched = fan_schedule(layout, num_micro, f, b, hop_cost)
-        self.pipe = FanPipe(mesh, st, self.sched)
+        stages = {}
+        for ws, wq in workers:
+            wr = layout.reps[ws]
+            p = self.plans[ws]
+            st = Stage(spec, p.layer_start, p.layer_end, micro_batch=micro_batch,
+                       num_micro=len(layout.local_micros(ws, wq, num_micro)),
+                       device=self.device, global_batch=self.global_batch, optim=self.optim,
+                       wgrad="batched", stage_index=ws, num_stages=layout.S,
+                       dp_shard=(wr, wq) if self.dp_reduce == "shard" and wr > 1 else None)
+            st.params.init_default(seed)
+            stages[ws] = st
+        self.stages = [stages[k] for k in sorted(stages)]
+        self.pipe = FanPipe(mesh, stages if len(stages) > 1 else stages[s], self.sched)
         self.boundary = "bf16"
-        sync = GradSync(mesh.dp_group, r, shard=self.dp_reduce == "shard") if r > 1 else None
-        self.executor = PipelineExecutor(self.stages, self.pipe, "1f1b", layout.S, [s], sync)
-        self.executor.ops = [self.sched.local_ops(s, q)]
-        if r == 1:  # the gradient is complete where it is produced: update in the epilogue
-            st.enable_fused_wgrad_update()
+        execs = {}
+        for ws, wq in workers:
+            wr = layout.reps[ws]
+            sync = GradSync(mesh.dp_groups.get(ws), wr,
+                            shard=self.dp_reduce == "shard") if wr > 1 else None
+            ex = PipelineExecutor([stages[ws]], self.pipe, "1f1b", layout.S, [ws], sync)
+            ex.ops = [self.sched.local_ops(ws, wq)]
+            execs[ws] = ex
+            if wr == 1:  # the gradient is complete where it is produced: update in the epilogue
+                stages[ws].enable_fused_wgrad_update()
+        if len(workers) == 1:
+            self.executor = execs[s]
+        else:
+            order = [(ws, op, layout.local_index(ws, j)) for ws, op, j in
+                     self.sched.rank_ops(mesh.rank)]
+            self.executor = _RankSteps(execs, order, self.pipe)
         if native_exec is None:
             native_exec = self.device.type == "cuda"
         self.native_exec = bool(native_exec)
         if self.native_exec:
-            st.compile_native()
+            for st in self.stages:
+                st.compile_native()
         self.native_step = None
         self.native_fallback = None
         self.transport = "rccl" if mesh.backend == "nccl" else mesh.backend
         self.transport_reason = (f"fan layout {layout.describe()}: fan-in / fan-out P2P "
-                                 f"({self.transport}), Python executor")
+                                 f"({self.transport}), Python executor" +
+                                 (", co-located hops as device copies" if len(workers) > 1
+                                  else ""))
         if mesh.backend == "nccl" and self.native_exec and \
                 switches.get("DNN_NATIVE_DIST") != "0":
             # the rank's whole step as one StepPlan call (fan.FanNativeStep, slotted RCCL form);
-            # agreed over the world like the uniform mesh's native step (trainer.py)
+            # agreed over the world like the uniform mesh's native step (trainer.py). A
+            # co-located layout runs the Python executor on every rank.
             from ..parallel.fan import FanNativeStep
 
             _warm_groups(mesh, self.device)
             err = None
             try:
+                if layout.colocated:
+                    raise ValueError("co-located fan layouts run the Python executor")
                 self.native_step = FanNativeStep(self.executor, mesh, self.sched)
             except Exception as e:
                 err = e
@@ -103,13 +162,31 @@ class FanTrainer(Trainer):
         self.graph_nodes = 0
         self.steps_done = 0
 
+    @property
+    def input_micros(self) -> list:
+        """Global micro-batches whose INPUT rows this rank holds (its stage-0 replica's)."""
+        q = next((wq for ws, wq in (self.mesh.workers or [(self.mesh.stage,
+                                                            self.mesh.replica)]) if ws == 0),
+                 None)
+        return [] if q is None else self.layout.local_micros(0, q, self.num_micro)
+
+    @property
+    def label_micros(self) -> list:
+        """Global micro-batches whose LABELS this rank holds (its last-stage replica's)."""
+        S = self.layout.S
+        q = next((wq for ws, wq in (self.mesh.workers or [(self.mesh.stage,
+                                                            self.mesh.replica)])
+                  if ws == S - 1), None)
+        return [] if q is None else self.layout.local_micros(S - 1, q, self.num_micro)
+
     def set_global_batch(self, x: Optional[torch.Tensor], labels: Optional[torch.Tensor]):
         """The GLOBAL batch (all micro-batches); this rank keeps its own micro-batches' rows
-        (first stage: inputs, last stage: labels)."""
-        s, q = self.mesh.stage, self.mesh.replica
-        rows = fan_rows(self.layout, s, q, self.num_micro, self.micro_batch)
-        xs = gather_rows(x, rows) if self.first is not None else None
-        ys = gather_rows(labels, rows) if self.last is not None else None
+        (its first-stage replica: inputs; its last-stage replica: labels)."""
+        mb = self.micro_batch
+        xs = gather_rows(x, [slice(j * mb, (j + 1) * mb) for j in self.input_micros]) \
+            if self.first is not None else None
+        ys = gather_rows(labels, [slice(j * mb, (j + 1) * mb) for j in self.label_micros]) \
+            if self.last is not None else None
         self.set_batch(xs, ys)
 
     def loss(self) -> Optional[float]:

@@ -62,6 +62,16 @@ class Rung:
     args: list = field(default_factory=list)    # extra command-line arguments (appended)
 
 
+def uniform_rungs() -> list[Rung]:
+    """The literal uniform ppS x dpD grid (bench ``--parallelism uniform``), measured after a
+    fan layout's number: its default transport, then the RCCL slotted plan, then the Python
+    executor -- eager, like every fallback rung."""
+    uni = ["--parallelism", "uniform", "--graph", "off"]
+    return [Rung("uniform", {}, uni),
+            Rung("uniform-rccl-slotted", {"DNN_PIPE": "rccl", "DNN_RCCL_PLAN": "slotted"}, uni),
+            Rung("uniform-python", {"DNN_PIPE": "rccl", "DNN_NATIVE_DIST": "0"}, uni)]
+
+
 def bench_rungs(n: int, dp_only: bool = False, fan: bool = False) -> list[Rung]:
     """The training benchmark's ladder for ``n`` ranks. ``dp_only``: the layout is already
     data-parallel (no hops), only the executor can fall back. ``fan``: the default layout is
@@ -373,6 +383,33 @@ class Supervisor:
 
     def seconds_left(self) -> Optional[float]:
         return None if self.deadline is None else self.deadline - time.monotonic()
+
+    def comparisons(self, items: Sequence[tuple[str, Sequence[Rung]]], need_s: float,
+                    on_done: Optional[Callable[[str, dict], None]] = None) -> dict:
+        """Further measurements after the main one (bench.py: the literal uniform pipeline,
+        then data parallelism), each climbing its own rungs -- but only while the deadline
+        leaves room for another attempt of ``need_s`` seconds. Rank 0 decides per item and
+        every rank reads the decision from the store, so all climb (or skip) together.
+        Returns key -> {"result": rank 0's child result or None, "attempts": [...]} or
+        {"skipped": "budget", "seconds_left", "seconds_needed"}; ``on_done(key, entry)`` sees
+        each entry as soon as it exists (the SIGTERM report uses what is known by then)."""
+        out: dict = {}
+        for key, rungs in items:
+            dk = f"compare/{key}/decision"
+            if self.rank == 0:
+                left = self.seconds_left()
+                self.store.set(dk, "run" if left is None or left > need_s else "skip")
+            if self.store.get(dk).decode() == "run":
+                n0 = len(self.attempts)
+                res, _ = self.climb(rungs)
+                out[key] = {"result": res, "attempts": self.attempts[n0:]}
+            else:
+                out[key] = {"skipped": "budget",
+                            "seconds_left": round(self.seconds_left() or 0.0, 1),
+                            "seconds_needed": round(need_s, 1)}
+            if on_done is not None:
+                on_done(key, out[key])
+        return out
 
 
 class OneLine:

@@ -42,12 +42,36 @@ import torch.distributed as dist
 class FanLayout:
     dist: tuple   # layers per stage
     reps: tuple   # GPUs (replicas) per stage
+    # per stage, the ranks of its replicas; None = every stage on ranks of its own, in stage
+    # order. A co-located stage shares ranks with another stage's replicas (VERDICT r5 #3:
+    # the light classifier stage of 784-512-256-128-10 on one of the heavy stage's GPUs
+    # instead of a GPU of its own)
+    place: Optional[tuple] = None
 
     def __post_init__(self):
         if len(self.dist) != len(self.reps) or not self.dist:
             raise ValueError("a fan layout needs one replica count per stage")
         if any(k < 1 for k in self.dist) or any(r < 1 for r in self.reps):
             raise ValueError(f"bad fan layout {self.dist} x {self.reps}")
+        if self.place is None:
+            out, o = [], 0
+            for r in self.reps:
+                out.append(tuple(range(o, o + r)))
+                o += r
+            object.__setattr__(self, "place", tuple(out))
+        else:
+            place = tuple(tuple(int(x) for x in p) for p in self.place)
+            object.__setattr__(self, "place", place)
+            if len(place) != len(self.reps) or any(len(p) != r for p, r in zip(place,
+                                                                               self.reps)):
+                raise ValueError(f"fan placement {place} does not match replicas {self.reps}")
+            if any(list(p) != sorted(set(p)) for p in place):
+                # distinct, and increasing: a replicated stage's DP group rank (its shard of
+                # the sharded optimizer) is the replica index
+                raise ValueError("the replicas of one stage need distinct, increasing ranks")
+            ranks = sorted({x for p in place for x in p})
+            if ranks != list(range(len(ranks))):
+                raise ValueError(f"fan placement {place} must use ranks 0..N-1")
 
     @property
     def S(self) -> int:
@@ -55,27 +79,59 @@ class FanLayout:
 
     @property
     def world(self) -> int:
-        return sum(self.reps)
+        return len({x for p in self.place for x in p})
+
+    @property
+    def colocated(self) -> bool:
+        return sum(self.reps) != self.world
 
     @property
     def offsets(self) -> list[int]:
-        out, o = [], 0
-        for r in self.reps:
-            out.append(o)
-            o += r
-        return out
+        """First rank of every stage (stage-contiguous layouts only)."""
+        if self.colocated:
+            raise ValueError("a co-located fan layout has no per-stage rank offsets")
+        return [p[0] for p in self.place]
 
     def rank_of(self, s: int, q: int) -> int:
-        return self.offsets[s] + q
+        return self.place[s][q]
+
+    def workers_of(self, rank: int) -> list[tuple[int, int]]:
+        """Every (stage, replica) this rank hosts, in stage order."""
+        out = [(s, p.index(rank)) for s, p in enumerate(self.place) if rank in p]
+        if not out:
+            raise ValueError(f"rank {rank} outside a {self.world}-rank fan layout")
+        return out
 
     def stage_of(self, rank: int) -> tuple[int, int]:
-        for s, (o, r) in enumerate(zip(self.offsets, self.reps)):
-            if o <= rank < o + r:
-                return s, rank - o
-        raise ValueError(f"rank {rank} outside a {self.world}-rank fan layout")
+        """The (stage, replica) of a rank hosting ONE worker; the first one it hosts else."""
+        return self.workers_of(rank)[0]
+
+    def boundary_ranks(self, b: int) -> list[int]:
+        """The ranks of the boundary group between stages b and b+1 (group rank = index)."""
+        return sorted(set(self.place[b]) | set(self.place[b + 1]))
 
     def replica_of(self, s: int, j: int) -> int:
         return j % self.reps[s]
+
+    def check_directions(self, M: int) -> None:
+        """Every boundary communicator carries, per rank and direction, remote hops one way
+        only (a rank sends or receives on it, not both): RCCL runs a communicator's
+        point-to-point operations in posting order on one stream, and a rank that had posted
+        a receive ahead of a send on the same communicator could wait on a peer that waits on
+        that send. Stage-contiguous layouts satisfy this trivially; co-location does when the
+        co-located stage has one replica on a rank of the stage before it."""
+        for b in range(self.S - 1):
+            snd, rcv = set(), set()
+            for j in range(M):
+                src = self.rank_of(b, self.replica_of(b, j))
+                dst = self.rank_of(b + 1, self.replica_of(b + 1, j))
+                if src != dst:
+                    snd.add(src)
+                    rcv.add(dst)
+            both = snd & rcv
+            if both:
+                raise ValueError(f"fan placement {self.place}: ranks {sorted(both)} both send "
+                                 f"and receive remote hops across boundary {b}")
 
     def local_micros(self, s: int, q: int, M: int) -> list[int]:
         return list(range(q, M, self.reps[s]))
@@ -84,27 +140,73 @@ class FanLayout:
         return j // self.reps[s]
 
     def describe(self) -> str:
-        return "fan" + "-".join(f"{k}L{'x' + str(r) if r > 1 else ''}"
-                                for k, r in zip(self.dist, self.reps))
+        out = []
+        for s, (k, r) in enumerate(zip(self.dist, self.reps)):
+            t = f"{k}L{'x' + str(r) if r > 1 else ''}"
+            if self.colocated and set(self.place[s]) & {x for p in self.place[:s] for x in p}:
+                t += "@" + "+".join(str(x) for x in self.place[s])
+            out.append(t)
+        return "fan" + "-".join(out)
+
+    def spec_text(self) -> str:
+        """The --parallelism text of this layout ('fan:3x4,1x1@3')."""
+        parts = []
+        for s, (k, r) in enumerate(zip(self.dist, self.reps)):
+            t = f"{k}x{r}"
+            if self.colocated and set(self.place[s]) & {x for p in self.place[:s] for x in p}:
+                t += "@" + "+".join(str(x) for x in self.place[s])
+            parts.append(t)
+        return "fan:" + ",".join(parts)
 
 
-def parse_fan(text: str) -> Optional[tuple[list[int], list[int]]]:
-    """'fan:3,1' -> (None, [3, 1]) (reps; the planner picks the split); 'fan:1x1,2x7' ->
-    ([1, 2], [1, 7]) (layers x replicas per stage); anything else -> None."""
+def colocated_place(reps: Sequence[int], co: Sequence[bool]) -> tuple:
+    """Placement with stage s (co[s]) sharing the LAST reps[s] ranks of stage s-1 (the light
+    stage beside the heavy stage's last replicas); other stages get ranks of their own."""
+    place, nxt = [], 0
+    for s, r in enumerate(reps):
+        if co[s]:
+            if s == 0 or r > len(place[s - 1]):
+                raise ValueError(f"stage {s} cannot share {r} ranks of stage {s - 1}")
+            place.append(tuple(place[s - 1][-r:]))
+        else:
+            place.append(tuple(range(nxt, nxt + r)))
+            nxt += r
+    return tuple(place)
+
+
+def parse_fan(text: str) -> Optional[tuple]:
+    """'fan:3,1' -> (None, [3, 1], None) (reps; the planner picks the split); 'fan:1x1,2x7' ->
+    ([1, 2], [1, 7], None) (layers x replicas per stage); 'fan:3x4,1x1@3' -> ([3, 1], [4, 1],
+    placement): '@r+r+...' puts a stage's replicas on ranks of the stages before it
+    (co-location); anything else -> None."""
     if not text.startswith("fan"):
         return None
     body = text[3:].lstrip(":")
     if not body:
-        return [], []
-    dist_, reps = [], []
+        return [], [], None
+    dist_, reps, at = [], [], []
     for part in body.split(","):
+        part, _, ranks = part.partition("@")
         if "x" in part:
             k, r = part.split("x")
             dist_.append(int(k))
             reps.append(int(r))
         else:
             reps.append(int(part))
-    return (dist_ if len(dist_) == len(reps) else None), reps
+        at.append(tuple(int(x) for x in ranks.split("+")) if ranks else None)
+    place = None
+    if any(a is not None for a in at):
+        place, nxt = [], 0
+        for r, a in zip(reps, at):
+            if a is None:
+                place.append(tuple(range(nxt, nxt + r)))
+                nxt += r
+            else:
+                if len(a) != r:
+                    raise ValueError(f"{text}: a stage of {r} replicas lists {len(a)} ranks")
+                place.append(a)
+        place = tuple(place)
+    return (dist_ if len(dist_) == len(reps) else None), reps, place
 
 
 @dataclass
@@ -122,6 +224,13 @@ class FanSchedule:
         loc = self.layout.local_index
         return [(op, loc(s, j)) for op, j in self.ops[(s, q)]] + [("W", -1), ("O", -1)]
 
+    def rank_ops(self, rank: int) -> list[tuple[int, str, int]]:
+        """Every compute op of the workers a rank hosts, as (stage, op, global j), in the
+        rank's execution order (simulated start order: co-located workers share the GPU's
+        one compute stream)."""
+        out = [(s, o, j) for s, q in self.layout.workers_of(rank) for o, j in self.ops[(s, q)]]
+        return sorted(out, key=lambda k: (self.start[k], k[0]))
+
     def send_order(self, s: int, q: int, direction: str, peer: int) -> list[int]:
         """Global micro-batches worker (s, q) sends in ``direction`` ('f' to stage s+1, 'b'
         to stage s-1) to replica ``peer`` of that stage, in send order (= its F / B order)."""
@@ -135,24 +244,33 @@ def fan_schedule(layout: FanLayout, M: int, f_cost: Optional[Sequence[float]] = 
                  b_cost: Optional[Sequence[float]] = None, hop: float = 0.0) -> FanSchedule:
     """Deterministic list scheduling of one step (see the module docstring). ``f_cost`` /
     ``b_cost``: per-stage time of one micro-batch's forward / backward (default 1 / 2);
-    ``hop``: time between a producer's end and the consumer's data (>= 0)."""
+    ``hop``: time between a producer's end and the consumer's data (>= 0) when they are on
+    different ranks (a co-located hop is a device copy: 0). The workers a rank hosts share
+    its GPU: one op at a time per rank."""
     S = layout.S
     f = list(f_cost) if f_cost is not None else [1.0] * S
     b = list(b_cost) if b_cost is not None else [2.0] * S
     if M < max(layout.reps):
         raise ValueError(f"{M} micro-batches cannot feed {max(layout.reps)} replicas")
+    rank = {(s, q): layout.rank_of(s, q) for s in range(S) for q in range(layout.reps[s])}
+
+    def hop_between(s0, s1, j):
+        return 0.0 if rank[(s0, layout.replica_of(s0, j))] == \
+            rank[(s1, layout.replica_of(s1, j))] else hop
+
     ready: dict = {}        # (s, op, j) -> time its inputs are available
     for j in range(M):
         ready[(0, "F", j)] = 0.0
-    free = {(s, q): 0.0 for s in range(S) for q in range(layout.reps[s])}
-    ops = {w: [] for w in free}
+    free = {r: 0.0 for r in set(rank.values())}
+    ops = {w: [] for w in rank}
     start, end = {}, {}
     done = 0
     total = 2 * S * M
     # event loop: repeatedly pick the worker that can start something earliest
     while done < total:
         best = None
-        for (s, q), tfree in free.items():
+        for (s, q), rk in rank.items():
+            tfree = free[rk]
             # candidates of this worker: its micro-batches whose inputs are ready
             cand = None
             for j in range(q, M, layout.reps[s]):
@@ -177,17 +295,18 @@ def fan_schedule(layout: FanLayout, M: int, f_cost: Optional[Sequence[float]] = 
         (t0, _, _), s, q, op, j = best
         dur = f[s] if op == "F" else b[s]
         start[(s, op, j)], end[(s, op, j)] = t0, t0 + dur
-        free[(s, q)] = t0 + dur
+        free[rank[(s, q)]] = t0 + dur
         ops[(s, q)].append((op, j))
         done += 1
         if op == "F":
             if s + 1 < S:
-                ready[(s + 1, "F", j)] = t0 + dur + hop
+                ready[(s + 1, "F", j)] = t0 + dur + hop_between(s, s + 1, j)
             else:
                 ready[(s, "B", j)] = t0 + dur  # the loss gradient: same worker
         else:
             if s > 0:
-                ready[(s - 1, "B", j)] = max(t0 + dur + hop, end.get((s - 1, "F", j), 0.0))
+                ready[(s - 1, "B", j)] = max(t0 + dur + hop_between(s, s - 1, j),
+                                             end.get((s - 1, "F", j), 0.0))
     sch = FanSchedule(layout, M, ops, start, end, max(end.values()))
     check_schedule(sch)
     return sch
@@ -217,6 +336,12 @@ def check_schedule(sch: FanSchedule) -> None:
         for d in deps:
             if sch.end[d] > t + 1e-12:
                 raise AssertionError(f"{(s, o, j)} starts before its dependency {d} ends")
+    for rank in range(lay.world):  # co-located workers never overlap on their one GPU
+        prev = None
+        for k in sch.rank_ops(rank):
+            if prev is not None and sch.start[k] < sch.end[prev] - 1e-12:
+                raise AssertionError(f"rank {rank}: {k} overlaps {prev}")
+            prev = k
 
 
 # ---- process groups -----------------------------------------------------------------------
@@ -226,21 +351,47 @@ class FanMesh:
     in the same order, as torch requires):
 
     * per boundary b (stage b -> b+1), a forward and a backward group over the ranks of both
-      stages: a rank's hops in one direction stay on one communicator, FIFO per rank pair;
+      stages (``FanLayout.boundary_ranks``): a rank's hops in one direction stay on one
+      communicator, FIFO per rank pair;
     * per stage with r_s > 1, the data-parallel group of its replicas.
-    """
+
+    A rank may host several workers (co-location); ``stage`` / ``replica`` are its first one
+    (the only one without co-location) and ``fwd_in`` ... ``dp_group`` that worker's groups."""
     layout: FanLayout
     rank: int
     stage: int
     replica: int
     backend: str = "gloo"
-    fwd_in: Optional[object] = None    # boundary stage-1 -> stage (receive forward)
-    fwd_out: Optional[object] = None   # boundary stage -> stage+1
-    bwd_in: Optional[object] = None    # gradients from stage+1
-    bwd_out: Optional[object] = None   # gradients to stage-1
-    dp_group: Optional[object] = None
-    dp_ranks: list = field(default_factory=list)
+    workers: list = field(default_factory=list)      # [(stage, replica)] hosted here
+    bnd_f: dict = field(default_factory=dict)        # boundary -> forward group
+    bnd_b: dict = field(default_factory=dict)        # boundary -> backward group
+    dp_groups: dict = field(default_factory=dict)    # stage -> DP group (r_s > 1)
     member_groups: list = field(default_factory=list)
+
+    @property
+    def fwd_in(self):
+        return self.bnd_f.get(self.stage - 1)
+
+    @property
+    def fwd_out(self):
+        return self.bnd_f.get(self.stage)
+
+    @property
+    def bwd_in(self):
+        return self.bnd_b.get(self.stage)
+
+    @property
+    def bwd_out(self):
+        return self.bnd_b.get(self.stage - 1)
+
+    @property
+    def dp_group(self):
+        return self.dp_groups.get(self.stage)
+
+    @property
+    def dp_ranks(self) -> list:
+        return list(self.layout.place[self.stage])
+
     # the Mesh interface the trainer reads
     @property
     def pp(self) -> int:
@@ -262,31 +413,34 @@ class FanMesh:
     def next_rank(self):
         return None if self.stage + 1 == self.layout.S else -1
 
+    def replica_at(self, s: int) -> int:
+        """The replica of stage ``s`` this rank hosts."""
+        for ws, wq in self.workers:
+            if ws == s:
+                return wq
+        raise ValueError(f"rank {self.rank} hosts no replica of stage {s}")
+
 
 def build_fan_mesh(layout: FanLayout) -> FanMesh:
     rank, world = dist.get_rank(), dist.get_world_size()
     if layout.world != world:
         raise ValueError(f"fan layout {layout.reps} needs {layout.world} ranks, world is {world}")
-    s, q = layout.stage_of(rank)
-    m = FanMesh(layout, rank, s, q, backend=dist.get_backend())
-    offs = layout.offsets
+    workers = layout.workers_of(rank)
+    s, q = workers[0]
+    m = FanMesh(layout, rank, s, q, backend=dist.get_backend(), workers=workers)
     for bnd in range(layout.S - 1):
-        ranks = list(range(offs[bnd], offs[bnd + 1] + layout.reps[bnd + 1]))
+        ranks = layout.boundary_ranks(bnd)
         gf = dist.new_group(ranks)
         gb = dist.new_group(ranks)
-        if s == bnd:
-            m.fwd_out, m.bwd_in = gf, gb
-        if s == bnd + 1:
-            m.fwd_in, m.bwd_out = gf, gb
         if rank in ranks:
+            m.bnd_f[bnd], m.bnd_b[bnd] = gf, gb
             m.member_groups += [gf, gb]
     for st in range(layout.S):
-        ranks = list(range(offs[st], offs[st] + layout.reps[st]))
+        ranks = list(layout.place[st])
         g = dist.new_group(ranks) if len(ranks) > 1 else None
-        if st == s:
-            m.dp_group, m.dp_ranks = g, ranks
-            if g is not None:
-                m.member_groups.append(g)
+        if rank in ranks and g is not None:
+            m.dp_groups[st] = g
+            m.member_groups.append(g)
     return m
 
 
@@ -294,22 +448,34 @@ def build_fan_mesh(layout: FanLayout) -> FanMesh:
 class FanPipe:
     """P2P hops of a fan layout through ``torch.distributed`` (gloo on CPU, RCCL on GPUs; GPU
     tensors over gloo are staged through host memory, as in DistPipe). Every receive of a step
-    is posted at step start, per peer in that peer's send order (FanSchedule.send_order), so
-    the FIFO matching of each rank pair delivers micro-batch j into j's rows."""
+    is posted at step start, per hosted worker in its consumption order, so the FIFO matching
+    of each rank pair delivers micro-batch j into j's rows. A hop between two workers of THIS
+    rank (co-location) is a device copy into the consumer's rows when the producer's op runs
+    (the rank executes its workers' ops in schedule order, so it precedes the consumer's).
 
-    def __init__(self, mesh: FanMesh, stage, sched: FanSchedule, staged: Optional[bool] = None):
-        self.mesh, self.stage, self.sched = mesh, stage, sched
+    ``stages``: the Stage object of every hosted worker, keyed by stage index (one Stage
+    alone: the rank's only worker)."""
+
+    def __init__(self, mesh: FanMesh, stages, sched: FanSchedule,
+                 staged: Optional[bool] = None):
+        self.mesh, self.sched = mesh, sched
         self.lay = mesh.layout
-        self.staged = staged if staged is not None else (stage.device.type == "cuda" and
+        if not isinstance(stages, dict):
+            stages = {mesh.stage: stages}
+        self.stages = stages
+        self.stage = stages[mesh.stage]
+        dev = next(iter(stages.values())).device
+        self.staged = staged if staged is not None else (dev.type == "cuda" and
                                                          mesh.backend == "gloo")
-        self.local = self.lay.local_micros(mesh.stage, mesh.replica, sched.M)
+        self.q = {s: mesh.replica_at(s) for s in stages}
+        self.local = {s: self.lay.local_micros(s, q, sched.M) for s, q in self.q.items()}
         self._recv_f: dict = {}
         self._recv_b: dict = {}
         self._sends: list = []
         self._host: dict = {}
 
-    def _g(self, j_local: int) -> int:
-        return self.local[j_local]
+    def _g(self, s: int, j_local: int) -> int:
+        return self.local[s][j_local]
 
     def _buf(self, key, t):
         b = self._host.get(key)
@@ -338,54 +504,76 @@ class FanPipe:
         else:
             self._sends.append(dist.isend(t, dst=dst, group=group))
 
+    def _local(self, s: int, j: int) -> bool:
+        return self.lay.rank_of(s, self.lay.replica_of(s, j)) == self.mesh.rank
+
     def begin_step(self):
-        """Post every receive of the step in THIS rank's consumption order (its F / B op
-        order), not grouped per peer: RCCL runs a rank's point-to-point operations in posting
-        order on one stream, so a receive from replica 1 posted behind all of replica 0's
-        could wait for data replica 0 sends only after it got our gradient.
-        Restricted to one peer the order must still be that peer's send order, for the FIFO
-        matching of each rank pair -- checked here."""
-        m, st, lay, sch = self.mesh, self.stage, self.lay, self.sched
-        s, q = m.stage, m.replica
-        mine = sch.ops[(s, q)]
-        for op, t, direction, grp, key, buf in (
-                ("F", s - 1, "f", m.fwd_in, "rf", st.x_in),
-                ("B", s + 1, "b", m.bwd_in, "rb", getattr(st, "grad_out", None))):
-            if not 0 <= t < lay.S:
-                continue
-            order = [j for o, j in mine if o == op]
-            for p in range(lay.reps[t]):
-                sent = sch.send_order(t, p, direction, q)
-                if [j for j in order if lay.replica_of(t, j) == p] != sent:
-                    raise RuntimeError(f"fan schedule: rank {m.rank} consumes the {op} hops "
-                                       f"from replica {p} out of that replica's send order")
-            recs = self._recv_f if op == "F" else self._recv_b
-            for j in order:
-                jj = lay.local_index(s, j)
-                recs[jj] = self._irecv(buf[st.rows_of(jj)],
-                                       lay.rank_of(t, lay.replica_of(t, j)), grp, (key, jj))
+        """Post every remote receive of the step in each hosted worker's consumption order
+        (its F / B op order), not grouped per peer: RCCL runs a rank's point-to-point
+        operations in posting order on one stream, so a receive from replica 1 posted behind
+        all of replica 0's could wait for data replica 0 sends only after it got our gradient
+        (ADVICE r5). Restricted to one peer the order must still be that peer's send order,
+        for the FIFO matching of each rank pair -- checked here."""
+        m, lay, sch = self.mesh, self.lay, self.sched
+        for s, st in self.stages.items():
+            q = self.q[s]
+            mine = sch.ops[(s, q)]
+            for op, t, direction, grp, key, buf in (
+                    ("F", s - 1, "f", m.bnd_f.get(s - 1), "rf", st.x_in),
+                    ("B", s + 1, "b", m.bnd_b.get(s), "rb", getattr(st, "grad_out", None))):
+                if not 0 <= t < lay.S:
+                    continue
+                order = [j for o, j in mine if o == op and not self._local(t, j)]
+                for p in range(lay.reps[t]):
+                    if lay.rank_of(t, p) == m.rank:
+                        continue
+                    sent = sch.send_order(t, p, direction, q)
+                    if [j for j in order if lay.replica_of(t, j) == p] != sent:
+                        raise RuntimeError(f"fan schedule: rank {m.rank} consumes the {op} "
+                                           f"hops from replica {p} of stage {t} out of that "
+                                           "replica's send order")
+                recs = self._recv_f if op == "F" else self._recv_b
+                for j in order:
+                    jj = lay.local_index(s, j)
+                    recs[(s, jj)] = self._irecv(buf[st.rows_of(jj)],
+                                                lay.rank_of(t, lay.replica_of(t, j)), grp,
+                                                (key, s, jj))
 
     def recv_fwd(self, stage, jj):
-        if self.mesh.stage > 0:
-            self._finish(self._recv_f.pop(jj))
+        s = stage.stage_index
+        if s > 0 and (s, jj) in self._recv_f:
+            self._finish(self._recv_f.pop((s, jj)))
 
     def send_fwd(self, stage, jj):
         m, lay = self.mesh, self.lay
-        if m.stage + 1 < lay.S:
-            j = self._g(jj)
-            dst = lay.rank_of(m.stage + 1, lay.replica_of(m.stage + 1, j))
-            self._isend(stage.output[stage.rows_of(jj)], dst, m.fwd_out, ("sf", jj))
+        s = stage.stage_index
+        if s + 1 < lay.S:
+            j = self._g(s, jj)
+            rows = stage.output[stage.rows_of(jj)]
+            if self._local(s + 1, j):  # co-located consumer: straight into its rows
+                nxt = self.stages[s + 1]
+                nxt.x_in[nxt.rows_of(lay.local_index(s + 1, j))].copy_(rows)
+                return
+            dst = lay.rank_of(s + 1, lay.replica_of(s + 1, j))
+            self._isend(rows, dst, m.bnd_f[s], ("sf", s, jj))
 
     def recv_bwd(self, stage, jj):
-        if self.mesh.stage + 1 < self.lay.S:
-            self._finish(self._recv_b.pop(jj))
+        s = stage.stage_index
+        if s + 1 < self.lay.S and (s, jj) in self._recv_b:
+            self._finish(self._recv_b.pop((s, jj)))
 
     def send_bwd(self, stage, jj):
         m, lay = self.mesh, self.lay
-        if m.stage > 0:
-            j = self._g(jj)
-            dst = lay.rank_of(m.stage - 1, lay.replica_of(m.stage - 1, j))
-            self._isend(stage.dx_send[stage.rows_of(jj)], dst, m.bwd_out, ("sb", jj))
+        s = stage.stage_index
+        if s > 0:
+            j = self._g(s, jj)
+            rows = stage.dx_send[stage.rows_of(jj)]
+            if self._local(s - 1, j):
+                prv = self.stages[s - 1]
+                prv.grad_out[prv.rows_of(lay.local_index(s - 1, j))].copy_(rows)
+                return
+            dst = lay.rank_of(s - 1, lay.replica_of(s - 1, j))
+            self._isend(rows, dst, m.bnd_b[s - 1], ("sb", s, jj))
 
     def end_step(self):
         for w in self._sends:
@@ -487,8 +675,9 @@ def _fan_native_step_class():
 
         def __init__(self, executor, mesh: FanMesh, sched: FanSchedule,
                      comms: Optional[dict] = None, build_only: bool = False):
-            if len(executor.stages) != 1:
-                raise ValueError("native fan step: one stage per rank")
+            if len(executor.stages) != 1 or mesh.layout.colocated:
+                raise ValueError("native fan step: one stage per rank (a co-located layout "
+                                 "runs the Python executor)")
             st = executor.stages[0]
             if st._prog is None or not st._has_w or not st._o_native:
                 raise ValueError("native fan step needs a recorded stage (compile_native)")

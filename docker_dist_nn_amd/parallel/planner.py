@@ -43,9 +43,20 @@ class Plan:
     samples_per_s: float
     detail: dict = field(default_factory=dict)
     reps: Optional[list] = None  # fan layout: GPUs per stage (parallel/fan.py)
+    place: Optional[tuple] = None  # fan layout with co-located stages: ranks per stage
+
+    @property
+    def colocated(self) -> bool:
+        return self.place is not None and sum(self.reps) != len({x for p in self.place
+                                                                  for x in p})
 
     @property
     def parallelism(self) -> str:
+        if self.colocated:
+            from .fan import FanLayout
+
+            lay = FanLayout(tuple(self.distribution), tuple(self.reps), self.place)
+            return "fan" + lay.spec_text()[4:]
         if self.reps is not None and len(set(self.reps)) > 1:
             return "fan" + ",".join(f"{k}x{r}" for k, r in zip(self.distribution, self.reps))
         if self.reps is not None:  # equal replica counts: the uniform grid
@@ -73,13 +84,91 @@ def compositions(n: int, k: int):
         yield [b[i + 1] - b[i] for i in range(k)]
 
 
-# Measured one-GPU training steps on MI355X with the round-2 own-kernel table
-# (profiles/r2_own_kernels, profiles/r2_epilogue): widths -> (rows, ms per step).
-MEASURED_STEP_MS = {  # round 3: driver BENCH_r03 (headline), profiles/r3b_final4 (others)
-    (784, 512, 256, 128, 10): (65536, 0.350),
-    (784, 1024, 1024, 1024, 1024, 1024, 1024, 1024, 10): (65536, 2.88),
-    (784, 8192, 8192, 10): (16384, 5.96),
+# Measured one-GPU training steps on MI355X (one micro-batch, the single-stage overlap plan):
+# widths -> (rows, ms per step). Headline: the driver's BENCH_r05 (0.3286 ms); mlp8 / wide:
+# the round-5 end-of-round A/B medians (profiles/r5_tables), re-checked in round 6.
+MEASURED_STEP_MS = {
+    (784, 512, 256, 128, 10): (65536, 0.3286),
+    (784, 1024, 1024, 1024, 1024, 1024, 1024, 1024, 10): (65536, 2.68),
+    (784, 8192, 8192, 10): (16384, 5.33),
 }
+
+
+class StageTimes:
+    """Measured compute of one pipeline-stage replica per step (bench/planner_calibrate.py,
+    ``stage_times_gfx950.json``): layers [a, b) of a model, n micro-batches of
+    mb rows through the recorded forward / backward segments, then the batched weight
+    gradient and the fused update.
+
+    Per (a, b, mb) the measured n are fit as t = fixed + n * per_micro (least squares: the
+    weight gradient and update scale with the rows, so ``fixed`` absorbs only what does not);
+    between measured micro-batch sizes both terms are interpolated linearly, outside them
+    extrapolated at the nearest size's per-row rate. A range that was not measured (mlp8's
+    middle ranges) is the sum of its single layers."""
+
+    def __init__(self, rows):
+        self.fit: dict = {}  # (widths, a, b) -> sorted [(mb, fixed_s, per_micro_s)]
+        pts: dict = {}
+        for widths, a, b, mb, n, ms in rows:
+            pts.setdefault((tuple(widths), a, b, mb), []).append((n, ms * 1e-3))
+        for (w, a, b, mb), v in pts.items():
+            if len(v) == 1:
+                n, t = v[0]
+                fixed, per = 0.0, t / n
+            else:
+                k = len(v)
+                sx = sum(n for n, _ in v)
+                sy = sum(t for _, t in v)
+                sxx = sum(n * n for n, _ in v)
+                sxy = sum(n * t for n, t in v)
+                per = (k * sxy - sx * sy) / (k * sxx - sx * sx)
+                fixed = max(0.0, (sy - per * sx) / k)
+            self.fit.setdefault((w, a, b), []).append((mb, fixed, per))
+        for v in self.fit.values():
+            v.sort()
+
+    @classmethod
+    def load(cls, path: Optional[str] = None) -> "StageTimes":
+        import json
+        import os
+
+        path = path or os.path.join(os.path.dirname(__file__), "stage_times_gfx950.json")
+        with open(path) as f:
+            return cls(json.load(f)["rows"])
+
+    def has(self, widths) -> bool:
+        w = tuple(widths)
+        return any(k[0] == w for k in self.fit)
+
+    def _terms(self, w, a, b, mb):
+        v = self.fit.get((w, a, b))
+        if v is None:
+            if b - a <= 1:
+                return None
+            parts = [self._terms(w, i, i + 1, mb) for i in range(a, b)]
+            if any(p is None for p in parts):
+                return None
+            return sum(p[0] for p in parts), sum(p[1] for p in parts)
+        if mb <= v[0][0]:
+            m0, f0, p0 = v[0]
+            return f0, p0 * mb / m0 if mb < m0 else p0
+        if mb >= v[-1][0]:
+            m1, f1, p1 = v[-1]
+            return f1, p1 * mb / m1
+        for (m0, f0, p0), (m1, f1, p1) in zip(v, v[1:]):
+            if m0 <= mb <= m1:
+                x = (mb - m0) / (m1 - m0)
+                return f0 + x * (f1 - f0), p0 + x * (p1 - p0)
+        return None
+
+    def step(self, widths, a: int, b: int, mb: int, n: int) -> Optional[float]:
+        """Seconds of one replica step of layers [a, b): n micro-batches of mb rows."""
+        t = self._terms(tuple(widths), a, b, mb)
+        return None if t is None else t[0] + n * t[1]
+
+    def per_micro(self, widths, a: int, b: int, mb: int) -> Optional[float]:
+        t = self._terms(tuple(widths), a, b, mb)
+        return None if t is None else t[1]
 
 
 class Planner:
@@ -89,7 +178,14 @@ class Planner:
     def __init__(self, tflops: float = 550.0, link_gbps: float = 64.0,
                  hop_latency_us: float = 15.0, allreduce_gbps: float = 150.0,
                  step_overhead_us: float = 20.0, boundary_bytes: float = 2.0,
-                 dp_grad_bytes: float = 2.0, relays=0, relay_eff: float = 0.8):
+                 dp_grad_bytes: float = 2.0, relays=0, relay_eff: float = 0.8,
+                 stage_times: Optional[StageTimes] = None,
+                 one_gpu_step: Optional[tuple] = None):
+        # stage_times: measured replica steps (calibrated planners); one_gpu_step: (rows, s)
+        # of the model's own single-stage one-micro-batch step (MEASURED_STEP_MS)
+        self.times = stage_times
+        self.one_step = one_gpu_step
+        self._memo: dict = {}
         self.rate = tflops * 1e12
         self.link = link_gbps * 1e9
         self.lat = hop_latency_us * 1e-6
@@ -109,13 +205,59 @@ class Planner:
 
     @classmethod
     def calibrated(cls, spec: MLPSpec, **kw) -> "Planner":
-        """A planner whose compute rate is this model's MEASURED one-GPU step rate (executed
-        FLOPs / step time), when one is on record; else the default rate."""
+        """A planner on this model's MEASURED one-GPU numbers: the single-stage step
+        (MEASURED_STEP_MS: the compute rate, and the data-parallel replica's step) and the
+        replica steps of every layer range at every micro-batch size and count
+        (stage_times_gfx950.json, round 6). Without measurements: the default FLOP rate."""
         m = MEASURED_STEP_MS.get(tuple(spec.widths))
         if m is not None and "tflops" not in kw:
             rows, ms = m
             kw["tflops"] = sum(layer_train_flops(spec)) * rows / (ms * 1e-3) / 1e12
+            kw.setdefault("one_gpu_step", (rows, ms * 1e-3))
+        if "stage_times" not in kw:
+            try:
+                t = StageTimes.load()
+                if t.has(spec.widths):
+                    kw["stage_times"] = t
+            except OSError:
+                pass
         return cls(**kw)
+
+    def replica_step(self, spec: MLPSpec, a: int, b: int, mb: int, n: int) -> float:
+        key = ("r", tuple(spec.widths), a, b, mb, n)
+        v = self._memo.get(key)
+        if v is None:
+            v = self._memo[key] = self._replica_step(spec, a, b, mb, n)
+        return v
+
+    def _replica_step(self, spec: MLPSpec, a: int, b: int, mb: int, n: int) -> float:
+        """Compute seconds of one replica of layers [a, b) per step: n micro-batches of mb
+        rows, batched weight gradient, update -- measured (StageTimes) when available, the
+        FLOP rate otherwise; the model's own one-micro-batch step when that is the case."""
+        L = len(spec.layers)
+        if (a, b) == (0, L) and n == 1 and self.one_step is not None and \
+                mb == self.one_step[0]:
+            return self.one_step[1]
+        if self.times is not None:
+            t = self.times.step(spec.widths, a, b, mb, n)
+            if t is not None:
+                return t
+        return sum(layer_train_flops(spec)[a:b]) * mb * n / self.rate
+
+    def micro_time(self, spec: MLPSpec, a: int, b: int, mb: int) -> float:
+        """Seconds one micro-batch of mb rows spends in layers [a, b) (forward + backward)."""
+        key = ("m", tuple(spec.widths), a, b, mb)
+        v = self._memo.get(key)
+        if v is None:
+            v = self._memo[key] = self._micro_time(spec, a, b, mb)
+        return v
+
+    def _micro_time(self, spec: MLPSpec, a: int, b: int, mb: int) -> float:
+        if self.times is not None:
+            t = self.times.per_micro(spec.widths, a, b, mb)
+            if t is not None:
+                return t
+        return sum(layer_train_flops(spec)[a:b]) * mb / self.rate
 
     def hop_ratios(self, spec: MLPSpec, dist: list[int], dp: int = 1,
                    rows: int = 65536) -> list[float]:
@@ -147,11 +289,10 @@ class Planner:
         return out
 
     def _stage_costs(self, spec: MLPSpec, dist: list[int], mb: int, dp: int = 1):
-        fl = layer_train_flops(spec)
         ratios = self.hop_ratios(spec, dist, dp, mb)
         comp, hops, g = [], [], 0
         for k in dist:
-            comp.append(sum(fl[g:g + k]) * mb / self.rate)
+            comp.append(self.micro_time(spec, g, g + k, mb))
             g += k
             if g < len(spec.layers):
                 hops.append(self.lat + mb * spec.layers[g - 1].out_dim * self.bb *
@@ -187,14 +328,23 @@ class Planner:
                                 else [len(L)])
         comp, hops = self._stage_costs(spec, dist, mb, dp)
         per_micro = max(comp + hops)
-        pipe = (M + pp - 1) * per_micro if pp > 1 else comp[0]
+        if pp > 1:
+            # the slowest stage's measured fixed part (batched wgrad + update beyond the
+            # per-micro-batch rate) ends the step after the pipeline drains
+            g, fixed = 0, 0.0
+            for k, c in zip(dist, comp):
+                fixed = max(fixed, self.replica_step(spec, g, g + k, mb, M) - M * c)
+                g += k
+            pipe = (M + pp - 1) * per_micro + fixed
+        else:
+            pipe = self.replica_step(spec, 0, len(L), mb, M)
         ar, g = 0.0, 0
         for k in dist:
             params = sum(l.params for l in L[g:g + k])
             g += k
             if dp > 1:
                 ar = max(ar, 2 * (dp - 1) / dp * params * self.gb / self.ar)
-        t = pipe + 0.5 * ar + self.ovh
+        t = pipe + 0.5 * ar + (0.0 if self.one_step is not None and pp == 1 else self.ovh)
         detail = {"stage_ms_per_micro": [round(c * 1e3, 4) for c in comp],
                   "hop_ms_per_micro": [round(h * 1e3, 4) for h in hops],
                   "bubble": round((pp - 1) / (M + pp - 1), 3) if pp > 1 else 0.0,
@@ -215,22 +365,28 @@ class Planner:
 
     # ---- replicated-stage ("fan") pipelines (parallel/fan.py) -----------------------------
     def evaluate_fan(self, spec: MLPSpec, dist: list[int], reps: list[int], rows_per_gpu: int,
-                     num_micro: Optional[int] = None) -> Plan:
+                     num_micro: Optional[int] = None, place: Optional[tuple] = None) -> Plan:
         """Predicted step of a fan layout: stage s (layers dist[s]) on reps[s] GPUs, micro-batch
-        j on replica j % r_s of every stage (parallel/fan.py).
+        j on replica j % r_s of every stage (parallel/fan.py); ``place`` co-locates stages
+        (FanLayout.place: a GPU hosting a replica of two stages runs both).
 
-        * compute: a replica of stage s runs ceil(M / r_s) micro-batches of ``c_s`` each;
-        * hops: the pair (producer p, consumer c) of boundary b carries the micro-batches with
-          j % r_b == p and j % r_{b+1} == c over its own direct xGMI link (every GPU pair of an
-          MI355X node has one), forward and backward on the two directions; the slowest pair
-          bounds the boundary (``link_gbps`` per direction, ``hop_latency_us`` per message);
+        * compute: every GPU runs the replica steps of the workers it hosts -- n micro-batches
+          of mb rows through the stage's layers, its batched weight gradient and update,
+          MEASURED at that micro-batch size and count (StageTimes) when calibrated;
+        * hops: micro-batch j crosses boundary b from the GPU of replica j % r_b to the GPU of
+          replica j % r_{b+1} (nothing when that is the same GPU: co-location), forward on one
+          direction of their direct xGMI link and its gradient back on the other; each
+          direction of each GPU pair carries its messages serially (``link_gbps``,
+          ``hop_latency_us`` per message) and the busiest one bounds the step with the busiest
+          GPU;
         * the pipeline fills and drains once per step: one micro-batch's trip through every
           other stage and hop;
         * a replicated stage exchanges its gradient over its own DP group of r_s GPUs (half
           hidden behind the weight gradients, as ``evaluate``)."""
-        from .fan import lcm_reps
+        from .fan import FanLayout, lcm_reps
 
-        S, N = len(reps), sum(reps)
+        lay = FanLayout(tuple(dist), tuple(reps), place)
+        S, N = len(reps), lay.world
         L = spec.layers
         G = rows_per_gpu * N
         if num_micro is None:  # ~8 micro-batches per GPU: GEMMs of >= 8192 rows at 65536
@@ -241,52 +397,104 @@ class Planner:
                     num_micro = max(reps)
                     break
         M = num_micro
+        lay.check_directions(M)
         mb = G // M
-        fl = layer_train_flops(spec)
-        comp, g = [], 0
+        bounds, g = [], 0
         for k in dist:
-            comp.append(sum(fl[g:g + k]) * mb / self.rate)
+            bounds.append((g, g + k))
             g += k
-        busy = [math.ceil(M / r) * c for r, c in zip(reps, comp)]
-        hops, g = [], 0
-        for b in range(S - 1):
-            g += dist[b]
-            width = L[g - 1].out_dim
+        comp = [self.micro_time(spec, a, b, mb) for a, b in bounds]
+        busy: dict = {}
+        for s_, (a, b) in enumerate(bounds):
+            for q in range(reps[s_]):
+                n = len(lay.local_micros(s_, q, M))
+                r = lay.rank_of(s_, q)
+                busy[r] = busy.get(r, 0.0) + self.replica_step(spec, a, b, mb, n)
+        link: dict = {}
+        msg = []
+        for bnd in range(S - 1):
+            width = L[bounds[bnd][1] - 1].out_dim
             per_msg = self.lat + mb * width * self.bb / self.link
-            ra, rb = reps[b], reps[b + 1]
-            most = max(sum(1 for j in range(M) if j % ra == p and j % rb == c)
-                       for p in range(ra) for c in range(rb))
-            hops.append((most * per_msg, per_msg))
-        fill = sum(comp) - max(comp) + 2 * sum(h[1] for h in hops)
-        pipe = max(busy + [h[0] for h in hops]) + fill
-        ar, g = 0.0, 0
-        for k, r in zip(dist, reps):
-            params = sum(l.params for l in L[g:g + k])
-            g += k
+            msg.append(per_msg)
+            ra, rb = reps[bnd], reps[bnd + 1]
+            per = ra * rb // math.gcd(ra, rb)  # the (producer, consumer) pattern repeats
+            cnt: dict = {}
+            for j in range(min(M, per)):
+                key = (j % ra, j % rb)
+                cnt[key] = len(range(j, M, per))
+            for (p_, c_), n_ in cnt.items():
+                src, dst = lay.rank_of(bnd, p_), lay.rank_of(bnd + 1, c_)
+                if src != dst:
+                    link[(src, dst)] = link.get((src, dst), 0.0) + n_ * per_msg  # forward
+                    link[(dst, src)] = link.get((dst, src), 0.0) + n_ * per_msg  # gradient
+        fill = sum(comp) - max(comp) + 2 * sum(msg)
+        pipe = max(list(busy.values()) + list(link.values())) + fill
+        ar = 0.0
+        for (a, b), r in zip(bounds, reps):
             if r > 1:
+                params = sum(l.params for l in L[a:b])
                 ar = max(ar, 2 * (r - 1) / r * params * self.gb / self.ar)
         t = pipe + 0.5 * ar + self.ovh
         detail = {"fan_reps": list(reps), "stage_ms_per_micro": [round(c * 1e3, 4) for c in comp],
-                  "stage_busy_ms": [round(x * 1e3, 4) for x in busy],
-                  "boundary_link_ms": [round(h[0] * 1e3, 4) for h in hops],
+                  "gpu_busy_ms": [round(busy[r] * 1e3, 4) for r in range(N)],
+                  "busiest_link_ms": round(max(link.values(), default=0.0) * 1e3, 4),
                   "fill_ms": round(fill * 1e3, 4), "allreduce_ms": round(ar * 1e3, 4),
-                  "lcm_reps": lcm_reps(reps)}
+                  "lcm_reps": lcm_reps(reps), "calibrated": self.times is not None}
+        if lay.colocated:
+            detail["place"] = [list(p) for p in lay.place]
         plan = Plan(S, 1, list(dist), M, mb, t, G / t, detail)
         plan.reps = list(reps)
+        plan.place = lay.place if lay.colocated else None
         return plan
 
+    def fan_candidates(self, spec: MLPSpec, n_gpus: int, min_stages: int = 2,
+                       colocate: bool = True):
+        """(dist, reps, place) of every fan layout on n_gpus GPUs with at least
+        ``min_stages`` stages: every contiguous layer split, every split of the GPUs into
+        per-stage replica counts, and -- with ``colocate`` -- the last stage with one replica
+        placed on the last GPU of the stage before it (the light classifier
+        stage beside a heavy replica instead of on a GPU of its own)."""
+        from .fan import colocated_place
+
+        L = len(spec.layers)
+        for S in range(min_stages, L + 1):
+            for dist in compositions(L, S):
+                cos = [(False,) * (S - 1)] + ([(False,) * (S - 2) + (True,)] if colocate
+                                                else [])
+                for co in cos:
+                    co = (False,) + tuple(co)
+                    if S - sum(co) < 1 or (sum(co) and S - sum(co) < min_stages - 1):
+                        continue
+                    k = S - sum(co)
+                    if k > n_gpus:
+                        continue
+                    for rr in compositions(n_gpus, k):
+                        it = iter(rr)
+                        reps = [1 if c else next(it) for c in co]
+                        yield dist, reps, (colocated_place(reps, co) if any(co) else None)
+
     def best_fan(self, spec: MLPSpec, n_gpus: int, rows_per_gpu: int,
-                 min_stages: int = 2) -> Plan:
+                 min_stages: int = 2, colocate: bool = True) -> Plan:
         """The best fan layout with at least ``min_stages`` stages over every contiguous layer
-        split and every split of the N GPUs (uniform ppS x dpD is the case of equal replica
-        counts; a single stage is plain data parallelism)."""
+        split, every split of the N GPUs and every co-location of one-replica stages (uniform
+        ppS x dpD is the case of equal replica counts; a single stage is plain data
+        parallelism)."""
         best = None
-        for S in range(min_stages, min(n_gpus, len(spec.layers)) + 1):
-            for dist in compositions(len(spec.layers), S):
-                for reps in compositions(n_gpus, S):
-                    p = self.evaluate_fan(spec, dist, reps, rows_per_gpu)
-                    if best is None or p.samples_per_s > best.samples_per_s:
-                        best = p
+        G = rows_per_gpu * n_gpus
+        for dist, reps, place in self.fan_candidates(spec, n_gpus, min_stages, colocate):
+            # micro-batch count: a few per GPU (bigger GEMMs, fewer messages) up to ~8 (less
+            # fill); the measured replica steps decide
+            for per_gpu in (1, 2, 4, 8):
+                M = max(per_gpu * n_gpus, max(reps))
+                if G % M or (G // M) % 64:
+                    continue
+                try:
+                    p = self.evaluate_fan(spec, dist, reps, rows_per_gpu, num_micro=M,
+                                          place=place)
+                except ValueError:  # a placement whose boundaries run both ways on a rank
+                    continue
+                if best is None or p.samples_per_s > best.samples_per_s:
+                    best = p
         if best is None:
             raise ValueError(f"no fan layout of >= {min_stages} stages for {n_gpus} GPUs")
         return best

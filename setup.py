@@ -25,5 +25,5 @@ class BuildPyWithNative(build_py):
 
 setup(
     cmdclass={"build_ext": BuildNative, "build_py": BuildPyWithNative},
-    package_data={"docker_dist_nn_amd": ["_native*.so"]},
+    package_data={"docker_dist_nn_amd": ["_native*.so", "ops/*.json", "parallel/*.json"]},
 )

@@ -75,9 +75,45 @@ def test_layout_helpers():
     assert [lay.stage_of(r) for r in range(4)] == [(0, 0), (0, 1), (0, 2), (1, 0)]
     assert lay.local_micros(0, 1, 8) == [1, 4, 7]
     assert fan_rows(lay, 0, 1, 8, 16) == [slice(16, 32), slice(64, 80), slice(112, 128)]
-    assert parse_fan("fan:1x3,2x1") == ([1, 2], [3, 1])
-    assert parse_fan("fan:3,1") == (None, [3, 1])
+    assert parse_fan("fan:1x3,2x1") == ([1, 2], [3, 1], None)
+    assert parse_fan("fan:3,1") == (None, [3, 1], None)
     assert parse_fan("pp4") is None
+    assert not lay.colocated and lay.boundary_ranks(0) == [0, 1, 2, 3]
+
+
+def test_colocated_layout_helpers():
+    """The light last stage on the heavy stage's last GPU ('fan:3x4,1x1@3'): 4 ranks, rank 3
+    hosts both workers; only one-replica co-located stages keep every boundary communicator
+    one-directional per rank."""
+    from docker_dist_nn_amd.parallel.fan import colocated_place
+
+    d, r, place = parse_fan("fan:3x4,1x1@3")
+    lay = FanLayout(tuple(d), tuple(r), place)
+    assert lay.colocated and lay.world == 4 and lay.place == ((0, 1, 2, 3), (3,))
+    assert lay.workers_of(3) == [(0, 3), (1, 0)] and lay.workers_of(0) == [(0, 0)]
+    assert lay.boundary_ranks(0) == [0, 1, 2, 3]
+    assert lay.spec_text() == "fan:3x4,1x1@3" and "@3" in lay.describe()
+    assert colocated_place((4, 1), (False, True)) == place
+    lay.check_directions(8)
+    with pytest.raises(ValueError):  # stage 1 on ranks 1..3 both send and receive
+        FanLayout((3, 1), (4, 3), ((0, 1, 2, 3), (1, 2, 3))).check_directions(12)
+    with pytest.raises(ValueError):  # replicas of a stage on one rank
+        FanLayout((3, 1), (2, 2), ((0, 1), (1, 1)))
+    with pytest.raises(ValueError):  # a rank gap
+        FanLayout((3, 1), (2, 1), ((0, 2), (2,)))
+    with pytest.raises(AttributeError if False else ValueError):
+        lay.offsets
+
+
+@pytest.mark.parametrize("M", [4, 8, 9])
+def test_colocated_schedule_serialises_each_rank(M):
+    lay = FanLayout((3, 1), (4, 1), ((0, 1, 2, 3), (3,)))
+    for hop in (0.0, 0.5, 2.0):
+        sch = fan_schedule(lay, M, [1.0, 0.05], [2.0, 0.1], hop)
+        check_schedule(sch)  # includes: no two ops of one rank overlap
+        rk = sch.rank_ops(3)
+        assert {s for s, _, _ in rk} == {0, 1}
+        assert len(rk) == 2 * (len(lay.local_micros(0, 3, M)) + M)
     f, b = stage_costs(MLPSpec.parse("784-512-256-128-10"), [1, 3])
     assert max(f + b) == 1.0 and b[0] > b[1]
 
@@ -101,7 +137,7 @@ def _global(rows):
     return xt, torch.from_numpy(y)
 
 
-def _worker(rank, world, port, dist_, reps, mb, M, steps, shard, out_dir):
+def _worker(rank, world, port, dist_, reps, mb, M, steps, shard, out_dir, place=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.set_num_threads(1)
@@ -110,7 +146,7 @@ def _worker(rank, world, port, dist_, reps, mb, M, steps, shard, out_dir):
     from docker_dist_nn_amd.engine.fan_trainer import FanTrainer
     from docker_dist_nn_amd.parallel.fan import build_fan_mesh
 
-    lay = FanLayout(tuple(dist_), tuple(reps))
+    lay = FanLayout(tuple(dist_), tuple(reps), place)
     mesh = build_fan_mesh(lay)
     tr = FanTrainer(MLPSpec.parse(SPEC), lay, mesh, micro_batch=mb, num_micro=M,
                     optim=OptimConfig(lr=0.1, momentum=0.9), device=torch.device("cpu"),
@@ -122,9 +158,11 @@ def _worker(rank, world, port, dist_, reps, mb, M, steps, shard, out_dir):
         tr.step()
         losses.append(tr.loss())
     for k, (w, b) in tr.local_weights().items():
-        np.save(os.path.join(out_dir, f"w{k}_s{mesh.stage}_q{mesh.replica}.npy"), w)
+        s = next(t for t in range(lay.S) if sum(dist_[:t]) <= k < sum(dist_[:t + 1]))
+        np.save(os.path.join(out_dir, f"w{k}_s{s}_q{mesh.replica_at(s)}.npy"), w)
     if losses[-1] is not None:
-        np.save(os.path.join(out_dir, f"loss_q{mesh.replica}.npy"), np.array(losses))
+        np.save(os.path.join(out_dir, f"loss_q{mesh.replica_at(lay.S - 1)}.npy"),
+                np.array(losses))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -275,11 +313,43 @@ def test_bench_plans_fan_layouts_at_the_default_batch():
 
     a = b.parse_args(["--gpus", "8"])
     spec = NAMED_MODELS["mnist-fcnn"]
+    # the calibrated planner (measured replica steps, round 6): at N = 2 the light classifier
+    # stage shares the second GPU with a heavy replica (co-location)
+    p2 = b._plan(a, spec, 2, 2, "pipeline")
+    assert p2.parallelism == "fan3x2,1x1@1" and p2.colocated and p2.place == ((0, 1), (1,))
     assert b._plan(a, spec, 4, 4, "pipeline").parallelism == "fan3x3,1x1"
     assert b._plan(a, spec, 8, 8, "pipeline").parallelism == "fan3x7,1x1"
-    assert b._plan(a, spec, 2, 2, "pipeline").parallelism == "pp2"
     assert b._uniform_prediction(a, spec, 4, 4)["parallelism"] == "pp4"
     w = NAMED_MODELS["wide"]
     assert b._plan(a, w, 8, 8, "pipeline").parallelism == "fan1x1,2x7"
     p = b._plan(a, spec, 4, 4, "fan:3x3,1x1")
     assert p.reps == [3, 1] and p.distribution == [3, 1]
+    p = b._plan(a, spec, 4, 4, "fan:3x4,1x1@3")
+    assert p.reps == [4, 1] and p.place == ((0, 1, 2, 3), (3,)) and p.colocated
+
+
+@pytest.mark.parametrize("dist_,reps,place,shard,M", [
+    # the headline's light classifier stage on the heavy stage's last GPU
+    ([3, 1], [2, 1], ((0, 1), (1,)), False, 6),
+    ([3, 1], [4, 1], ((0, 1, 2, 3), (3,)), False, 7),
+    ([3, 1], [3, 1], ((0, 1, 2), (2,)), True, 6),
+    ([1, 2, 1], [2, 2, 1], ((0, 1), (2, 3), (3,)), False, 6)])
+def test_colocated_fan_training_matches_single_process(tmp_path, dist_, reps, place, shard, M):
+    """A rank hosting a replica of the heavy stage AND the light stage: local hops are device
+    copies, remote hops fan in to it; training equals one process on the global batch."""
+    mb, steps = 64, 3
+    world = FanLayout(tuple(dist_), tuple(reps), place).world
+    mp.spawn(_worker, args=(world, _port(), dist_, reps, mb, M, steps, shard, str(tmp_path),
+                            place), nprocs=world, join=True)
+    ref_losses, ref_w = _single(mb, M, steps)
+    got = sum(np.load(tmp_path / f"loss_q{q}.npy") for q in range(reps[-1]))
+    tol = dict(rtol=2e-2, atol=3e-4) if shard else dict(rtol=1e-4, atol=2e-5)
+    np.testing.assert_allclose(got, ref_losses, rtol=1e-4 if not shard else 1e-2)
+    g = 0
+    for s, k in enumerate(dist_):
+        for i in range(g, g + k):
+            ws = [np.load(tmp_path / f"w{i}_s{s}_q{q}.npy") for q in range(reps[s])]
+            for w in ws[1:]:
+                np.testing.assert_array_equal(w, ws[0])
+            np.testing.assert_allclose(ws[0], ref_w[i], **tol)
+        g += k

@@ -24,7 +24,8 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, dist_, reps, M, dp_reduce, use_interp, steps, out_dir, tag):
+def _worker(rank, world, port, dist_, reps, M, dp_reduce, use_interp, steps, out_dir, tag,
+            place=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DNN_DP_DEFER="0")
     import torch.distributed as dist
 
@@ -38,7 +39,7 @@ def _worker(rank, world, port, dist_, reps, M, dp_reduce, use_interp, steps, out
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    lay = FanLayout(tuple(dist_), tuple(reps))
+    lay = FanLayout(tuple(dist_), tuple(reps), place)
     mesh = build_fan_mesh(lay)
     mb = 256
     tr = FanTrainer(MLPSpec.parse(SPEC), lay, mesh, micro_batch=mb, num_micro=M, device=dev,
@@ -65,12 +66,15 @@ def _worker(rank, world, port, dist_, reps, M, dp_reduce, use_interp, steps, out
                 st.begin_step()
             it.run_step()
     torch.cuda.synchronize()
+    bounds = np.cumsum([0] + list(dist_))
     for k, (w, b) in tr.local_weights().items():
-        if mesh.replica == 0:
+        s = int(np.searchsorted(bounds, k, side="right")) - 1
+        if mesh.replica_at(s) == 0:
             np.save(os.path.join(out_dir, f"{tag}_w{k}.npy"), w)
             np.save(os.path.join(out_dir, f"{tag}_b{k}.npy"), b)
     if tr.last is not None:
-        np.save(os.path.join(out_dir, f"{tag}_loss{mesh.replica}.npy"), np.array([tr.loss()]))
+        np.save(os.path.join(out_dir, f"{tag}_loss{mesh.replica_at(lay.S - 1)}.npy"),
+                np.array([tr.loss()]))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -125,3 +129,59 @@ def test_bench_runs_the_fan_layout(tmp_path):
     assert out["ladder"]["rung"] == "default"
     assert out["ladder"]["attempts"][0]["rung"] == "default"
     assert 0 < out["last_loss"] < 10
+    # the literal grid is measured after the fan number (--no-dp-compare skips only DP)
+    assert out["uniform_pipeline"]["value"] > 0, out["uniform_pipeline"]
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("reps,place,M,dp_reduce", [([2, 1], ((0, 1), (1,)), 6, "allreduce"),
+                                                    ([3, 1], ((0, 1, 2), (2,)), 7, "shard")])
+def test_colocated_fan_bitwise_equals_separate_gpus(dev, reps, place, M, dp_reduce):
+    """The light last stage co-located with the heavy stage's last replica (its hops to that
+    replica become device copies, the others fan in over the boundary communicator) trains bit
+    for bit like the same layout with the light stage on a rank of its own (VERDICT r5 #3)."""
+    dist_, steps = [3, 1], 3
+    with tempfile.TemporaryDirectory() as d:
+        for pl, tag in ((None, "sep"), (place, "colo")):
+            world = sum(reps) if pl is None else len({x for p in pl for x in p})
+            mp.start_processes(_worker, args=(world, _port(), dist_, reps, M, dp_reduce, False,
+                                              steps, d, tag, pl),
+                               nprocs=world, join=True, start_method="spawn")
+        for k in range(4):
+            for wb in ("w", "b"):
+                a = np.load(os.path.join(d, f"sep_{wb}{k}.npy"))
+                b = np.load(os.path.join(d, f"colo_{wb}{k}.npy"))
+                assert np.array_equal(a, b), (wb, k)
+        assert np.array_equal(np.load(os.path.join(d, "sep_loss0.npy")),
+                              np.load(os.path.join(d, "colo_loss0.npy")))
+
+
+@pytest.mark.timeout(400)
+def test_bench_colocated_fan_with_uniform_and_dp_measured(tmp_path):
+    """bench.py at N = 4 (four ranks sharing cuda:0 over gloo, through the ladder) on the
+    co-located layout fan:3x4,1x1@3 -- then, as comparisons inside the deadline, the literal
+    uniform grid (pp4) and data parallelism, all in ONE JSON line (VERDICT r5 #5)."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, DNN_FORCE_DEVICE="0", DNN_DIST_BACKEND="gloo", TMPDIR=str(tmp_path))
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "4", "--master-addr", "127.0.0.1",
+                        "--master-port", str(_port()), os.path.join(root, "bench.py"),
+                        "--gpus", "4", "--steps", "3", "--warmup", "1", "--batch", "4096",
+                        "--parallelism", "fan:3x4,1x1@3"],
+                       env=env, stdout=subprocess.PIPE, stderr=None, text=True, timeout=380,
+                       cwd=root)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert r.returncode == 0 and len(lines) == 1, r.stdout[-3000:]
+    out = json.loads(lines[0])
+    assert out["value"] > 0 and out["n_gpus"] == 4
+    cfg = out["config"]
+    assert cfg["parallelism"] == "fan3x4,1x1@3" and cfg["stage_place"] == [[0, 1, 2, 3], [3]]
+    u, dp = out["uniform_pipeline"], out["dp_only"]
+    assert u["value"] > 0 and u["parallelism"] == "pp4", u
+    assert dp["value"] > 0 and dp["parallelism"] == "dp4", dp
+    assert out["ladder"]["seconds"] < 540
+    assert [a["rung"] for a in out["ladder"]["compare_attempts"]] == ["uniform", "dp-native"]

@@ -201,3 +201,79 @@ def test_fan_rungs():
     assert names == ["default", "fan-python", "uniform-rccl-slotted", "uniform-python",
                      "dp-native", "dp-python"]
     assert "--parallelism" in bench_rungs(8, fan=True)[2].args
+
+
+# Main measurement + two comparisons (bench.py supervise: the literal uniform pipeline, then
+# data parallelism), each run only while the deadline leaves room for one more attempt.
+COMPARE_SCRIPT = textwrap.dedent("""
+    import json, os, sys, time
+    sys.path.insert(0, {root!r})
+    from docker_dist_nn_amd import ladder
+    rank = int(os.environ["RANK"])
+    if ladder.is_child():
+        ladder.heartbeat("start")
+        rung = os.environ[ladder.RUNG_ENV]
+        time.sleep({child_s} if rung.startswith("u") else 0.2)
+        ladder.write_result({{"rung": rung, "value": len(rung)}})
+        sys.exit(0)
+    world = int(os.environ["WORLD_SIZE"])
+    sup = ladder.Supervisor(lambda r: [sys.executable, __file__], rank=rank, world=world,
+                            stall=30.0, deadline=time.monotonic() + float({deadline}))
+    res, rung = sup.climb([ladder.Rung("main")])
+    seen = []
+    out = sup.comparisons([("uniform_pipeline", [ladder.Rung("u1")]),
+                           ("dp_only", [ladder.Rung("dp1")])], need_s=float({need}),
+                          on_done=lambda k, e: seen.append(k))
+    print(json.dumps({{"rank": rank, "res": res, "out": out, "seen": seen}}), flush=True)
+""")
+
+
+def _compare_run(tmp_path, deadline, need, child_s):
+    script = tmp_path / "cmp.py"
+    script.write_text(COMPARE_SCRIPT.format(root=ROOT, deadline=deadline, need=need,
+                                            child_s=child_s))
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+                        "--master-port", str(_port()), str(script)],
+                       env=_env(tmp_path), capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    recs = sorted((json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")),
+                  key=lambda x: x["rank"])
+    assert [x["rank"] for x in recs] == [0, 1]
+    assert recs[0]["out"].keys() == recs[1]["out"].keys()
+    for k in recs[0]["out"]:  # every rank took the same decision
+        assert ("skipped" in recs[0]["out"][k]) == ("skipped" in recs[1]["out"][k])
+    return recs[0]
+
+
+@pytest.mark.timeout(120)
+def test_comparisons_all_run_when_time_allows(tmp_path):
+    r = _compare_run(tmp_path, deadline=100, need=5, child_s=0.2)
+    assert r["res"]["rung"] == "main"
+    assert r["out"]["uniform_pipeline"]["result"] == {"rung": "u1", "value": 2}
+    assert r["out"]["dp_only"]["result"] == {"rung": "dp1", "value": 3}
+    assert r["seen"] == ["uniform_pipeline", "dp_only"]
+
+
+@pytest.mark.timeout(120)
+def test_comparisons_skip_past_the_budget(tmp_path):
+    """The uniform measurement runs (enough time left), takes long, and the data-parallel
+    comparison is then skipped for the budget -- on every rank."""
+    r = _compare_run(tmp_path, deadline=14, need=6, child_s=7)
+    assert r["out"]["uniform_pipeline"]["result"]["rung"] == "u1"
+    assert r["out"]["dp_only"]["skipped"] == "budget"
+    assert r["out"]["dp_only"]["seconds_left"] < 6
+
+
+@pytest.mark.timeout(120)
+def test_comparisons_all_skipped_without_time(tmp_path):
+    r = _compare_run(tmp_path, deadline=100, need=1000, child_s=0.2)
+    assert all(e["skipped"] == "budget" for e in r["out"].values())
+
+
+def test_uniform_rungs():
+    from docker_dist_nn_amd.ladder import uniform_rungs
+
+    rr = uniform_rungs()
+    assert [r.name for r in rr] == ["uniform", "uniform-rccl-slotted", "uniform-python"]
+    assert all(r.args[:2] == ["--parallelism", "uniform"] for r in rr)
