@@ -140,3 +140,74 @@ def test_cross_step_overlap_bitwise(dev, monkeypatch):
     for r in res[1:]:  # DNN_XSTEP and DNN_H0_DOUBLE: bitwise the same training
         assert r[0] == res[0][0]
         assert torch.equal(r[1], res[0][1])
+
+
+def _xstep_trainer(dev, seed, lr):
+    from docker_dist_nn_amd import NAMED_MODELS
+    from docker_dist_nn_amd.engine import OptimConfig, Trainer
+
+    return Trainer(NAMED_MODELS["mnist-fcnn"], micro_batch=8192, num_micro=1, seed=seed,
+                   optim=OptimConfig(lr=lr, momentum=0.9), device=dev)
+
+
+def _xstep_batches(dev):
+    from docker_dist_nn_amd.data import synthetic_mnist
+
+    rows = 8192
+    x, y = synthetic_mnist(2 * rows, seed=11)
+    xb = torch.zeros(2 * rows, 832, dtype=torch.bfloat16)
+    xb[:, :784] = torch.from_numpy(x).to(torch.bfloat16)
+    xb, yb = xb.to(dev), torch.from_numpy(y).to(dev)
+    return [(xb[k * rows:(k + 1) * rows], yb[k * rows:(k + 1) * rows]) for k in range(2)]
+
+
+def test_interleaved_cross_step_trainers_bitwise(dev, monkeypatch):
+    """the cross-step events belong to each executor. Two DNN_XSTEP trainers
+    stepping in turn on one thread must each wait on THEIR OWN side stream's marks -- bitwise
+    the same training as each trainer stepping alone."""
+    monkeypatch.setenv("DNN_BW_OVERLAP_MIN_ROWS", "0")
+    monkeypatch.setenv("DNN_SPLIT_FINO", "1")
+    monkeypatch.setenv("DNN_XSTEP", "1")
+    bat = _xstep_batches(dev)
+    alone = []
+    for seed, lr in ((0, 0.1), (1, 0.05)):
+        tr = _xstep_trainer(dev, seed, lr)
+        for k in range(6):
+            tr.set_batch(*bat[k % 2], zero_copy=True)
+            tr.step()
+        tr.flush()
+        alone.append(tr.stages[0].params.master.clone())
+    a, b = _xstep_trainer(dev, 0, 0.1), _xstep_trainer(dev, 1, 0.05)
+    for k in range(6):
+        for tr in (a, b):
+            tr.set_batch(*bat[k % 2], zero_copy=True)
+            tr.step()
+    a.flush()
+    b.flush()
+    assert torch.equal(a.stages[0].params.master, alone[0])
+    assert torch.equal(b.stages[0].params.master, alone[1])
+
+
+def test_capture_after_eager_cross_step_bitwise(dev, monkeypatch):
+    """capture() after eager DNN_XSTEP steps joins the pending side-stream update
+    first -- 2 eager steps, a capture (1 executed step) and 2 replays train bit for bit like 5
+    eager steps."""
+    monkeypatch.setenv("DNN_BW_OVERLAP_MIN_ROWS", "0")
+    monkeypatch.setenv("DNN_SPLIT_FINO", "1")
+    monkeypatch.setenv("DNN_XSTEP", "1")
+    x, y = _xstep_batches(dev)[0]
+    ref = _xstep_trainer(dev, 0, 0.1)
+    for _ in range(5):
+        ref.set_batch(x, y)
+        ref.step()
+    ref.flush()
+    tr = _xstep_trainer(dev, 0, 0.1)
+    for _ in range(2):
+        tr.set_batch(x, y)
+        tr.step()
+    tr.set_batch(x, y)
+    tr.capture(copies=1)
+    for _ in range(2):
+        tr.step()
+    torch.cuda.synchronize()
+    assert torch.equal(tr.stages[0].params.master, ref.stages[0].params.master)
