@@ -284,7 +284,8 @@ def measure(a, spec, n, world, dev, text):
         tr.set_batch(xb if tr.first else None, yb if tr.last else None)
         tr.capture(copies=a.graph_copies)
     elif a.graph == "auto" and world > 1 and tr.transport == "ipc" and \
-            tr.native_step is not None:
+            tr.native_step is not None and not fan:
+        # (fan plans hold their replicated stages' RCCL all-reduce: they stay eager)
         # the relayed IPC plan is hundreds of ops per rank: replayed as a graph when that
         # measures faster (RCCL plans stay eager: capturing RCCL calls is not validated here)
         eager_s = timed(3)

@@ -16,7 +16,8 @@ from typing import Optional
 import torch
 
 from ..models.mlp import MLPSpec
-from ..parallel.fan import FanLayout, FanMesh, FanPipe, fan_schedule, gather_rows, stage_costs
+from ..parallel.fan import (FanIpcPipe, FanLayout, FanMesh, FanPipe, fan_schedule,
+                             gather_rows, stage_costs)
 from ..parallel.pipeline import GradSync, PipelineExecutor
 from ..partition import plan_stages
 from .stage import OptimConfig, Stage
@@ -65,7 +66,10 @@ class FanTrainer(Trainer):
                  num_micro: int, optim: Optional[OptimConfig] = None,
                  device: Optional[torch.device] = None, seed: int = 0,
                  dp_reduce: str = "allreduce", native_exec: Optional[bool] = None,
-                 hop_cost: float = 0.0):
+                 hop_cost: float = 0.0, ipc_rehearsal: bool = False):
+        """``ipc_rehearsal`` (one-GPU tests: ranks sharing a GPU over gloo): set up the IPC
+        transport (``self.ipc_pipe``) whatever the backend, for a test that runs the IPC fan
+        plan through the plan interpreter; the Python executor keeps the gloo FanPipe."""
         if sum(layout.dist) != len(spec.layers):
             raise ValueError(f"fan layout {layout.dist} does not cover {len(spec.layers)} layers")
         layout.check_directions(num_micro)
@@ -102,6 +106,30 @@ class FanTrainer(Trainer):
             stages[ws] = st
         self.stages = [stages[k] for k in sorted(stages)]
         self.pipe = FanPipe(mesh, stages if len(stages) > 1 else stages[s], self.sched)
+        if native_exec is None:
+            native_exec = self.device.type == "cuda"
+        # xGMI peer writes (FanIpcPipe) on RCCL jobs, like the uniform pipeline's DNN_PIPE=auto:
+        # set up before the stage records its launches (the receive buffers move to uncached
+        # memory); verified bitwise against the RCCL plan on the first step
+        self._ipc_verify = None
+        self._fallback_step = None
+        ipc, ipc_why = None, None
+        self.ipc_pipe = None
+        if ipc_rehearsal:
+            self.ipc_pipe = FanIpcPipe(mesh, stages[s], self.sched)
+        mode = switches.get("DNN_PIPE")
+        if mesh.backend == "nccl" and self.device.type == "cuda" and native_exec and \
+                not layout.colocated and mode in ("auto", "ipc") and \
+                switches.get("DNN_NATIVE_DIST") != "0":
+            if mode == "ipc" or self._peers_mappable(mesh):
+                try:
+                    ipc = FanIpcPipe(mesh, stages[s], self.sched)  # errors agreed inside
+                except RuntimeError as e:
+                    if mode == "ipc":
+                        raise
+                    ipc_why = f"IPC set-up failed: {e}"[:200]
+            else:
+                ipc_why = "a GPU pair of the plan has no peer access"
         self.boundary = "bf16"
         execs = {}
         for ws, wq in workers:
@@ -119,8 +147,6 @@ class FanTrainer(Trainer):
             order = [(ws, op, layout.local_index(ws, j)) for ws, op, j in
                      self.sched.rank_ops(mesh.rank)]
             self.executor = _RankSteps(execs, order, self.pipe)
-        if native_exec is None:
-            native_exec = self.device.type == "cuda"
         self.native_exec = bool(native_exec)
         if self.native_exec:
             for st in self.stages:
@@ -154,8 +180,33 @@ class FanTrainer(Trainer):
                 self.executor.native_step = self.native_step
                 self.transport_reason = (f"fan layout {layout.describe()}: slotted RCCL plan "
                                          "(one group per clock slot), native step")
-        self._ipc_verify = None
-        self._fallback_step = None
+            if ipc is not None:
+                ipc_step, err = None, None
+                try:
+                    if self.native_step is None:
+                        raise RuntimeError("no RCCL plan to verify the IPC plan against")
+                    ipc_step = FanNativeStep(self.executor, mesh, self.sched, ipc=ipc)
+                except Exception as e:
+                    err = e
+                if _any_rank(ipc_step is None, self.device):
+                    ipc.close()
+                    ipc_why = f"IPC fan plan unavailable ({err!r} here)"[:200]
+                else:
+                    # the first step runs on IPC, then from the same state on the RCCL plan;
+                    # IPC stays only if every rank's weights agree bit for bit
+                    # (Trainer._verify_first_step, the uniform pipeline's protocol)
+                    self._fallback_step = self.native_step
+                    self.native_step = ipc_step
+                    self.executor.native_step = ipc_step
+                    self.executor.pipe = ipc
+                    self._ipc_verify = (ipc, self.pipe)
+                    self.pipe = ipc
+                    self.transport = "ipc"
+                    self.transport_reason = (
+                        f"fan layout {layout.describe()}: ipc, peer copies + flags in clock "
+                        "order on one stream (verification pending: first step)")
+            if ipc_why is not None and self.transport != "ipc":
+                self.transport_reason += f"; IPC not used: {ipc_why}"
         self._graph = None
         self._graphs = []
         self._stream = None

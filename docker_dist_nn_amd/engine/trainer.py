@@ -336,7 +336,9 @@ class Trainer:
         self.native_step = self._fallback_step
         self.executor.native_step = self._fallback_step
         self._fallback_step = None
-        self.transport_reason = f"{self.transport} (IPC not used: {why})"[:300]
+        mode = getattr(self.native_step, "mode", None) if self.native_step is not None else None
+        self.transport_reason = (f"{self.transport}{', ' + mode if mode else ''} "
+                                 f"(IPC not used: {why})")[:300]
 
     def _state_tensors(self) -> list:
         out = []

@@ -75,8 +75,9 @@ def uniform_rungs() -> list[Rung]:
 def bench_rungs(n: int, dp_only: bool = False, fan: bool = False) -> list[Rung]:
     """The training benchmark's ladder for ``n`` ranks. ``dp_only``: the layout is already
     data-parallel (no hops), only the executor can fall back. ``fan``: the default layout is
-    a replicated-stage pipeline (parallel/fan.py: RCCL slotted plan, no IPC form): its Python
-    executor, then the uniform ppS x dpD grid with its own rungs, then data parallelism."""
+    a replicated-stage pipeline (parallel/fan.py: IPC plan verified against the RCCL slotted
+    plan): the RCCL plan alone, its Python executor, then the uniform ppS x dpD grid with its
+    own rungs, then data parallelism."""
     # every rung after the first replays eagerly: a failed first attempt may have been the
     # graph replay itself (bench --graph auto)
     eager = ["--graph", "off"]
@@ -87,6 +88,7 @@ def bench_rungs(n: int, dp_only: bool = False, fan: bool = False) -> list[Rung]:
     if fan:
         uni = ["--parallelism", "uniform", *eager]
         return [Rung("default"),
+                Rung("fan-rccl", {"DNN_PIPE": "rccl"}, eager),
                 Rung("fan-python", {"DNN_NATIVE_DIST": "0"}, eager),
                 Rung("uniform-rccl-slotted", {"DNN_PIPE": "rccl", "DNN_RCCL_PLAN": "slotted"},
                      uni),

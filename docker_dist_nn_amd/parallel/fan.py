@@ -583,6 +583,207 @@ class FanPipe:
             raise RuntimeError("step ended with unconsumed fan receives")
 
 
+class FanIpcPipe:
+    """Fan hops as direct writes into IPC-mapped peer buffers (one stage per rank; the
+    xGMI peer-write transport of the uniform pipeline, comm.IpcPipe, for fan-in / fan-out).
+
+    Every rank exports its receive buffers (x_in: the forward rows its stage-(s-1) producers
+    write; grad_out: the gradient rows its stage-(s+1) consumers write back) and a flag block
+    ``[f[0..n-1], b[0..n-1], ackf[0..W-1], ackb[0..W-1]]`` (n = its micro-batches, W = world):
+
+      send_fwd(j) to consumer c: wait ackf[c] >= s-1 (c finished reading, in step s-1, the rows
+                  I write -- once per consumer and step) -> copy my output rows of j into c's
+                  x_in rows of j (c's local index) -> c.f[j] = s
+      recv_fwd(j): wait f[j] >= s
+      send_bwd / recv_bwd: the same with dx_send -> the producer's grad_out, b[j], ackb
+      end_step:   every producer p that wrote my x_in: p.ackf[me] = s; every consumer c that
+                  wrote my grad_out: c.ackb[me] = s (after every kernel of the step that
+                  reads them, the weight gradients included)
+
+    Flags carry the step number s = 1, 2, ...: nothing is ever reset. The receive buffers are
+    re-homed in L2-uncached memory before the stage records its launches (comm.IpcPipe: a
+    peer's xGMI stores are not snooped by this GPU's L2s). ``exchange`` (tests / plan
+    simulator): rank -> {"x_in", "grad_out", "flags"} addresses instead of a real export."""
+
+    def __init__(self, mesh: FanMesh, stage, sched: FanSchedule, exchange: Optional[dict] = None,
+                 uncached: bool = True):
+        lay = mesh.layout
+        if lay.colocated:
+            raise ValueError("IPC fan hops: one stage per rank (co-located layouts use FanPipe)")
+        self.mesh, self.stage, self.sched, self.lay = mesh, stage, sched, lay
+        self.s, self.q, self.me = mesh.stage, mesh.replica, mesh.rank
+        self.W = lay.world
+        self.nloc = stage.nm
+        self.local = lay.local_micros(self.s, self.q, sched.M)
+        s = self.s
+        # the peers: ranks I send forward to (= send me gradients) and that send me forward
+        # rows (= receive my gradients)
+        self.fwd_peers = sorted({lay.rank_of(s + 1, lay.replica_of(s + 1, j))
+                                 for j in self.local}) if s + 1 < lay.S else []
+        self.bwd_peers = sorted({lay.rank_of(s - 1, lay.replica_of(s - 1, j))
+                                 for j in self.local}) if s > 0 else []
+        self.seq = 0
+        self._acked: set = set()
+        if exchange is not None:
+            self.n = None
+            self.flags_addr = exchange[self.me]["flags"]
+            self.flags = None
+            self.peers = {r: exchange[r] for r in self.fwd_peers + self.bwd_peers}
+            self.row_bytes_f = stage.geoms[-1].np_ * 2 if s + 1 < lay.S else 0
+            self.row_bytes_b = stage.geoms[0].kp * 2 if s > 0 else 0
+            return
+        self._export_import(uncached)
+
+    # flag word indices
+    def fidx(self, jj: int) -> int:
+        return jj
+
+    def bidx(self, jj: int) -> int:
+        return self.nloc + jj
+
+    def ackf(self, r: int) -> int:
+        return 2 * self.nloc + r
+
+    def ackb(self, r: int) -> int:
+        return 2 * self.nloc + self.W + r
+
+    def n_flags(self) -> int:
+        return 2 * self.nloc + 2 * self.W
+
+    def _export_import(self, uncached: bool) -> None:
+        import torch.distributed as dist
+
+        from ..utils.native import native
+        from .comm import _cpu_group
+
+        st, s = self.stage, self.s
+        if st.device.type != "cuda":
+            raise ValueError("FanIpcPipe needs GPU stages")
+        self.n = native()
+        err, mine = None, {}
+        try:
+            if uncached:  # before compile_native: the recorded launches bind these buffers
+                from ..utils.devmem import uncached_zeros
+
+                if st._prog is not None:
+                    raise RuntimeError("receive buffers must be re-homed before compile_native")
+                if s > 0:
+                    st.x_buf = uncached_zeros(tuple(st.x_buf.shape), st.x_buf.dtype, st.device)
+                    st.x_in = st.x_buf
+                if s + 1 < self.lay.S:
+                    st.dz[-1] = uncached_zeros(tuple(st.dz[-1].shape), st.dz[-1].dtype,
+                                               st.device)
+            self.flags = torch.zeros(self.n_flags(), dtype=torch.int32, device=st.device)
+            self.flags_addr = self.flags.data_ptr()
+            torch.cuda.synchronize(st.device)
+            mine = {"x_in": self.n.ipc_export(st.x_in.data_ptr()),
+                    "grad_out": (self.n.ipc_export(st.grad_out.data_ptr())
+                                 if s + 1 < self.lay.S else None),
+                    "flags": self.n.ipc_export(self.flags.data_ptr())}
+            self.row_bytes_f = st.output.stride(0) * st.output.element_size() \
+                if s + 1 < self.lay.S else 0
+            self.row_bytes_b = st.dx_send.stride(0) * st.dx_send.element_size() if s > 0 else 0
+        except Exception as e:  # noqa: BLE001 -- agreed on below
+            err = e
+        if err is not None:
+            mine = {"error": repr(err)}
+        everyone = [None] * self.W
+        dist.all_gather_object(everyone, mine)
+        bad = [(r, e["error"]) for r, e in enumerate(everyone) if "error" in e]
+        if bad:
+            raise RuntimeError(f"IPC fan transport unavailable: {bad}")
+        err = None
+        self.peers = {}
+        try:
+            for r in self.fwd_peers + self.bwd_peers:
+                d = everyone[r]
+                self.peers[r] = {k: (self.n.ipc_import(*d[k]) if d[k] is not None else None)
+                                 for k in ("x_in", "grad_out", "flags")}
+        except Exception as e:  # noqa: BLE001
+            err = e
+        failed = torch.tensor([1 if err is not None else 0], dtype=torch.int32)
+        dist.all_reduce(failed, op=dist.ReduceOp.MAX, group=_cpu_group())
+        if int(failed.item()):
+            raise RuntimeError(f"IPC fan transport unavailable (peer mapping failed on a rank; "
+                               f"here: {err!r})")
+
+    def close(self) -> None:
+        self.peers = {}
+        self.flags = None
+
+    # ---- hop descriptions (shared by the Python path and the native plan) --------------------
+    def send_desc(self, direction: str, jj: int):
+        """(peer rank, destination byte address, source address, bytes, peer flag address) of
+        my local micro-batch jj's hop in ``direction``."""
+        lay, st, s = self.lay, self.stage, self.s
+        j = self.local[jj]
+        t = s + 1 if direction == "f" else s - 1
+        peer = lay.rank_of(t, lay.replica_of(t, j))
+        pj = lay.local_index(t, j)  # the peer's local index of j (its rows / flag)
+        src_t = st.output if direction == "f" else st.dx_send
+        src = src_t[st.rows_of(jj)]
+        rb = self.row_bytes_f if direction == "f" else self.row_bytes_b
+        nb = st.mb * rb
+        pd = self.peers[peer]
+        dst = pd["x_in" if direction == "f" else "grad_out"] + pj * st.mb * rb
+        nloc_peer = len(lay.local_micros(t, lay.replica_of(t, j), self.sched.M))
+        fi = pj if direction == "f" else nloc_peer + pj
+        return peer, dst, src.data_ptr(), nb, pd["flags"] + 4 * fi
+
+    def ack_wait_addr(self, direction: str, peer: int) -> int:
+        return self.flags_addr + 4 * (self.ackf(peer) if direction == "f" else self.ackb(peer))
+
+    def ack_signals(self) -> list[int]:
+        """Peer flag addresses I raise at the end of a step: my producers' ackf[me] (my x_in
+        is free again) and my gradient producers' ackb[me] (my grad_out)."""
+        out = []
+        for r in self.bwd_peers:  # they wrote my x_in
+            nl = len(self.lay.local_micros(*self.lay.stage_of(r), self.sched.M))
+            out.append(self.peers[r]["flags"] + 4 * (2 * nl + self.me))
+        for r in self.fwd_peers:  # they wrote my grad_out
+            nl = len(self.lay.local_micros(*self.lay.stage_of(r), self.sched.M))
+            out.append(self.peers[r]["flags"] + 4 * (2 * nl + self.W + self.me))
+        return out
+
+    # ---- Python executor path ---------------------------------------------------------------
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.stage.device).cuda_stream
+
+    def begin_step(self):
+        self.seq += 1
+        self._acked = set()
+
+    def _send(self, direction: str, stage, jj: int):
+        peer, dst, src, nb, flag = self.send_desc(direction, jj)
+        s = self._stream()
+        if (direction, peer) not in self._acked:
+            self.n.wait_geq_u32(s, self.ack_wait_addr(direction, peer), self.seq - 1)
+            self._acked.add((direction, peer))
+        self.n.copy_async(dst, src, nb, s)
+        self.n.signal_u32(s, flag, self.seq)
+
+    def recv_fwd(self, stage, jj):
+        if self.s > 0:
+            self.n.wait_geq_u32(self._stream(), self.flags_addr + 4 * self.fidx(jj), self.seq)
+
+    def send_fwd(self, stage, jj):
+        if self.s + 1 < self.lay.S:
+            self._send("f", stage, jj)
+
+    def recv_bwd(self, stage, jj):
+        if self.s + 1 < self.lay.S:
+            self.n.wait_geq_u32(self._stream(), self.flags_addr + 4 * self.bidx(jj), self.seq)
+
+    def send_bwd(self, stage, jj):
+        if self.s > 0:
+            self._send("b", stage, jj)
+
+    def end_step(self):
+        s = self._stream()
+        for a in self.ack_signals():
+            self.n.signal_u32(s, a, self.seq)
+
+
 def fan_rows(layout: FanLayout, s: int, q: int, M: int, mb: int) -> list[slice]:
     """Rows of the GLOBAL batch that replica q of stage s holds, in local order (the first
     stage's inputs, the last stage's labels)."""
@@ -659,8 +860,9 @@ def fan_messages(sched: FanSchedule) -> list[tuple[int, str, int, int, int]]:
 
 
 def _fan_native_step_class():
-    from .native_step import (COMM, GROUP, MAIN, NCCL_BF16, REC, RECV, SEG, SEND, WAIT,
-                              NativeStep, comm_ptr, flatten, torch_rccl_path, PLAN_KEYS)
+    from .native_step import (COMM, COPY, GROUP, MAIN, NCCL_BF16, REC, RECV, SEG, SEND, SIGNAL,
+                              WAIT, WAITV, NativeStep, comm_ptr, flatten, torch_rccl_path,
+                              PLAN_KEYS)
     from ..utils.native import native
 
     class FanNativeStep(NativeStep):
@@ -674,7 +876,8 @@ def _fan_native_step_class():
         stream 1; the DP buckets of a replicated stage follow the last group."""
 
         def __init__(self, executor, mesh: FanMesh, sched: FanSchedule,
-                     comms: Optional[dict] = None, build_only: bool = False):
+                     comms: Optional[dict] = None, build_only: bool = False,
+                     ipc: Optional[FanIpcPipe] = None):
             if len(executor.stages) != 1 or mesh.layout.colocated:
                 raise ValueError("native fan step: one stage per rank (a co-located layout "
                                  "runs the Python executor)")
@@ -683,7 +886,11 @@ def _fan_native_step_class():
                 raise ValueError("native fan step needs a recorded stage (compile_native)")
             self.ex, self.mesh, self.st, self.sched = executor, mesh, st, sched
             self.lay = mesh.layout
-            self.transport, self.ipc, self.mode = "rccl", None, "fan-slotted"
+            # transport "ipc" (a FanIpcPipe): the hops are peer copies + flags on ONE stream in
+            # the schedule's clock order; "rccl": one grouped RCCL call per clock slot
+            self.transport = "ipc" if ipc is not None else "rccl"
+            self.ipc = ipc
+            self.mode = "fan-ipc-slotted" if ipc is not None else "fan-slotted"
             self.dp = mesh.dp
             self.sharded = st.params.sharded
             self.pp = self.lay.S
@@ -693,15 +900,19 @@ def _fan_native_step_class():
                 self.n.nccl_load(torch_rccl_path())
                 for name, g in (("f_in", mesh.fwd_in), ("f_out", mesh.fwd_out),
                                 ("b_in", mesh.bwd_in), ("b_out", mesh.bwd_out)):
-                    if g is not None:
+                    if g is not None and ipc is None:
                         self.comms[name] = comm_ptr(g, st.device)
                 if self.dp > 1 or self.sharded:
                     self.comms["dp"] = comm_ptr(mesh.dp_group, st.device)
                 self._check_comm_ranks()
             self._ev = 0
             self.ops = []
-            self._build()
-            self.n_streams = 2
+            if ipc is not None:
+                self._build_fan_ipc()
+                self.n_streams = 1
+            else:
+                self._build()
+                self.n_streams = 2
             if build_only:
                 return
             import os
@@ -718,7 +929,55 @@ def _fan_native_step_class():
             """First global rank of the boundary group a link channel lives on."""
             s = self.mesh.stage
             b = s - 1 if name in ("f_in", "b_out") else s
-            return self.lay.offsets[b]
+            return self.lay.boundary_ranks(b)[0]
+
+        def _build_fan_ipc(self) -> None:
+            """The IPC form: at clock slot t a rank enqueues (0) its sends of slot t -- before
+            the first write to a peer in a step, the wait for that peer's ack of the previous
+            step; then the copy and the peer's flag --, (2) its flag waits of slot t, (3) its
+            compute of slot t, all on ONE stream. A wait of slot t is released only by sends of
+            slot t, which every rank enqueues before its own waits of slot t, and a send waits
+            on nothing but the previous step's acks: the plan completes whatever order an
+            executor runs independent work in (the uniform pipeline's ipc-slotted argument,
+            native_step._build_ipc_slotted), and its graph is a single chain."""
+            self._check_w(self.ex.ops[0])
+            m, st, lay, p = self.mesh, self.st, self.lay, self.ipc
+            me, s = m.rank, m.stage
+            slot = fan_slots(self.sched)
+            entries = []
+            for op, j in self.sched.ops[(s, m.replica)]:
+                jj = lay.local_index(s, j)
+                entries.append((slot[(s, op, j)], 3,
+                                [dict(kind=SEG, stream=MAIN, prog=st._prog, seg=f"{op}{jj}")]))
+            for t, d, j, src, dst in fan_messages(self.sched):
+                if src == me:
+                    jj = lay.local_index(s, j)
+                    peer, dst_a, src_a, nb, flag = p.send_desc(d, jj)
+                    entries.append((t, 0, [("ack", d, peer),
+                                           dict(kind=COPY, stream=MAIN, a=src_a, b=dst_a,
+                                                count=nb, tag=(d, j, 0), gpeer=peer),
+                                           dict(kind=SIGNAL, stream=MAIN, a=flag, delta=0,
+                                                tag=(d, j, 0), gpeer=peer)]))
+                if dst == me:
+                    jj = lay.local_index(s, j)
+                    idx = p.fidx(jj) if d == "f" else p.bidx(jj)
+                    entries.append((t, 2, [dict(kind=WAITV, stream=MAIN,
+                                                a=p.flags_addr + 4 * idx, delta=0,
+                                                tag=(d, j, 0), gpeer=src)]))
+            acked = set()
+            for _, _, ops in sorted(entries, key=lambda e: (e[0], e[1])):
+                for o in ops:
+                    if isinstance(o, tuple):  # the previous step's ack, before the 1st write
+                        _, d, peer = o
+                        if (d, peer) not in acked:
+                            acked.add((d, peer))
+                            self.ops.append(dict(kind=WAITV, stream=MAIN,
+                                                 a=p.ack_wait_addr(d, peer), delta=-1))
+                        continue
+                    self.ops.append(o)
+            self._wgrad_update(MAIN)
+            for a in p.ack_signals():  # my receive buffers are free for the next step
+                self.ops.append(dict(kind=SIGNAL, stream=MAIN, a=a, delta=0))
 
         def _check_comm_ranks(self) -> None:
             n, m, lay = self.n, self.mesh, self.lay

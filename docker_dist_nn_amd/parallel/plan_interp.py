@@ -13,6 +13,9 @@ every RCCL operation mapped onto gloo on host copies of the addressed bytes:
   ALLREDUCE      in-place sum over the group;  REDUCE_SCATTER ``a`` (count x group size) -> ``b``;
   ALL_GATHER     ``a`` (count) -> ``b`` (count x group size)
   REC / WAIT     host-side event flags between the plan's streams
+  COPY / SIGNAL / WAITV   (IPC plans) the real device ops on the interpreter's stream: a peer
+                 copy into an IPC-mapped buffer, a flag store / wait at step number + delta
+                 (processes sharing one GPU map each other's memory)
 
 Streams are interpreted cooperatively (each advances while its head op can), so a plan whose
 streams block each other shows up as an interpreter stall (a timeout naming the stream heads),
@@ -28,8 +31,8 @@ from typing import Optional
 import torch
 import torch.distributed as dist
 
-from .native_step import (ALL_GATHER, ALLREDUCE, ESIZE, GROUP, NCCL_BF16, NCCL_F32, NCCL_U8,
-                          REC, RECV, REDUCE_SCATTER, SEG, SEND, WAIT)
+from .native_step import (ALL_GATHER, ALLREDUCE, COPY, ESIZE, GROUP, NCCL_BF16, NCCL_F32,
+                          NCCL_U8, REC, RECV, REDUCE_SCATTER, SEG, SEND, SIGNAL, WAIT, WAITV)
 
 DTYPES = {NCCL_BF16: torch.bfloat16, NCCL_F32: torch.float32, NCCL_U8: torch.uint8}
 
@@ -142,6 +145,13 @@ class PlanInterpreter:
         ns = self.ns
         p = ns.st.params
         p.set_lr(p.optim.lr)
+        ipc = getattr(ns, "ipc", None)
+        if ipc is not None:
+            from ..utils.native import native
+
+            nat = native()
+            ipc.seq += 1
+            seq = ipc.seq
         head = {s: 0 for s in self.queues}
         events: set = set()
         inflight: dict[int, list] = {}
@@ -163,6 +173,12 @@ class PlanInterpreter:
                             del inflight[s]
                         elif k == SEG:
                             o["prog"].run([o["seg"]], self.stream.cuda_stream)
+                        elif k == COPY:
+                            nat.copy_async(o["b"], o["a"], o["count"], self.stream.cuda_stream)
+                        elif k == SIGNAL:
+                            nat.signal_u32(self.stream.cuda_stream, o["a"], seq + o["delta"])
+                        elif k == WAITV:
+                            nat.wait_geq_u32(self.stream.cuda_stream, o["a"], seq + o["delta"])
                         elif k == REC:
                             events.add(o["event"])
                         elif k == WAIT:

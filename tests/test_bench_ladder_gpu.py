@@ -2,7 +2,9 @@
 launched by torch.distributed.run exactly as the driver launches bench.py. Rung 1 hangs on
 rank 0 (the first-step watchdog ends it), rung 2 crashes on rank 1 (rank 0's child is killed
 by its supervisor), rung 3 measures -- and rank 0 still prints ONE JSON line, with the
-attempts listed, followed by the data-parallel comparison run the same way."""
+attempts listed, followed by the data-parallel comparison run the same way. (The literal
+uniform grid: at N = 2 the planner's default is a co-located fan layout, whose own rungs
+tests/test_fan_gpu.py covers.)"""
 import json
 import os
 import socket
@@ -34,7 +36,8 @@ def test_bench_ladder_survives_hang_and_crash(tmp_path):
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                         "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
                         "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
-                        "--gpus", "2", "--steps", "3", "--warmup", "1", "--batch", "2048"],
+                        "--gpus", "2", "--steps", "3", "--warmup", "1", "--batch", "2048",
+                        "--parallelism", "uniform"],
                        env=env, stdout=subprocess.PIPE, stderr=None, text=True, timeout=280,
                        cwd=ROOT)  # stderr streams (run with -s): the attempts' progress
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -53,7 +56,7 @@ def test_bench_ladder_survives_hang_and_crash(tmp_path):
     assert att[2]["ok"] and att[2]["rc"] == {"0": "0", "1": "0"}
     assert out["ladder_rung"] == "rccl-slotted"
     assert out["dp_only"]["value"] > 0 and out["dp_only"]["parallelism"] == "dp2"
-    assert [a["rung"] for a in lad["dp_attempts"]] == ["dp-native"]
+    assert [a["rung"] for a in lad["compare_attempts"]] == ["dp-native"]
 
 
 @pytest.mark.timeout(300)
@@ -74,7 +77,8 @@ def test_bench_ladder_steady_state_hangs_and_sigterm(tmp_path):
     p = subprocess.Popen([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                           "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
                           "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
-                          "--gpus", "2", "--steps", "20", "--warmup", "2", "--batch", "2048"],
+                          "--gpus", "2", "--steps", "20", "--warmup", "2", "--batch", "2048",
+                          "--parallelism", "uniform"],
                          env=env, stdout=subprocess.PIPE, stderr=None, text=True, cwd=ROOT)
     # every rung hangs after its first steps: two stalled attempts (spawn + steps + 12 s
     # stall each, ~16-18 s on the box) fit well inside 75 s, and no rung can succeed

@@ -25,7 +25,7 @@ def _port():
 
 
 def _worker(rank, world, port, dist_, reps, M, dp_reduce, use_interp, steps, out_dir, tag,
-            place=None):
+            place=None, ipc=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DNN_DP_DEFER="0")
     import torch.distributed as dist
 
@@ -43,10 +43,17 @@ def _worker(rank, world, port, dist_, reps, M, dp_reduce, use_interp, steps, out
     mesh = build_fan_mesh(lay)
     mb = 256
     tr = FanTrainer(MLPSpec.parse(SPEC), lay, mesh, micro_batch=mb, num_micro=M, device=dev,
-                    dp_reduce=dp_reduce, optim=OptimConfig(name="sgd", lr=0.05, momentum=0.9))
+                    dp_reduce=dp_reduce, optim=OptimConfig(name="sgd", lr=0.05, momentum=0.9),
+                    ipc_rehearsal=ipc)
     assert tr.native_step is None  # gloo: the Python executor, unless interpreted below
     it = None
-    if use_interp:
+    if ipc:  # the IPC fan plan: real peer copies + flags, the DP buckets over gloo
+        groups = {"dp": mesh.dp_group} if mesh.dp_group is not None else {}
+        ns = FanNativeStep(tr.executor, mesh, tr.sched, comms={k: k for k in groups},
+                           build_only=True, ipc=tr.ipc_pipe)
+        assert ns.transport == "ipc" and ns.mode == "fan-ipc-slotted"
+        it = PlanInterpreter(ns, groups, timeout_s=60)
+    elif use_interp:
         names = {"f_in": mesh.fwd_in, "f_out": mesh.fwd_out, "b_in": mesh.bwd_in,
                  "b_out": mesh.bwd_out, "dp": mesh.dp_group}
         comms = {k: k for k, g in names.items() if g is not None}
@@ -185,3 +192,28 @@ def test_bench_colocated_fan_with_uniform_and_dp_measured(tmp_path):
     assert dp["value"] > 0 and dp["parallelism"] == "dp4", dp
     assert out["ladder"]["seconds"] < 540
     assert [a["rung"] for a in out["ladder"]["compare_attempts"]] == ["uniform", "dp-native"]
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("dist_,reps,M,dp_reduce", [([3, 1], [3, 1], 7, "allreduce"),
+                                                    ([2, 2], [1, 3], 6, "shard")])
+def test_fan_ipc_plan_bitwise_equals_python(dev, dist_, reps, M, dp_reduce):
+    """the fan step on the xGMI peer-write transport -- the EXACT op list of
+    FanNativeStep's IPC form (one stream, copies into IPC-mapped L2-uncached receive rows +
+    step-numbered flags + per-peer acks) with real device copies / flags between processes
+    sharing cuda:0 -- trains bit for bit like the Python executor over gloo, for three steps
+    (the acks of one step gate the writes of the next)."""
+    world, steps = sum(reps), 3
+    with tempfile.TemporaryDirectory() as d:
+        for ipc, tag in ((False, "py"), (True, "ipc")):
+            mp.start_processes(_worker, args=(world, _port(), dist_, reps, M, dp_reduce, False,
+                                              steps, d, tag, None, ipc),
+                               nprocs=world, join=True, start_method="spawn")
+        for k in range(4):
+            for wb in ("w", "b"):
+                a = np.load(os.path.join(d, f"py_{wb}{k}.npy"))
+                b = np.load(os.path.join(d, f"ipc_{wb}{k}.npy"))
+                assert np.array_equal(a, b), (wb, k)
+        for q in range(reps[-1]):
+            assert np.array_equal(np.load(os.path.join(d, f"py_loss{q}.npy")),
+                                  np.load(os.path.join(d, f"ipc_loss{q}.npy")))

@@ -198,9 +198,9 @@ def test_fan_rungs():
     from docker_dist_nn_amd.ladder import bench_rungs
 
     names = [r.name for r in bench_rungs(8, fan=True)]
-    assert names == ["default", "fan-python", "uniform-rccl-slotted", "uniform-python",
-                     "dp-native", "dp-python"]
-    assert "--parallelism" in bench_rungs(8, fan=True)[2].args
+    assert names == ["default", "fan-rccl", "fan-python", "uniform-rccl-slotted",
+                     "uniform-python", "dp-native", "dp-python"]
+    assert "--parallelism" in bench_rungs(8, fan=True)[3].args
 
 
 # Main measurement + two comparisons (bench.py supervise: the literal uniform pipeline, then

@@ -206,7 +206,7 @@ def test_capture_after_eager_cross_step_bitwise(dev, monkeypatch):
         tr.set_batch(x, y)
         tr.step()
     tr.set_batch(x, y)
-    tr.capture(copies=1)
+    tr.capture(warmup=0, copies=1)  # executes one real step
     for _ in range(2):
         tr.step()
     torch.cuda.synchronize()
