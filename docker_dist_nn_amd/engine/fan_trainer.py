@@ -69,7 +69,10 @@ class FanTrainer(Trainer):
                  hop_cost: float = 0.0, ipc_rehearsal: bool = False):
         """``ipc_rehearsal`` (one-GPU tests: ranks sharing a GPU over gloo): set up the IPC
         transport (``self.ipc_pipe``) whatever the backend, for a test that runs the IPC fan
-        plan through the plan interpreter; the Python executor keeps the gloo FanPipe."""
+        plan through the plan interpreter; the Python executor keeps the gloo FanPipe.
+        ``ipc_rehearsal="native"``: the IPC fan plan as the rank's real StepPlan (eager or
+        captured, Trainer.capture) -- layouts without replicated stages only, since a DP
+        group's buckets are RCCL calls and RCCL runs one rank per GPU."""
         if sum(layout.dist) != len(spec.layers):
             raise ValueError(f"fan layout {layout.dist} does not cover {len(spec.layers)} layers")
         layout.check_directions(num_micro)
@@ -207,6 +210,17 @@ class FanTrainer(Trainer):
                         "order on one stream (verification pending: first step)")
             if ipc_why is not None and self.transport != "ipc":
                 self.transport_reason += f"; IPC not used: {ipc_why}"
+        if ipc_rehearsal == "native":
+            from ..parallel.fan import FanNativeStep
+
+            if max(layout.reps) > 1 or layout.colocated:
+                raise ValueError("native IPC fan rehearsal: one replica per stage (DP buckets "
+                                 "are RCCL calls, one rank per GPU)")
+            self.native_step = FanNativeStep(self.executor, mesh, self.sched, comms={},
+                                             ipc=self.ipc_pipe)
+            self.executor.native_step = self.native_step
+            self.executor.pipe = self.pipe = self.ipc_pipe
+            self.transport = "ipc"
         self._graph = None
         self._graphs = []
         self._stream = None

@@ -369,7 +369,12 @@ class Supervisor:
                 key = self._key(self._n, f"skip{k}")
                 if self.rank == 0:
                     now = time.monotonic()
-                    why = ("deadline" if self.deadline is not None and now > self.deadline else
+                    # a peer whose (own-clock) deadline ended the last attempt ends the ladder
+                    # too, even when rank 0's clock has a moment left
+                    peer_late = bool(self.attempts) and \
+                        "deadline" in self.attempts[-1].get("rc", {}).values()
+                    why = ("deadline" if self.deadline is not None and
+                           (now > self.deadline or peer_late) else
                            "budget" if budget_s is not None and k < len(rungs) - 1 and
                            now - t0 > budget_s else "")
                     self.store.set(key, why)

@@ -25,7 +25,7 @@ def _port():
 
 
 def _worker(rank, world, port, dist_, reps, M, dp_reduce, use_interp, steps, out_dir, tag,
-            place=None, ipc=False):
+            place=None, ipc=False, graph=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DNN_DP_DEFER="0")
     import torch.distributed as dist
 
@@ -45,9 +45,9 @@ def _worker(rank, world, port, dist_, reps, M, dp_reduce, use_interp, steps, out
     tr = FanTrainer(MLPSpec.parse(SPEC), lay, mesh, micro_batch=mb, num_micro=M, device=dev,
                     dp_reduce=dp_reduce, optim=OptimConfig(name="sgd", lr=0.05, momentum=0.9),
                     ipc_rehearsal=ipc)
-    assert tr.native_step is None  # gloo: the Python executor, unless interpreted below
+    assert (tr.native_step is None) == (ipc != "native")  # gloo: the Python executor
     it = None
-    if ipc:  # the IPC fan plan: real peer copies + flags, the DP buckets over gloo
+    if ipc and ipc != "native":  # the IPC fan plan: real peer copies + flags, the DP buckets over gloo
         groups = {"dp": mesh.dp_group} if mesh.dp_group is not None else {}
         ns = FanNativeStep(tr.executor, mesh, tr.sched, comms={k: k for k in groups},
                            build_only=True, ipc=tr.ipc_pipe)
@@ -64,7 +64,13 @@ def _worker(rank, world, port, dist_, reps, M, dp_reduce, use_interp, steps, out
     xt = torch.zeros(mb * M, 832, dtype=torch.bfloat16)
     xt[:, :784] = torch.from_numpy(x).to(torch.bfloat16)
     xt, yt = xt.to(dev), torch.from_numpy(y).to(dev)
-    for _ in range(steps):
+    done = 0
+    if graph:  # the capture executes one real step; the rest are replays
+        tr.set_global_batch(xt, yt)
+        tr.capture(warmup=0)
+        assert tr.graph_nodes > 0
+        done = 1
+    for _ in range(steps - done):
         tr.set_global_batch(xt, yt)
         if it is None:
             tr.step()
@@ -217,3 +223,29 @@ def test_fan_ipc_plan_bitwise_equals_python(dev, dist_, reps, M, dp_reduce):
         for q in range(reps[-1]):
             assert np.array_equal(np.load(os.path.join(d, f"py_loss{q}.npy")),
                                   np.load(os.path.join(d, f"ipc_loss{q}.npy")))
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("dist_,M", [([3, 1], 4), ([1, 1, 2], 5)])
+def test_fan_ipc_native_step_graph_capture(dev, dist_, M):
+    """the IPC fan plan as the rank's real StepPlan (device step-number flags,
+    per-peer acks, peer copies in clock order on one stream) -- eager, and captured into a HIP
+    graph and replayed -- trains bit for bit like the Python executor. One replica per stage:
+    on one GPU the ranks cannot open an RCCL DP group (one rank per GPU), so replicated stages
+    are rehearsed through the plan interpreter above."""
+    reps, steps = [1] * len(dist_), 4
+    world = len(dist_)
+    with tempfile.TemporaryDirectory() as d:
+        for ipc, graph, tag in ((False, False, "py"), ("native", False, "eager"),
+                                ("native", True, "graph")):
+            mp.start_processes(_worker, args=(world, _port(), dist_, reps, M, "allreduce", False,
+                                              steps, d, tag, None, ipc, graph),
+                               nprocs=world, join=True, start_method="spawn")
+        for tag in ("eager", "graph"):
+            for k in range(4):
+                for wb in ("w", "b"):
+                    a = np.load(os.path.join(d, f"py_{wb}{k}.npy"))
+                    b = np.load(os.path.join(d, f"{tag}_{wb}{k}.npy"))
+                    assert np.array_equal(a, b), (tag, wb, k)
+            assert np.array_equal(np.load(os.path.join(d, "py_loss0.npy")),
+                                  np.load(os.path.join(d, f"{tag}_loss0.npy")))
