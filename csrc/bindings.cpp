@@ -725,8 +725,7 @@ PYBIND11_MODULE(_native, m) {
   m.def(
       "run_plan",
       [](const std::vector<std::tuple<const dnn::Program*, std::string, int>>& plan,
-         uintptr_t stream, uintptr_t side, bool device_fence, uint64_t xkey, uintptr_t flags,
-         uint32_t epoch, uintptr_t err, double timeout_s) {
+         uintptr_t stream, uintptr_t side, bool device_fence, uint64_t xkey) {
         py::gil_scoped_release nogil;
         // fork / join events: both streams are on this device, so the ordering needs no
         // system-scope fence (cache write-back / invalidate at every record: the ~6 us
@@ -761,42 +760,7 @@ PYBIND11_MODULE(_native, m) {
           return e;
         };
         std::vector<std::string> one(1);
-        // flag edges ("@sig:<k>", "@gate:<k>:<delta>", "@gatev:<k>:<delta>"): stream order
-        // through a per-executor flag word instead of an event record + wait. "@sig" is a
-        // one-lane kernel storing `epoch` (system-scope release, after the kernels before it on
-        // its stream); "@gate" a one-lane kernel spinning until the word reaches epoch + delta
-        // (bounded: after timeout_s it gives up and sets *err); "@gatev" the same wait as a
-        // hipStreamWaitValue32 packet. A signal costs its stream a tiny kernel, not a barrier
-        // packet (~4-6 us of queue time each on the main stream: profiles/r6_headline).
-        auto flag_word = [&](const std::string& rest, int* delta) -> uint32_t* {
-          if (!flags) throw std::invalid_argument("run_plan: flag edge without a flag block");
-          const size_t c = rest.find(':');
-          const int k = std::stoi(rest.substr(0, c));
-          *delta = c == std::string::npos ? 0 : std::stoi(rest.substr(c + 1));
-          return reinterpret_cast<uint32_t*>(flags) + k;
-        };
         for (const auto& [pr, seg, si] : plan) {
-          if (seg.rfind("@sig:", 0) == 0 || seg.rfind("@gate:", 0) == 0 ||
-              seg.rfind("@gatev:", 0) == 0) {
-            if (si && !side) throw std::invalid_argument("run_plan: flag edge without a side");
-            hipStream_t st = si ? S(side) : S(stream);
-            int delta = 0;
-            if (seg[1] == 's') {
-              if (dnn::p2p_signal(flag_word(seg.substr(5), &delta), epoch, st) != 0)
-                throw std::runtime_error("run_plan: @sig failed");
-            } else if (seg[5] == 'v') {
-              uint32_t* w = flag_word(seg.substr(7), &delta);
-              if (hipStreamWaitValue32(st, w, epoch + (uint32_t)delta, hipStreamWaitValueGte,
-                                       0xFFFFFFFFu) != hipSuccess)
-                throw std::runtime_error("run_plan: @gatev failed");
-            } else {
-              uint32_t* w = flag_word(seg.substr(6), &delta);
-              if (dnn::p2p_wait_val(w, epoch + (uint32_t)delta,
-                                    reinterpret_cast<uint32_t*>(err), timeout_s, st) != 0)
-                throw std::runtime_error("run_plan: @gate failed");
-            }
-            continue;
-          }
           if (seg.rfind("@xmark:", 0) == 0 || seg.rfind("@xwait:", 0) == 0) {
             if (!side) throw std::invalid_argument("run_plan: cross-step event without a side");
             hipEvent_t e = xevent(seg.substr(7));
@@ -820,8 +784,7 @@ PYBIND11_MODULE(_native, m) {
         }
       },
       py::arg("plan"), py::arg("stream"), py::arg("side") = 0, py::arg("device_fence") = false,
-      py::arg("xkey") = 0, py::arg("flags") = 0, py::arg("epoch") = 0, py::arg("err") = 0,
-      py::arg("timeout_s") = 2.0);
+      py::arg("xkey") = 0);
   m.def("record_begin", [](dnn::Program& pr) {
     if (dnn::recording_program()) throw std::runtime_error("already recording a Program");
     dnn::recording_program() = &pr;

@@ -860,38 +860,6 @@ __global__ void p2p_wait_seq_kernel(const unsigned* flag, const unsigned* seq, i
   }
 }
 
-// Host-value form (single-process step plans' "@gate" edges): wait until *flag >= target
-// (wrapping compare), same bounded spin as p2p_wait_seq_kernel.
-__global__ void p2p_wait_val_kernel(const unsigned* flag, unsigned target, unsigned* err,
-                                    unsigned long long timeout_ticks) {
-  const unsigned l = threadIdx.x;
-  if (l != 0) return;
-  const unsigned long long t0 = wall_clock64();
-  while ((int)(__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - target) <
-         0) {
-    __builtin_amdgcn_s_sleep(2);
-    if (wall_clock64() - t0 > timeout_ticks) {
-      __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      return;
-    }
-  }
-}
-
-int p2p_wait_val(const uint32_t* flag, uint32_t target, uint32_t* err, double timeout_s,
-                 hipStream_t stream) {
-  if (reinterpret_cast<uintptr_t>(flag) & 3) return -1;
-  static int rate_khz = [] {  // wall_clock64 ticks per ms (100 MHz on gfx9)
-    int r = 0, dev = 0;
-    if (hipGetDevice(&dev) == hipSuccess)
-      (void)hipDeviceGetAttribute(&r, hipDeviceAttributeWallClockRate, dev);
-    return r > 0 ? r : 100000;
-  }();
-  const unsigned long long ticks = (unsigned long long)(timeout_s * 1e3 * (double)rate_khz);
-  hipLaunchKernelGGL(p2p_wait_val_kernel, dim3(1), dim3(64), 0, stream, flag, target, err,
-                     ticks);
-  return hipGetLastError() == hipSuccess ? 0 : -9;
-}
-
 int p2p_seq_advance(uint32_t* seq, hipStream_t stream) {
   hipLaunchKernelGGL(p2p_seq_advance_kernel, dim3(1), dim3(64), 0, stream, seq);
   return hipGetLastError() == hipSuccess ? 0 : -9;

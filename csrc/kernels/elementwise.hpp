@@ -111,9 +111,6 @@ int bias_act_cast(const float* in, long ld_in, const float* bias, int act, uint1
 // Peer copy (16-byte aligned) and flag write as kernels: never block the issuing host thread.
 int p2p_copy(void* dst, const void* src, size_t bytes, hipStream_t stream);
 int p2p_signal(uint32_t* flag, uint32_t value, hipStream_t stream);
-// Wait until *flag >= target (host value; bounded: gives up after timeout_s, *err = 1).
-int p2p_wait_val(const uint32_t* flag, uint32_t target, uint32_t* err, double timeout_s,
-                 hipStream_t stream);
 // Device-sequence flag protocol (graph-capturable): seq advanced in-stream, signal writes
 // *seq + delta, wait spins until flag >= *seq + delta or times out (sets *err).
 int p2p_seq_advance(uint32_t* seq, hipStream_t stream);

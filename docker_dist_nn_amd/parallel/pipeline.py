@@ -258,8 +258,6 @@ class PipelineExecutor:
     def flush(self) -> None:
         """Apply every deferred update now (end of training / before reading weights)."""
         self.xstep_join()
-        if getattr(self, "_ferr", None) is not None and int(self._ferr.item()):
-            raise RuntimeError("DNN_FLAG_EDGES: a flag gate timed out (stream order lost)")
         for st in self.stages:
             pend = self._pending.pop(id(st), None)
             if pend is not None:
@@ -530,9 +528,6 @@ class PipelineExecutor:
                 self.stages[0].flip_h0()
             if switches.get("DNN_XSTEP") == "1":
                 plan = self._xstep_plan(plan)
-            fe = switches.get("DNN_FLAG_EDGES")
-            if fe != "0":
-                plan = self._flag_plan(plan, fe)
         if plan is not None:
             dev = self.stages[0].device
             if getattr(self, "_xprimed", False) and any(
@@ -547,17 +542,11 @@ class PipelineExecutor:
                                        any(e[1] == "@fork" for e in plan)):
                 self._side = torch.cuda.Stream(dev)
             main = cur = torch.cuda.current_stream(dev)
-            fl = getattr(self, "_flags", None)
-            if fl is not None:
-                self._fepoch += 1
             native().run_plan([(st._prog if st is not None else None, seg, si)
                                for st, seg, si in plan],
                               main.cuda_stream,
                               self._side.cuda_stream if self._side is not None else 0,
-                              switches.get("DNN_EVENT_FENCE") == "device", id(self),
-                              fl.data_ptr() if fl is not None else 0,
-                              self._fepoch if fl is not None else 0,
-                              self._ferr.data_ptr() if fl is not None else 0)
+                              switches.get("DNN_EVENT_FENCE") == "device", id(self))
             for st in self.stages:
                 st.params.step_count += 1
             self.pipe.end_step()
@@ -609,49 +598,6 @@ class PipelineExecutor:
             self._xprimed = True
             return [e for e in out if not e[1].startswith("@xwait")]
         self._xpending = True
-        return out
-
-    def _flag_plan(self, plan, mode: str):
-        """DNN_FLAG_EDGES (opt-in A/B, round 6): the cross-stream edges of a single-stage
-        overlap plan as flag words instead of event record / wait pairs. A run of forks with no
-        main-stream work between them becomes ONE "@sig" (a one-lane kernel) on the main stream,
-        and each fork's side-stream wait a "@gate" on that word (mode 1: a one-lane wait kernel;
-        2: a hipStreamWaitValue32 packet) -- the side keeps its stagger, the main stream loses
-        its record packets. The cross-step "@xwait:end" becomes a main-stream gate kernel on a
-        word the side stream signals after its last op. Mode 3: only that cross-step edge."""
-        if self._side is None:
-            return plan
-        if getattr(self, "_flags", None) is None:
-            dev = self.stages[0].device
-            self._flags = torch.zeros(8, dtype=torch.int32, device=dev)
-            self._ferr = torch.zeros(1, dtype=torch.int32, device=dev)
-            self._fepoch = 0
-        END = 7
-        gate = "@gatev" if mode == "2" else "@gate"
-        out, k, sig_k, main_work = [], -1, None, True
-        for e in plan:
-            st, seg, si = e
-            if seg == "@fork" and mode in ("1", "2"):
-                if main_work or sig_k is None:
-                    k += 1
-                    if k >= END:
-                        return plan
-                    sig_k = k
-                    out.append((None, f"@sig:{k}", 0))
-                    main_work = False
-                out.append((None, f"{gate}:{sig_k}:0", 1))
-                continue
-            if seg == "@xwait:end" and getattr(self, "_fsig_end", None) == self._fepoch:
-                out.append((None, f"@gate:{END}:-1", 0))  # the previous step signalled it
-                continue
-            if seg == "@xmark:end":
-                self._fsig_end = self._fepoch + 1  # this step's epoch (run_step advances it)
-                out.append((None, f"@sig:{END}", 1))
-                out.append(e)
-                continue
-            if st is not None and si == 0 and st._prog.segment_size(seg) > 0:
-                main_work = True
-            out.append(e)
         return out
 
     def xstep_join(self) -> None:

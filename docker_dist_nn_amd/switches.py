@@ -59,10 +59,6 @@ SWITCHES: dict[str, tuple[str, str]] = {
                        "stream during W0, only layer 0's after it (SGD); auto = when no layer "
                        "updates in its wgrad epilogue (mlp8 2.918 -> 2.889 ms, headline "
                        "0.350 -> 0.346, wide excluded: 6.04 -> 6.21)"),
-    "DNN_FLAG_EDGES": ("0", "single-stage overlap plans: cross-stream edges as flag words "
-                            "(a one-lane signal kernel instead of event records on the main "
-                            "stream); 1 = gate kernels on the side, 2 = wait-value packets on "
-                            "the side, 3 = only the cross-step edge; 0 = events (A/B)"),
     "DNN_FIN_WT": ("1", "the fused reduce + SGD/Adam launch (FINO) also writes the W^T "
                         "shadows of the layers it updates (no transpose launch per step)"),
     "DNN_FAULT_NATIVE_STEP": ("", "fault injection (tests): comma-separated ranks whose "

@@ -211,31 +211,3 @@ def test_capture_after_eager_cross_step_bitwise(dev, monkeypatch):
         tr.step()
     torch.cuda.synchronize()
     assert torch.equal(tr.stages[0].params.master, ref.stages[0].params.master)
-
-
-@pytest.mark.parametrize("xstep", ["0", "1"])
-def test_flag_edges_bitwise(dev, monkeypatch, xstep):
-    """DNN_FLAG_EDGES (opt-in): the plan's cross-stream edges as flag words (gate kernels,
-    wait-value packets, or only the cross-step edge) train bit for bit like the event plan,
-    and no gate timed out."""
-    monkeypatch.setenv("DNN_BW_OVERLAP_MIN_ROWS", "0")
-    monkeypatch.setenv("DNN_SPLIT_FINO", "1")
-    monkeypatch.setenv("DNN_XSTEP", xstep)
-    bat = _xstep_batches(dev)
-    res = []
-    for fe in ("0", "1", "2", "3"):
-        monkeypatch.setenv("DNN_FLAG_EDGES", fe)
-        tr = _xstep_trainer(dev, 0, 0.1)
-        losses = []
-        for k in range(6):
-            tr.set_batch(*bat[k % 2], zero_copy=True)
-            tr.step()
-            losses.append(tr.loss())
-        tr.flush()
-        if fe in ("1", "2"):
-            segs = [e[1] for e in tr.executor._flag_plan(tr.executor._native_plan(), fe)]
-            assert any(s.startswith("@sig:") for s in segs) and "@fork" not in segs, segs
-        res.append((losses, tr.stages[0].params.master.clone()))
-    for r in res[1:]:
-        assert r[0] == res[0][0]
-        assert torch.equal(r[1], res[0][1])
