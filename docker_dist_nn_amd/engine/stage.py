@@ -1015,7 +1015,7 @@ class Stage:
         L = len(self.geoms)
         self.h0_double = (switches.get("DNN_H0_DOUBLE") == "1" and self.device.type == "cuda"
                           and self.first and self.last and self.nm == 1 and L >= 2 and
-                          self.relu_mask[0] is None and 0 not in self.actT and
+                          0 not in self.actT and
                           not (self.tail and L - 2 <= 0))
         self._rh0 = None
         if self.h0_double:

@@ -211,3 +211,43 @@ def test_capture_after_eager_cross_step_bitwise(dev, monkeypatch):
         tr.step()
     torch.cuda.synchronize()
     assert torch.equal(tr.stages[0].params.master, ref.stages[0].params.master)
+
+
+def test_cross_step_with_layer0_mask_bitwise(dev, monkeypatch):
+    """The layer-0 fragment-order ReLU mask (DNN_RELU_MASK=2) together with the cross-step plan
+    and the double-buffered layer-0 activation -- overlap modes 1 and 5 -- trains bit for bit
+    like the joined plan with the same mask (the mask is written by the forward and read by
+    the dgrad of the same step, both on the main stream)."""
+    monkeypatch.setenv("DNN_BW_OVERLAP_MIN_ROWS", "0")
+    monkeypatch.setenv("DNN_SPLIT_FINO", "1")
+    monkeypatch.setenv("DNN_RELU_MASK", "2")
+    from docker_dist_nn_amd import NAMED_MODELS
+    from docker_dist_nn_amd.data import synthetic_mnist
+    from docker_dist_nn_amd.engine import OptimConfig, Trainer
+
+    rows = 65536  # the tuned table gives both GEMMs one register-direct tile at this size
+    x, y = synthetic_mnist(2 * rows, seed=11)
+    xb = torch.zeros(2 * rows, 832, dtype=torch.bfloat16)
+    xb[:, :784] = torch.from_numpy(x).to(torch.bfloat16)
+    xb, yb = xb.to(dev), torch.from_numpy(y).to(dev)
+    bat = [(xb[k * rows:(k + 1) * rows], yb[k * rows:(k + 1) * rows]) for k in range(2)]
+    res = []
+    for xs, dbl, mode in (("0", "0", "1"), ("1", "1", "1"), ("1", "1", "5")):
+        monkeypatch.setenv("DNN_XSTEP", xs)
+        monkeypatch.setenv("DNN_H0_DOUBLE", dbl)
+        monkeypatch.setenv("DNN_BW_OVERLAP", mode)
+        tr = Trainer(NAMED_MODELS["mnist-fcnn"], micro_batch=rows, num_micro=1, seed=0,
+                     optim=OptimConfig(lr=0.1, momentum=0.9), device=dev)
+        assert tr.stages[0].relu_mask[0] is not None
+        assert tr.stages[0].h0_double == (dbl == "1")
+        losses = []
+        for k in range(6):
+            tr.set_batch(*bat[k % 2], zero_copy=True)
+            tr.step()
+            losses.append(tr.loss())
+        tr.flush()
+        res.append((losses, tr.stages[0].params.master.clone()))
+    for r in res[1:]:
+        assert r[0] == res[0][0]
+        assert torch.equal(r[1], res[0][1])
+
