@@ -38,6 +38,11 @@ class _RankSteps:
         self.capturing = False
 
     def run_step(self) -> None:
+        if self.native_step is not None:  # the co-located slotted RCCL plan (fan.FanNativeStep)
+            for st in self.stages:
+                st.begin_step()
+            self.native_step.run(torch.cuda.current_stream(self.stages[0].device).cuda_stream)
+            return
         self.pipe.begin_step()
         for ex in self.execs.values():
             st = ex.stages[0]
@@ -163,16 +168,14 @@ class FanTrainer(Trainer):
                                   else ""))
         if mesh.backend == "nccl" and self.native_exec and \
                 switches.get("DNN_NATIVE_DIST") != "0":
-            # the rank's whole step as one StepPlan call (fan.FanNativeStep, slotted RCCL form);
-            # agreed over the world like the uniform mesh's native step (trainer.py). A
-            # co-located layout runs the Python executor on every rank.
+            # the rank's whole step as one StepPlan call (fan.FanNativeStep, slotted RCCL form;
+            # a co-located rank runs all its workers in it); agreed over the world like the
+            # uniform mesh's native step (trainer.py)
             from ..parallel.fan import FanNativeStep
 
             _warm_groups(mesh, self.device)
             err = None
             try:
-                if layout.colocated:
-                    raise ValueError("co-located fan layouts run the Python executor")
                 self.native_step = FanNativeStep(self.executor, mesh, self.sched)
             except Exception as e:
                 err = e

@@ -878,9 +878,14 @@ def _fan_native_step_class():
         def __init__(self, executor, mesh: FanMesh, sched: FanSchedule,
                      comms: Optional[dict] = None, build_only: bool = False,
                      ipc: Optional[FanIpcPipe] = None):
-            if len(executor.stages) != 1 or mesh.layout.colocated:
-                raise ValueError("native fan step: one stage per rank (a co-located layout "
-                                 "runs the Python executor)")
+            if mesh.layout.colocated:
+                if ipc is not None:
+                    raise ValueError("IPC fan step: one stage per rank")
+                self._init_colocated(executor, mesh, sched, comms, build_only)
+                return
+            if len(executor.stages) != 1:
+                raise ValueError("native fan step: one stage per rank")
+            self.colo = False
             st = executor.stages[0]
             if st._prog is None or not st._has_w or not st._o_native:
                 raise ValueError("native fan step needs a recorded stage (compile_native)")
@@ -924,6 +929,171 @@ def _fan_native_step_class():
             self.plan = self.n.StepPlan(self.n_streams, max(1, self._ev))
             for o in flatten(self.ops):
                 self.plan.add(**{k: v for k, v in o.items() if k in PLAN_KEYS})
+
+        # ---- co-located layouts: several workers (stages) on this rank ------------------------
+        def _init_colocated(self, executor, mesh, sched, comms, build_only) -> None:
+            """The slotted RCCL step of a rank hosting several workers (FanLayout.place). Every
+            worker's compute runs on the one compute stream in the rank's clock-slot order; a
+            hop between two workers of this rank is a device copy on that stream right after
+            the producing op (its consumer sits at least one slot later); the other hops are
+            grouped per slot on the boundary communicators ("f<b>" / "b<b>": boundary b's
+            forward / backward group, peers indexed by FanLayout.boundary_ranks) exactly as in
+            the one-worker plan; after the last group each worker's weight gradients and update,
+            stages in descending order (the Python _RankSteps order), a replicated stage's DP
+            buckets on its group ("dp<s>")."""
+            self.colo = True
+            self.ex, self.mesh, self.sched = executor, mesh, sched
+            self.lay = mesh.layout
+            self.workers = list(mesh.workers)
+            self.wstages = {s: executor.execs[s].stages[0] for s, _ in self.workers}
+            for st in self.wstages.values():
+                if st._prog is None or not st._has_w or not st._o_native:
+                    raise ValueError("native fan step needs recorded stages (compile_native)")
+            self.st = self.wstages[mesh.stage]
+            self.stages_all = [self.wstages[k] for k in sorted(self.wstages)]
+            self.transport, self.ipc = "rccl", None
+            self.mode = "fan-slotted-colocated"
+            self.pp = self.lay.S
+            self.dp = mesh.dp
+            self.sharded = self.st.params.sharded
+            self.comms = dict(comms or {})
+            if comms is None and not build_only:
+                self.n = native()
+                self.n.nccl_load(torch_rccl_path())
+                dev = self.st.device
+                for b, g in mesh.bnd_f.items():
+                    self.comms[f"f{b}"] = comm_ptr(g, dev)
+                for b, g in mesh.bnd_b.items():
+                    self.comms[f"b{b}"] = comm_ptr(g, dev)
+                for s_, g in mesh.dp_groups.items():
+                    self.comms[f"dp{s_}"] = comm_ptr(g, dev)
+                for name, comm in self.comms.items():
+                    size, rank = self.n.nccl_comm_info(comm)
+                    if name.startswith("dp"):
+                        s_ = int(name[2:])
+                        want = (self.lay.reps[s_], mesh.replica_at(s_))
+                    else:
+                        ranks = self.lay.boundary_ranks(int(name[1:]))
+                        want = (len(ranks), ranks.index(mesh.rank))
+                    if (size, rank) != want:
+                        raise RuntimeError(f"communicator {name}: (size, rank) = "
+                                           f"{(size, rank)}, the plan assumes {want}")
+            self._ev = 0
+            self.ops = []
+            self._build_colocated()
+            self.n_streams = 2
+            if build_only:
+                return
+            import os
+
+            hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+            if self.n_streams > hwq:
+                raise RuntimeError(f"native fan step needs {self.n_streams} hardware queues")
+            self.n = native()
+            self.plan = self.n.StepPlan(self.n_streams, max(1, self._ev))
+            for o in flatten(self.ops):
+                self.plan.add(**{k: v for k, v in o.items() if k in PLAN_KEYS})
+
+        def _build_colocated(self) -> None:
+            lay, m, sch = self.lay, self.mesh, self.sched
+            me = m.rank
+            slot = fan_slots(sch)
+            mine = {s for s, _ in self.workers}
+            # every hop with its stages: (slot, direction, j, src stage, dst stage)
+            msgs = []
+            for (s, op, j), t in slot.items():
+                if op == "F" and s + 1 < lay.S:
+                    msgs.append((t + 1, "f", j, s, s + 1))
+                elif op == "B" and s > 0:
+                    msgs.append((t + 1, "b", j, s, s - 1))
+            rank_of = lambda s_, j_: lay.rank_of(s_, lay.replica_of(s_, j_))  # noqa: E731
+            sends, recvs, local = {}, {}, set()
+            for t, d, j, s0, s1 in sorted(msgs):
+                src, dst = rank_of(s0, j), rank_of(s1, j)
+                if src == me and dst == me:
+                    local.add((d, j, s0))
+                elif src == me:
+                    sends.setdefault(t, []).append((d, j, s0, s1, dst))
+                elif dst == me:
+                    recvs.setdefault(t, []).append((d, j, s0, s1, src))
+            consumed, produced, group_ev = {}, {}, {}
+            for t in sorted(recvs):
+                group_ev[t] = self._event()
+                for d, j, s0, s1, _ in recvs[t]:
+                    consumed[(d, j, s1)] = group_ev[t]
+            entries = []
+            for s, q in self.workers:
+                st = self.wstages[s]
+                for op, j in sch.ops[(s, q)]:
+                    d, ops = op.lower(), []
+                    if (d, j, s) in consumed:
+                        ops.append(dict(kind=WAIT, stream=MAIN, event=consumed[(d, j, s)]))
+                    jj = lay.local_index(s, j)
+                    ops.append(dict(kind=SEG, stream=MAIN, prog=st._prog, seg=f"{op}{jj}"))
+                    t1 = s + 1 if d == "f" else s - 1
+                    if 0 <= t1 < lay.S:
+                        if (d, j, s) in local:  # the consumer is on this rank: device copy
+                            dst_st = self.wstages[t1]
+                            jt = lay.local_index(t1, j)
+                            src_t = st.output if d == "f" else st.dx_send
+                            dst_t = dst_st.x_in if d == "f" else dst_st.grad_out
+                            sv, dv = src_t[st.rows_of(jj)], dst_t[dst_st.rows_of(jt)]
+                            ops.append(dict(kind=COPY, stream=MAIN, a=sv.data_ptr(),
+                                            b=dv.data_ptr(), count=sv.numel() * 2,
+                                            tag=(d, j, 0), gpeer=me))
+                        else:
+                            produced[(d, j, s)] = e = self._event()
+                            ops.append(dict(kind=REC, stream=MAIN, event=e))
+                    entries.append((slot[(s, op, j)], 1, s, ops))
+            for t in sorted(set(sends) | set(recvs)):
+                ops, members = [], []
+                for d, j, s0, s1, dst in sends.get(t, []):
+                    ops.append(dict(kind=WAIT, stream=COMM, event=produced[(d, j, s0)]))
+                    members.append(self._colo_p2p(SEND, d, j, s0, dst))
+                for d, j, s0, s1, src in recvs.get(t, []):
+                    members.append(self._colo_p2p(RECV, d, j, s1, src))
+                ops.append(dict(kind=GROUP, stream=COMM, ops=members, tag=("slot", t)))
+                if t in group_ev:
+                    ops.append(dict(kind=REC, stream=COMM, event=group_ev[t]))
+                entries.append((t, 0, -1, ops))
+            for _, _, _, ops in sorted(entries, key=lambda e: (e[0], e[1], e[2])):
+                self.ops += ops
+            for s in sorted(mine, reverse=True):  # weight gradients + update per worker
+                st = self.wstages[s]
+                self._check_w(self.ex.execs[s].ops[0])
+                self.st, self.dp, self.sharded = st, lay.reps[s], st.params.sharded
+                self.comms["dp"] = self.comms.get(f"dp{s}", 0)
+                self._wgrad_update(COMM)
+            self.comms.pop("dp", None)
+            self.st, self.dp = self.wstages[m.stage], m.dp
+
+        def _colo_p2p(self, kind: int, d: str, j: int, s: int, other: int) -> dict:
+            """Member of a slot group for worker ``s``'s side of micro-batch j's hop: its own
+            rows, on the boundary communicator of that hop, peer = the other rank's index in
+            the boundary's rank list."""
+            lay, st = self.lay, self.wstages[s]
+            inbound = kind == RECV
+            if d == "f":
+                b = s - 1 if inbound else s
+            else:
+                b = s if inbound else s - 1
+            t = (st.x_in if d == "f" else st.grad_out) if inbound else \
+                (st.output if d == "f" else st.dx_send)
+            v = t[st.rows_of(lay.local_index(s, j))]
+            name = f"{d}{b}"
+            return dict(kind=kind, stream=COMM, comm=self.comms.get(name, 0), a=v.data_ptr(),
+                        count=v.numel(), dtype=NCCL_BF16,
+                        peer=lay.boundary_ranks(b).index(other), gpeer=other,
+                        tag=(d, j, 0))
+
+        def run(self, stream: int) -> None:
+            if not self.colo:
+                return NativeStep.run(self, stream)
+            for st in self.stages_all:
+                st.params.set_lr(st.params.optim.lr)
+            self.plan.run(stream)
+            for st in self.stages_all:
+                st.params.step_count += 1
 
         def _base(self, name: str) -> int:
             """First global rank of the boundary group a link channel lives on."""

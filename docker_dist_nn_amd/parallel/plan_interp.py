@@ -96,7 +96,11 @@ class PlanInterpreter:
 
     def __init__(self, ns, groups: dict, timeout_s: float = 120.0):
         self.ns, self.groups, self.timeout = ns, groups, timeout_s
-        self.mem = stage_memory(ns.st)
+        # a co-located fan rank's plan addresses every hosted worker's buffers
+        self.stages = list(getattr(ns, "stages_all", None) or [ns.st])
+        self.mem = DeviceMemory([])
+        for st in self.stages:
+            self.mem.ranges += stage_memory(st).ranges
         self.stream = torch.cuda.current_stream(ns.st.device)
         self.queues: dict[int, list] = {}
         for o in ns.ops:
@@ -143,8 +147,8 @@ class PlanInterpreter:
     # ---- one step ------------------------------------------------------------------------------
     def run_step(self) -> None:
         ns = self.ns
-        p = ns.st.params
-        p.set_lr(p.optim.lr)
+        for st in self.stages:
+            st.params.set_lr(st.params.optim.lr)
         ipc = getattr(ns, "ipc", None)
         if ipc is not None:
             from ..utils.native import native
@@ -201,7 +205,8 @@ class PlanInterpreter:
                         raise RuntimeError(f"plan interpreter stalled: {heads}")
                     time.sleep(0.0005)
         torch.cuda.synchronize()
-        p.step_count += 1
+        for st in self.stages:
+            st.params.step_count += 1
 
 
 def interp_groups(mesh, names: Optional[dict] = None) -> tuple[dict, dict]:

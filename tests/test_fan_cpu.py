@@ -395,3 +395,81 @@ def test_fan_ipc_plans_deadlock_free_and_matched(dist_, reps):
             elif o["kind"] == nsmod.WAITV and "tag" in o:
                 waits.append((o["a"], o["tag"]))
     assert sorted(signals) == sorted(waits) and len(set(signals)) == len(signals)
+
+
+def _colo_builds(dist_, reps, place, M, mb=256, spec="784-512-256-128-10"):
+    """build_only FanNativeStep of every rank of a co-located layout over fake stages."""
+    from types import SimpleNamespace as NS
+
+    from docker_dist_nn_amd.engine.stage import OptimConfig, StageParams
+    from docker_dist_nn_amd.models.mlp import LayerGeom
+    from docker_dist_nn_amd.parallel.fan import FanNativeStep
+    from docker_dist_nn_amd.partition import plan_stages
+
+    spec = MLPSpec.parse(spec)
+    lay = FanLayout(tuple(dist_), tuple(reps), place)
+    f, b = stage_costs(spec, dist_)
+    sch = fan_schedule(lay, M, f, b)
+    plans = plan_stages(len(spec.layers), list(dist_))
+    out = {}
+    for rank in range(lay.world):
+        workers = lay.workers_of(rank)
+        execs = {}
+        for s, q in workers:
+            p = plans[s]
+            geoms = [LayerGeom(i, spec.layers[i]) for i in range(p.layer_start, p.layer_end)]
+            params = StageParams(geoms, torch.device("cpu"), OptimConfig())
+            nm = len(lay.local_micros(s, q, M))
+            base = (rank + 1) << 40 | (s + 1) << 36
+            st = NS(nm=nm, mb=mb, boundary="bf16", _has_w=True, _o_native=True,
+                    _prog=NS(segments=lambda: {"FINO", "W"}), params=params, geoms=geoms,
+                    rows_of=lambda j, mb=mb: slice(j * mb, (j + 1) * mb))
+            for k, (key, w) in enumerate((("x_in", geoms[0].kp), ("grad_out", geoms[-1].np_),
+                                          ("output", geoms[-1].np_),
+                                          ("dx_send", geoms[0].kp))):
+                setattr(st, key, _FT(base | (k + 1) << 32, nm * mb, w))
+            execs[s] = NS(stages=[st], ops=[sch.local_ops(s, q)])
+        s0, q0 = workers[0]
+        mesh = NS(rank=rank, stage=s0, replica=q0, layout=lay, dp=reps[s0], workers=workers,
+                  replica_at=lambda s, w=dict(workers): w[s])
+        comms = {f"{d}{bb}": (d, bb) for d in "fb" for bb in range(lay.S - 1)}
+        comms.update({f"dp{st_}": ("dp", st_) for st_ in range(lay.S) if reps[st_] > 1})
+        ex = NS(execs=execs, stages=[execs[k].stages[0] for k in sorted(execs)])
+        out[rank] = FanNativeStep(ex, mesh, sch, comms=comms, build_only=True)
+    return lay, out
+
+
+@pytest.mark.parametrize("dist_,reps,place", [([3, 1], [2, 1], ((0, 1), (1,))),
+                                              ([3, 1], [4, 1], ((0, 1, 2, 3), (3,))),
+                                              ([3, 1], [7, 1], ((0, 1, 2, 3, 4, 5, 6), (6,))),
+                                              ([1, 2, 1], [2, 2, 1], ((0, 1), (2, 3), (3,)))])
+def test_colocated_fan_native_plans_deadlock_free(dist_, reps, place):
+    """The native step of a co-located layout (several workers per rank: their compute in slot
+    order on one stream, hops between them as device copies, the rest in per-slot RCCL groups
+    on the boundary communicators) completes in the plan simulator, also with one resident RCCL
+    kernel per rank; every remote hop is one send matched by one receive, every local hop one
+    copy."""
+    from docker_dist_nn_amd.parallel import native_step as nsmod
+    from docker_dist_nn_amd.parallel import plan_sim
+
+    M = 2 * max(reps) + 1
+    lay, builds = _colo_builds(dist_, reps, place, M)
+    plans = {r: plan_sim.RankPlan(ns.ops, ns.n_streams) for r, ns in builds.items()}
+    for serial in (False, True):
+        assert plan_sim.simulate(plans, steps=2, serial_rccl=serial).makespan > 0
+    sends, recvs, copies = [], [], 0
+    for r, ns in builds.items():
+        assert ns.mode == "fan-slotted-colocated" and ns.n_streams == 2
+        for o in nsmod.flatten(ns.ops):
+            if o["kind"] == nsmod.SEND:
+                sends.append((r, o["gpeer"], o["tag"][:2]))
+            elif o["kind"] == nsmod.RECV:
+                recvs.append((o["gpeer"], r, o["tag"][:2]))
+            elif o["kind"] == nsmod.COPY:
+                copies += 1
+    assert sorted(sends) == sorted(recvs)
+    local = sum(1 for s in range(lay.S - 1) for j in range(M)
+                if lay.rank_of(s, lay.replica_of(s, j)) ==
+                lay.rank_of(s + 1, lay.replica_of(s + 1, j)))
+    assert copies == 2 * local and len(sends) == 2 * M * (lay.S - 1) - 2 * local
+

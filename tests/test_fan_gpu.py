@@ -53,6 +53,14 @@ def _worker(rank, world, port, dist_, reps, M, dp_reduce, use_interp, steps, out
                            build_only=True, ipc=tr.ipc_pipe)
         assert ns.transport == "ipc" and ns.mode == "fan-ipc-slotted"
         it = PlanInterpreter(ns, groups, timeout_s=60)
+    elif use_interp and lay.colocated:  # boundary-indexed communicators (co-located plan)
+        names = {f"f{b}": g for b, g in mesh.bnd_f.items()}
+        names.update({f"b{b}": g for b, g in mesh.bnd_b.items()})
+        names.update({f"dp{s_}": g for s_, g in mesh.dp_groups.items()})
+        ns = FanNativeStep(tr.executor, mesh, tr.sched, comms={k: k for k in names},
+                           build_only=True)
+        assert ns.mode == "fan-slotted-colocated"
+        it = PlanInterpreter(ns, names, timeout_s=60)
     elif use_interp:
         names = {"f_in": mesh.fwd_in, "f_out": mesh.fwd_out, "b_in": mesh.bwd_in,
                  "b_out": mesh.bwd_out, "dp": mesh.dp_group}
@@ -249,3 +257,29 @@ def test_fan_ipc_native_step_graph_capture(dev, dist_, M):
                     assert np.array_equal(a, b), (tag, wb, k)
             assert np.array_equal(np.load(os.path.join(d, "py_loss0.npy")),
                                   np.load(os.path.join(d, f"{tag}_loss0.npy")))
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("reps,place,M,dp_reduce", [([2, 1], ((0, 1), (1,)), 6, "allreduce"),
+                                                    ([3, 1], ((0, 1, 2), (2,)), 7, "shard")])
+def test_colocated_fan_plan_interpreted_bitwise_equals_python(dev, reps, place, M, dp_reduce):
+    """The native step of a co-located layout -- the EXACT op list FanNativeStep builds for the
+    rank hosting a heavy-stage replica AND the light stage (both workers' segments on one
+    stream in slot order, the hops between them as device copies, the others in per-slot
+    groups on the boundary communicators, each worker's DP buckets) -- run by the gloo plan
+    interpreter trains bit for bit like the Python executor (processes sharing cuda:0)."""
+    dist_, steps = [3, 1], 3
+    world = len({x for p in place for x in p})
+    with tempfile.TemporaryDirectory() as d:
+        for use, tag in ((False, "py"), (True, "plan")):
+            mp.start_processes(_worker, args=(world, _port(), dist_, reps, M, dp_reduce, use,
+                                              steps, d, tag, place),
+                               nprocs=world, join=True, start_method="spawn")
+        for k in range(4):
+            for wb in ("w", "b"):
+                a = np.load(os.path.join(d, f"py_{wb}{k}.npy"))
+                b = np.load(os.path.join(d, f"plan_{wb}{k}.npy"))
+                assert np.array_equal(a, b), (wb, k)
+        assert np.array_equal(np.load(os.path.join(d, "py_loss0.npy")),
+                              np.load(os.path.join(d, "plan_loss0.npy")))
+
