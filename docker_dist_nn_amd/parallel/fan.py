@@ -944,8 +944,10 @@ def _fan_native_step_class():
             self.colo = True
             self.ex, self.mesh, self.sched = executor, mesh, sched
             self.lay = mesh.layout
-            self.workers = list(mesh.workers)
-            self.wstages = {s: executor.execs[s].stages[0] for s, _ in self.workers}
+            self.workers = list(mesh.workers or [(mesh.stage, mesh.replica)])
+            # a rank hosting one worker of a co-located layout runs a plain PipelineExecutor
+            self.execs = getattr(executor, "execs", None) or {mesh.stage: executor}
+            self.wstages = {s: self.execs[s].stages[0] for s, _ in self.workers}
             for st in self.wstages.values():
                 if st._prog is None or not st._has_w or not st._o_native:
                     raise ValueError("native fan step needs recorded stages (compile_native)")
@@ -1060,7 +1062,7 @@ def _fan_native_step_class():
                 self.ops += ops
             for s in sorted(mine, reverse=True):  # weight gradients + update per worker
                 st = self.wstages[s]
-                self._check_w(self.ex.execs[s].ops[0])
+                self._check_w(self.execs[s].ops[0])
                 self.st, self.dp, self.sharded = st, lay.reps[s], st.params.sharded
                 self.comms["dp"] = self.comms.get(f"dp{s}", 0)
                 self._wgrad_update(COMM)

@@ -150,10 +150,13 @@ class PlanInterpreter:
         for st in self.stages:
             st.params.set_lr(st.params.optim.lr)
         ipc = getattr(ns, "ipc", None)
-        if ipc is not None:
+        nat = None
+        if ipc is not None or any(o["kind"] == COPY for q in self.queues.values() for o in q):
             from ..utils.native import native
 
-            nat = native()
+            nat = native()  # device copies: IPC hops, and a co-located rank's local hops
+        seq = 0
+        if ipc is not None:
             ipc.seq += 1
             seq = ipc.seq
         head = {s: 0 for s in self.queues}

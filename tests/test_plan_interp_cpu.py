@@ -64,6 +64,7 @@ def _worker(rank, world, port, out):
             params=NS(set_lr=lambda lr: None, optim=NS(lr=0.1), step_count=0))
     it = pi.PlanInterpreter.__new__(pi.PlanInterpreter)
     it.ns, it.groups, it.timeout = NS(st=st, ops=ops), groups, 30
+    it.stages = [st]
     it.mem = pi.stage_memory(st)
     it.stream = None
     it.queues = {}
