@@ -57,7 +57,7 @@ static void check(int rc, const char* what) {
   if (rc != 0) {
     std::string msg = std::string(what) + " failed: ";
     if (std::string(what).rfind("gemm_bf16", 0) == 0) msg += dnn::gemm_error_string(rc);
-    else if (std::string(what) == "mlp_tail" || std::string(what) == "mlp_fwd_tail")
+    else if (std::string(what) == "mlp_tail")
       msg += dnn::mlp_tail_error(rc);
     else if (std::string(what) == "blas_gemm") msg += dnn::blas_error(rc);
     else msg += "precondition/launch error code " + std::to_string(rc);
@@ -287,77 +287,6 @@ PYBIND11_MODULE(_native, m) {
       py::arg("M"), py::arg("K3"), py::arg("N3"), py::arg("N4"), py::arg("n_cls"),
       py::arg("scale"), py::arg("act3"), py::arg("act2"), py::arg("stream"));
   m.def("mlp_tail_blocks", &dnn::mlp_tail_blocks);
-  // The forward of the layer before the tail fused in front of it (a: [M][K] input, w: [256][K],
-  // bias fp32, output x of the tail): same tail arguments as mlp_tail.
-  static constexpr int kActRelu = 1;  // dnn::ACT_RELU (kernels/common.hpp, device header)
-  m.def(
-      "mlp_fwd_tail",
-      [](uintptr_t a, long lda, uintptr_t w, long ldw, uintptr_t bias, int K, uintptr_t x,
-         long ldx, uintptr_t w3, long ldw3, uintptr_t b3, uintptr_t w4, long ldw4, uintptr_t b4,
-         uintptr_t labels, uintptr_t h3, long ldh3, uintptr_t dz4, long lddz4, uintptr_t dz3,
-         long lddz3, uintptr_t dz2, long lddz2, uintptr_t loss_part, uintptr_t correct,
-         uintptr_t cs4, long ld_cs4, uintptr_t cs3, long ld_cs3, uintptr_t cs2, long ld_cs2,
-         int M, int N4, int n_cls, float scale, uintptr_t stream) {
-        launch(
-            "mlp_fwd_tail",
-            [=](hipStream_t s, const dnn::Program& R) {
-              GemmParams g{};
-              g.A = R.fix(P<const uint16_t>(a));
-              g.lda = lda;
-              g.B = R.fix(P<const uint16_t>(w));
-              g.ldb = ldw;
-              g.C = R.fix(P<void>(x));
-              g.ldc = ldx;
-              g.bias = R.fix(P<const float>(bias));
-              g.M = M;
-              g.N = 256;
-              g.K = K;
-              g.act = kActRelu;
-              dnn::TailParams p{};
-              p.X = R.fix(P<const uint16_t>(x));
-              p.ldx = ldx;
-              p.W3 = R.fix(P<const uint16_t>(w3));
-              p.ldw3 = ldw3;
-              p.b3 = R.fix(P<const float>(b3));
-              p.W4 = R.fix(P<const uint16_t>(w4));
-              p.ldw4 = ldw4;
-              p.b4 = R.fix(P<const float>(b4));
-              p.labels = R.fix(P<const int>(labels));
-              p.H3 = R.fix(P<uint16_t>(h3));
-              p.ldh3 = ldh3;
-              p.DZ4 = R.fix(P<uint16_t>(dz4));
-              p.lddz4 = lddz4;
-              p.DZ3 = R.fix(P<uint16_t>(dz3));
-              p.lddz3 = lddz3;
-              p.DZ2 = R.fix(P<uint16_t>(dz2));
-              p.lddz2 = lddz2;
-              p.loss_part = R.fix(P<float>(loss_part));
-              p.correct = R.fix(P<int>(correct));
-              p.cs4 = R.fix(P<float>(cs4));
-              p.ld_cs4 = ld_cs4;
-              p.cs3 = R.fix(P<float>(cs3));
-              p.ld_cs3 = ld_cs3;
-              p.cs2 = R.fix(P<float>(cs2));
-              p.ld_cs2 = ld_cs2;
-              p.M = M;
-              p.K3 = 256;
-              p.N3 = 128;
-              p.N4 = N4;
-              p.n_cls = n_cls;
-              p.scale = scale;
-              p.act3 = kActRelu;
-              p.act2 = kActRelu;
-              return dnn::mlp_fwd_tail(g, p, s);
-            },
-            stream);
-      },
-      py::arg("a"), py::arg("lda"), py::arg("w"), py::arg("ldw"), py::arg("bias"), py::arg("K"),
-      py::arg("x"), py::arg("ldx"), py::arg("w3"), py::arg("ldw3"), py::arg("b3"), py::arg("w4"),
-      py::arg("ldw4"), py::arg("b4"), py::arg("labels"), py::arg("h3"), py::arg("ldh3"),
-      py::arg("dz4"), py::arg("lddz4"), py::arg("dz3"), py::arg("lddz3"), py::arg("dz2"),
-      py::arg("lddz2"), py::arg("loss_part"), py::arg("correct"), py::arg("cs4"),
-      py::arg("ld_cs4"), py::arg("cs3"), py::arg("ld_cs3"), py::arg("cs2"), py::arg("ld_cs2"),
-      py::arg("M"), py::arg("N4"), py::arg("n_cls"), py::arg("scale"), py::arg("stream"));
   // Grouped GEMM launch (no epilogue extras: the split-K weight gradients of a step). problems:
   // (a, lda, b, ldb, c, ldc, c_split_stride, M, N, K, k_total, accumulate, splits)
   m.def(

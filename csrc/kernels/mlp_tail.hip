@@ -48,9 +48,9 @@ namespace tail {
 // Waves per workgroup of the standalone launch: 16 (four per SIMD, <= 128 registers each) for
 // the branch-free ReLU form, so one 16-row block per wave covers 65536 rows in one round and
 // four independent block chains share each SIMD; the generic-activation form (runtime
-// activation branches, <= 128 registers; not on the benchmarked models) runs 8. The fused
-// forward + tail launch (mlp_fwd_tail_kernel) runs the body with the 8 waves of its 256x256
-// GEMM tile.
+// activation branches, <= 128 registers; not on the benchmarked models) runs 8. (A launch
+// fusing the previous layer's forward in front of the tail lost in the step twice, rounds 2
+// and 6: profiles/r6_prune/restore_fwd_tail.patch.)
 template <bool RELU>
 constexpr int waves() { return RELU ? 16 : 8; }
 constexpr int MAX_CLS = 16;  // classes held by one 16-wide MFMA block
@@ -375,32 +375,6 @@ __global__ __launch_bounds__(64 * tail::waves<RELU>()) void mlp_tail_kernel(Tail
                               p.M >> 4, blockIdx.x);
 }
 
-// Forward of the layer BEFORE the tail fused in front of it (ReLU everywhere): workgroup t
-// first computes the 256-row tile t of X = relu(A . W^T + b) (K3 = 256 = one 256x256 tile,
-// 8 waves, the one-tile main loop and staged epilogue of gemm.hip) and stores it, then runs
-// the tail over exactly those 256 rows -- read back from L2, no kernel boundary in between, and
-// one launch fewer. The tail's per-row math is unchanged; its partials are per 256-row tile.
-template <int K3, int N3>
-__global__ __launch_bounds__(512) void mlp_fwd_tail_kernel(GemmParams g, TailParams p) {
-  using C = Cfg<256, 256, 4, 2, 2>;
-  constexpr int NW = C::NW;
-  static_assert(K3 == C::BN, "one tile = the tail input");
-  constexpr int SM = cmax<C::SMEM, tail::Geo<K3, N3, NW>::SMEM>::v;
-  __shared__ __attribute__((aligned(16))) char smem[SM];
-  char LDS_AS* lds = (char LDS_AS*)smem;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int tm = blockIdx.x;
-  f32x4_t acc[C::FM][C::FN];
-  mma_tile<C, KMAJ, KMAJ>(g, tm * C::BM, 0, 0, g.K >> 6, lds, acc, wave, lane);
-  epilogue_staged<C, false>(g, acc, lds, tm * C::BM, 0, tm, 0, wave, lane);
-  // workgroup-scope release/acquire + barrier: the tile's stores (this CU, never read here
-  // before, so no stale L1 lines) are visible to every wave, and the LDS is free for the
-  // tail's weight images. (An agent-scope __threadfence() writes back L2 per workgroup.)
-  __syncthreads();
-  tail_body<K3, N3, NW, true>(p, lds, tm * (C::BM / 16), 1, NW, (tm + 1) * (C::BM / 16), tm);
-}
-
 int mlp_tail_blocks(int M) {
   static int cus = 0;
   if (!cus) {
@@ -424,22 +398,6 @@ const char* mlp_tail_error(int code) {
     case -9: return "mlp_tail: kernel launch failed";
     default: return "mlp_tail: unknown error";
   }
-}
-
-int mlp_fwd_tail(const GemmParams& g, const TailParams& p, hipStream_t stream) {
-  if (p.M <= 0 || p.M % 256 || g.M != p.M || g.N != 256 || p.K3 != 256 || p.N3 != 128 ||
-      g.K <= 0 || g.K % 64 || g.act != ACT_RELU || p.act2 != ACT_RELU || p.act3 != ACT_RELU ||
-      !g.bias || g.aux || g.colsum || g.xent_labels || g.mask_out || g.mask_in || g.ct ||
-      g.accumulate || g.k_total || g.C != (const void*)p.X || g.ldc != p.ldx ||
-      mlp_tail_blocks(p.M) != p.M / 256)
-    return -2;
-  if (p.n_cls < 1 || p.n_cls > tail::MAX_CLS || (p.N4 != 64 && p.N4 != 128)) return -3;
-  const long lds[] = {g.lda, g.ldb, p.ldx, p.ldw3, p.ldw4, p.ldh3, p.lddz4, p.lddz3, p.lddz2};
-  for (long l : lds)
-    if (l % 8) return -4;
-  hipLaunchKernelGGL((mlp_fwd_tail_kernel<256, 128>), dim3(p.M / 256), dim3(512), 0, stream, g,
-                     p);
-  return hipGetLastError() == hipSuccess ? 0 : -9;
 }
 
 int mlp_tail(const TailParams& p, hipStream_t stream) {

@@ -56,7 +56,6 @@ int mlp_tail(const TailParams& p, hipStream_t stream);
 // tail's X) fused in front of the tail: one workgroup per 256-row tile, M / 256 partials, which
 // must equal mlp_tail_blocks(M). -2 = unsupported geometry (the caller keeps two launches).
 struct GemmParams;
-int mlp_fwd_tail(const GemmParams& g, const TailParams& p, hipStream_t stream);
 const char* mlp_tail_error(int code);
 
 }  // namespace dnn

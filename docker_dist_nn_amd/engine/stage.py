@@ -491,9 +491,6 @@ class Stage:
                 if big and dz_by_dgrad and x_by_fwd:
                     self.dzT[i] = torch.zeros(g.np_, R, dtype=bf, device=dev)
                     self.actT[i - 1] = torch.zeros(g.kp, R, dtype=bf, device=dev)
-        # ... and the forward of the layer before the tail fused in front of it (one launch
-        # fewer, the tail reads its input rows back from L2): ReLU, 256-wide, 256-row tiles
-        self.fwd_tail = self._fwd_tail_ok()
         # dgrad GEMMs read W^T (contraction-contiguous B operand, see ops.linear_dgrad)
         if dev.type == "cuda" and switches.get("DNN_DGRAD_WT") == "1":
             L = len(self.geoms)
@@ -561,15 +558,6 @@ class Stage:
         return (ops.tail_supported(g3.kp, g3.np_, g4.np_, self.n_cls) and
                 g3.spec.activation in acts and g2.spec.activation in acts and
                 self.mb % 16 == 0)
-
-    def _fwd_tail_ok(self) -> bool:
-        L = len(self.geoms)
-        if not self.tail or switches.get("DNN_FWD_TAIL") != "1":
-            return False
-        g1, g2 = self.geoms[L - 3], self.geoms[L - 2]
-        return (g1.spec.activation == "relu" and g2.spec.activation == "relu" and
-                self.relu_mask[L - 3] is None and (L - 3) not in self.actT and
-                ops.fwd_tail_supported(self.mb, g1.np_, g2.kp, g2.np_))
 
     # ---- fp8 pipeline boundary (opt-in: Trainer(boundary="fp8")) -------------------------
     def enable_fp8_boundary(self, has_prev: bool, has_next: bool) -> None:
@@ -661,20 +649,9 @@ class Stage:
         x = self.input_of(i)[r]
         y = self.acts[i][r]
         L = len(self.geoms)
-        if self.tail and (i == L - 2 or (self.fwd_tail and i == L - 3)):
+        if self.tail and i == L - 2:
             return  # computed by the tail kernel at i == L - 1
-        if self.tail and i == L - 1 and self.fwd_tail:
-            k = j * self.xent_per_micro
-            ops.mlp_fwd_tail(self.input_of(L - 3)[r], p.wbf(L - 3), p.b32(L - 3),
-                             self.acts[L - 3][r], p.wbf(L - 2), p.b32(L - 2), p.wbf(L - 1),
-                             p.b32(L - 1), self.labels[r], self.acts[L - 2][r],
-                             self.dz[L - 1][r], self.dz[L - 2][r], self.dz[L - 3][r],
-                             self.n_cls, 1.0 / self.global_batch,
-                             loss_part=self.loss_part[k:k + self.xent_per_micro],
-                             correct=self.correct[k:k + self.xent_per_micro],
-                             cs4=self._bpart(L - 1, j), cs3=self._bpart(L - 2, j),
-                             cs2=self._bpart(L - 3, j))
-        elif self.tail and i == L - 1:
+        if self.tail and i == L - 1:
             k = j * self.xent_per_micro
             ops.mlp_tail(self.acts[L - 3][r], p.wbf(L - 2), p.b32(L - 2), p.wbf(L - 1),
                          p.b32(L - 1), self.labels[r], self.acts[L - 2][r], self.dz[L - 1][r],

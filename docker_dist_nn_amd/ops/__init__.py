@@ -3,7 +3,7 @@ from .kernels import (GEMV_MAX_ROWS, KMAJ, MNMAJ, STREAMK_WG, adam_update, blas_
                       colsum_partial, dact_colsum, dequant_rows_fp8, quant_rows_fp8,
                       dgrad_tiles, gemm, gemv, linear_dgrad, linear_fwd, linear_fwd_xent,
                       linear_wgrad, linear_wgrad_group, linear_wgrad_streamk, mlp_tail, pack_bf16, pick_splits, pick_tiles,
-                      fwd_tail_supported, mlp_fwd_tail, reduce_multi, reduce_slabs, sgd_update, softmax_rows, softmax_xent,
+                      reduce_multi, reduce_slabs, sgd_update, softmax_rows, softmax_xent,
                       step_advance, streamk_partial_elems, streamk_tiles, tail_blocks,
                       tail_supported, transpose_bf16, transpose_multi, unpack_bf16, bias_act_cast, wgrad_config, xent_blocks,
                       xent_tiles)
@@ -13,6 +13,6 @@ __all__ = ["GEMV_MAX_ROWS", "KMAJ", "MNMAJ", "STREAMK_WG", "adam_update", "blas_
            "colsum_partial", "dact_colsum", "dequant_rows_fp8", "quant_rows_fp8",
            "dgrad_tiles", "gemm", "gemv", "linear_dgrad", "linear_fwd", "linear_fwd_xent",
            "linear_wgrad", "linear_wgrad_group", "linear_wgrad_streamk", "mlp_tail", "pack_bf16", "pick_splits", "pick_tiles",
-           "fwd_tail_supported", "mlp_fwd_tail", "reduce_multi", "reduce_slabs", "sgd_update", "softmax_rows", "softmax_xent",
+           "reduce_multi", "reduce_slabs", "sgd_update", "softmax_rows", "softmax_xent",
            "step_advance", "streamk_partial_elems", "streamk_tiles", "tail_blocks", "tail_supported",
            "transpose_bf16", "transpose_multi", "unpack_bf16", "bias_act_cast", "wgrad_config", "xent_blocks", "xent_tiles"]

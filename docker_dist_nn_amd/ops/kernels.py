@@ -893,49 +893,6 @@ def mlp_tail(x, w3, b3, w4, b4, labels, h3, dz4, dz3, dz2, n_cls, scale, act3="r
                       _act(act2), _stream(x))
 
 
-def fwd_tail_supported(rows: int, n_prev: int, k3: int, n3: int) -> bool:
-    """mlp_fwd_tail applies: 256-row tiles that match the tail's partial count, the previous
-    layer's output = the tail's 256-wide input, N3 = 128 (ReLU checked by the caller)."""
-    return (rows > 0 and rows % 256 == 0 and tail_blocks(rows) == rows // 256 and
-            n_prev == 256 and k3 == 256 and n3 == 128)
-
-
-def mlp_fwd_tail(a, w, bias, x, w3, b3, w4, b4, labels, h3, dz4, dz3, dz2, n_cls, scale,
-                 loss_part=None, correct=None, cs4=None, cs3=None, cs2=None):
-    """x = relu(a . w^T + bias) (the layer before the tail, 256 outputs) followed by mlp_tail
-    on x, as ONE launch (csrc/kernels/mlp_tail.hip mlp_fwd_tail_kernel; ReLU activations).
-    Same outputs as linear_fwd + mlp_tail; CPU runs exactly those two."""
-    rows, K = a.shape
-    if not fwd_tail_supported(rows, w.shape[0], x.shape[1], w3.shape[0]) or w.shape[1] != K:
-        raise ValueError("mlp_fwd_tail: unsupported geometry")
-    if not a.is_cuda:
-        linear_fwd(a, w, bias, x, act="relu")
-        return mlp_tail(x, w3, b3, w4, b4, labels, h3, dz4, dz3, dz2, n_cls, scale,
-                        loss_part=loss_part, correct=correct, cs4=cs4, cs3=cs3, cs2=cs2)
-    nb = tail_blocks(rows)
-    for t, name, cols in ((cs4, "cs4", w4.shape[0]), (cs3, "cs3", w3.shape[0]),
-                          (cs2, "cs2", x.shape[1])):
-        if t is None or t.dtype != torch.float32 or t.dim() != 2 or t.shape[0] < nb or \
-                t.shape[1] < cols or t.stride(1) != 1:
-            raise ValueError(f"{name} must be fp32 [{nb}][>={cols}] row-major")
-    if loss_part is None or loss_part.numel() < nb or correct is None or \
-            correct.dtype != torch.int32 or correct.numel() < nb:
-        raise ValueError(f"loss_part / correct (int32) need {nb} entries")
-    for t, name in ((a, "a"), (w, "w"), (x, "x"), (w3, "w3"), (w4, "w4"), (h3, "h3"),
-                    (dz4, "dz4"), (dz3, "dz3"), (dz2, "dz2")):
-        _rows(t, name, torch.bfloat16)
-    if bias.dtype != torch.float32 or bias.numel() < 256:
-        raise ValueError("bias must be fp32 with >= 256 entries")
-    if labels.dtype != torch.int32 or labels.numel() < rows:
-        raise ValueError("labels must be int32 with one entry per row")
-    native().mlp_fwd_tail(_p(a), a.stride(0), _p(w), w.stride(0), _p(bias), K, _p(x),
-                          x.stride(0), _p(w3), w3.stride(0), _p(b3), _p(w4), w4.stride(0),
-                          _p(b4), _p(labels), _p(h3), h3.stride(0), _p(dz4), dz4.stride(0),
-                          _p(dz3), dz3.stride(0), _p(dz2), dz2.stride(0), _p(loss_part),
-                          _p(correct), _p(cs4), cs4.stride(0), _p(cs3), cs3.stride(0), _p(cs2),
-                          cs2.stride(0), rows, w4.shape[0], n_cls, float(scale), _stream(a))
-
-
 def softmax_rows(logits, out, n_cls, labels=None, pred=None, correct=None):
     rows = logits.shape[0]
     if not logits.is_cuda:

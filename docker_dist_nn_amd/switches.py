@@ -64,9 +64,6 @@ SWITCHES: dict[str, tuple[str, str]] = {
     "DNN_FAULT_NATIVE_STEP": ("", "fault injection (tests): comma-separated ranks whose "
                                    "native multi-rank step construction raises; all ranks "
                                    "then fall back to the Python executor together"),
-    "DNN_FWD_TAIL": ("0", "fuse the forward of the layer before the classifier tail into the "
-                          "tail launch (mlp_fwd_tail_kernel; ReLU, 256-wide, 256-row tiles); "
-                          "headline 0.375 vs 0.372 ms (71 us = the two kernels' sum), opt-in"),
     "DNN_H0_DOUBLE": ("1", "single-stage native steps: the layer-0 activation alternates between "
                            "two buffers from step to step (a relocatable Program region), so "
                            "with DNN_XSTEP the next step's layer-0 forward does not wait for "

@@ -166,81 +166,3 @@ def test_loopback_pipeline_last_stage_uses_tail(dev, monkeypatch, schedule):
     for a, b in zip(res[0][0], res[1][0]):
         assert abs(a - b) <= 1e-4 * abs(a) + 1e-5
     torch.testing.assert_close(res[1][1], res[0][1], rtol=1e-3, atol=1e-5)
-
-
-def test_fwd_tail_equals_fwd_then_tail(dev):
-    """mlp_fwd_tail (the 512 -> 256 forward fused in front of the tail, one workgroup per
-    256-row tile) stores the same activation and the same per-row tail outputs bit for bit as
-    linear_fwd + mlp_tail; the partials group rows per tile instead, so their sums agree to
-    rounding."""
-    rows, k = 65536, 512
-    if not ops.fwd_tail_supported(rows, 256, 256, 128):
-        pytest.skip("needs one 256-row tile per tail workgroup (256-CU part)")
-    g = torch.Generator().manual_seed(11)
-    a = torch.relu(torch.randn(rows, k, generator=g)).to(torch.bfloat16).to(dev)
-    w = (torch.randn(256, k, generator=g) / k ** 0.5).to(torch.bfloat16).to(dev)
-    b = (torch.randn(256, generator=g) * 0.1).to(dev)
-    _, w3, b3, w4, b4, labels = _case(rows, 256, 128, 64, 10, seed=12)
-    t = [v.to(dev) for v in (w3, b3, w4, b4, labels)]
-    res = []
-    for fused in (False, True):
-        x = torch.full((rows, 256), 7.0, dtype=torch.bfloat16, device=dev)
-        nb = ops.tail_blocks(rows)
-        bf, f32 = torch.bfloat16, torch.float32
-        out = dict(x=x, h3=torch.full((rows, 128), 7.0, dtype=bf, device=dev),
-                   dz4=torch.zeros(rows, 64, dtype=bf, device=dev),
-                   dz3=torch.full((rows, 128), 7.0, dtype=bf, device=dev),
-                   dz2=torch.full((rows, 256), 7.0, dtype=bf, device=dev),
-                   loss=torch.zeros(nb, dtype=f32, device=dev),
-                   corr=torch.zeros(nb, dtype=torch.int32, device=dev),
-                   cs4=torch.full((nb, 64), 7.0, dtype=f32, device=dev),
-                   cs3=torch.full((nb, 128), 7.0, dtype=f32, device=dev),
-                   cs2=torch.full((nb, 256), 7.0, dtype=f32, device=dev))
-        args = (*t, out["h3"], out["dz4"], out["dz3"], out["dz2"], 10, 1.0 / rows)
-        kw = dict(loss_part=out["loss"], correct=out["corr"], cs4=out["cs4"], cs3=out["cs3"],
-                  cs2=out["cs2"])
-        if fused:
-            ops.mlp_fwd_tail(a, w, b, x, *args, **kw)
-        else:
-            ops.linear_fwd(a, w, b, x, act="relu")
-            ops.mlp_tail(x, *args, **kw)
-        torch.cuda.synchronize(dev)
-        res.append(out)
-    want, got = res
-    for key in ("x", "h3", "dz4", "dz3", "dz2"):
-        assert torch.equal(got[key], want[key]), key
-    assert int(got["corr"].sum()) == int(want["corr"].sum())
-    torch.testing.assert_close(got["loss"].sum(), want["loss"].sum(), rtol=1e-5, atol=1e-3)
-    for key in ("cs4", "cs3", "cs2"):
-        torch.testing.assert_close(got[key].sum(0), want[key].sum(0), rtol=1e-4, atol=1e-5)
-
-
-def test_engine_fwd_tail_trains_like_two_launches(dev, monkeypatch):
-    """DNN_FWD_TAIL=1 on the headline model at 65536 rows: same losses to rounding and the
-    same weights to rounding (bias-gradient partials are grouped per tile)."""
-    from docker_dist_nn_amd import NAMED_MODELS
-    from docker_dist_nn_amd.data import synthetic_mnist
-    from docker_dist_nn_amd.engine import OptimConfig, Trainer
-
-    rows = 65536
-    if not ops.fwd_tail_supported(rows, 256, 256, 128):
-        pytest.skip("needs one 256-row tile per tail workgroup (256-CU part)")
-    x, y = synthetic_mnist(rows, seed=4)
-    xb = torch.zeros(rows, 832, dtype=torch.bfloat16)
-    xb[:, :784] = torch.from_numpy(x).to(torch.bfloat16)
-    xb, yb = xb.to(dev), torch.from_numpy(y).to(dev)
-    res = []
-    for flag in ("0", "1"):
-        monkeypatch.setenv("DNN_FWD_TAIL", flag)
-        tr = Trainer(NAMED_MODELS["mnist-fcnn"], micro_batch=rows, num_micro=1,
-                     optim=OptimConfig(lr=0.05, momentum=0.9), device=dev)
-        assert tr.stages[0].fwd_tail == (flag == "1")
-        losses = []
-        for _ in range(3):
-            tr.set_batch(xb, yb)
-            tr.step()
-            losses.append(tr.loss())
-        res.append((losses, tr.stages[0].params.master.clone()))
-    for a, b in zip(res[0][0], res[1][0]):
-        assert abs(a - b) < 1e-4 * max(1.0, abs(a))
-    torch.testing.assert_close(res[1][1], res[0][1], rtol=1e-3, atol=1e-4)
