@@ -434,7 +434,11 @@ def _colo_builds(dist_, reps, place, M, mb=256, spec="784-512-256-128-10"):
                   replica_at=lambda s, w=dict(workers): w[s])
         comms = {f"{d}{bb}": (d, bb) for d in "fb" for bb in range(lay.S - 1)}
         comms.update({f"dp{st_}": ("dp", st_) for st_ in range(lay.S) if reps[st_] > 1})
-        ex = NS(execs=execs, stages=[execs[k].stages[0] for k in sorted(execs)])
+        # as FanTrainer builds them: a rank hosting several workers gets the multi-worker
+        # executor (engine/fan_trainer._RankSteps: .execs), a one-worker rank a plain
+        # PipelineExecutor (.stages / .ops only)
+        ex = NS(execs=execs, stages=[execs[k].stages[0] for k in sorted(execs)]) \
+            if len(workers) > 1 else execs[s0]
         out[rank] = FanNativeStep(ex, mesh, sch, comms=comms, build_only=True)
     return lay, out
 
