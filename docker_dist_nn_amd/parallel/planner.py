@@ -121,8 +121,14 @@ class StageTimes:
                 sy = sum(t for _, t in v)
                 sxx = sum(n * n for n, _ in v)
                 sxy = sum(n * t for n, t in v)
-                per = (k * sxy - sx * sy) / (k * sxx - sx * sx)
-                fixed = max(0.0, (sy - per * sx) / k)
+                den = k * sxx - sx * sx
+                if den <= 0:  # every point at the same micro-batch count: no fixed term
+                    fixed, per = 0.0, sy / sx
+                else:
+                    per = (k * sxy - sx * sy) / den
+                    fixed = (sy - per * sx) / k
+                    if fixed < 0.0:  # refit through the origin rather than clamp
+                        fixed, per = 0.0, sxy / sxx
             self.fit.setdefault((w, a, b), []).append((mb, fixed, per))
         for v in self.fit.values():
             v.sort()
